@@ -1,0 +1,171 @@
+#!/usr/bin/env python3
+"""Flagship benchmark: whole-node decode tokens/s + per-stage ms, Llama-2-7B split over N stages.
+
+Metric/config from BASELINE.json: "tokens/sec (whole node) + per-stage ms, Llama-7B split
+over 1/2/4/8 stages".  One process per GPU (torchrun); rank r serves an even contiguous block
+range of Llama-2-7B (bf16, synthetic random-init weights: no checkpoints on the box), hidden
+states hop stage->stage over RCCL (xGMI), the last stage samples server-side with the
+reference CLI's defaults (temperature 1.0, top_p 0.92, top_k 50, repetition penalty 1.5) and
+returns token ids to rank 0.
+
+Work per GPU is fixed as N grows ("weak" scaling): N micro-batches x --batch sessions are in
+flight, so every GPU processes N micro-batch ticks of its 32/N blocks per step.  A step
+advances every session by one token; value = generated tokens/s over the whole node.
+
+    python bench.py                       # N=1 (defaults finish in ~1-2 minutes)
+    torchrun --nproc-per-node N bench.py --gpus N --steps K --warmup W
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+METRIC = "tokens/sec (whole node) + per-stage ms, Llama-7B split over 1/2/4/8 stages"
+
+
+def baseline_value():
+    """Reference-equivalent number recorded in BASELINE.json (filled from a measured run)."""
+    try:
+        with open(os.path.join(HERE, "BASELINE.json")) as f:
+            b = json.load(f)
+        v = b.get("measured_reference_equivalent", {}).get("decode_tokens_per_s_same_batch")
+        return float(v) if v else None
+    except Exception:
+        return None
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=None)
+    ap.add_argument("--steps", type=int, default=32)
+    ap.add_argument("--warmup", type=int, default=8)
+    ap.add_argument("--model", default="llama2-7b")
+    ap.add_argument("--batch", type=int, default=64, help="sessions per micro-batch")
+    ap.add_argument("--micro", type=int, default=None, help="micro-batches in flight (default: N stages)")
+    ap.add_argument("--prompt-len", type=int, default=128)
+    ap.add_argument("--temperature", type=float, default=1.0)
+    ap.add_argument("--top-p", type=float, default=0.92)
+    ap.add_argument("--top-k", type=int, default=50)
+    ap.add_argument("--repetition-penalty", type=float, default=1.5)
+    ap.add_argument("--gemm", default=os.environ.get("MPAMD_GEMM", "auto"), choices=["auto", "native", "hipblaslt"])
+    ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--device", default=None)
+    a = ap.parse_args(argv)
+
+    from src import ops
+    from src.models.config import resolve_model
+    from src.models.weights import random_stage_weights
+    from src.parallel import dist as pdist
+    from src.parallel.pipeline import PipelineEngine
+    from src.partition import even_splits, stage_ranges
+    from src.runtime.executor import StageExecutor
+    from src.runtime.sampler import SamplingParams
+
+    dev_type = a.device or ("cuda" if torch.cuda.is_available() else "cpu")
+    rank, world, local, device = pdist.init_distributed(dev_type)
+    n = a.gpus or world
+    if n != world:
+        raise SystemExit(f"--gpus {n} but WORLD_SIZE={world}: launch with torchrun --nproc-per-node {n}")
+    ops.set_gemm_policy(a.gemm)
+    cfg = resolve_model(a.model)
+    cuts = even_splits(cfg.num_hidden_layers, world)
+    start, end = stage_ranges(cuts, cfg.num_hidden_layers)[rank]
+    M = a.micro or world
+    B = a.batch
+    dtype = torch.bfloat16
+    t0 = time.time()
+    w = random_stage_weights(cfg, start, end, has_embed=rank == 0, has_head=rank == world - 1, device=device,
+                             dtype=dtype, seed=a.seed)
+    max_len = a.prompt_len + a.warmup + a.steps + 8
+    max_len = 64 * math.ceil(max_len / 64)
+    kv_bytes = None if device.type == "cuda" else 256 << 20
+    ex = StageExecutor(cfg, w, device, dtype=dtype, max_sessions=M * B, max_seq_len=max(max_len, 256),
+                       kv_cache_bytes=kv_bytes, use_graphs=not a.no_graphs, graph_max_batch=max(B, 1),
+                       max_tokens_per_step=max(B * a.prompt_len, B))
+    sp = SamplingParams(a.temperature, a.top_p, a.top_k, a.repetition_penalty)
+    eng = PipelineEngine(ex, rank, world, sp, n_micro=M, batch=B, seed=a.seed)
+    gen = torch.Generator().manual_seed(1234)
+    prompts = [torch.randint(0, cfg.vocab_size, (B, a.prompt_len), generator=gen) for _ in range(M)]
+    load_s = time.time() - t0
+
+    def sync():
+        if device.type == "cuda":
+            torch.cuda.synchronize()
+
+    # prefill (TTFT of the whole batch through the pipeline)
+    pdist.barrier(device)
+    sync()
+    tp0 = time.perf_counter()
+    eng.prefill(prompts)
+    eng.decode(1)  # first decode round also captures the decode hipGraphs
+    sync()
+    pdist.barrier(device)
+    prefill_s = time.perf_counter() - tp0
+
+    eng.decode(a.warmup)
+    sync()
+    pdist.barrier(device)
+    sync()
+    t1 = time.perf_counter()
+    eng.timing = True
+    eng.decode(a.steps)
+    sync()
+    pdist.barrier(device)
+    sync()
+    dt_local = time.perf_counter() - t1
+    eng.timing = False
+    stage_ms = eng.stage_ms() or 0.0
+    eng.finish()
+    dt = pdist.all_max(dt_local, device)
+    per_stage = pdist.all_gather_floats([stage_ms, float(end - start)], device)
+    tokens = a.steps * M * B
+    value = tokens / dt
+    base = baseline_value()
+    if rank == 0:
+        rec = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "tokens/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(1000 * dt / a.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": (round(value / base, 3) if base else None),
+            "dtype": "bf16",
+            "data": "synthetic (random-init Llama-2-7B weights, random prompt ids)",
+            "config": {
+                "model": "Llama-2-7B" if a.model == "llama2-7b" else a.model,
+                "global_batch": M * B,
+                "seq_len": a.prompt_len,
+                "parallelism": f"pp{world}",
+                "micro_batches": M,
+                "sessions_per_micro_batch": B,
+                "splits": cuts,
+                "sampling": {"temperature": a.temperature, "top_p": a.top_p, "top_k": a.top_k,
+                             "repetition_penalty": a.repetition_penalty},
+                "gemm": a.gemm,
+                "graphs": not a.no_graphs,
+            },
+            "per_stage_ms": [round(p[0], 3) for p in per_stage],
+            "per_stage_blocks": [int(p[1]) for p in per_stage],
+            "prefill_plus_first_token_s": round(prefill_s, 3),
+            "load_s": round(load_s, 1),
+        }
+        print(json.dumps(rec), flush=True)
+    pdist.shutdown()
+
+
+if __name__ == "__main__":
+    main()

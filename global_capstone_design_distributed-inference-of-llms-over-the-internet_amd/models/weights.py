@@ -1,0 +1,262 @@
+"""Per-stage weights: synthetic random init or HF checkpoint loading of ONLY the stage's keys.
+
+The reference loads the whole HF model on CPU in every stage process and then prunes
+``model.layers`` (reference src/llama_partition.py:495-530); the vendored Petals server
+instead reads only ``model.layers.{i}.*`` from the sharded checkpoint
+(reference petals/server/from_pretrained.py:35-128).  Here a stage reads only its own
+blocks (plus embeddings / final norm / lm_head when its role needs them) straight from
+the safetensors shards, and lays them out for the MI355X kernels:
+
+* q/k/v fused into one ``qkv`` matrix [(nh + 2 nkv) * D, H] -> one GEMM per layer;
+* gate/up fused into ``gate_up`` [2F, H] with rows interleaved in 16-row blocks
+  ([g0..g15, u0..u15, g16..g31, ...]) so the GEMM epilogue can apply SwiGLU in registers;
+* everything resident on the GPU (no per-forward CPU<->GPU streaming, unlike
+  src/llama_partition.py:169-180, :233-293 of the reference).
+
+Random init is deterministic per (seed, block index): a model split into any number of
+stages gets bit-identical weights, which the pipeline-equivalence tests rely on.
+"""
+from __future__ import annotations
+
+import dataclasses
+import glob
+import json
+import os
+from typing import Dict, List, Optional
+
+import torch
+
+from .config import ModelConfig
+from ..ops.reference import GU_BLOCK
+
+INIT_STD = 0.02
+
+
+def interleave_gate_up(gate: torch.Tensor, up: torch.Tensor) -> torch.Tensor:
+    F, H = gate.shape
+    assert F % GU_BLOCK == 0, "intermediate_size must be a multiple of 16"
+    return torch.stack([gate.view(F // GU_BLOCK, GU_BLOCK, H), up.view(F // GU_BLOCK, GU_BLOCK, H)], 1).reshape(2 * F, H)
+
+
+def split_gate_up(gu: torch.Tensor):
+    F2, H = gu.shape
+    v = gu.view(F2 // (2 * GU_BLOCK), 2, GU_BLOCK, H)
+    return v[:, 0].reshape(F2 // 2, H), v[:, 1].reshape(F2 // 2, H)
+
+
+@dataclasses.dataclass
+class LlamaLayer:
+    input_norm: torch.Tensor
+    qkv: torch.Tensor
+    o: torch.Tensor
+    post_norm: torch.Tensor
+    gate_up: torch.Tensor
+    down: torch.Tensor
+
+
+@dataclasses.dataclass
+class GPT2Layer:
+    ln1_w: torch.Tensor
+    ln1_b: torch.Tensor
+    attn_w: torch.Tensor  # [3H, H] (HF Conv1D weight transposed)
+    attn_b: torch.Tensor
+    proj_w: torch.Tensor
+    proj_b: torch.Tensor
+    ln2_w: torch.Tensor
+    ln2_b: torch.Tensor
+    fc_w: torch.Tensor
+    fc_b: torch.Tensor
+    fc2_w: torch.Tensor
+    fc2_b: torch.Tensor
+
+
+@dataclasses.dataclass
+class StageWeights:
+    cfg: ModelConfig
+    start: int
+    end: int
+    layers: list
+    embed: Optional[torch.Tensor] = None        # [V, H] (gpt2: wte)
+    pos_embed: Optional[torch.Tensor] = None    # gpt2 wpe [P, H]
+    final_norm: Optional[torch.Tensor] = None   # llama [H]; gpt2 ln_f weight
+    final_norm_b: Optional[torch.Tensor] = None  # gpt2 ln_f bias
+    lm_head: Optional[torch.Tensor] = None      # [V, H]
+
+    @property
+    def has_embed(self) -> bool:
+        return self.embed is not None
+
+    @property
+    def has_head(self) -> bool:
+        return self.lm_head is not None
+
+    def nbytes(self) -> int:
+        n = 0
+        for t in self.tensors():
+            n += t.numel() * t.element_size()
+        return n
+
+    def tensors(self):
+        seen = set()
+        for lay in self.layers:
+            for f in dataclasses.fields(lay):
+                t = getattr(lay, f.name)
+                if id(t) not in seen:
+                    seen.add(id(t))
+                    yield t
+        for t in (self.embed, self.pos_embed, self.final_norm, self.final_norm_b, self.lm_head):
+            if t is not None and id(t) not in seen:
+                seen.add(id(t))
+                yield t
+
+
+def _gen(device, seed: int):
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    return g
+
+
+def _randn(shape, g, device, dtype, std=INIT_STD):
+    t = torch.empty(shape, dtype=torch.float32, device=device)
+    t.normal_(0.0, std, generator=g)
+    return t.to(dtype)
+
+
+def _random_llama_layer(cfg: ModelConfig, idx: int, device, dtype, seed: int) -> LlamaLayer:
+    g = _gen(device, seed * 100003 + idx + 1)
+    H, F = cfg.hidden_size, cfg.intermediate_size
+    qkv = _randn((cfg.q_dim + 2 * cfg.kv_dim, H), g, device, dtype)
+    o = _randn((H, cfg.q_dim), g, device, dtype)
+    gate = _randn((F, H), g, device, dtype)
+    up = _randn((F, H), g, device, dtype)
+    down = _randn((H, F), g, device, dtype)
+    ones = torch.ones(H, dtype=dtype, device=device)
+    return LlamaLayer(ones, qkv, o, ones.clone(), interleave_gate_up(gate, up), down)
+
+
+def _random_gpt2_layer(cfg: ModelConfig, idx: int, device, dtype, seed: int) -> GPT2Layer:
+    g = _gen(device, seed * 100003 + idx + 1)
+    H, F = cfg.hidden_size, cfg.intermediate_size
+    z = lambda n: torch.zeros(n, dtype=dtype, device=device)  # noqa: E731
+    o = lambda n: torch.ones(n, dtype=dtype, device=device)  # noqa: E731
+    return GPT2Layer(o(H), z(H), _randn((3 * H, H), g, device, dtype), z(3 * H), _randn((H, H), g, device, dtype),
+                     z(H), o(H), z(H), _randn((F, H), g, device, dtype), z(F), _randn((H, F), g, device, dtype), z(H))
+
+
+def random_stage_weights(cfg: ModelConfig, start: int, end: int, *, has_embed: bool, has_head: bool, device,
+                         dtype=torch.bfloat16, seed: int = 0) -> StageWeights:
+    device = torch.device(device)
+    mk = _random_gpt2_layer if cfg.model_type == "gpt2" else _random_llama_layer
+    layers = [mk(cfg, i, device, dtype, seed) for i in range(start, end)]
+    sw = StageWeights(cfg, start, end, layers)
+    H, V = cfg.hidden_size, cfg.vocab_size
+    if has_embed or (has_head and cfg.tie_word_embeddings):
+        g = _gen(device, seed * 100003 + 7919)
+        emb = _randn((V, H), g, device, dtype)
+        if has_embed:
+            sw.embed = emb
+        if cfg.model_type == "gpt2" and has_embed:
+            sw.pos_embed = _randn((cfg.max_position_embeddings, H), _gen(device, seed * 100003 + 7927), device,
+                                  dtype, std=0.01)
+        if has_head and cfg.tie_word_embeddings:
+            sw.lm_head = emb
+    if has_head:
+        sw.final_norm = torch.ones(H, dtype=dtype, device=device)
+        if cfg.model_type == "gpt2":
+            sw.final_norm_b = torch.zeros(H, dtype=dtype, device=device)
+        if sw.lm_head is None:
+            sw.lm_head = _randn((V, H), _gen(device, seed * 100003 + 7937), device, dtype)
+    return sw
+
+
+# ------------------------------------------------------------------ checkpoint loading
+class _Checkpoint:
+    """Key -> shard lookup over a local HF directory (sharded or single-file safetensors)."""
+
+    def __init__(self, path: str):
+        from safetensors import safe_open  # noqa: F401
+
+        self.path = path
+        self.key_to_file: Dict[str, str] = {}
+        idx = os.path.join(path, "model.safetensors.index.json")
+        if os.path.exists(idx):
+            with open(idx) as f:
+                wm = json.load(f)["weight_map"]
+            self.key_to_file = {k: os.path.join(path, v) for k, v in wm.items()}
+        else:
+            files = sorted(glob.glob(os.path.join(path, "*.safetensors")))
+            if not files:
+                raise FileNotFoundError(f"no safetensors weights under {path}")
+            from safetensors import safe_open
+
+            for fn in files:
+                with safe_open(fn, framework="pt") as f:
+                    for k in f.keys():
+                        self.key_to_file[k] = fn
+        self._handles = {}
+
+    def has(self, key: str) -> bool:
+        return key in self.key_to_file
+
+    def get(self, key: str) -> torch.Tensor:
+        from safetensors import safe_open
+
+        fn = self.key_to_file[key]
+        if fn not in self._handles:
+            self._handles[fn] = safe_open(fn, framework="pt")
+        return self._handles[fn].get_tensor(key)
+
+
+def load_stage_weights(cfg: ModelConfig, path: str, start: int, end: int, *, has_embed: bool, has_head: bool,
+                       device, dtype=torch.bfloat16) -> StageWeights:
+    ck = _Checkpoint(path)
+    dev = torch.device(device)
+
+    def t(key):
+        return ck.get(key).to(device=dev, dtype=dtype)
+
+    layers: List = []
+    if cfg.model_type == "gpt2":
+        pre = "transformer." if ck.has("transformer.wte.weight") else ""
+        for i in range(start, end):
+            p = f"{pre}h.{i}."
+            layers.append(GPT2Layer(t(p + "ln_1.weight"), t(p + "ln_1.bias"), t(p + "attn.c_attn.weight").t().contiguous(),
+                                    t(p + "attn.c_attn.bias"), t(p + "attn.c_proj.weight").t().contiguous(),
+                                    t(p + "attn.c_proj.bias"), t(p + "ln_2.weight"), t(p + "ln_2.bias"),
+                                    t(p + "mlp.c_fc.weight").t().contiguous(), t(p + "mlp.c_fc.bias"),
+                                    t(p + "mlp.c_proj.weight").t().contiguous(), t(p + "mlp.c_proj.bias")))
+        sw = StageWeights(cfg, start, end, layers)
+        if has_embed:
+            sw.embed = t(pre + "wte.weight")
+            sw.pos_embed = t(pre + "wpe.weight")
+        if has_head:
+            sw.final_norm, sw.final_norm_b = t(pre + "ln_f.weight"), t(pre + "ln_f.bias")
+            sw.lm_head = sw.embed if sw.embed is not None else t(pre + "wte.weight")
+        return sw
+    for i in range(start, end):
+        p = f"model.layers.{i}."
+        qkv = torch.cat([t(p + "self_attn.q_proj.weight"), t(p + "self_attn.k_proj.weight"),
+                         t(p + "self_attn.v_proj.weight")], 0).contiguous()
+        gu = interleave_gate_up(t(p + "mlp.gate_proj.weight"), t(p + "mlp.up_proj.weight")).contiguous()
+        layers.append(LlamaLayer(t(p + "input_layernorm.weight"), qkv, t(p + "self_attn.o_proj.weight"),
+                                 t(p + "post_attention_layernorm.weight"), gu, t(p + "mlp.down_proj.weight")))
+    sw = StageWeights(cfg, start, end, layers)
+    if has_embed:
+        sw.embed = t("model.embed_tokens.weight")
+    if has_head:
+        sw.final_norm = t("model.norm.weight")
+        if ck.has("lm_head.weight"):
+            sw.lm_head = t("lm_head.weight")
+        else:  # tied embeddings
+            sw.lm_head = sw.embed if sw.embed is not None else t("model.embed_tokens.weight")
+    return sw
+
+
+def build_stage_weights(cfg: ModelConfig, model: str, start: int, end: int, *, has_embed: bool, has_head: bool,
+                        device, dtype=torch.bfloat16, seed: int = 0) -> StageWeights:
+    """Checkpoint weights when ``model`` is a local HF directory with safetensors, else synthetic."""
+    if os.path.isdir(model) and (glob.glob(os.path.join(model, "*.safetensors"))):
+        return load_stage_weights(cfg, model, start, end, has_embed=has_embed, has_head=has_head, device=device,
+                                  dtype=dtype)
+    return random_stage_weights(cfg, start, end, has_embed=has_embed, has_head=has_head, device=device, dtype=dtype,
+                                seed=seed)

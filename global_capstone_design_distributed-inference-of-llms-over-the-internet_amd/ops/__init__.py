@@ -1,0 +1,217 @@
+"""Device-dispatching op layer.
+
+GPU tensors go to the hand-written gfx950 HIP kernels (``torch.ops.mpamd.*`` from
+``ops/_mpamd_kernels.so``); CPU tensors go to the plain-PyTorch implementations in
+``ops.reference``.  There is no silent fallback on the GPU: if the kernel library is
+missing on a GPU host the first GPU op raises (``require_native``).
+
+Projection GEMMs (``linear``) are dispatched by shape: decode-sized inputs (M <= 64,
+K % 256 == 0) use the native weight-streaming MFMA kernel with fused epilogues;
+larger (prefill) GEMMs go to hipBLASLt through ``torch.nn.functional.linear`` plus the
+native epilogue kernels.  ``MPAMD_GEMM=native|hipblaslt|auto`` overrides the policy.
+"""
+from __future__ import annotations
+
+import math
+import os
+import threading
+from typing import Optional, Tuple
+
+import torch
+
+from . import reference as ref
+from .reference import GU_BLOCK, rope_cos_sin  # noqa: F401  (re-export)
+
+_LOCK = threading.Lock()
+_LOADED: Optional[bool] = None
+_LOAD_ERROR: Optional[str] = None
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_mpamd_kernels.so")
+
+
+def load_library(build_if_missing: bool = True) -> bool:
+    """Load (building first if needed and possible) the HIP kernel library."""
+    global _LOADED, _LOAD_ERROR
+    with _LOCK:
+        if _LOADED is not None:
+            return _LOADED
+        try:
+            if build_if_missing:
+                try:
+                    from .build import build
+
+                    build()
+                except Exception as e:  # no hipcc / read-only tree: use a prebuilt library if present
+                    if not os.path.exists(LIB_PATH):
+                        raise
+                    _LOAD_ERROR = f"rebuild skipped: {e}"
+            torch.ops.load_library(LIB_PATH)
+            _LOADED = True
+        except Exception as e:  # pragma: no cover - depends on host toolchain
+            _LOADED = False
+            _LOAD_ERROR = str(e)
+        return _LOADED
+
+
+def native_available() -> bool:
+    return load_library()
+
+
+def require_native() -> None:
+    if not load_library():
+        raise RuntimeError(
+            "mpamd HIP kernels are not available on this GPU host "
+            f"({_LOAD_ERROR}); build them with `python -m src.ops.build`")
+
+
+def _native(t: torch.Tensor) -> bool:
+    if t.is_cuda:
+        require_native()
+        return True
+    return False
+
+
+_GEMM_POLICY = os.environ.get("MPAMD_GEMM", "auto")
+
+
+def set_gemm_policy(policy: str) -> None:
+    global _GEMM_POLICY
+    assert policy in ("auto", "native", "hipblaslt")
+    _GEMM_POLICY = policy
+
+
+def gemm_policy() -> str:
+    return _GEMM_POLICY
+
+
+# ---------------------------------------------------------------------------------------
+def rmsnorm(x, w, eps, out=None, residual=None, mode=0, rows=None):
+    """mode 0: y = norm(x)*w; 1: residual += x, y = norm(residual)*w; 2: residual = x, y = norm(x)*w."""
+    if not _native(x):
+        return ref.rmsnorm(x, w, eps, out=out, residual=residual, mode=mode, rows=rows)
+    if out is None:
+        n = rows.numel() if rows is not None else x.shape[0]
+        out = torch.empty(n, x.shape[1], dtype=x.dtype, device=x.device)
+    torch.ops.mpamd.rmsnorm(x, residual if residual is not None else x, w, out, float(eps), int(mode), rows)
+    return out
+
+
+def rope_kv_write(qkv, positions, cos, sin, k_cache, v_cache, slots, nh, nkv):
+    if not _native(qkv):
+        return ref.rope_kv_write(qkv, positions, cos, sin, k_cache, v_cache, slots, nh, nkv)
+    torch.ops.mpamd.rope_kv_write(qkv, positions, cos, sin, k_cache, v_cache, slots, int(nh), int(nkv))
+
+
+def kv_write(k, v, k_cache, v_cache, slots):
+    if not _native(k):
+        return ref.kv_write(k, v, k_cache, v_cache, slots)
+    torch.ops.mpamd.kv_write(k, v, k_cache, v_cache, slots)
+
+
+def attention_partition(num_queries: int, nkv: int, max_ctx: int, target_wgs: int = 1024) -> Tuple[int, int]:
+    """(part_size, num_parts) for split-K flash decoding: enough workgroups to fill 256 CUs."""
+    max_ctx = max(int(max_ctx), 1)
+    want = max(1, math.ceil(target_wgs / max(1, num_queries * nkv)))
+    np_ = max(1, min(want, math.ceil(max_ctx / 64)))
+    ps = 64 * math.ceil(math.ceil(max_ctx / np_) / 64)
+    ps = min(ps, 2048)
+    np_ = math.ceil(max_ctx / ps)
+    return ps, np_
+
+
+def attention_workspace(num_queries: int, nh: int, head_dim: int, num_parts: int, device) -> torch.Tensor:
+    return torch.empty(max(1, num_queries * nh * num_parts * (head_dim + 2)), dtype=torch.float32, device=device)
+
+
+def paged_attention(q, k_cache, v_cache, block_tables, q_seq, q_ctx, nh, nkv, scale, out=None, workspace=None,
+                    part_size=None, num_parts=None, max_ctx=None):
+    if not _native(q):
+        return ref.paged_attention(q, k_cache, v_cache, block_tables, q_seq, q_ctx, nh, nkv, scale, out=out)
+    T = q.shape[0]
+    D = k_cache.shape[-1]
+    if part_size is None:
+        if max_ctx is None:
+            max_ctx = int(q_ctx.max().item()) if T else 1
+        part_size, num_parts = attention_partition(T, nkv, max_ctx)
+    if out is None:
+        out = torch.empty(T, nh * D, dtype=q.dtype, device=q.device)
+    if workspace is None:
+        workspace = attention_workspace(T, nh, D, num_parts, q.device)
+    torch.ops.mpamd.paged_attention(q, k_cache, v_cache, block_tables, q_seq, q_ctx, out, workspace, int(nh), int(nkv),
+                                    float(scale), int(part_size), int(num_parts))
+    return out
+
+
+def embedding(ids, table, out=None):
+    if not _native(table):
+        return ref.embedding(ids, table, out=out)
+    if out is None:
+        out = torch.empty(ids.numel(), table.shape[1], dtype=table.dtype, device=table.device)
+    torch.ops.mpamd.embedding(ids, table, out)
+    return out
+
+
+def swiglu(gu, out=None):
+    if not _native(gu):
+        return ref.swiglu(gu, out=out)
+    if out is None:
+        out = torch.empty(gu.shape[0], gu.shape[1] // 2, dtype=gu.dtype, device=gu.device)
+    torch.ops.mpamd.swiglu(gu, out)
+    return out
+
+
+def add(a, b, out=None):
+    if not _native(a):
+        return ref.add(a, b, out=out)
+    if out is None:
+        out = torch.empty_like(a)
+    torch.ops.mpamd.add(a, b, out)
+    return out
+
+
+def argmax(logits, out=None):
+    if not _native(logits):
+        return ref.argmax(logits, out=out)
+    if out is None:
+        out = torch.empty(logits.shape[0], dtype=torch.long, device=logits.device)
+    torch.ops.mpamd.argmax(logits, out)
+    return out
+
+
+def sample(logits, temps, top_ps, top_ks, rep_pens, recent, recent_len, seeds, workspace=None, out=None):
+    if not _native(logits):
+        return ref.sample(logits, temps, top_ps, top_ks, rep_pens, recent, recent_len, seeds, out=out)
+    R, V = logits.shape
+    if out is None:
+        out = torch.empty(R, dtype=torch.long, device=logits.device)
+    if workspace is None:
+        workspace = torch.empty(max(1, R * V), dtype=torch.float32, device=logits.device)
+    torch.ops.mpamd.sample(logits, temps, top_ps, top_ks, rep_pens, recent, recent_len, seeds, workspace, out)
+    return out
+
+
+def native_gemm_ok(M: int, N: int, K: int, epilogue: int = 0) -> bool:
+    return 0 < M <= 64 and K % 256 == 0 and N % (32 if epilogue == 1 else 16) == 0
+
+
+def linear(x, w, out=None, epilogue=0, residual=None, policy=None):
+    """y = epilogue(x @ w^T). epilogue 0: none; 1: SwiGLU (16-row interleaved gate/up w); 2: + residual."""
+    if not _native(x):
+        return ref.linear(x, w, out=out, epilogue=epilogue, residual=residual)
+    M, K = x.shape
+    N = w.shape[0]
+    policy = policy or _GEMM_POLICY
+    use_native = policy == "native" or (policy == "auto" and native_gemm_ok(M, N, K, epilogue))
+    if use_native and native_gemm_ok(M, N, K, epilogue) and x.stride(0) % 8 == 0 and x.stride(1) == 1:
+        if out is None:
+            out = torch.empty(M, N // 2 if epilogue == 1 else N, dtype=x.dtype, device=x.device)
+        torch.ops.mpamd.gemm(x, w, out, residual, int(epilogue))
+        return out
+    y = torch.nn.functional.linear(x, w)  # hipBLASLt
+    if epilogue == 1:
+        return swiglu(y, out=out)
+    if epilogue == 2:
+        return add(y, residual, out=out)
+    if out is not None:
+        out.copy_(y)
+        return out
+    return y

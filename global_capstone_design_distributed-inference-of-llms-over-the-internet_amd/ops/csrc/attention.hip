@@ -1,0 +1,292 @@
+// Paged flash-decoding attention for gfx950 (survey K6 + K7).
+//
+// The reference materialises repeat_kv'd K/V and a full [B, H, T, P+T] fp32
+// score matrix with two matmuls (reference petals/llama/block.py:131-141).
+// This kernel reads each cached K/V row once, straight from its page:
+//
+//   grid  = (num_parts, nkv, T)   one workgroup per (query row, kv head, context slice)
+//   block = 256 threads (4 waves of 64)
+//
+// Each workgroup serves all NREP = nh / nkv query heads of its kv head (GQA without
+// materialising repeat_kv).  Lane mapping: LPT = D/8 lanes per token, each lane owns 8
+// head dims (one 16-B load); a wave-instruction covers 64/LPT consecutive tokens, i.e.
+// 1 KiB of contiguous cache.  Partial dot products are summed over the LPT lanes with
+// DPP row permutes (no LDS traffic), scores live in LDS, softmax is done in the exp2
+// domain, and P.V accumulates in fp32 registers.  With num_parts > 1 each slice
+// writes (o, m, l) partials that `paged_attn_reduce` combines (split-K over context).
+//
+// Queries carry their own (sequence row, context length), so the same kernel runs
+// decode (one query per sequence), chunked prefill (query i of a chunk sees
+// ctx = start + i + 1 -> causal) and replay.  ctx == 0 rows (batch padding) output 0.
+#include "common.h"
+
+namespace mp {
+
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+
+// Sum over groups of LPT consecutive lanes (LPT in {8, 16}); result valid in every lane.
+template <int LPT>
+__device__ __forceinline__ float group_sum(float v) {
+  v += dpp_mov<0xB1>(v);   // quad_perm [1,0,3,2]  (xor 1)
+  v += dpp_mov<0x4E>(v);   // quad_perm [2,3,0,1]  (xor 2)
+  v += dpp_mov<0x141>(v);  // row_half_mirror      (8-lane total)
+  if constexpr (LPT == 16) v += dpp_mov<0x140>(v);  // row_mirror (16-lane total)
+  return v;
+}
+
+template <int D, int NREP>
+__global__ __launch_bounds__(256) void paged_attn_kernel(
+    const bf16_t* __restrict__ q, int64_t q_stride, const bf16_t* __restrict__ kc,
+    const bf16_t* __restrict__ vc, const int32_t* __restrict__ block_tables, int bt_stride,
+    const int32_t* __restrict__ q_seq, const int32_t* __restrict__ q_ctx, bf16_t* __restrict__ out,
+    float* __restrict__ part_o, float* __restrict__ part_ml, int nkv, int page_log2, int PS, int NP,
+    float scale_log2) {
+  constexpr int LPT = D / 8;
+  constexpr int TPI = 64 / LPT;
+  constexpr int U = 4;
+  constexpr int TPW = TPI * U;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* s_p = smem;                  // [NREP][PS] scores -> probabilities
+  float* s_red = smem + NREP * PS;    // [4][NREP] per-wave maxes, then [4][NREP] sums
+  float* s_o = s_red + 8 * NREP;      // [4][NREP][D]
+
+  const int t = blockIdx.z, g = blockIdx.y, p = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int sl = lane % LPT, tg = lane / LPT;
+  const int nh = nkv * NREP;
+  const int ctx = q_ctx[t];
+  const int start = p * PS;
+  const int end = min(start + PS, ctx);
+  const int64_t obase = ((int64_t)t * nh + (int64_t)g * NREP) * D;
+  if (start >= end) {
+    if (NP == 1) {
+      for (int i = tid; i < NREP * D; i += 256) out[obase + i] = 0;
+    } else if (tid < NREP) {
+      float* ml = part_ml + (((int64_t)t * nh + g * NREP + tid) * NP + p) * 2;
+      ml[0] = -INFINITY;
+      ml[1] = 0.f;
+    }
+    return;
+  }
+  const int page_size = 1 << page_log2;
+  const int32_t* bt = block_tables + (int64_t)q_seq[t] * bt_stride;
+  const int64_t head_off = (int64_t)g * page_size * D + sl * 8;
+  const int64_t page_stride = (int64_t)nkv * page_size * D;
+
+  float qf[NREP][8];
+#pragma unroll
+  for (int r = 0; r < NREP; ++r) {
+    const u16x8 v = *reinterpret_cast<const u16x8*>(q + (int64_t)t * q_stride + (g * NREP + r) * D + sl * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) qf[r][j] = bf2f(v[j]) * scale_log2;
+  }
+
+  // ---- pass 1: scores (log2 domain) into LDS, running max per head ----
+  float mloc[NREP];
+#pragma unroll
+  for (int r = 0; r < NREP; ++r) mloc[r] = -INFINITY;
+  for (int base = start + w * TPW; base < end; base += 4 * TPW) {
+    u16x8 kv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int tok = base + u * TPI + tg;
+      if (tok < end) {
+        const int64_t pg = bt[tok >> page_log2];
+        kv[u] = *reinterpret_cast<const u16x8*>(kc + pg * page_stride + head_off +
+                                                 (int64_t)(tok & (page_size - 1)) * D);
+      } else {
+        kv[u] = (u16x8)(0);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int tok = base + u * TPI + tg;
+#pragma unroll
+      for (int r = 0; r < NREP; ++r) {
+        float d = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) d += qf[r][j] * bf2f(kv[u][j]);
+        d = group_sum<LPT>(d);
+        if (sl == 0 && tok < end) {
+          s_p[r * PS + (tok - start)] = d;
+          mloc[r] = fmaxf(mloc[r], d);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < NREP; ++r) {
+    const float m = wave_max(mloc[r]);
+    if (lane == 0) s_red[w * NREP + r] = m;
+  }
+  __syncthreads();
+  float mrow[NREP];
+#pragma unroll
+  for (int r = 0; r < NREP; ++r)
+    mrow[r] = fmaxf(fmaxf(s_red[r], s_red[NREP + r]), fmaxf(s_red[2 * NREP + r], s_red[3 * NREP + r]));
+
+  // ---- pass 2: probabilities p = exp2(s - m) in place ----
+  const int n = end - start;
+  for (int i = tid; i < NREP * n; i += 256) {
+    const int r = i / n, j = i - r * n;
+    float m = mrow[0];
+#pragma unroll
+    for (int rr = 1; rr < NREP; ++rr)
+      if (r == rr) m = mrow[rr];
+    s_p[r * PS + j] = exp2f(s_p[r * PS + j] - m);
+  }
+  __syncthreads();
+
+  // ---- pass 3: o = sum_t p_t * V_t, l = sum_t p_t ----
+  float acc[NREP][8];
+  float lsum[NREP];
+#pragma unroll
+  for (int r = 0; r < NREP; ++r) {
+    lsum[r] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[r][j] = 0.f;
+  }
+  for (int base = start + w * TPW; base < end; base += 4 * TPW) {
+    u16x8 vv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int tok = base + u * TPI + tg;
+      if (tok < end) {
+        const int64_t pg = bt[tok >> page_log2];
+        vv[u] = *reinterpret_cast<const u16x8*>(vc + pg * page_stride + head_off +
+                                                 (int64_t)(tok & (page_size - 1)) * D);
+      } else {
+        vv[u] = (u16x8)(0);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int tok = base + u * TPI + tg;
+      if (tok < end) {
+#pragma unroll
+        for (int r = 0; r < NREP; ++r) {
+          const float pr = s_p[r * PS + (tok - start)];
+          lsum[r] += pr;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[r][j] += pr * bf2f(vv[u][j]);
+        }
+      }
+    }
+  }
+  // reduce over the token groups of the wave (lanes sl, sl+LPT, ...)
+#pragma unroll
+  for (int o = LPT; o < 64; o <<= 1) {
+#pragma unroll
+    for (int r = 0; r < NREP; ++r) {
+      lsum[r] += __shfl_xor(lsum[r], o, 64);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[r][j] += __shfl_xor(acc[r][j], o, 64);
+    }
+  }
+  float* s_l = s_red + 4 * NREP;
+  if (tg == 0) {
+#pragma unroll
+    for (int r = 0; r < NREP; ++r) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s_o[(w * NREP + r) * D + sl * 8 + j] = acc[r][j];
+      if (sl == 0) s_l[w * NREP + r] = lsum[r];
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < NREP * D; i += 256) {
+    const int r = i / D, d = i - r * D;
+    const float o = s_o[r * D + d] + s_o[(NREP + r) * D + d] + s_o[(2 * NREP + r) * D + d] +
+                    s_o[(3 * NREP + r) * D + d];
+    const float l = s_l[r] + s_l[NREP + r] + s_l[2 * NREP + r] + s_l[3 * NREP + r];
+    if (NP == 1) {
+      out[obase + i] = f2bf(o / l);
+    } else {
+      const int64_t hp = ((int64_t)t * nh + g * NREP + r) * NP + p;
+      part_o[hp * D + d] = o;
+      if (d == 0) {
+        float m = mrow[0];
+#pragma unroll
+        for (int rr = 1; rr < NREP; ++rr)
+          if (r == rr) m = mrow[rr];
+        part_ml[hp * 2] = m;
+        part_ml[hp * 2 + 1] = l;
+      }
+    }
+  }
+}
+
+// Combine split-K partials: one workgroup (D threads) per (query row, head).
+__global__ void paged_attn_reduce_kernel(const float* __restrict__ part_o, const float* __restrict__ part_ml,
+                                         bf16_t* __restrict__ out, int NP, int D) {
+  const int64_t h = blockIdx.x;
+  const float* ml = part_ml + h * NP * 2;
+  float M = -INFINITY;
+  for (int p = 0; p < NP; ++p)
+    if (ml[2 * p + 1] > 0.f) M = fmaxf(M, ml[2 * p]);
+  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+    float num = 0.f, den = 0.f;
+    for (int p = 0; p < NP; ++p) {
+      const float l = ml[2 * p + 1];
+      if (l > 0.f) {
+        const float wgt = exp2f(ml[2 * p] - M);
+        num += wgt * part_o[(h * NP + p) * D + d];
+        den += wgt * l;
+      }
+    }
+    out[h * D + d] = f2bf(den > 0.f ? num / den : 0.f);
+  }
+}
+
+template <int D, int NREP>
+static void launch_attn(const void* q, int64_t q_stride, const void* kc, const void* vc, const int32_t* bt,
+                        int bt_stride, const int32_t* q_seq, const int32_t* q_ctx, void* out, float* ws_o,
+                        float* ws_ml, int T, int nkv, int page_log2, int PS, int NP, float scale_log2,
+                        hipStream_t stream) {
+  const size_t lds = (size_t)(NREP * PS + 8 * NREP + 4 * NREP * D) * sizeof(float);
+  hipLaunchKernelGGL((paged_attn_kernel<D, NREP>), dim3(NP, nkv, T), dim3(256), lds, stream, (const bf16_t*)q,
+                     q_stride, (const bf16_t*)kc, (const bf16_t*)vc, bt, bt_stride, q_seq, q_ctx, (bf16_t*)out,
+                     ws_o, ws_ml, nkv, page_log2, PS, NP, scale_log2);
+}
+
+}  // namespace mp
+
+extern "C" int mp_paged_attention(const void* q, int64_t q_stride, const void* kc, const void* vc,
+                                  const int32_t* bt, int bt_stride, const int32_t* q_seq, const int32_t* q_ctx,
+                                  void* out, float* workspace, int T, int nh, int nkv, int D, int page_size,
+                                  int PS, int NP, float scale, hipStream_t stream) {
+  using namespace mp;
+  if (T == 0) return 0;
+  if (nh % nkv != 0 || PS % 64 != 0 || PS > 2048 || NP < 1) return -1;
+  int page_log2 = 0;
+  while ((1 << page_log2) < page_size) ++page_log2;
+  if ((1 << page_log2) != page_size) return -2;
+  const int nrep = nh / nkv;
+  const float scale_log2 = scale * 1.4426950408889634f;
+  float* ws_o = workspace;
+  float* ws_ml = workspace + (int64_t)T * nh * NP * D;
+#define MP_ATTN_CASE(DD, RR)                                                                                  \
+  if (D == DD && nrep == RR) {                                                                                \
+    launch_attn<DD, RR>(q, q_stride, kc, vc, bt, bt_stride, q_seq, q_ctx, out, ws_o, ws_ml, T, nkv, page_log2, \
+                        PS, NP, scale_log2, stream);                                                          \
+    goto launched;                                                                                            \
+  }
+  MP_ATTN_CASE(128, 1)
+  MP_ATTN_CASE(128, 2)
+  MP_ATTN_CASE(128, 4)
+  MP_ATTN_CASE(128, 8)
+  MP_ATTN_CASE(64, 1)
+  MP_ATTN_CASE(64, 2)
+  MP_ATTN_CASE(64, 4)
+  MP_ATTN_CASE(64, 8)
+#undef MP_ATTN_CASE
+  return -3;
+launched:
+  if (NP > 1) {
+    hipLaunchKernelGGL(paged_attn_reduce_kernel, dim3(T * nh), dim3(D), 0, stream, ws_o, ws_ml, (bf16_t*)out, NP,
+                       D);
+  }
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,271 @@
+// torch custom-op registrations (namespace `mpamd`) for the gfx950 kernels.
+//
+// Every op writes into caller-provided outputs and launches on the current HIP
+// stream, so a whole stage step can be captured into one hipGraph.  Shape and
+// dtype checks happen here, on the host, before any kernel sees a pointer.
+#include <ATen/ATen.h>
+#include <ATen/hip/HIPContext.h>
+#include <torch/library.h>
+
+#include <cmath>
+
+extern "C" {
+int mp_rmsnorm(const void* x, int64_t x_stride, void* res, int64_t res_stride, const void* w, void* y,
+               int64_t y_stride, const int32_t* rows, int nrows, int H, float eps, int mode, hipStream_t stream);
+int mp_rope_kv_write(void* qkv, int64_t qkv_stride, const int64_t* pos, const float* cos_t, const float* sin_t,
+                     void* kc, void* vc, const int64_t* slots, int T, int nh, int nkv, int D, int page_size,
+                     hipStream_t stream);
+int mp_kv_write(const void* k, int64_t k_stride, const void* v, int64_t v_stride, void* kc, void* vc,
+                const int64_t* slots, int T, int nkv, int D, int page_size, hipStream_t stream);
+int mp_paged_attention(const void* q, int64_t q_stride, const void* kc, const void* vc, const int32_t* bt,
+                       int bt_stride, const int32_t* q_seq, const int32_t* q_ctx, void* out, float* workspace, int T,
+                       int nh, int nkv, int D, int page_size, int PS, int NP, float scale, hipStream_t stream);
+int mp_embedding(const int64_t* ids, const void* table, void* out, int T, int H, int64_t vocab, hipStream_t stream);
+int mp_swiglu(const void* gu, void* out, int64_t T, int F, hipStream_t stream);
+int mp_add(const void* a, const void* b, void* y, int64_t n, hipStream_t stream);
+int mp_argmax(const void* logits, int64_t stride, int R, int V, int64_t* out, hipStream_t stream);
+int mp_sample(const void* logits, int64_t stride, int R, int V, const float* temps, const float* top_ps,
+              const int32_t* top_ks, const float* rep_pens, const int32_t* recent, int recent_stride,
+              const int32_t* recent_len, const int64_t* seeds, float* ws, int64_t* out, hipStream_t stream);
+int mp_gemm_bf16(const void* x, int64_t x_stride, const void* w, void* y, int64_t y_stride, const void* res,
+                 int64_t res_stride, int M, int N, int K, int epilogue, hipStream_t stream);
+}
+
+namespace {
+
+#define MP_CHECK(cond, msg) TORCH_CHECK(cond, "mpamd: ", msg)
+
+inline void check_launch(int rc, const char* what) {
+  TORCH_CHECK(rc == 0, "mpamd: ", what, " launch failed with code ", rc);
+}
+
+inline hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
+
+inline void check_bf16_cuda(const at::Tensor& t, const char* name) {
+  MP_CHECK(t.is_cuda(), std::string(name) + " must be on the GPU");
+  MP_CHECK(t.scalar_type() == at::kBFloat16, std::string(name) + " must be bf16");
+}
+
+inline void check_rows(const at::Tensor& t, const char* name) {
+  MP_CHECK(t.dim() == 2, std::string(name) + " must be 2-D [rows, cols]");
+  MP_CHECK(t.stride(1) == 1, std::string(name) + " must have unit inner stride");
+  MP_CHECK(t.stride(0) % 8 == 0, std::string(name) + " row stride must be a multiple of 8");
+  MP_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, std::string(name) + " must be 16-B aligned");
+}
+
+void rmsnorm(const at::Tensor& x, at::Tensor& residual, const at::Tensor& w, at::Tensor& y, double eps, int64_t mode,
+             const c10::optional<at::Tensor>& rows) {
+  check_bf16_cuda(x, "x");
+  check_bf16_cuda(w, "w");
+  check_bf16_cuda(y, "y");
+  check_rows(x, "x");
+  check_rows(y, "y");
+  const int H = x.size(1);
+  MP_CHECK(w.numel() == H && w.is_contiguous(), "weight shape");
+  MP_CHECK(y.size(1) == H, "y cols");
+  MP_CHECK(mode >= 0 && mode <= 2, "mode");
+  if (mode != 0) {
+    check_bf16_cuda(residual, "residual");
+    check_rows(residual, "residual");
+    MP_CHECK(residual.size(0) == x.size(0) && residual.size(1) == H, "residual shape");
+  }
+  const int32_t* rp = nullptr;
+  int nrows = x.size(0);
+  if (rows.has_value()) {
+    MP_CHECK(rows->scalar_type() == at::kInt && rows->is_contiguous() && rows->is_cuda(), "rows: int32 cuda");
+    MP_CHECK(mode == 0, "row gather only with mode 0");
+    rp = rows->data_ptr<int32_t>();
+    nrows = rows->numel();
+  }
+  MP_CHECK(y.size(0) >= nrows, "y rows");
+  check_launch(mp_rmsnorm(x.data_ptr(), x.stride(0), mode ? residual.data_ptr() : nullptr,
+                          mode ? residual.stride(0) : 0, w.data_ptr(), y.data_ptr(), y.stride(0), rp, nrows, H,
+                          (float)eps, (int)mode, cur_stream()),
+               "rmsnorm");
+}
+
+void rope_kv_write(at::Tensor& qkv, const at::Tensor& positions, const at::Tensor& cos, const at::Tensor& sin,
+                   at::Tensor& k_cache, at::Tensor& v_cache, const at::Tensor& slots, int64_t nh, int64_t nkv) {
+  check_bf16_cuda(qkv, "qkv");
+  check_rows(qkv, "qkv");
+  check_bf16_cuda(k_cache, "k_cache");
+  check_bf16_cuda(v_cache, "v_cache");
+  MP_CHECK(k_cache.dim() == 4 && k_cache.is_contiguous() && v_cache.is_contiguous(), "cache [pages, nkv, page, D]");
+  MP_CHECK(k_cache.sizes() == v_cache.sizes(), "k/v cache shapes differ");
+  const int D = k_cache.size(3), page = k_cache.size(2);
+  MP_CHECK(k_cache.size(1) == nkv, "cache kv heads");
+  MP_CHECK(qkv.size(1) == (nh + 2 * nkv) * D, "qkv width");
+  const int T = qkv.size(0);
+  MP_CHECK(positions.scalar_type() == at::kLong && positions.numel() == T && positions.is_contiguous(), "positions");
+  MP_CHECK(slots.scalar_type() == at::kLong && slots.numel() == T && slots.is_contiguous(), "slots");
+  MP_CHECK(cos.scalar_type() == at::kFloat && sin.scalar_type() == at::kFloat && cos.is_contiguous() &&
+               sin.is_contiguous() && cos.size(1) == D / 2 && sin.sizes() == cos.sizes(),
+           "cos/sin tables fp32 [max_pos, D/2]");
+  check_launch(mp_rope_kv_write(qkv.data_ptr(), qkv.stride(0), positions.data_ptr<int64_t>(), cos.data_ptr<float>(),
+                                sin.data_ptr<float>(), k_cache.data_ptr(), v_cache.data_ptr(),
+                                slots.data_ptr<int64_t>(), T, nh, nkv, D, page, cur_stream()),
+               "rope_kv_write");
+}
+
+void kv_write(const at::Tensor& k, const at::Tensor& v, at::Tensor& k_cache, at::Tensor& v_cache,
+              const at::Tensor& slots) {
+  check_bf16_cuda(k, "k");
+  check_bf16_cuda(v, "v");
+  check_rows(k, "k");
+  check_rows(v, "v");
+  MP_CHECK(k_cache.dim() == 4 && k_cache.is_contiguous() && v_cache.is_contiguous(), "cache layout");
+  const int nkv = k_cache.size(1), page = k_cache.size(2), D = k_cache.size(3);
+  MP_CHECK(k.size(1) == nkv * D && v.size(1) == nkv * D, "k/v width");
+  MP_CHECK(slots.scalar_type() == at::kLong && slots.numel() == k.size(0), "slots");
+  check_launch(mp_kv_write(k.data_ptr(), k.stride(0), v.data_ptr(), v.stride(0), k_cache.data_ptr(),
+                           v_cache.data_ptr(), slots.data_ptr<int64_t>(), k.size(0), nkv, D, page, cur_stream()),
+               "kv_write");
+}
+
+void paged_attention(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
+                     const at::Tensor& block_tables, const at::Tensor& q_seq, const at::Tensor& q_ctx,
+                     at::Tensor& out, at::Tensor& workspace, int64_t nh, int64_t nkv, double scale, int64_t part_size,
+                     int64_t num_parts) {
+  check_bf16_cuda(q, "q");
+  check_rows(q, "q");
+  check_bf16_cuda(out, "out");
+  MP_CHECK(out.is_contiguous(), "out contiguous");
+  const int D = k_cache.size(3);
+  const int T = q.size(0);
+  MP_CHECK(q.size(1) >= nh * D, "q width");
+  MP_CHECK(out.numel() == (int64_t)T * nh * D, "out numel");
+  MP_CHECK(k_cache.size(1) == nkv && k_cache.is_contiguous() && v_cache.is_contiguous(), "cache");
+  MP_CHECK(block_tables.scalar_type() == at::kInt && block_tables.dim() == 2 && block_tables.stride(1) == 1,
+           "block_tables int32 [S, max_pages]");
+  MP_CHECK(q_seq.scalar_type() == at::kInt && q_seq.numel() == T, "q_seq");
+  MP_CHECK(q_ctx.scalar_type() == at::kInt && q_ctx.numel() == T, "q_ctx");
+  MP_CHECK(workspace.scalar_type() == at::kFloat, "workspace fp32");
+  if (num_parts > 1) MP_CHECK(workspace.numel() >= (int64_t)T * nh * num_parts * (D + 2), "workspace too small");
+  check_launch(mp_paged_attention(q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
+                                  block_tables.data_ptr<int32_t>(), block_tables.stride(0), q_seq.data_ptr<int32_t>(),
+                                  q_ctx.data_ptr<int32_t>(), out.data_ptr(), workspace.data_ptr<float>(), T, nh, nkv,
+                                  D, k_cache.size(2), part_size, num_parts, (float)scale, cur_stream()),
+               "paged_attention");
+}
+
+void embedding(const at::Tensor& ids, const at::Tensor& table, at::Tensor& out) {
+  check_bf16_cuda(table, "table");
+  check_bf16_cuda(out, "out");
+  MP_CHECK(ids.scalar_type() == at::kLong && ids.is_contiguous(), "ids int64");
+  MP_CHECK(table.is_contiguous() && out.is_contiguous(), "contiguous");
+  MP_CHECK(out.numel() == ids.numel() * table.size(1), "out shape");
+  check_launch(mp_embedding(ids.data_ptr<int64_t>(), table.data_ptr(), out.data_ptr(), ids.numel(), table.size(1),
+                            table.size(0), cur_stream()),
+               "embedding");
+}
+
+void swiglu(const at::Tensor& gu, at::Tensor& out) {
+  check_bf16_cuda(gu, "gu");
+  check_bf16_cuda(out, "out");
+  MP_CHECK(gu.is_contiguous() && out.is_contiguous(), "contiguous");
+  const int64_t T = gu.size(0);
+  const int F = gu.size(1) / 2;
+  MP_CHECK(out.numel() == T * F, "out shape");
+  check_launch(mp_swiglu(gu.data_ptr(), out.data_ptr(), T, F, cur_stream()), "swiglu");
+}
+
+void add(const at::Tensor& a, const at::Tensor& b, at::Tensor& y) {
+  check_bf16_cuda(a, "a");
+  check_bf16_cuda(b, "b");
+  check_bf16_cuda(y, "y");
+  MP_CHECK(a.is_contiguous() && b.is_contiguous() && y.is_contiguous(), "contiguous");
+  MP_CHECK(a.numel() == b.numel() && a.numel() == y.numel(), "numel");
+  check_launch(mp_add(a.data_ptr(), b.data_ptr(), y.data_ptr(), a.numel(), cur_stream()), "add");
+}
+
+void argmax(const at::Tensor& logits, at::Tensor& out) {
+  check_bf16_cuda(logits, "logits");
+  check_rows(logits, "logits");
+  MP_CHECK(out.scalar_type() == at::kLong && out.numel() == logits.size(0), "out int64 [R]");
+  check_launch(mp_argmax(logits.data_ptr(), logits.stride(0), logits.size(0), logits.size(1),
+                         out.data_ptr<int64_t>(), cur_stream()),
+               "argmax");
+}
+
+void sample(const at::Tensor& logits, const at::Tensor& temps, const at::Tensor& top_ps, const at::Tensor& top_ks,
+            const at::Tensor& rep_pens, const at::Tensor& recent, const at::Tensor& recent_len,
+            const at::Tensor& seeds, at::Tensor& workspace, at::Tensor& out) {
+  check_bf16_cuda(logits, "logits");
+  check_rows(logits, "logits");
+  const int R = logits.size(0), V = logits.size(1);
+  MP_CHECK(temps.scalar_type() == at::kFloat && temps.numel() == R, "temps");
+  MP_CHECK(top_ps.scalar_type() == at::kFloat && top_ps.numel() == R, "top_ps");
+  MP_CHECK(top_ks.scalar_type() == at::kInt && top_ks.numel() == R, "top_ks");
+  MP_CHECK(rep_pens.scalar_type() == at::kFloat && rep_pens.numel() == R, "rep_pens");
+  MP_CHECK(recent.scalar_type() == at::kInt && recent.dim() == 2 && recent.size(0) == R && recent.is_contiguous(),
+           "recent int32 [R, n]");
+  MP_CHECK(recent_len.scalar_type() == at::kInt && recent_len.numel() == R, "recent_len");
+  MP_CHECK(seeds.scalar_type() == at::kLong && seeds.numel() == R, "seeds");
+  MP_CHECK(workspace.scalar_type() == at::kFloat && workspace.numel() >= (int64_t)R * V, "workspace");
+  MP_CHECK(out.scalar_type() == at::kLong && out.numel() == R, "out");
+  check_launch(mp_sample(logits.data_ptr(), logits.stride(0), R, V, temps.data_ptr<float>(), top_ps.data_ptr<float>(),
+                         top_ks.data_ptr<int32_t>(), rep_pens.data_ptr<float>(), recent.data_ptr<int32_t>(),
+                         recent.size(1), recent_len.data_ptr<int32_t>(), seeds.data_ptr<int64_t>(),
+                         workspace.data_ptr<float>(), out.data_ptr<int64_t>(), cur_stream()),
+               "sample");
+}
+
+void gemm(const at::Tensor& x, const at::Tensor& w, at::Tensor& y, const c10::optional<at::Tensor>& residual,
+          int64_t epilogue) {
+  check_bf16_cuda(x, "x");
+  check_bf16_cuda(w, "w");
+  check_bf16_cuda(y, "y");
+  check_rows(x, "x");
+  check_rows(y, "y");
+  MP_CHECK(w.dim() == 2 && w.is_contiguous(), "w [N, K] contiguous");
+  const int M = x.size(0), K = x.size(1), N = w.size(0);
+  MP_CHECK(w.size(1) == K, "K mismatch");
+  const int ncols = epilogue == 1 ? N / 2 : N;
+  MP_CHECK(y.size(0) == M && y.size(1) == ncols, "y shape");
+  const void* rp = nullptr;
+  int64_t rs = 0;
+  if (residual.has_value()) {
+    check_bf16_cuda(*residual, "residual");
+    check_rows(*residual, "residual");
+    rp = residual->data_ptr();
+    rs = residual->stride(0);
+  }
+  MP_CHECK(epilogue != 2 || rp != nullptr, "residual epilogue needs residual");
+  check_launch(mp_gemm_bf16(x.data_ptr(), x.stride(0), w.data_ptr(), y.data_ptr(), y.stride(0), rp, rs, M, N, K,
+                            (int)epilogue, cur_stream()),
+               "gemm");
+}
+
+}  // namespace
+
+TORCH_LIBRARY(mpamd, m) {
+  m.def("rmsnorm(Tensor x, Tensor(a!) residual, Tensor w, Tensor(b!) y, float eps, int mode, Tensor? rows) -> ()");
+  m.def(
+      "rope_kv_write(Tensor(a!) qkv, Tensor positions, Tensor cos, Tensor sin, Tensor(b!) k_cache, "
+      "Tensor(c!) v_cache, Tensor slots, int nh, int nkv) -> ()");
+  m.def("kv_write(Tensor k, Tensor v, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor slots) -> ()");
+  m.def(
+      "paged_attention(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor q_seq, Tensor q_ctx, "
+      "Tensor(a!) out, Tensor(b!) workspace, int nh, int nkv, float scale, int part_size, int num_parts) -> ()");
+  m.def("embedding(Tensor ids, Tensor table, Tensor(a!) out) -> ()");
+  m.def("swiglu(Tensor gu, Tensor(a!) out) -> ()");
+  m.def("add(Tensor a, Tensor b, Tensor(a!) y) -> ()");
+  m.def("argmax(Tensor logits, Tensor(a!) out) -> ()");
+  m.def(
+      "sample(Tensor logits, Tensor temps, Tensor top_ps, Tensor top_ks, Tensor rep_pens, Tensor recent, "
+      "Tensor recent_len, Tensor seeds, Tensor(a!) workspace, Tensor(b!) out) -> ()");
+  m.def("gemm(Tensor x, Tensor w, Tensor(a!) y, Tensor? residual, int epilogue) -> ()");
+}
+
+TORCH_LIBRARY_IMPL(mpamd, CUDA, m) {
+  m.impl("rmsnorm", &rmsnorm);
+  m.impl("rope_kv_write", &rope_kv_write);
+  m.impl("kv_write", &kv_write);
+  m.impl("paged_attention", &paged_attention);
+  m.impl("embedding", &embedding);
+  m.impl("swiglu", &swiglu);
+  m.impl("add", &add);
+  m.impl("argmax", &argmax);
+  m.impl("sample", &sample);
+  m.impl("gemm", &gemm);
+}

@@ -1,0 +1,73 @@
+// Shared device helpers for the gfx950 (MI355X / CDNA4) kernels of this framework.
+//
+// Conventions used by every kernel in ops/csrc:
+//   * bf16 tensors travel as raw 16-bit patterns (unsigned short); math is fp32.
+//   * global loads/stores of bf16 are always vectorised (8 x bf16 = 16 B per lane),
+//     the wave is 64 lanes wide, and blocks are multiples of 64 threads.
+//   * every launcher takes the caller's hipStream_t so the ops are capturable
+//     into hipGraphs (no allocation, no synchronisation inside a launcher).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mp {
+
+typedef unsigned short bf16_t;
+typedef __attribute__((ext_vector_type(8))) unsigned short u16x8;
+typedef __attribute__((ext_vector_type(4))) unsigned short u16x4;
+typedef __attribute__((ext_vector_type(2))) unsigned short u16x2;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(8))) short s16x8;
+
+constexpr int WAVE = 64;
+
+__device__ __forceinline__ float bf2f(bf16_t u) {
+  return __uint_as_float(((unsigned)u) << 16);
+}
+
+// Round-to-nearest-even fp32 -> bf16 (hipcc lowers the cast to v_cvt_pk_bf16_f32,
+// which also keeps NaN a NaN).
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;
+  return __builtin_bit_cast(bf16_t, b);
+}
+
+__device__ __forceinline__ float round_bf(float f) { return bf2f(f2bf(f)); }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, WAVE);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, WAVE));
+  return v;
+}
+
+// Block-wide sum for blockDim.x <= 1024 (multiple of 64). `red` needs >= 16 floats.
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  v = wave_sum(v);
+  __syncthreads();
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  float t = 0.f;
+  for (int i = 0; i < nw; ++i) t += red[i];
+  return t;
+}
+
+__device__ __forceinline__ float block_max(float v, float* red) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  v = wave_max(v);
+  __syncthreads();
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  float t = -INFINITY;
+  for (int i = 0; i < nw; ++i) t = fmaxf(t, red[i]);
+  return t;
+}
+
+}  // namespace mp

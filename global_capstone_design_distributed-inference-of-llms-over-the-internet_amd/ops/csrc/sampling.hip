@@ -1,0 +1,297 @@
+// Server-side token sampler for gfx950 (survey K13).
+//
+// Semantics follow the reference's `_sample_token` (reference
+// src/rpc_handler.py:327-403), batched over rows with per-row parameters:
+//   temperature <= 0           -> argmax of the raw logits
+//   repetition penalty          -> every distinct id among the last <= 50 generated ids gets
+//                                  logit /= rp**count (logit > 0) or *= rp**count (else);
+//                                  if the last 3 ids are equal that id gets rp**3 more
+//   softmax(logits / max(T, 1e-5)), top-k mask (0 < k < V), top-p "keep cum <= p, always
+//   keep the first", renormalise, draw one id.
+// Instead of a Python loop, torch.topk, a full sort and a cumsum, one 1024-thread block per
+// row does: fp32 copy -> penalty -> softmax -> radix-select top-k threshold (4 x 8-bit
+// histogram passes) -> radix top-p threshold on probability MASS histograms -> one
+// inverse-CDF draw with a block scan.  Ties at a threshold value are kept together
+// (torch.topk/sort break them by position; documented divergence).
+#include "common.h"
+
+namespace mp {
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+constexpr int SB = 1024;  // threads per block
+
+__device__ __forceinline__ float block_sum_1k(float v, float* red) { return block_sum(v, red); }
+
+// Exclusive block scan of one float per thread (blockDim == SB).
+__device__ __forceinline__ float block_excl_scan(float v, float* red, float* total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float inc = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const float n = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += n;
+  }
+  __syncthreads();
+  if (lane == 63) red[w] = inc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float acc = 0.f;
+    for (int i = 0; i < SB / 64; ++i) {
+      const float t = red[i];
+      red[i] = acc;
+      acc += t;
+    }
+    red[SB / 64] = acc;
+  }
+  __syncthreads();
+  *total = red[SB / 64];
+  return red[w] + inc - v;
+}
+
+__global__ __launch_bounds__(SB) void sample_kernel(const bf16_t* __restrict__ logits, int64_t stride, int V,
+                                                    const float* __restrict__ temps, const float* __restrict__ top_ps,
+                                                    const int32_t* __restrict__ top_ks,
+                                                    const float* __restrict__ rep_pens,
+                                                    const int32_t* __restrict__ recent, int recent_stride,
+                                                    const int32_t* __restrict__ recent_len,
+                                                    const int64_t* __restrict__ seeds, float* __restrict__ ws,
+                                                    int64_t* __restrict__ out) {
+  __shared__ float red[SB / 64 + 1];
+  __shared__ unsigned hist[256];
+  __shared__ float mass[256];
+  __shared__ unsigned s_u[4];
+  __shared__ int s_i[2];
+  const int row = blockIdx.x, tid = threadIdx.x;
+  const bf16_t* lrow = logits + (int64_t)row * stride;
+  float* x = ws + (int64_t)row * V;
+  const float temp = temps[row];
+
+  // ---- fp32 copy + max (max is needed by both the greedy and the sampling path) ----
+  float mx = -INFINITY;
+  int mi = 0x7fffffff;
+  for (int i = tid; i < V; i += SB) {
+    const float f = bf2f(lrow[i]);
+    x[i] = f;
+    if (f > mx) { mx = f; mi = i; }
+  }
+  if (temp <= 0.f) {  // greedy: first maximum of the raw logits
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ov = __shfl_xor(mx, o, 64);
+      const int oi = __shfl_xor(mi, o, 64);
+      if (ov > mx || (ov == mx && oi < mi)) { mx = ov; mi = oi; }
+    }
+    __shared__ float bv[SB / 64];
+    __shared__ int bi[SB / 64];
+    if ((tid & 63) == 0) { bv[tid >> 6] = mx; bi[tid >> 6] = mi; }
+    __syncthreads();
+    if (tid == 0) {
+      float b = bv[0];
+      int ix = bi[0];
+      for (int k = 1; k < SB / 64; ++k)
+        if (bv[k] > b || (bv[k] == b && bi[k] < ix)) { b = bv[k]; ix = bi[k]; }
+      out[row] = ix == 0x7fffffff ? 0 : ix;
+    }
+    return;
+  }
+  __syncthreads();
+
+  // ---- repetition penalty (reference src/rpc_handler.py:345-374) ----
+  const float rp = rep_pens[row];
+  const int nrec = recent_len[row];
+  const int32_t* rec = recent + (int64_t)row * recent_stride;
+  if (rp != 1.f && nrec > 0) {
+    if (tid < nrec) {
+      const int tok = rec[tid];
+      bool first = true;
+      int count = 0;
+      for (int j = 0; j < nrec; ++j) {
+        if (rec[j] == tok) {
+          ++count;
+          if (j < tid) first = false;
+        }
+      }
+      if (first && tok >= 0 && tok < V) {
+        const float pen = powf(rp, (float)count);
+        const float v = x[tok];
+        x[tok] = v > 0.f ? v / pen : v * pen;
+      }
+    }
+    __syncthreads();
+    if (tid == 0 && nrec >= 3) {
+      const int a = rec[nrec - 1];
+      if (rec[nrec - 2] == a && rec[nrec - 3] == a && a >= 0 && a < V) {
+        const float pen = rp * rp * rp;
+        const float v = x[a];
+        x[a] = v > 0.f ? v / pen : v * pen;
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---- softmax(x / T) ----
+  const float inv_t = 1.f / fmaxf(temp, 1e-5f);
+  float lm = -INFINITY;
+  for (int i = tid; i < V; i += SB) lm = fmaxf(lm, x[i]);
+  const float m = block_max(lm, red);
+  float ls = 0.f;
+  for (int i = tid; i < V; i += SB) {
+    const float e = __expf((x[i] - m) * inv_t);
+    x[i] = e;
+    ls += e;
+  }
+  const float s = block_sum(ls, red);
+  const float inv_s = 1.f / s;
+  unsigned maxbits = 0;
+  for (int i = tid; i < V; i += SB) {
+    const float pv = x[i] * inv_s;
+    x[i] = pv;
+    maxbits = max(maxbits, __float_as_uint(pv));
+  }
+  // block max of bits
+  {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) maxbits = max(maxbits, (unsigned)__shfl_xor((int)maxbits, o, 64));
+    __syncthreads();
+    if ((tid & 63) == 0) red[tid >> 6] = __uint_as_float(maxbits);
+    __syncthreads();
+    unsigned mb = 0;
+    for (int k = 0; k < SB / 64; ++k) mb = max(mb, __float_as_uint(red[k]));
+    maxbits = mb;
+  }
+
+  // ---- top-k: radix-select the k-th largest probability (bits are order-preserving, p >= 0) ----
+  const int k = top_ks[row];
+  if (k > 0 && k < V) {
+    unsigned prefix = 0, msk = 0;
+    int kk = k;
+    for (int shift = 24; shift >= 0; shift -= 8) {
+      for (int i = tid; i < 256; i += SB) hist[i] = 0;
+      __syncthreads();
+      for (int i = tid; i < V; i += SB) {
+        const unsigned b = __float_as_uint(x[i]);
+        if ((b & msk) == prefix) atomicAdd(&hist[(b >> shift) & 255u], 1u);
+      }
+      __syncthreads();
+      if (tid == 0) {
+        int cum = 0, sel = 0;
+        for (int d = 255; d >= 0; --d) {
+          if (cum + (int)hist[d] >= kk) { sel = d; break; }
+          cum += hist[d];
+        }
+        s_u[0] = (unsigned)sel;
+        s_i[0] = kk - cum;
+      }
+      __syncthreads();
+      prefix |= s_u[0] << shift;
+      msk |= 255u << shift;
+      kk = s_i[0];
+      __syncthreads();
+    }
+    for (int i = tid; i < V; i += SB)
+      if (__float_as_uint(x[i]) < prefix) x[i] = 0.f;
+    __syncthreads();
+  }
+
+  // ---- top-p: smallest kept value = first value whose cumulative (descending) mass > p ----
+  const float tp = top_ps[row];
+  if (tp > 0.f && tp < 1.f) {
+    unsigned prefix = 0, msk = 0;
+    float above = 0.f;
+    unsigned crit = 0;      // keep iff bits > crit
+    bool crossed = false;
+    for (int shift = 24; shift >= 0; shift -= 8) {
+      for (int i = tid; i < 256; i += SB) mass[i] = 0.f;
+      __syncthreads();
+      for (int i = tid; i < V; i += SB) {
+        const float pv = x[i];
+        const unsigned b = __float_as_uint(pv);
+        if (pv > 0.f && (b & msk) == prefix) atomicAdd(&mass[(b >> shift) & 255u], pv);
+      }
+      __syncthreads();
+      if (tid == 0) {
+        int sel = -1;
+        float a = above;
+        for (int d = 255; d >= 0; --d) {
+          if (mass[d] == 0.f) continue;
+          if (a + mass[d] <= tp) { a += mass[d]; continue; }
+          sel = d;
+          break;
+        }
+        s_u[0] = (unsigned)(sel < 0 ? 0 : sel);
+        s_i[0] = sel;
+        red[0] = a;
+      }
+      __syncthreads();
+      const int sel = s_i[0];
+      above = red[0];
+      __syncthreads();
+      if (sel < 0) {  // every candidate under this prefix is kept
+        crit = prefix > 0 ? prefix - 1 : 0;
+        crossed = true;
+        break;
+      }
+      prefix |= (unsigned)sel << shift;
+      msk |= 255u << shift;
+    }
+    if (!crossed) crit = prefix;  // the crossing value itself is dropped
+    if (crit >= maxbits) crit = maxbits - 1;  // always keep the most likely id
+    for (int i = tid; i < V; i += SB)
+      if (__float_as_uint(x[i]) <= crit) x[i] = 0.f;
+    __syncthreads();
+  }
+
+  // ---- one inverse-CDF draw over contiguous per-thread chunks ----
+  const int C = (V + SB - 1) / SB;
+  const int lo = tid * C, hi = min(lo + C, V);
+  float loc = 0.f;
+  for (int i = lo; i < hi; ++i) loc += x[i];
+  float total;
+  const float excl = block_excl_scan(loc, red, &total);
+  const uint64_t r = splitmix64((uint64_t)seeds[row] * 0x9E3779B97F4A7C15ull + (uint64_t)row);
+  const float u = (float)((double)(r >> 11) * (1.0 / 9007199254740992.0)) * total;
+  if (tid == 0) s_i[1] = -1;
+  __syncthreads();
+  if (loc > 0.f && u >= excl && u < excl + loc) {
+    float c = excl;
+    int pick = -1;
+    for (int i = lo; i < hi; ++i) {
+      const float pv = x[i];
+      if (pv > 0.f) {
+        pick = i;
+        c += pv;
+        if (u < c) break;
+      }
+    }
+    s_i[1] = pick;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int pick = s_i[1];
+    if (pick < 0) {  // rounding pushed u past the last interval: take the most likely id
+      for (int i = 0; i < V; ++i)
+        if (__float_as_uint(x[i]) == maxbits) { pick = i; break; }
+    }
+    out[row] = pick < 0 ? 0 : pick;
+  }
+}
+
+}  // namespace mp
+
+extern "C" int mp_sample(const void* logits, int64_t stride, int R, int V, const float* temps, const float* top_ps,
+                         const int32_t* top_ks, const float* rep_pens, const int32_t* recent, int recent_stride,
+                         const int32_t* recent_len, const int64_t* seeds, float* ws, int64_t* out,
+                         hipStream_t stream) {
+  using namespace mp;
+  if (R == 0) return 0;
+  if (recent_stride > SB) return -1;
+  hipLaunchKernelGGL(sample_kernel, dim3(R), dim3(SB), 0, stream, (const bf16_t*)logits, stride, V, temps, top_ps,
+                     top_ks, rep_pens, recent, recent_stride, recent_len, seeds, ws, out);
+  return (int)hipGetLastError();
+}

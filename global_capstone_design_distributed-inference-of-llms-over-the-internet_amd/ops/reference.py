@@ -1,0 +1,232 @@
+"""Plain-PyTorch reference implementations of every HIP op.
+
+Two uses:
+* the CPU data path (tests, the GPT-2 plumbing config, any host without a GPU);
+* numerics oracles for the GPU kernel tests (computed in fp32 from the same inputs).
+
+Rounding points mirror the kernels (and HF): values are rounded to the activation
+dtype where the HF LLaMA modules round them (reference petals/llama/block.py).
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+
+GU_BLOCK = 16  # gate/up weights are interleaved in blocks of 16 rows: [g16 u16 g16 u16 ...]
+
+
+def rmsnorm(x, w, eps, out=None, residual=None, mode=0, rows=None):
+    dt = x.dtype
+    if mode == 1:
+        residual.copy_((residual.float() + x.float()).to(dt))
+        src = residual
+    elif mode == 2:
+        residual.copy_(x)
+        src = x
+    else:
+        src = x
+    if rows is not None:
+        src = src.index_select(0, rows.long())
+    xf = src.float()
+    n = (xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps)).to(dt)
+    y = (n.float() * w.float()).to(dt)
+    if out is not None:
+        out[: y.shape[0]].copy_(y)
+        return out
+    return y
+
+
+def rope_cos_sin(head_dim: int, max_pos: int, theta: float, device=None, scaling: Optional[dict] = None):
+    """fp32 cos/sin tables [max_pos, head_dim/2] (HF LlamaRotaryEmbedding, incl. llama3 scaling)."""
+    inv = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.float64) / head_dim))
+    if scaling and scaling.get("rope_type", scaling.get("type")) == "llama3":
+        factor = scaling.get("factor", 8.0)
+        lo, hi = scaling.get("low_freq_factor", 1.0), scaling.get("high_freq_factor", 4.0)
+        old = scaling.get("original_max_position_embeddings", 8192)
+        lo_wl, hi_wl = old / lo, old / hi
+        wl = 2 * math.pi / inv
+        scaled = torch.where(wl > lo_wl, inv / factor, inv)
+        smooth = (old / wl - lo) / (hi - lo)
+        mid = (1 - smooth) * scaled / factor + smooth * scaled
+        is_mid = (wl <= lo_wl) & (wl >= hi_wl)
+        inv = torch.where(is_mid, mid, scaled)
+    t = torch.arange(max_pos, dtype=torch.float64)
+    f = torch.outer(t, inv)
+    return f.cos().float().to(device), f.sin().float().to(device)
+
+
+def _rotate(x, cos, sin):
+    half = x.shape[-1] // 2
+    x1, x2 = x[..., :half].float(), x[..., half:].float()
+    c, s = cos.unsqueeze(-2), sin.unsqueeze(-2)
+    return torch.cat([x1 * c - x2 * s, x2 * c + x1 * s], -1)
+
+
+def _scatter_cache(cache, slots, rows):
+    """rows [T, nkv, D] -> cache[page, :, off, :] for slots >= 0."""
+    P, nkv, ps, D = cache.shape
+    valid = slots >= 0
+    if not bool(valid.any()):
+        return
+    s = slots[valid]
+    page, off = s // ps, s % ps
+    cache[page, :, off, :] = rows[valid].to(cache.dtype)
+
+
+def rope_kv_write(qkv, positions, cos, sin, k_cache, v_cache, slots, nh, nkv):
+    T = qkv.shape[0]
+    D = k_cache.shape[-1]
+    view = qkv[:, : (nh + 2 * nkv) * D].view(T, nh + 2 * nkv, D)
+    c, s = cos[positions.long()], sin[positions.long()]
+    q = _rotate(view[:, :nh], c, s).to(qkv.dtype)
+    k = _rotate(view[:, nh : nh + nkv], c, s).to(qkv.dtype)
+    v = view[:, nh + nkv :]
+    view[:, :nh] = q
+    _scatter_cache(k_cache, slots, k)
+    _scatter_cache(v_cache, slots, v)
+
+
+def kv_write(k, v, k_cache, v_cache, slots):
+    nkv, D = k_cache.shape[1], k_cache.shape[3]
+    _scatter_cache(k_cache, slots, k.reshape(k.shape[0], nkv, D))
+    _scatter_cache(v_cache, slots, v.reshape(v.shape[0], nkv, D))
+
+
+def paged_attention(q, k_cache, v_cache, block_tables, q_seq, q_ctx, nh, nkv, scale, out=None):
+    """softmax(q k^T * scale) v over the first q_ctx[t] cached tokens of sequence q_seq[t]."""
+    T = q.shape[0]
+    D = k_cache.shape[-1]
+    ps = k_cache.shape[2]
+    rep = nh // nkv
+    res = torch.zeros(T, nh, D, dtype=torch.float32, device=q.device)
+    qv = q[:, : nh * D].reshape(T, nh, D).float()
+    for t in range(T):
+        n = int(q_ctx[t])
+        if n <= 0:
+            continue
+        pages = block_tables[int(q_seq[t])][: (n + ps - 1) // ps].long()
+        k = k_cache[pages].permute(1, 0, 2, 3).reshape(nkv, -1, D)[:, :n].float()
+        v = v_cache[pages].permute(1, 0, 2, 3).reshape(nkv, -1, D)[:, :n].float()
+        k = k.repeat_interleave(rep, 0)
+        v = v.repeat_interleave(rep, 0)
+        s = torch.einsum("hd,hnd->hn", qv[t], k) * scale
+        p = torch.softmax(s, -1)
+        res[t] = torch.einsum("hn,hnd->hd", p, v)
+    y = res.reshape(T, nh * D).to(q.dtype)
+    if out is not None:
+        out.view(T, nh * D).copy_(y)
+        return out
+    return y
+
+
+def embedding(ids, table, out=None):
+    y = table[ids.long()]
+    if out is not None:
+        out.copy_(y.view_as(out))
+        return out
+    return y
+
+
+def swiglu(gu, out=None):
+    """gu [T, 2F] with 16-row interleaved gate/up blocks -> silu(g) * u, HF rounding."""
+    T, F2 = gu.shape
+    F = F2 // 2
+    v = gu.view(T, F // GU_BLOCK, 2, GU_BLOCK)
+    g, u = v[:, :, 0].reshape(T, F), v[:, :, 1].reshape(T, F)
+    a = torch.nn.functional.silu(g.float()).to(gu.dtype)
+    y = (a.float() * u.float()).to(gu.dtype)
+    if out is not None:
+        out.copy_(y)
+        return out
+    return y
+
+
+def add(a, b, out=None):
+    y = (a.float() + b.float()).to(a.dtype)
+    if out is not None:
+        out.copy_(y)
+        return out
+    return y
+
+
+def argmax(logits, out=None):
+    y = torch.argmax(logits.float(), dim=-1)
+    if out is not None:
+        out.copy_(y)
+        return out
+    return y
+
+
+def linear(x, w, out=None, epilogue=0, residual=None):
+    y = torch.nn.functional.linear(x, w) if x.dtype == w.dtype else torch.nn.functional.linear(x.to(w.dtype), w)
+    y = y.to(x.dtype)
+    if epilogue == 1:
+        y = swiglu(y)
+    elif epilogue == 2:
+        y = add(y, residual)
+    if out is not None:
+        out.copy_(y)
+        return out
+    return y
+
+
+def sample_row(logits_row: torch.Tensor, temperature: float, top_p: float, top_k: int,
+               repetition_penalty: float = 1.5, generated_tokens=None, generator=None) -> int:
+    """One-row sampler with the reference semantics (reference src/rpc_handler.py:327-403)."""
+    logits = logits_row.detach().float().clone().view(1, -1)
+    if temperature <= 0.0:
+        return int(torch.argmax(logits, dim=-1).item())
+    temp = max(temperature, 1e-5)
+    V = logits.shape[-1]
+    if repetition_penalty != 1.0 and generated_tokens:
+        recent = list(generated_tokens[-50:])
+        counts = {}
+        for tok in recent:
+            counts[tok] = counts.get(tok, 0) + 1
+        for tok, cnt in counts.items():
+            if 0 <= tok < V:
+                pen = repetition_penalty ** cnt
+                if logits[0, tok] > 0:
+                    logits[0, tok] /= pen
+                else:
+                    logits[0, tok] *= pen
+        if len(generated_tokens) >= 3:
+            last3 = list(generated_tokens[-3:])
+            if len(set(last3)) == 1 and 0 <= last3[0] < V:
+                pen = repetition_penalty ** 3
+                if logits[0, last3[0]] > 0:
+                    logits[0, last3[0]] /= pen
+                else:
+                    logits[0, last3[0]] *= pen
+    probs = torch.softmax(logits / temp, dim=-1)
+    if 0 < top_k < V:
+        tv, ti = torch.topk(probs, top_k, dim=-1)
+        probs = torch.zeros_like(probs).scatter(-1, ti, tv)
+    if 0.0 < top_p < 1.0:
+        sp, si = torch.sort(probs, descending=True, dim=-1)
+        cum = torch.cumsum(sp, dim=-1)
+        keep = cum <= top_p
+        keep[..., 0] = True
+        filt = sp * keep
+        filt = filt / filt.sum(dim=-1, keepdim=True)
+        probs = torch.zeros_like(probs).scatter(-1, si, filt)
+    probs = probs / probs.sum(dim=-1, keepdim=True)
+    return int(torch.multinomial(probs, 1, generator=generator).item())
+
+
+def sample(logits, temps, top_ps, top_ks, rep_pens, recent, recent_len, seeds, workspace=None, out=None):
+    R = logits.shape[0]
+    res = torch.empty(R, dtype=torch.long, device=logits.device)
+    for r in range(R):
+        n = int(recent_len[r])
+        hist = [int(t) for t in recent[r, :n].tolist()]
+        g = torch.Generator(device="cpu")
+        g.manual_seed(int(seeds[r]) & 0x7FFFFFFFFFFFFFFF)
+        res[r] = sample_row(logits[r].cpu(), float(temps[r]), float(top_ps[r]), int(top_ks[r]),
+                            float(rep_pens[r]), hist, generator=g)
+    if out is not None:
+        out.copy_(res)
+        return out
+    return res

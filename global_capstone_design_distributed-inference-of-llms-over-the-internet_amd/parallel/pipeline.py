@@ -1,0 +1,198 @@
+"""Single-node pipeline-parallel serving over RCCL point-to-point (xGMI).
+
+Reference: the Stage-0 client sends hidden states to each remote stage in turn over
+hivemind RPC in a star topology and gets a token back from the last stage
+(reference src/rpc_transport.py:738-766, :802-833; src/main.py:164-211), one session at a
+time.  On one MI355X node the same dataflow becomes a chain of RCCL send/recv over the
+direct xGMI link between neighbouring GPUs:
+
+    rank 0 (embed + blocks [0,s0)) -> rank 1 -> ... -> rank N-1 (blocks + norm + lm_head + sampler)
+         ^                                                                       |
+         +----------------------- token ids int64[B] ----------------------------+
+
+* M micro-batches of B sessions are in flight (M >= N keeps every stage busy); every
+  "step" advances all M*B sessions by one token.
+* Receives are pre-posted one micro-batch ahead so the hop overlaps compute; outputs are
+  copied into a ring of send buffers so a pending send never aliases the hipGraph output.
+* Sampling happens on the last stage (reference semantics) with the repetition-penalty
+  history kept ON DEVICE (no host round trip per token).
+* gloo carries the identical protocol on CPU (tests).
+"""
+from __future__ import annotations
+
+import dataclasses
+import time
+from typing import List, Optional, Sequence
+
+import torch
+import torch.distributed as dist
+
+from .. import ops
+from ..runtime.executor import StageExecutor
+from ..runtime.sampler import RECENT, SamplingParams
+
+
+@dataclasses.dataclass
+class MicroBatch:
+    sids: List[str]
+    tokens: Optional[torch.Tensor] = None      # stage 0: next input ids [B] (device)
+    recent: Optional[torch.Tensor] = None      # last stage: [B, RECENT] int32
+    recent_len: Optional[torch.Tensor] = None  # last stage: [B] int32
+    step: int = 0
+    index: int = 0
+
+
+class PipelineEngine:
+    def __init__(self, executor: StageExecutor, rank: int, world: int, sampling: SamplingParams,
+                 n_micro: int, batch: int, seed: int = 0, send_ring: int = 4, timing: bool = False):
+        self.ex = executor
+        self.rank, self.world = rank, world
+        self.dev = executor.device
+        self.sp = sampling
+        self.B, self.M = batch, n_micro
+        self.seed = seed
+        self.first = rank == 0
+        self.last = rank == world - 1
+        H = executor.cfg.hidden_size
+        self.H = H
+        self.mbs = [MicroBatch([f"s{m}_{b}" for b in range(batch)], index=m) for m in range(n_micro)]
+        # send ring (hidden for mid stages, tokens for the last stage)
+        self._ring = [None] * send_ring
+        self._ring_work = [None] * send_ring
+        self._ring_k = 0
+        self._pending_recv = None  # (tag, work, buffer)
+        self.timing = timing
+        self._events: List = []
+        self.tokens_out: List[List[torch.Tensor]] = [[] for _ in range(n_micro)]  # last stage (world==1) history
+        if self.last:
+            dev = self.dev
+            B = batch
+            self._temps = torch.full((B,), sampling.temperature, dtype=torch.float32, device=dev)
+            self._topp = torch.full((B,), sampling.top_p, dtype=torch.float32, device=dev)
+            self._topk = torch.full((B,), sampling.top_k, dtype=torch.int32, device=dev)
+            self._rp = torch.full((B,), sampling.repetition_penalty, dtype=torch.float32, device=dev)
+            self._arange = torch.arange(B, dtype=torch.int64, device=dev)
+            for mb in self.mbs:
+                mb.recent = torch.zeros(B, RECENT, dtype=torch.int32, device=dev)
+                mb.recent_len = torch.zeros(B, dtype=torch.int32, device=dev)
+
+    # ------------------------------------------------------------------ comm helpers
+    def _send(self, t: torch.Tensor, dst: int):
+        k = self._ring_k
+        self._ring_k = (k + 1) % len(self._ring)
+        w = self._ring_work[k]
+        if w is not None:
+            w.wait()
+        buf = self._ring[k]
+        if buf is None or buf.shape != t.shape or buf.dtype != t.dtype:
+            buf = torch.empty_like(t)
+            self._ring[k] = buf
+        buf.copy_(t)
+        self._ring_work[k] = dist.isend(buf, dst)
+
+    def _post_recv(self, shape, dtype, src):
+        buf = torch.empty(shape, dtype=dtype, device=self.dev)
+        return dist.irecv(buf, src), buf
+
+    def _flush_sends(self):
+        for i, w in enumerate(self._ring_work):
+            if w is not None:
+                w.wait()
+                self._ring_work[i] = None
+
+    # ------------------------------------------------------------------ sampling on the last stage
+    def _sample(self, mb: MicroBatch, logits: torch.Tensor) -> torch.Tensor:
+        B = logits.shape[0]
+        if self.sp.temperature <= 0:
+            tok = ops.argmax(logits)
+        else:
+            seeds = (self._arange[:B] + (self.seed * 1000003 + mb.step * 7919 + mb.index * 104729) * 4096)
+            tok = ops.sample(logits, self._temps[:B], self._topp[:B], self._topk[:B], self._rp[:B], mb.recent,
+                             mb.recent_len, seeds)
+        # device-side rolling history (left-aligned, newest at recent_len-1)
+        full = (mb.recent_len >= RECENT).unsqueeze(1)
+        mb.recent.copy_(torch.where(full, torch.roll(mb.recent, -1, 1), mb.recent))
+        pos = torch.clamp(mb.recent_len, max=RECENT - 1).long().unsqueeze(1)
+        mb.recent.scatter_(1, pos, tok.to(torch.int32).unsqueeze(1))
+        mb.recent_len.copy_(torch.clamp(mb.recent_len + 1, max=RECENT))
+        mb.step += 1
+        return tok
+
+    # ------------------------------------------------------------------ one micro-batch on this stage
+    def _compute(self, mb: MicroBatch, x: torch.Tensor, n_tokens: int, reset: bool):
+        seqs = [(sid, n_tokens) for sid in mb.sids]
+        if self.timing and self.dev.type == "cuda":
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        out = self.ex.forward(seqs, x, reset=[reset] * len(seqs))
+        if self.timing and self.dev.type == "cuda":
+            e1.record()
+            self._events.append((e0, e1))
+        return out
+
+    def _input_shape(self, n_tokens):
+        return (self.B * n_tokens, self.H)
+
+    def run_round(self, n_tokens: int, prompts: Optional[Sequence[torch.Tensor]] = None, reset: bool = False):
+        """Advance every micro-batch by one step (``n_tokens`` per session; prompts for prefill)."""
+        M = self.M
+        dt = self.ex.dtype
+        for m, mb in enumerate(self.mbs):
+            # ---------------- input
+            if self.first:
+                if prompts is not None:
+                    x = prompts[m].to(self.dev).view(-1)
+                elif self.world == 1:
+                    x = mb.tokens
+                else:
+                    w, buf = self._tok_recv[m]
+                    w.wait()
+                    x = buf
+            else:
+                if self._pending_recv is None:
+                    self._pending_recv = self._post_recv(self._input_shape(n_tokens), dt, self.rank - 1)
+                w, x = self._pending_recv
+                w.wait()
+                self._pending_recv = None
+                if m + 1 < M:  # pre-post the next micro-batch's receive (overlaps this compute)
+                    self._pending_recv = self._post_recv(self._input_shape(n_tokens), dt, self.rank - 1)
+            # ---------------- compute
+            out = self._compute(mb, x, n_tokens, reset)
+            # ---------------- output
+            if self.last:
+                tok = self._sample(mb, out)
+                if self.world == 1:
+                    mb.tokens = tok
+                else:
+                    self._send(tok, 0)
+            else:
+                self._send(out, self.rank + 1)
+        if self.first and self.world > 1:
+            # receive this round's tokens (posted after all sends of the round, in micro-batch order)
+            self._tok_recv = [self._post_recv((self.B,), torch.long, self.world - 1) for _ in range(M)]
+
+    def prefill(self, prompts: Sequence[torch.Tensor]):
+        """prompts[m]: int64 [B, L] token ids for micro-batch m (stage 0 only reads them)."""
+        L = int(prompts[0].shape[1]) if prompts is not None else 0
+        self.run_round(L, prompts=prompts if self.first else None, reset=True)
+
+    def decode(self, n_steps: int):
+        for _ in range(n_steps):
+            self.run_round(1)
+
+    def finish(self):
+        self._flush_sends()
+        if self.first and self.world > 1:
+            # tokens of the final round are still in flight; consume them
+            for w, buf in getattr(self, "_tok_recv", []):
+                w.wait()
+            self._tok_recv = []
+            self._tok_recv_consumed = True
+
+    def stage_ms(self) -> Optional[float]:
+        if not self._events:
+            return None
+        torch.cuda.synchronize()
+        ms = [a.elapsed_time(b) for a, b in self._events]
+        self._events.clear()
+        return sum(ms) / len(ms)

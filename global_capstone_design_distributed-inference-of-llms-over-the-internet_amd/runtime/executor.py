@@ -1,0 +1,369 @@
+"""StageExecutor: one pipeline stage (a contiguous block range) on one device.
+
+Replaces the reference's Stage0 / StageSegment / StageLast modules
+(reference src/llama_partition.py:76-474) and the optimized HF layer they wrap
+(petals/llama/block.py:39-248) with an MI355X-first step function:
+
+* weights resident in HBM (no per-forward CPU<->GPU layer streaming),
+* a paged KV cache written in place by the fused RoPE kernel,
+* ragged batches: any mix of sessions, each contributing ``n_tokens`` (prefill chunks,
+  decode steps, replays) executed as ONE forward over the concatenated tokens,
+* per layer 7 launches on the decode path: add+RMSNorm, QKV GEMM, RoPE+KV write,
+  paged attention, O GEMM, add+RMSNorm, gate/up GEMM with fused SwiGLU, down GEMM,
+* decode steps replayed from hipGraphs captured per (batch bucket, context bucket);
+* the last stage applies the final norm and ``lm_head`` to the LAST token of each
+  sequence only (the reference projects every prefill position, src/llama_partition.py:470).
+
+Attention is causal for prefill (the reference's optimized layer gets no mask and is
+NOT causal: src/llama_partition.py:118 -> petals/llama/block.py:136-137).
+"""
+from __future__ import annotations
+
+import dataclasses
+import logging
+import math
+import os
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from .. import native, ops
+from ..models.config import ModelConfig
+from ..models.weights import StageWeights
+from .kv_cache import PagedKVCache
+from .session import SessionManager, SessionState
+
+logger = logging.getLogger(__name__)
+
+
+@dataclasses.dataclass
+class Plan:
+    """Host-side description of one ragged step."""
+    sessions: List[SessionState]
+    ntoks: np.ndarray
+    starts: np.ndarray
+    T: int
+    max_ctx: int
+    is_decode: bool
+    meta_i64: torch.Tensor  # [2, T] positions, slots (device)
+    meta_i32: torch.Tensor  # [2*T + S] q_seq, q_ctx, last_rows (device)
+
+    @property
+    def positions(self):
+        return self.meta_i64[0]
+
+    @property
+    def slots(self):
+        return self.meta_i64[1]
+
+    @property
+    def q_seq(self):
+        return self.meta_i32[: self.T]
+
+    @property
+    def q_ctx(self):
+        return self.meta_i32[self.T: 2 * self.T]
+
+    @property
+    def last_rows(self):
+        return self.meta_i32[2 * self.T:]
+
+
+class _Pinned:
+    """Double-buffered pinned host staging for per-step metadata (async H2D without races)."""
+
+    def __init__(self, n_i64: int, n_i32: int, device):
+        self.device = torch.device(device)
+        pin = self.device.type == "cuda"
+        self.i64 = [torch.empty(n_i64, dtype=torch.int64, pin_memory=pin) for _ in range(2)]
+        self.i32 = [torch.empty(n_i32, dtype=torch.int32, pin_memory=pin) for _ in range(2)]
+        self.events = [None, None]
+        self.k = 0
+
+    def next(self):
+        self.k ^= 1
+        ev = self.events[self.k]
+        if ev is not None:
+            ev.synchronize()
+        return self.i64[self.k], self.i32[self.k]
+
+    def mark(self):
+        if self.device.type == "cuda":
+            ev = torch.cuda.Event()
+            ev.record()
+            self.events[self.k] = ev
+
+
+class StageExecutor:
+    def __init__(self, cfg: ModelConfig, weights: StageWeights, device, *, dtype=torch.bfloat16,
+                 page_size: int = 64, max_sessions: int = 256, max_seq_len: Optional[int] = None,
+                 kv_cache_bytes: Optional[int] = None, kv_fraction: float = 0.9, use_graphs: Optional[bool] = None,
+                 graph_max_batch: int = 256, max_tokens_per_step: int = 8192):
+        cfg.validate()
+        self.cfg = cfg
+        self.w = weights
+        self.device = torch.device(device)
+        self.dtype = dtype
+        self.n_layers = len(weights.layers)
+        self.start, self.end = weights.start, weights.end
+        self.is_first = weights.has_embed
+        self.is_last = weights.has_head
+        self.nh, self.nkv, self.D = cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim
+        self.scale = 1.0 / math.sqrt(self.D)
+        self.max_seq_len = int(max_seq_len or cfg.max_position_embeddings)
+        self.max_tokens = max_tokens_per_step
+        if cfg.model_type != "gpt2":
+            self.cos, self.sin = ops.rope_cos_sin(self.D, self.max_seq_len, cfg.rope_theta, self.device,
+                                                  cfg.rope_scaling)
+        if kv_cache_bytes is None:
+            kv_cache_bytes = PagedKVCache.auto_budget_bytes(self.device, fraction=kv_fraction)
+        num_pages = PagedKVCache.pages_for_bytes(kv_cache_bytes, self.n_layers, self.nkv, self.D, page_size)
+        max_useful = max_sessions * math.ceil(self.max_seq_len / page_size)
+        num_pages = max(1, min(num_pages, max_useful))
+        self.cache = PagedKVCache(self.n_layers, num_pages, self.nkv, self.D, page_size, dtype, self.device)
+        self.sessions = SessionManager(self.cache, max_sessions, self.max_seq_len)
+        self.use_graphs = (self.device.type == "cuda") if use_graphs is None else bool(use_graphs)
+        self.use_graphs = self.use_graphs and self.device.type == "cuda" and cfg.model_type != "gpt2" and \
+            os.environ.get("MPAMD_GRAPHS", "1") != "0"
+        self.graph_max_batch = graph_max_batch
+        self._graphs: Dict[Tuple[int, int, int], "_DecodeGraph"] = {}
+        self._graph_pool = None
+        self._pinned = _Pinned(2 * max_tokens_per_step, 2 * max_tokens_per_step + max_sessions, self.device)
+        self.last_step_ms: Optional[float] = None
+        self.timing = False
+        if self.device.type == "cuda":
+            ops.require_native()
+        logger.info(f"StageExecutor blocks [{self.start},{self.end}) embed={self.is_first} head={self.is_last} "
+                    f"kv_pages={num_pages} x {page_size} tokens ({self.cache.nbytes / 2**30:.2f} GiB) "
+                    f"graphs={self.use_graphs}")
+
+    # ================================================================== planning
+    def plan(self, seqs: Sequence[Tuple[str, int]], *, reset: Sequence[bool] = (), max_length: Optional[int] = None,
+             starts: Optional[Sequence[int]] = None) -> Plan:
+        """Open/extend sessions and build device metadata for a ragged step.
+
+        ``seqs``: (session_id, n_tokens) pairs.  ``reset[i]`` clears the session first
+        (prefill / replay).  ``starts[i]`` (optional) rewinds a session to that position
+        (Petals' ``start_from_position``).
+        """
+        S = len(seqs)
+        sess: List[SessionState] = []
+        ntoks = np.empty(S, dtype=np.int32)
+        st = np.empty(S, dtype=np.int32)
+        for i, (sid, n) in enumerate(seqs):
+            s = self.sessions.open(sid, max_length)
+            if reset and reset[i]:
+                self.sessions.reset(sid)
+            if starts is not None and starts[i] is not None and starts[i] < s.length:
+                s.length = int(starts[i])
+            self.sessions.reserve(s, s.length + int(n))
+            sess.append(s)
+            ntoks[i] = n
+            st[i] = s.length
+        T = int(ntoks.sum())
+        if T > self.max_tokens:
+            raise ValueError(f"step has {T} tokens > max_tokens_per_step {self.max_tokens}")
+        rows = np.fromiter((s.row for s in sess), dtype=np.int32, count=S)
+        h64, h32 = self._pinned.next()
+        n64 = h64[: 2 * T].numpy().reshape(2, T) if T else np.empty((2, 0), np.int64)
+        n32 = h32[: 2 * T + S].numpy()
+        native.build_meta(rows, st, ntoks, self.sessions.table, self.cache.page_size, n64[0], n64[1], n32[:T],
+                          n32[T:2 * T], n32[2 * T:])
+        table = self.sessions.sync_table()
+        del table
+        if self.device.type == "cuda":
+            meta64 = h64[: 2 * T].view(2, T).to(self.device, non_blocking=True)
+            meta32 = h32[: 2 * T + S].to(self.device, non_blocking=True)
+        else:
+            meta64 = h64[: 2 * T].view(2, T).clone()
+            meta32 = h32[: 2 * T + S].clone()
+        self._pinned.mark()
+        max_ctx = int((st + ntoks).max()) if S else 0
+        return Plan(sess, ntoks, st, T, max_ctx, bool(S and (ntoks == 1).all()), meta64, meta32)
+
+    def commit(self, plan: Plan) -> None:
+        for s, n in zip(plan.sessions, plan.ntoks):
+            s.length += int(n)
+            s.step += 1
+
+    # ================================================================== execution
+    def forward(self, seqs: Sequence[Tuple[str, int]], x: torch.Tensor, **plan_kw) -> torch.Tensor:
+        """One ragged step.  ``x``: token ids [T] (first stage) or hidden [T, H].
+
+        Returns hidden [T, H] (non-last stage) or last-token logits [S, V] (last stage).
+        """
+        plan = self.plan(seqs, **plan_kw)
+        out = self.run(plan, x)
+        self.commit(plan)
+        return out
+
+    def run(self, plan: Plan, x: torch.Tensor) -> torch.Tensor:
+        if plan.T == 0:
+            H = self.cfg.hidden_size
+            return torch.empty(0, self.cfg.vocab_size if self.is_last else H, dtype=self.dtype, device=self.device)
+        x = x.to(self.device)
+        if not self.is_first and x.dtype != self.dtype:
+            x = x.to(self.dtype)
+        ev = None
+        if self.timing and self.device.type == "cuda":
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
+        if self.use_graphs and plan.is_decode and plan.T <= self.graph_max_batch:
+            out = self._run_graph(plan, x)
+        elif self.cfg.model_type == "gpt2":
+            out = self._forward_gpt2(plan, x)
+        else:
+            out = self._forward_llama(x, plan.positions, plan.slots, plan.q_seq, plan.q_ctx, plan.last_rows,
+                                      plan.T, plan.max_ctx, None)
+        if ev is not None:
+            ev[1].record()
+            ev[1].synchronize()
+            self.last_step_ms = ev[0].elapsed_time(ev[1])
+        return out
+
+    # ------------------------------------------------------------------ llama
+    def _forward_llama(self, x, positions, slots, q_seq, q_ctx, last_rows, T, max_ctx, attn_part,
+                       bufs: Optional[dict] = None):
+        cfg, w = self.cfg, self.w
+        H, eps = cfg.hidden_size, cfg.rms_norm_eps
+        dev, dt = self.device, self.dtype
+        table = self.sessions.table_dev
+        if bufs is None:
+            bufs = {}
+        e = lambda name, shape, dtype=dt: bufs.get(name) if name in bufs else torch.empty(shape, dtype=dtype, device=dev)  # noqa: E731
+        if self.is_first:
+            h = ops.embedding(x, w.embed, out=e("h", (T, H)))
+        else:
+            h = x
+        if attn_part is None:
+            attn_part = ops.attention_partition(T, self.nkv, max_ctx)
+        ps, np_ = attn_part
+        ws = e("attn_ws", (max(1, T * self.nh * np_ * (self.D + 2)),), torch.float32)
+        res = e("res", (T, H))
+        xn = e("xn", (T, H))
+        qkv = e("qkv", (T, cfg.q_dim + 2 * cfg.kv_dim))
+        attn = e("attn", (T, cfg.q_dim))
+        o = e("o", (T, H))
+        act = e("act", (T, cfg.intermediate_size))
+        mlp = e("mlp", (T, H))
+        for li, L in enumerate(w.layers):
+            if li == 0:
+                ops.rmsnorm(h, L.input_norm, eps, out=xn, residual=res, mode=2)
+            else:
+                ops.rmsnorm(mlp, L.input_norm, eps, out=xn, residual=res, mode=1)
+            ops.linear(xn, L.qkv, out=qkv)
+            kc, vc = self.cache.layer(li)
+            ops.rope_kv_write(qkv, positions, self.cos, self.sin, kc, vc, slots, self.nh, self.nkv)
+            ops.paged_attention(qkv, kc, vc, table, q_seq, q_ctx, self.nh, self.nkv, self.scale, out=attn,
+                                workspace=ws, part_size=ps, num_parts=np_)
+            ops.linear(attn, L.o, out=o)
+            ops.rmsnorm(o, L.post_norm, eps, out=xn, residual=res, mode=1)
+            ops.linear(xn, L.gate_up, out=act, epilogue=1)
+            ops.linear(act, L.down, out=mlp)
+        hout = ops.add(res, mlp, out=e("hout", (T, H)))
+        if not self.is_last:
+            return hout
+        S = last_rows.numel()
+        fn = ops.rmsnorm(hout, w.final_norm, eps, out=e("fn", (S, H)), rows=last_rows)
+        return ops.linear(fn, w.lm_head, out=e("logits", (S, cfg.vocab_size)))
+
+    # ------------------------------------------------------------------ gpt2 (plumbing family)
+    def _forward_gpt2(self, plan: Plan, x):
+        cfg, w = self.cfg, self.w
+        F = torch.nn.functional
+        T, H = plan.T, cfg.hidden_size
+        table = self.sessions.table_dev
+        if self.is_first:
+            h = w.embed[x.long()] + w.pos_embed[plan.positions]
+        else:
+            h = x
+        for li, L in enumerate(w.layers):
+            a = F.layer_norm(h, (H,), L.ln1_w, L.ln1_b, cfg.layer_norm_eps)
+            qkv = F.linear(a, L.attn_w, L.attn_b)
+            q, k, v = qkv.split(H, dim=1)
+            kc, vc = self.cache.layer(li)
+            ops.kv_write(k.contiguous(), v.contiguous(), kc, vc, plan.slots)
+            att = ops.paged_attention(q.contiguous(), kc, vc, table, plan.q_seq, plan.q_ctx, self.nh, self.nkv,
+                                      self.scale, max_ctx=plan.max_ctx)
+            h = h + F.linear(att, L.proj_w, L.proj_b)
+            m = F.layer_norm(h, (H,), L.ln2_w, L.ln2_b, cfg.layer_norm_eps)
+            m = F.gelu(F.linear(m, L.fc_w, L.fc_b), approximate="tanh")
+            h = h + F.linear(m, L.fc2_w, L.fc2_b)
+        if not self.is_last:
+            return h
+        hl = h.index_select(0, plan.last_rows.long())
+        hl = F.layer_norm(hl, (H,), w.final_norm, w.final_norm_b, cfg.layer_norm_eps)
+        return F.linear(hl, w.lm_head)
+
+    # ------------------------------------------------------------------ hipGraph decode
+    def _bucket(self, b: int) -> int:
+        for cand in (1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 192, 256):
+            if b <= cand:
+                return min(cand, self.graph_max_batch)
+        return b
+
+    def _ctx_bucket(self, c: int) -> int:
+        c = max(c, 256)
+        return 1 << (c - 1).bit_length()
+
+    def _run_graph(self, plan: Plan, x: torch.Tensor) -> torch.Tensor:
+        B = self._bucket(plan.T)
+        ctxb = min(self._ctx_bucket(plan.max_ctx), self._ctx_bucket(self.max_seq_len))
+        part = ops.attention_partition(B, self.nkv, ctxb)
+        key = (B, part[0], part[1])
+        g = self._graphs.get(key)
+        if g is None:
+            if self._graph_pool is None:
+                self._graph_pool = torch.cuda.graph_pool_handle()
+            g = _DecodeGraph(self, B, part, self._graph_pool)
+            self._graphs[key] = g
+        return g.replay(plan, x)
+
+    def clear_graphs(self):
+        self._graphs.clear()
+
+
+class _DecodeGraph:
+    """A captured decode step for a fixed (batch bucket, attention partition)."""
+
+    def __init__(self, ex: StageExecutor, B: int, part: Tuple[int, int], pool):
+        self.ex, self.B, self.part = ex, B, part
+        dev, H, dt = ex.device, ex.cfg.hidden_size, ex.dtype
+        if ex.is_first:
+            self.x = torch.zeros(B, dtype=torch.long, device=dev)
+        else:
+            self.x = torch.zeros(B, H, dtype=dt, device=dev)
+        self.meta64 = torch.zeros(2, B, dtype=torch.int64, device=dev)
+        self.meta32 = torch.zeros(3 * B, dtype=torch.int32, device=dev)
+        self.meta64[1].fill_(-1)
+        self.meta32[B: 2 * B].fill_(0)
+        self.meta32[2 * B:] = torch.arange(B, dtype=torch.int32, device=dev)
+        self.bufs: dict = {}
+        args = (self.x, self.meta64[0], self.meta64[1], self.meta32[:B], self.meta32[B:2 * B], self.meta32[2 * B:], B,
+                0, part)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(2):  # warm up (allocator, hipBLASLt heuristics) outside capture
+                ex._forward_llama(*args)
+        torch.cuda.current_stream().wait_stream(s)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph, pool=pool):
+            self.out = ex._forward_llama(*args)
+
+    def replay(self, plan: Plan, x: torch.Tensor) -> torch.Tensor:
+        b, B = plan.T, self.B
+        if b < B:
+            self.meta64[1, b:].fill_(-1)
+            self.meta32[B + b: 2 * B].fill_(0)
+            self.meta32[b:B].fill_(0)
+        self.meta64[:, :b].copy_(plan.meta_i64)
+        self.meta32[:b].copy_(plan.q_seq)
+        self.meta32[B: B + b].copy_(plan.q_ctx)
+        if self.ex.is_first:
+            self.x[:b].copy_(x.view(-1))
+        else:
+            self.x[:b].copy_(x)
+        self.graph.replay()
+        return self.out[:b]

@@ -1,0 +1,129 @@
+"""Per-stage session table over the paged KV cache.
+
+Reference: the stage handler keeps ``self._kv_cache[session_id]`` forever
+(reference src/rpc_handler.py:70,266; "no eviction") and ignores
+``max_length``.  Here a session owns a row of a block table and a list of KV pages;
+``max_length`` is enforced, pages are returned on close, and idle sessions expire after
+a TTL (``evict_expired``) so a crashed client cannot leak HBM.
+"""
+from __future__ import annotations
+
+import dataclasses
+import threading
+import time
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+from .kv_cache import AllocationFailed, PagedKVCache, pages_needed
+
+
+@dataclasses.dataclass
+class SessionState:
+    sid: str
+    row: int
+    max_length: int
+    length: int = 0
+    pages: List[int] = dataclasses.field(default_factory=list)
+    created: float = dataclasses.field(default_factory=time.monotonic)
+    last_used: float = dataclasses.field(default_factory=time.monotonic)
+    generated: List[int] = dataclasses.field(default_factory=list)
+    step: int = 0
+
+
+class SessionManager:
+    def __init__(self, cache: PagedKVCache, max_sessions: int = 256, max_seq_len: int = 4096,
+                 ttl_seconds: float = 600.0):
+        self.cache = cache
+        self.page_size = cache.page_size
+        self.max_sessions = max_sessions
+        self.max_seq_len = max_seq_len
+        self.max_pages = pages_needed(max_seq_len, cache.page_size)
+        self.ttl = ttl_seconds
+        self.table = np.full((max_sessions, self.max_pages), -1, dtype=np.int32)
+        self.table_dev = torch.from_numpy(self.table.copy()).to(cache.device)
+        self._dirty = False
+        self._free_rows = list(range(max_sessions - 1, -1, -1))
+        self.sessions: Dict[str, SessionState] = {}
+        self.lock = threading.RLock()
+
+    # ------------------------------------------------------------------ lifecycle
+    def open(self, sid: str, max_length: Optional[int] = None) -> SessionState:
+        with self.lock:
+            if sid in self.sessions:
+                return self.sessions[sid]
+            if not self._free_rows:
+                self.evict_expired()
+            if not self._free_rows:
+                raise AllocationFailed(f"too many concurrent sessions (max {self.max_sessions})")
+            ml = min(int(max_length or self.max_seq_len), self.max_seq_len)
+            s = SessionState(sid=sid, row=self._free_rows.pop(), max_length=ml)
+            self.sessions[sid] = s
+            return s
+
+    def get(self, sid: str) -> Optional[SessionState]:
+        return self.sessions.get(sid)
+
+    def reset(self, sid: str) -> None:
+        """Drop the session's cached tokens (prefill / replay restart) but keep its row."""
+        with self.lock:
+            s = self.sessions.get(sid)
+            if s is None:
+                return
+            self.cache.allocator.free(s.pages)
+            s.pages = []
+            s.length = 0
+            s.generated = []
+            self.table[s.row, :] = -1
+            self._dirty = True
+
+    def close(self, sid: str) -> None:
+        with self.lock:
+            s = self.sessions.pop(sid, None)
+            if s is None:
+                return
+            self.cache.allocator.free(s.pages)
+            self.table[s.row, :] = -1
+            self._dirty = True
+            self._free_rows.append(s.row)
+
+    def evict_expired(self, now: Optional[float] = None) -> int:
+        now = time.monotonic() if now is None else now
+        with self.lock:
+            dead = [sid for sid, s in self.sessions.items() if now - s.last_used > self.ttl]
+            for sid in dead:
+                self.close(sid)
+            return len(dead)
+
+    # ------------------------------------------------------------------ pages
+    def reserve(self, s: SessionState, total_len: int) -> None:
+        """Make sure pages exist for positions [0, total_len)."""
+        if total_len > s.max_length:
+            raise ValueError(f"session {s.sid[:8]}: length {total_len} exceeds max_length {s.max_length}")
+        need = pages_needed(total_len, self.page_size) - len(s.pages)
+        if need > 0:
+            with self.lock:
+                try:
+                    new = self.cache.allocator.alloc(need)
+                except AllocationFailed:
+                    self.evict_expired()
+                    new = self.cache.allocator.alloc(need)
+                self.table[s.row, len(s.pages):len(s.pages) + need] = new
+                s.pages.extend(new)
+                self._dirty = True
+        s.last_used = time.monotonic()
+
+    def sync_table(self, stream=None) -> torch.Tensor:
+        if self._dirty:
+            with self.lock:
+                self.table_dev.copy_(torch.from_numpy(self.table), non_blocking=False)
+                self._dirty = False
+        return self.table_dev
+
+    @property
+    def free_pages(self) -> int:
+        return self.cache.allocator.free_pages
+
+    def cache_tokens_left(self) -> int:
+        return self.free_pages * self.page_size

@@ -1,0 +1,238 @@
+"""Numerics of every gfx950 HIP kernel against a plain-PyTorch fp32 reference of the same op."""
+import math
+
+import pytest
+import torch
+
+from src import ops
+from src.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _native():
+    assert ops.load_library(), "HIP kernel library must load on the GPU box"
+    torch.manual_seed(0)
+
+
+def bf(x):
+    return x.to(torch.bfloat16)
+
+
+@pytest.mark.parametrize("H", [256, 4096, 8192, 768])
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_rmsnorm(H, mode):
+    T = 37
+    x = bf(torch.randn(T, H, device=DEV))
+    w = bf(torch.rand(H, device=DEV) + 0.5)
+    res = bf(torch.randn(T, H, device=DEV))
+    res_ref = res.clone()
+    y = ops.rmsnorm(x, w, 1e-5, residual=res, mode=mode)
+    yr = ref.rmsnorm(x.cpu(), w.cpu(), 1e-5, residual=res_ref.cpu() if mode else None, mode=mode)
+    torch.testing.assert_close(y.cpu().float(), yr.float(), atol=2e-2, rtol=2e-2)
+    if mode == 1:
+        torch.testing.assert_close(res.cpu().float(), (res_ref.float() + x.float()).cpu(), atol=3e-2, rtol=1e-2)
+    if mode == 2:
+        assert torch.equal(res, x)
+    # fp32 oracle
+    src = (res_ref.float() + x.float()) if mode == 1 else x.float()
+    o = src * torch.rsqrt(src.pow(2).mean(-1, keepdim=True) + 1e-5) * w.float()
+    torch.testing.assert_close(y.float(), o, atol=5e-2, rtol=3e-2)
+
+
+def test_rmsnorm_rows():
+    x = bf(torch.randn(20, 512, device=DEV))
+    w = bf(torch.rand(512, device=DEV))
+    rows = torch.tensor([3, 19, 0], dtype=torch.int32, device=DEV)
+    y = ops.rmsnorm(x, w, 1e-6, rows=rows)
+    yr = ref.rmsnorm(x[rows.long()], w, 1e-6)
+    torch.testing.assert_close(y, yr, atol=1e-2, rtol=1e-2)
+
+
+def _make_cache(P, nkv, ps, D):
+    k = bf(torch.randn(P, nkv, ps, D, device=DEV))
+    v = bf(torch.randn(P, nkv, ps, D, device=DEV))
+    return k, v
+
+
+@pytest.mark.parametrize("nh,nkv,D", [(32, 32, 128), (8, 2, 128), (12, 12, 64), (64, 8, 128)])
+def test_rope_kv_write(nh, nkv, D):
+    T, P, ps = 19, 16, 64
+    qkv = bf(torch.randn(T, (nh + 2 * nkv) * D, device=DEV))
+    pos = torch.randint(0, 1000, (T,), device=DEV)
+    slots = torch.randperm(P * ps, device=DEV)[:T]
+    slots[3] = -1
+    cos, sin = ops.rope_cos_sin(D, 2048, 10000.0, DEV)
+    kc, vc = _make_cache(P, nkv, ps, D)
+    kr, vr, qr = kc.clone(), vc.clone(), qkv.clone()
+    ops.rope_kv_write(qkv, pos, cos, sin, kc, vc, slots, nh, nkv)
+    ref.rope_kv_write(qr, pos, cos, sin, kr, vr, slots, nh, nkv)
+    torch.testing.assert_close(qkv.float(), qr.float(), atol=2e-2, rtol=1e-2)
+    torch.testing.assert_close(kc.float(), kr.float(), atol=2e-2, rtol=1e-2)
+    assert torch.equal(vc, vr)
+
+
+def _attn_case(nh, nkv, D, ctxs, ps=64, multi_q=False):
+    S = len(ctxs)
+    maxp = max(math.ceil(c / ps) for c in ctxs) + 1
+    P = S * maxp + 3
+    kc, vc = _make_cache(P, nkv, ps, D)
+    perm = torch.randperm(P, device=DEV)[: S * maxp].view(S, maxp).to(torch.int32)
+    if multi_q:  # every position of every sequence is a query (prefill-as-decode, causal)
+        q_seq = torch.cat([torch.full((c,), i, dtype=torch.int32) for i, c in enumerate(ctxs)]).to(DEV)
+        q_ctx = torch.cat([torch.arange(1, c + 1, dtype=torch.int32) for c in ctxs]).to(DEV)
+    else:
+        q_seq = torch.arange(S, dtype=torch.int32, device=DEV)
+        q_ctx = torch.tensor(ctxs, dtype=torch.int32, device=DEV)
+    T = q_seq.numel()
+    q = bf(torch.randn(T, (nh + 2 * nkv) * D, device=DEV))  # strided q view like the executor's qkv
+    return q, kc, vc, perm, q_seq, q_ctx
+
+
+@pytest.mark.parametrize("nh,nkv,D", [(32, 32, 128), (32, 8, 128), (64, 8, 128), (16, 8, 128), (12, 12, 64),
+                                      (8, 2, 64)])
+@pytest.mark.parametrize("ctxs", [[1, 5, 64, 200], [1000, 3], [4097]])
+def test_paged_attention_decode(nh, nkv, D, ctxs):
+    q, kc, vc, bt, q_seq, q_ctx = _attn_case(nh, nkv, D, ctxs)
+    scale = 1 / math.sqrt(D)
+    out = ops.paged_attention(q, kc, vc, bt, q_seq, q_ctx, nh, nkv, scale)
+    o_ref = ref.paged_attention(q.float(), kc.float(), vc.float(), bt, q_seq, q_ctx, nh, nkv, scale)
+    torch.testing.assert_close(out.float(), o_ref.float(), atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("parts", [(64, 1), (64, 8), (128, 4), (2048, 1)])
+def test_paged_attention_explicit_partitions(parts):
+    nh, nkv, D = 32, 8, 128
+    q, kc, vc, bt, q_seq, q_ctx = _attn_case(nh, nkv, D, [300, 17, 1])
+    ps, np_ = parts
+    if ps * np_ < 300:
+        np_ = math.ceil(300 / ps)
+    out = ops.paged_attention(q, kc, vc, bt, q_seq, q_ctx, nh, nkv, 0.088, part_size=ps, num_parts=np_)
+    o_ref = ref.paged_attention(q.float(), kc.float(), vc.float(), bt, q_seq, q_ctx, nh, nkv, 0.088)
+    torch.testing.assert_close(out.float(), o_ref.float(), atol=2e-2, rtol=2e-2)
+
+
+def test_paged_attention_prefill_causal_and_padding():
+    nh, nkv, D = 16, 4, 128
+    q, kc, vc, bt, q_seq, q_ctx = _attn_case(nh, nkv, D, [70, 9], multi_q=True)
+    q_ctx[5] = 0  # padded row -> zeros
+    out = ops.paged_attention(q, kc, vc, bt, q_seq, q_ctx, nh, nkv, 0.1)
+    o_ref = ref.paged_attention(q.float(), kc.float(), vc.float(), bt, q_seq, q_ctx, nh, nkv, 0.1)
+    torch.testing.assert_close(out.float(), o_ref.float(), atol=2e-2, rtol=2e-2)
+    assert out[5].abs().max().item() == 0
+
+
+def test_paged_attention_spike_forces_rescale():
+    """One huge K row makes a single partition dominate: exercises the split-K combine."""
+    nh, nkv, D = 8, 8, 128
+    q, kc, vc, bt, q_seq, q_ctx = _attn_case(nh, nkv, D, [1500])
+    page = int(bt[0, 10])
+    kc[page, :, 5, :] = q[0, : nh * D].view(nh, D)[::1][:nkv] * 8
+    out = ops.paged_attention(q, kc, vc, bt, q_seq, q_ctx, nh, nkv, 1 / math.sqrt(D), part_size=64, num_parts=24)
+    o_ref = ref.paged_attention(q.float(), kc.float(), vc.float(), bt, q_seq, q_ctx, nh, nkv, 1 / math.sqrt(D))
+    torch.testing.assert_close(out.float(), o_ref.float(), atol=2e-2, rtol=2e-2)
+
+
+def test_swiglu_add_embedding_argmax():
+    T, F = 33, 11008
+    gu = bf(torch.randn(T, 2 * F, device=DEV))
+    torch.testing.assert_close(ops.swiglu(gu).float(), ref.swiglu(gu.cpu()).float().to(DEV), atol=1e-2, rtol=1e-2)
+    a, b = bf(torch.randn(T, 4096, device=DEV)), bf(torch.randn(T, 4096, device=DEV))
+    assert torch.equal(ops.add(a, b), (a.float() + b.float()).to(torch.bfloat16))
+    table = bf(torch.randn(1000, 4096, device=DEV))
+    ids = torch.randint(0, 1000, (T,), device=DEV)
+    assert torch.equal(ops.embedding(ids, table), table[ids])
+    logits = bf(torch.randn(T, 32000, device=DEV))
+    logits[3, 7] = 100
+    logits[3, 9] = 100  # tie -> first index
+    am = ops.argmax(logits)
+    assert torch.equal(am, torch.argmax(logits.float(), -1))
+    assert am[3].item() == 7
+
+
+@pytest.mark.parametrize("M", [1, 7, 16, 33, 64])
+@pytest.mark.parametrize("N,K", [(4096, 4096), (12288, 4096), (4096, 11008), (768, 768)])
+def test_gemm_native(M, N, K):
+    x = bf(torch.randn(M, K, device=DEV))
+    w = bf(torch.randn(N, K, device=DEV) * 0.02)
+    y = ops.linear(x, w, policy="native")
+    yr = (x.float() @ w.float().t())
+    torch.testing.assert_close(y.float(), yr, atol=3e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("M", [1, 40, 64])
+def test_gemm_swiglu_and_residual_epilogues(M):
+    K, F = 4096, 1024
+    x = bf(torch.randn(M, K, device=DEV))
+    gate = bf(torch.randn(F, K, device=DEV) * 0.02)
+    up = bf(torch.randn(F, K, device=DEV) * 0.02)
+    from src.models.weights import interleave_gate_up
+
+    gu = interleave_gate_up(gate, up)
+    y = ops.linear(x, gu, epilogue=1, policy="native")
+    g, u = x.float() @ gate.float().t(), x.float() @ up.float().t()
+    torch.testing.assert_close(y.float(), torch.nn.functional.silu(g) * u, atol=3e-2, rtol=3e-2)
+    y_lib = ops.linear(x, gu, epilogue=1, policy="hipblaslt")
+    torch.testing.assert_close(y.float(), y_lib.float(), atol=3e-2, rtol=3e-2)
+    r = bf(torch.randn(M, F, device=DEV))
+    w2 = bf(torch.randn(F, K, device=DEV) * 0.02)
+    y2 = ops.linear(x, w2, epilogue=2, residual=r, policy="native")
+    torch.testing.assert_close(y2.float(), x.float() @ w2.float().t() + r.float(), atol=5e-2, rtol=3e-2)
+
+
+def test_sampler_greedy_and_topk1():
+    R, V = 6, 32000
+    logits = bf(torch.randn(R, V, device=DEV) * 3)
+    z = torch.zeros(R, dtype=torch.float32, device=DEV)
+    args = dict(top_ps=torch.full((R,), 0.9, device=DEV), top_ks=torch.zeros(R, dtype=torch.int32, device=DEV),
+                rep_pens=torch.ones(R, device=DEV), recent=torch.zeros(R, 50, dtype=torch.int32, device=DEV),
+                recent_len=torch.zeros(R, dtype=torch.int32, device=DEV),
+                seeds=torch.arange(R, dtype=torch.long, device=DEV))
+    out = ops.sample(logits, z, **args)
+    assert torch.equal(out, torch.argmax(logits.float(), -1))
+    args["top_ks"] = torch.ones(R, dtype=torch.int32, device=DEV)
+    out = ops.sample(logits, torch.ones(R, device=DEV), **args)
+    assert torch.equal(out, torch.argmax(logits.float(), -1))
+
+
+def test_sampler_repetition_penalty_blocks_repeats():
+    V = 1000
+    logits = torch.zeros(1, V, device=DEV)
+    logits[0, 5] = 4.0
+    logits[0, 6] = 3.9
+    logits = bf(logits)
+    hist = torch.zeros(1, 50, dtype=torch.int32, device=DEV)
+    hist[0, :3] = 5
+    kw = dict(top_ps=torch.ones(1, device=DEV), top_ks=torch.ones(1, dtype=torch.int32, device=DEV),
+              rep_pens=torch.full((1,), 1.5, device=DEV), recent=hist,
+              recent_len=torch.tensor([3], dtype=torch.int32, device=DEV),
+              seeds=torch.tensor([1], device=DEV))
+    out = ops.sample(logits, torch.ones(1, device=DEV), **kw)
+    assert out.item() == 6  # 5 was penalised by 1.5**3 * 1.5**3
+    assert ref.sample_row(logits[0].cpu(), 1.0, 1.0, 1, 1.5, [5, 5, 5]) == 6
+
+
+def test_sampler_distribution_matches_reference():
+    V = 64
+    base = torch.randn(V) * 2
+    logits = bf(base.to(DEV).unsqueeze(0).repeat(4096, 1))
+    R = logits.shape[0]
+    kw = dict(top_ps=torch.full((R,), 0.8, device=DEV), top_ks=torch.full((R,), 10, dtype=torch.int32, device=DEV),
+              rep_pens=torch.ones(R, device=DEV), recent=torch.zeros(R, 50, dtype=torch.int32, device=DEV),
+              recent_len=torch.zeros(R, dtype=torch.int32, device=DEV),
+              seeds=torch.arange(R, dtype=torch.long, device=DEV) * 7 + 3)
+    out = ops.sample(logits, torch.full((R,), 0.7, device=DEV), **kw).cpu()
+    # expected distribution: reference semantics computed exactly
+    p = torch.softmax(logits[0].float().cpu() / 0.7, -1)
+    tv, ti = torch.topk(p, 10)
+    q = torch.zeros_like(p).scatter(0, ti, tv)
+    sp, si = torch.sort(q, descending=True)
+    keep = torch.cumsum(sp, 0) <= 0.8
+    keep[0] = True
+    f = torch.zeros_like(p).scatter(0, si, sp * keep)
+    f = f / f.sum()
+    freq = torch.bincount(out, minlength=V).float() / R
+    assert set(out.unique().tolist()) <= set(torch.nonzero(f).flatten().tolist())
+    assert (freq - f).abs().max().item() < 0.04

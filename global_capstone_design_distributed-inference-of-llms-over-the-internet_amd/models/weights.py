@@ -52,6 +52,11 @@ class LlamaLayer:
     post_norm: torch.Tensor
     gate_up: torch.Tensor
     down: torch.Tensor
+    # fragment-native packed copies for the decode GEMM (ops.pack_weight); None until packed
+    qkv_p: Optional[torch.Tensor] = None
+    o_p: Optional[torch.Tensor] = None
+    gate_up_p: Optional[torch.Tensor] = None
+    down_p: Optional[torch.Tensor] = None
 
 
 @dataclasses.dataclass
@@ -81,6 +86,7 @@ class StageWeights:
     final_norm: Optional[torch.Tensor] = None   # llama [H]; gpt2 ln_f weight
     final_norm_b: Optional[torch.Tensor] = None  # gpt2 ln_f bias
     lm_head: Optional[torch.Tensor] = None      # [V, H]
+    lm_head_p: Optional[torch.Tensor] = None    # packed lm_head (V padded to a multiple of 16)
 
     @property
     def has_embed(self) -> bool:
@@ -96,15 +102,36 @@ class StageWeights:
             n += t.numel() * t.element_size()
         return n
 
+    def pack_for_decode(self) -> None:
+        """Add fragment-native copies of every projection (MI355X decode GEMM layout).
+
+        The row-major weights stay for the hipBLASLt prefill path: 2x weight bytes, which
+        288 GB of HBM affords (13.5 GB -> 27 GB for Llama-2-7B on one GPU).
+        """
+        from .. import ops
+
+        for lay in self.layers:
+            if isinstance(lay, LlamaLayer) and lay.qkv_p is None:
+                lay.qkv_p = ops.pack_weight(lay.qkv)
+                lay.o_p = ops.pack_weight(lay.o)
+                lay.gate_up_p = ops.pack_weight(lay.gate_up)
+                lay.down_p = ops.pack_weight(lay.down)
+        if self.lm_head is not None and self.lm_head_p is None and self.cfg.model_type != "gpt2":
+            V, H = self.lm_head.shape
+            if H % 32 == 0:
+                pad = (-V) % 16
+                w = self.lm_head if pad == 0 else torch.cat([self.lm_head, self.lm_head.new_zeros(pad, H)])
+                self.lm_head_p = ops.pack_weight(w.contiguous())
+
     def tensors(self):
         seen = set()
         for lay in self.layers:
             for f in dataclasses.fields(lay):
                 t = getattr(lay, f.name)
-                if id(t) not in seen:
+                if t is not None and id(t) not in seen:
                     seen.add(id(t))
                     yield t
-        for t in (self.embed, self.pos_embed, self.final_norm, self.final_norm_b, self.lm_head):
+        for t in (self.embed, self.pos_embed, self.final_norm, self.final_norm_b, self.lm_head, self.lm_head_p):
             if t is not None and id(t) not in seen:
                 seen.add(id(t))
                 yield t

@@ -190,22 +190,41 @@ def sample(logits, temps, top_ps, top_ks, rep_pens, recent, recent_len, seeds, w
 
 
 def native_gemm_ok(M: int, N: int, K: int, epilogue: int = 0) -> bool:
-    return 0 < M <= 64 and K % 256 == 0 and N % (32 if epilogue == 1 else 16) == 0
+    return 0 < M <= 64 and K % 128 == 0 and N % (32 if epilogue == 1 else 16) == 0
 
 
-def linear(x, w, out=None, epilogue=0, residual=None, policy=None):
-    """y = epilogue(x @ w^T). epilogue 0: none; 1: SwiGLU (16-row interleaved gate/up w); 2: + residual."""
+def pack_weight(w: torch.Tensor) -> torch.Tensor:
+    """W [N, K] -> fragment-native layout [N/16, K/32, 64, 8] consumed by the decode GEMM."""
+    if not _native(w):
+        N, K = w.shape
+        return w.view(N // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4).reshape(N // 16, K // 32, 64, 8).contiguous()
+    return torch.ops.mpamd.pack_weight(w.contiguous())
+
+
+def unpack_weight(wp: torch.Tensor) -> torch.Tensor:
+    nt, ks = wp.shape[0], wp.shape[1]
+    return wp.view(nt, ks, 4, 16, 8).permute(0, 3, 1, 2, 4).reshape(nt * 16, ks * 32)
+
+
+def linear(x, w, out=None, epilogue=0, residual=None, policy=None, wp=None):
+    """y = epilogue(x @ w^T). epilogue 0: none; 1: SwiGLU (16-row interleaved gate/up w); 2: + residual.
+
+    ``wp`` is the packed copy of ``w`` (``pack_weight``); the native decode GEMM needs it.
+    """
     if not _native(x):
-        return ref.linear(x, w, out=out, epilogue=epilogue, residual=residual)
+        return ref.linear(x, w if w is not None else unpack_weight(wp), out=out, epilogue=epilogue,
+                          residual=residual)
     M, K = x.shape
-    N = w.shape[0]
+    N = w.shape[0] if w is not None else 16 * wp.shape[0]
     policy = policy or _GEMM_POLICY
-    use_native = policy == "native" or (policy == "auto" and native_gemm_ok(M, N, K, epilogue))
-    if use_native and native_gemm_ok(M, N, K, epilogue) and x.stride(0) % 8 == 0 and x.stride(1) == 1:
+    ok = wp is not None and native_gemm_ok(M, N, K, epilogue) and x.stride(0) % 8 == 0 and x.stride(1) == 1
+    if ok and policy in ("auto", "native"):
         if out is None:
             out = torch.empty(M, N // 2 if epilogue == 1 else N, dtype=x.dtype, device=x.device)
-        torch.ops.mpamd.gemm(x, w, out, residual, int(epilogue))
+        torch.ops.mpamd.gemm(x, wp, out, residual, int(epilogue))
         return out
+    if w is None:
+        raise RuntimeError(f"no row-major weight for the hipBLASLt path (M={M}, N={N}, K={K})")
     y = torch.nn.functional.linear(x, w)  # hipBLASLt
     if epilogue == 1:
         return swiglu(y, out=out)

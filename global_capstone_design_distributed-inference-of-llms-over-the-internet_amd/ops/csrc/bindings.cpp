@@ -29,6 +29,7 @@ int mp_sample(const void* logits, int64_t stride, int R, int V, const float* tem
               const int32_t* recent_len, const int64_t* seeds, float* ws, int64_t* out, hipStream_t stream);
 int mp_gemm_bf16(const void* x, int64_t x_stride, const void* w, void* y, int64_t y_stride, const void* res,
                  int64_t res_stride, int M, int N, int K, int epilogue, hipStream_t stream);
+int mp_pack_weight(const void* w, void* wp, int N, int K, hipStream_t stream);
 }
 
 namespace {
@@ -210,16 +211,17 @@ void sample(const at::Tensor& logits, const at::Tensor& temps, const at::Tensor&
                "sample");
 }
 
-void gemm(const at::Tensor& x, const at::Tensor& w, at::Tensor& y, const c10::optional<at::Tensor>& residual,
+void gemm(const at::Tensor& x, const at::Tensor& wp, at::Tensor& y, const c10::optional<at::Tensor>& residual,
           int64_t epilogue) {
   check_bf16_cuda(x, "x");
-  check_bf16_cuda(w, "w");
+  check_bf16_cuda(wp, "wp");
   check_bf16_cuda(y, "y");
   check_rows(x, "x");
   check_rows(y, "y");
-  MP_CHECK(w.dim() == 2 && w.is_contiguous(), "w [N, K] contiguous");
-  const int M = x.size(0), K = x.size(1), N = w.size(0);
-  MP_CHECK(w.size(1) == K, "K mismatch");
+  MP_CHECK(wp.dim() == 4 && wp.size(2) == 64 && wp.size(3) == 8 && wp.is_contiguous(),
+           "wp must be a packed weight [N/16, K/32, 64, 8] (ops.pack_weight)");
+  const int M = x.size(0), K = x.size(1), N = 16 * wp.size(0);
+  MP_CHECK(32 * wp.size(1) == K, "K mismatch between x and packed weight");
   const int ncols = epilogue == 1 ? N / 2 : N;
   MP_CHECK(y.size(0) == M && y.size(1) == ncols, "y shape");
   const void* rp = nullptr;
@@ -227,13 +229,25 @@ void gemm(const at::Tensor& x, const at::Tensor& w, at::Tensor& y, const c10::op
   if (residual.has_value()) {
     check_bf16_cuda(*residual, "residual");
     check_rows(*residual, "residual");
+    MP_CHECK(residual->size(0) == M && residual->size(1) == N, "residual shape");
     rp = residual->data_ptr();
     rs = residual->stride(0);
   }
   MP_CHECK(epilogue != 2 || rp != nullptr, "residual epilogue needs residual");
-  check_launch(mp_gemm_bf16(x.data_ptr(), x.stride(0), w.data_ptr(), y.data_ptr(), y.stride(0), rp, rs, M, N, K,
+  MP_CHECK(epilogue >= 0 && epilogue <= 2, "epilogue");
+  check_launch(mp_gemm_bf16(x.data_ptr(), x.stride(0), wp.data_ptr(), y.data_ptr(), y.stride(0), rp, rs, M, N, K,
                             (int)epilogue, cur_stream()),
                "gemm");
+}
+
+at::Tensor pack_weight(const at::Tensor& w) {
+  check_bf16_cuda(w, "w");
+  MP_CHECK(w.dim() == 2 && w.is_contiguous(), "w [N, K] contiguous");
+  const int N = w.size(0), K = w.size(1);
+  MP_CHECK(N % 16 == 0 && K % 32 == 0, "pack_weight needs N % 16 == 0 and K % 32 == 0");
+  auto wp = at::empty({N / 16, K / 32, 64, 8}, w.options());
+  check_launch(mp_pack_weight(w.data_ptr(), wp.data_ptr(), N, K, cur_stream()), "pack_weight");
+  return wp;
 }
 
 }  // namespace
@@ -254,7 +268,8 @@ TORCH_LIBRARY(mpamd, m) {
   m.def(
       "sample(Tensor logits, Tensor temps, Tensor top_ps, Tensor top_ks, Tensor rep_pens, Tensor recent, "
       "Tensor recent_len, Tensor seeds, Tensor(a!) workspace, Tensor(b!) out) -> ()");
-  m.def("gemm(Tensor x, Tensor w, Tensor(a!) y, Tensor? residual, int epilogue) -> ()");
+  m.def("gemm(Tensor x, Tensor wp, Tensor(a!) y, Tensor? residual, int epilogue) -> ()");
+  m.def("pack_weight(Tensor w) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(mpamd, CUDA, m) {
@@ -268,4 +283,5 @@ TORCH_LIBRARY_IMPL(mpamd, CUDA, m) {
   m.impl("argmax", &argmax);
   m.impl("sample", &sample);
   m.impl("gemm", &gemm);
+  m.impl("pack_weight", &pack_weight);
 }

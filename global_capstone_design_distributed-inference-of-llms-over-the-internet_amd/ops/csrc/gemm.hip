@@ -8,18 +8,19 @@
 // projections are bound by streaming W from HBM once, so this kernel is organised around
 // that stream:
 //
-//   * MFMA v_mfma_f32_16x16x32_bf16, W as the B operand straight from HBM to VGPRs (no LDS
-//     round trip: guide "GEMV / M <= 16" row), x as the A operand (L1/L2-resident).
-//   * K-permuted fragments: within a 256-deep chunk, lane (c = l&15, q = l>>4) of MFMA i
-//     holds k = 64q + 8i + j for both operands, so every lane reads 128 contiguous bytes
-//     of one W row (eight 16-B loads in flight per lane) instead of 16-B pieces of 16 rows.
-//   * one workgroup = 8 waves = NCT column tiles (16 cols each) x (8/NCT) K-slices; the
-//     K-slices are combined through LDS inside the workgroup (no atomics, no second pass).
-//   * fused epilogues: 0 = store bf16; 1 = SwiGLU for a gate/up weight stored as
-//     16-row interleaved [g(16) u(16) g(16) u(16) ...] (output N/2 columns);
-//     2 = y = bf16(bf16(acc) + residual).
-// Grid: one workgroup per (16 * NCT)-column slab of W -> N/16 (or N/32) workgroups, i.e.
-// 256-1376 workgroups x 8 waves for Llama-2-7B projections.
+//   * W is stored PRE-PACKED in MFMA fragment order (ops.pack_weight):
+//       Wp[n/16][k/32][lane][8],  lane = 16*q + c  holds  W[16*nt + c][32*ks + 8*q + j]
+//     so the B operand of every v_mfma_f32_16x16x32_bf16 is ONE contiguous 1 KiB read
+//     (64 lanes x 16 B), and a wave walking K streams a contiguous region: perfectly
+//     coalesced, non-temporal (read once), straight to VGPRs (guide: "GEMV / M <= 16" row).
+//   * x (A operand) is read row-major from L2: lane (r, q) reads 16 B of row r at k offset
+//     8q, i.e. 16 rows x 64 contiguous bytes per wave-instruction.
+//   * one workgroup = 8 waves over NT column tiles (16 cols each) x all of K; the waves take
+//     interleaved groups of U k-slices and their partial tiles are combined through LDS
+//     (no atomics, no second pass); B is double-buffered in registers across groups.
+//   * fused epilogues: 0 = store bf16; 1 = SwiGLU for a gate/up weight whose rows are
+//     interleaved in 16-row blocks [g16 u16 g16 u16 ...] (tile 2t = gate, 2t+1 = up;
+//     output N/2 columns); 2 = y = bf16(bf16(acc) + residual).
 #include "common.h"
 
 namespace mp {
@@ -31,102 +32,110 @@ __device__ __forceinline__ f32x4 mfma16(const u16x8& a, const u16x8& b, const f3
                                                   0, 0, 0);
 }
 
-template <int MT, int NCT, int EPI>
-__global__ __launch_bounds__(512) void gemm_skinny_kernel(const bf16_t* __restrict__ x, int64_t x_stride,
-                                                          const bf16_t* __restrict__ w, bf16_t* __restrict__ y,
+constexpr int GU = 4;  // k-slices (of 32) per wave group
+
+template <int MT, int NT, int EPI>
+__global__ __launch_bounds__(512) void gemm_packed_kernel(const bf16_t* __restrict__ x, int64_t x_stride,
+                                                          const bf16_t* __restrict__ wp, bf16_t* __restrict__ y,
                                                           int64_t y_stride, const bf16_t* __restrict__ res,
                                                           int64_t res_stride, int M, int N, int K) {
-  constexpr int NKS = 8 / NCT;  // K-slices per workgroup
-  __shared__ __attribute__((aligned(16))) float red[8][MT * 4][64];
+  __shared__ __attribute__((aligned(16))) float red[8][MT * NT * 4][64];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int ct = wid % NCT, ks = wid / NCT;
   const int c = lane & 15, q = lane >> 4;
-  const int n0 = blockIdx.x * (16 * NCT) + ct * 16;
-  const bf16_t* wrow = w + (int64_t)(n0 + c) * K + 64 * q;
-  const int nchunks = K >> 8;
+  const int nks = K >> 5;
+  const int ngroups = nks / GU;
+  const int nt0 = blockIdx.x * NT;
 
-  f32x4 acc[MT];
+  const bf16_t* wbase[NT];
 #pragma unroll
-  for (int mt = 0; mt < MT; ++mt) acc[mt] = (f32x4)(0.f);
+  for (int t = 0; t < NT; ++t) wbase[t] = wp + ((int64_t)(nt0 + t) * nks) * 512 + lane * 8;
 
-  // x rows this lane feeds (A operand row = lane & 15 within each 16-row tile)
   const bf16_t* xrow[MT];
   bool xok[MT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
     const int r = mt * 16 + c;
     xok[mt] = r < M;
-    xrow[mt] = x + (int64_t)(xok[mt] ? r : 0) * x_stride + 64 * q;
+    xrow[mt] = x + (int64_t)(xok[mt] ? r : 0) * x_stride + 8 * q;
   }
 
-  int ch = ks;
-  u16x8 b[8];
-  if (ch < nchunks) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) b[i] = __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(wrow + (ch << 8) + 8 * i));
-  }
-  for (; ch < nchunks; ch += NKS) {
-    const int nxt = ch + NKS;
-    u16x8 bn[8];
-    if (nxt < nchunks) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-        bn[i] = __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(wrow + (nxt << 8) + 8 * i));
-    }
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      u16x8 a[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-        a[i] = xok[mt] ? *reinterpret_cast<const u16x8*>(xrow[mt] + (ch << 8) + 8 * i) : (u16x8)(0);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) acc[mt] = mfma16(a[i], b[i], acc[mt]);
-    }
-    if (nxt < nchunks) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i) b[i] = bn[i];
-    }
-  }
-
-  // ---- combine the K-slices through LDS ----
+  f32x4 acc[MT][NT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) red[wid][mt * 4 + r][lane] = acc[mt][r];
-  __syncthreads();
-  if (ks != 0) return;
-  float sum[MT * 4];
+    for (int t = 0; t < NT; ++t) acc[mt][t] = (f32x4)(0.f);
+
+  u16x8 b[NT][GU], bn[NT][GU];
+  int g = wid;
+  if (g < ngroups) {
 #pragma unroll
-  for (int i = 0; i < MT * 4; ++i) {
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int u = 0; u < GU; ++u)
+        b[t][u] = __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(wbase[t] + (int64_t)(g * GU + u) * 512));
+  }
+  for (; g < ngroups; g += 8) {
+    const int gn = g + 8;
+    if (gn < ngroups) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int u = 0; u < GU; ++u)
+          bn[t][u] =
+              __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(wbase[t] + (int64_t)(gn * GU + u) * 512));
+    }
+    const int k0 = g * GU * 32;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      u16x8 a[GU];
+#pragma unroll
+      for (int u = 0; u < GU; ++u)
+        a[u] = xok[mt] ? *reinterpret_cast<const u16x8*>(xrow[mt] + k0 + 32 * u) : (u16x8)(0);
+#pragma unroll
+      for (int u = 0; u < GU; ++u)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[mt][t] = mfma16(a[u], b[t][u], acc[mt][t]);
+    }
+    if (gn < ngroups) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int u = 0; u < GU; ++u) b[t][u] = bn[t][u];
+    }
+  }
+
+  // ---- combine the 8 waves' partial tiles through LDS ----
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[wid][(mt * NT + t) * 4 + r][lane] = acc[mt][t][r];
+  __syncthreads();
+  // wave w finalises element slots i = w, w + 8, ... of the MT*NT*4 per-lane slots
+  for (int i = wid; i < MT * NT * 4; i += 8) {
+    const int mt = i / (NT * 4), t = (i / 4) % NT, r = i & 3;
+    const int row = mt * 16 + q * 4 + r;
     float s = 0.f;
 #pragma unroll
-    for (int k2 = 0; k2 < NKS; ++k2) s += red[k2 * NCT + ct][i][lane];
-    sum[i] = s;
-  }
-  if constexpr (EPI == 1) {
-    // wave ct==0 holds the gate tile, ct==1 the matching up tile
-    if (ct != 0) return;
-    const int ncol = blockIdx.x * 16 + c;  // output column (N/2 wide)
-#pragma unroll
-    for (int i = 0; i < MT * 4; ++i) {
+    for (int w = 0; w < 8; ++w) s += red[w][i][lane];
+    if constexpr (EPI == 1) {
+      if (t & 1) continue;  // the up tile is consumed by its gate tile
       float up = 0.f;
 #pragma unroll
-      for (int k2 = 0; k2 < NKS; ++k2) up += red[k2 * NCT + 1][i][lane];
-      const int row = (i >> 2) * 16 + q * 4 + (i & 3);
+      for (int w = 0; w < 8; ++w) up += red[w][i + 4][lane];
       if (row < M) {
-        const float g = round_bf(sum[i]);
-        const float a = round_bf(g / (1.f + __expf(-g)));
+        const int ncol = ((nt0 + t) >> 1) * 16 + c;
+        const float gg = round_bf(s);
+        const float a = round_bf(gg / (1.f + __expf(-gg)));
         y[(int64_t)row * y_stride + ncol] = f2bf(a * round_bf(up));
       }
-    }
-  } else {
-#pragma unroll
-    for (int i = 0; i < MT * 4; ++i) {
-      const int row = (i >> 2) * 16 + q * 4 + (i & 3);
+    } else {
       if (row < M) {
-        float v = sum[i];
-        if constexpr (EPI == 2) v = round_bf(v) + bf2f(res[(int64_t)row * res_stride + n0 + c]);
-        y[(int64_t)row * y_stride + n0 + c] = f2bf(v);
+        const int col = (nt0 + t) * 16 + c;
+        float v = s;
+        if constexpr (EPI == 2) v = round_bf(v) + bf2f(res[(int64_t)row * res_stride + col]);
+        y[(int64_t)row * y_stride + col] = f2bf(v);
       }
     }
   }
@@ -135,18 +144,40 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(const bf16_t* __restri
 template <int MT>
 static int launch_gemm(const void* x, int64_t xs, const void* w, void* y, int64_t ys, const void* res, int64_t rs,
                        int M, int N, int K, int epi, hipStream_t stream) {
+  const int ntiles = N / 16;
+  // two column tiles per wave when there are enough workgroups to fill the 256 CUs
+  const bool two = epi == 1 || (ntiles % 2 == 0 && ntiles / 2 >= 256);
+#define MP_LAUNCH(NT_, EPI_)                                                                                   \
+  hipLaunchKernelGGL((gemm_packed_kernel<MT, NT_, EPI_>), dim3(ntiles / NT_), dim3(512), 0, stream,             \
+                     (const bf16_t*)x, xs, (const bf16_t*)w, (bf16_t*)y, ys, (const bf16_t*)res, rs, M, N, K)
   if (epi == 1) {
-    if (N % 32) return -2;
-    hipLaunchKernelGGL((gemm_skinny_kernel<MT, 2, 1>), dim3(N / 32), dim3(512), 0, stream, (const bf16_t*)x, xs,
-                       (const bf16_t*)w, (bf16_t*)y, ys, (const bf16_t*)res, rs, M, N, K);
+    if (ntiles % 2) return -2;
+    MP_LAUNCH(2, 1);
   } else if (epi == 2) {
-    hipLaunchKernelGGL((gemm_skinny_kernel<MT, 1, 2>), dim3(N / 16), dim3(512), 0, stream, (const bf16_t*)x, xs,
-                       (const bf16_t*)w, (bf16_t*)y, ys, (const bf16_t*)res, rs, M, N, K);
+    if (two) MP_LAUNCH(2, 2);
+    else MP_LAUNCH(1, 2);
   } else {
-    hipLaunchKernelGGL((gemm_skinny_kernel<MT, 1, 0>), dim3(N / 16), dim3(512), 0, stream, (const bf16_t*)x, xs,
-                       (const bf16_t*)w, (bf16_t*)y, ys, (const bf16_t*)res, rs, M, N, K);
+    if (two) MP_LAUNCH(2, 0);
+    else MP_LAUNCH(1, 0);
   }
+#undef MP_LAUNCH
   return 0;
+}
+
+// Pack W[N, K] (row-major) into the fragment-native layout Wp[N/16][K/32][64][8].
+__global__ __launch_bounds__(256) void pack_weight_kernel(const bf16_t* __restrict__ w, bf16_t* __restrict__ wp,
+                                                          int N, int K) {
+  const int nks = K >> 5;
+  const int64_t total = (int64_t)(N >> 4) * nks * 64;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int lane = (int)(i & 63);
+    const int64_t tile = i >> 6;
+    const int ks = (int)(tile % nks);
+    const int64_t nt = tile / nks;
+    const int c = lane & 15, q = lane >> 4;
+    const u16x8 v = *reinterpret_cast<const u16x8*>(w + (nt * 16 + c) * (int64_t)K + ks * 32 + q * 8);
+    *reinterpret_cast<u16x8*>(wp + i * 8) = v;
+  }
 }
 
 }  // namespace mp
@@ -156,12 +187,22 @@ extern "C" int mp_gemm_bf16(const void* x, int64_t x_stride, const void* w, void
                             hipStream_t stream) {
   using namespace mp;
   if (M == 0) return 0;
-  if (M > 64 || K % 256 || N % 16 || x_stride % 8) return -1;
+  if (M > 64 || K % (32 * GU) || N % 16 || x_stride % 8) return -1;
   int rc;
   if (M <= 16) rc = launch_gemm<1>(x, x_stride, w, y, y_stride, res, res_stride, M, N, K, epilogue, stream);
   else if (M <= 32) rc = launch_gemm<2>(x, x_stride, w, y, y_stride, res, res_stride, M, N, K, epilogue, stream);
   else if (M <= 48) rc = launch_gemm<3>(x, x_stride, w, y, y_stride, res, res_stride, M, N, K, epilogue, stream);
   else rc = launch_gemm<4>(x, x_stride, w, y, y_stride, res, res_stride, M, N, K, epilogue, stream);
   if (rc) return rc;
+  return (int)hipGetLastError();
+}
+
+extern "C" int mp_pack_weight(const void* w, void* wp, int N, int K, hipStream_t stream) {
+  using namespace mp;
+  if (N % 16 || K % 32) return -1;
+  const int64_t total = (int64_t)(N / 16) * (K / 32) * 64;
+  int64_t g = (total + 255) / 256;
+  if (g > 8192) g = 8192;
+  hipLaunchKernelGGL(pack_weight_kernel, dim3((int)g), dim3(256), 0, stream, (const bf16_t*)w, (bf16_t*)wp, N, K);
   return (int)hipGetLastError();
 }

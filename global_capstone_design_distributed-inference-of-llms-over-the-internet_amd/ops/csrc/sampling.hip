@@ -26,8 +26,6 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
 
 constexpr int SB = 1024;  // threads per block
 
-__device__ __forceinline__ float block_sum_1k(float v, float* red) { return block_sum(v, red); }
-
 // Exclusive block scan of one float per thread (blockDim == SB).
 __device__ __forceinline__ float block_excl_scan(float v, float* red, float* total) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -179,14 +177,30 @@ __global__ __launch_bounds__(SB) void sample_kernel(const bf16_t* __restrict__ l
         if ((b & msk) == prefix) atomicAdd(&hist[(b >> shift) & 255u], 1u);
       }
       __syncthreads();
-      if (tid == 0) {
-        int cum = 0, sel = 0;
-        for (int d = 255; d >= 0; --d) {
-          if (cum + (int)hist[d] >= kk) { sel = d; break; }
-          cum += hist[d];
+      if (tid < 64) {  // wave 0: parallel suffix count over bins 255..0, lane l owns bins 4l..4l+3
+        const int l = tid;
+        const unsigned h0 = hist[4 * l], h1 = hist[4 * l + 1], h2 = hist[4 * l + 2], h3 = hist[4 * l + 3];
+        const int own = (int)(h0 + h1 + h2 + h3);
+        int incl = own;  // inclusive suffix sum over lanes >= l
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const int nb = __shfl_down(incl, o, 64);
+          if (l + o < 64) incl += nb;
         }
-        s_u[0] = (unsigned)sel;
-        s_i[0] = kk - cum;
+        const unsigned long long hit = __ballot(incl >= kk);
+        const int cl = hit ? 63 - __builtin_clzll(hit) : 0;  // highest lane whose suffix reaches kk
+        if (l == cl) {
+          int cum = incl - own;  // count strictly above this lane's bins
+          int sel = 4 * l;
+          const unsigned hb[4] = {h3, h2, h1, h0};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            if (cum + (int)hb[j] >= kk) { sel = 4 * l + 3 - j; break; }
+            cum += hb[j];
+          }
+          s_u[0] = (unsigned)sel;
+          s_i[0] = kk - cum;
+        }
       }
       __syncthreads();
       prefix |= s_u[0] << shift;
@@ -215,18 +229,38 @@ __global__ __launch_bounds__(SB) void sample_kernel(const bf16_t* __restrict__ l
         if (pv > 0.f && (b & msk) == prefix) atomicAdd(&mass[(b >> shift) & 255u], pv);
       }
       __syncthreads();
-      if (tid == 0) {
-        int sel = -1;
-        float a = above;
-        for (int d = 255; d >= 0; --d) {
-          if (mass[d] == 0.f) continue;
-          if (a + mass[d] <= tp) { a += mass[d]; continue; }
-          sel = d;
-          break;
+      if (tid < 64) {  // wave 0: first bin (from the top) whose cumulative mass crosses tp
+        const int l = tid;
+        const float m0 = mass[4 * l], m1 = mass[4 * l + 1], m2 = mass[4 * l + 2], m3 = mass[4 * l + 3];
+        const float own = (m0 + m1) + (m2 + m3);
+        float incl = own;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const float nb = __shfl_down(incl, o, 64);
+          if (l + o < 64) incl += nb;
         }
-        s_u[0] = (unsigned)(sel < 0 ? 0 : sel);
-        s_i[0] = sel;
-        red[0] = a;
+        const unsigned long long hit = __ballot(above + incl > tp);
+        if (!hit) {
+          if (l == 0) { s_i[0] = -1; red[0] = above + incl; }
+        } else {
+          const int cl = 63 - __builtin_clzll(hit);
+          if (l == cl) {
+            float a = above + (incl - own);
+            int sel = -1;
+            const float mb[4] = {m3, m2, m1, m0};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              if (mb[j] == 0.f) continue;
+              if (a + mb[j] <= tp) { a += mb[j]; continue; }
+              sel = 4 * l + 3 - j;
+              break;
+            }
+            if (sel < 0) sel = 4 * l;  // rounding: the crossing sits in this lane's lowest non-empty bin
+            s_u[0] = (unsigned)sel;
+            s_i[0] = sel;
+            red[0] = a;
+          }
+        }
       }
       __syncthreads();
       const int sel = s_i[0];

@@ -134,6 +134,8 @@ class StageExecutor:
         self.timing = False
         if self.device.type == "cuda":
             ops.require_native()
+            if cfg.model_type != "gpt2" and ops.gemm_policy() != "hipblaslt":
+                weights.pack_for_decode()
         logger.info(f"StageExecutor blocks [{self.start},{self.end}) embed={self.is_first} head={self.is_last} "
                     f"kv_pages={num_pages} x {page_size} tokens ({self.cache.nbytes / 2**30:.2f} GiB) "
                     f"graphs={self.use_graphs}")
@@ -252,21 +254,26 @@ class StageExecutor:
                 ops.rmsnorm(h, L.input_norm, eps, out=xn, residual=res, mode=2)
             else:
                 ops.rmsnorm(mlp, L.input_norm, eps, out=xn, residual=res, mode=1)
-            ops.linear(xn, L.qkv, out=qkv)
+            ops.linear(xn, L.qkv, out=qkv, wp=L.qkv_p)
             kc, vc = self.cache.layer(li)
             ops.rope_kv_write(qkv, positions, self.cos, self.sin, kc, vc, slots, self.nh, self.nkv)
             ops.paged_attention(qkv, kc, vc, table, q_seq, q_ctx, self.nh, self.nkv, self.scale, out=attn,
                                 workspace=ws, part_size=ps, num_parts=np_)
-            ops.linear(attn, L.o, out=o)
+            ops.linear(attn, L.o, out=o, wp=L.o_p)
             ops.rmsnorm(o, L.post_norm, eps, out=xn, residual=res, mode=1)
-            ops.linear(xn, L.gate_up, out=act, epilogue=1)
-            ops.linear(act, L.down, out=mlp)
+            ops.linear(xn, L.gate_up, out=act, epilogue=1, wp=L.gate_up_p)
+            ops.linear(act, L.down, out=mlp, wp=L.down_p)
         hout = ops.add(res, mlp, out=e("hout", (T, H)))
         if not self.is_last:
             return hout
         S = last_rows.numel()
         fn = ops.rmsnorm(hout, w.final_norm, eps, out=e("fn", (S, H)), rows=last_rows)
-        return ops.linear(fn, w.lm_head, out=e("logits", (S, cfg.vocab_size)))
+        V = cfg.vocab_size
+        Vp = 16 * w.lm_head_p.shape[0] if w.lm_head_p is not None else V
+        logits = ops.linear(fn, w.lm_head if Vp == V else None, out=e("logits", (S, Vp)), wp=w.lm_head_p) \
+            if (Vp == V or ops.native_gemm_ok(S, Vp, H)) else \
+            ops.linear(fn, w.lm_head, out=e("logits", (S, V)))
+        return logits[:, :V]
 
     # ------------------------------------------------------------------ gpt2 (plumbing family)
     def _forward_gpt2(self, plan: Plan, x):

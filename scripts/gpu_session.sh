@@ -27,6 +27,7 @@ for s in $STEPS; do
     benchgemm) step bench1_hipblaslt 600 python bench.py --gemm hipblaslt ;;
     prof) step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o bench -- python bench.py --steps 8 --warmup 2 ;;
     hf) step hf_baseline 600 python scripts/hf_baseline.py ;;
+    kern) step bench_kernels 600 python scripts/bench_kernels.py ;;
     *) echo "unknown step $s" ;;
   esac
 done

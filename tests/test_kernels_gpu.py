@@ -153,11 +153,14 @@ def test_swiglu_add_embedding_argmax():
 
 
 @pytest.mark.parametrize("M", [1, 7, 16, 33, 64])
-@pytest.mark.parametrize("N,K", [(4096, 4096), (12288, 4096), (4096, 11008), (768, 768)])
+@pytest.mark.parametrize("N,K", [(4096, 4096), (12288, 4096), (4096, 11008), (768, 768), (8192, 384), (32000, 4096)])
 def test_gemm_native(M, N, K):
     x = bf(torch.randn(M, K, device=DEV))
     w = bf(torch.randn(N, K, device=DEV) * 0.02)
-    y = ops.linear(x, w, policy="native")
+    wp = ops.pack_weight(w)
+    assert torch.equal(ops.unpack_weight(wp), w)
+    assert torch.equal(wp.cpu(), ops.pack_weight(w.cpu()))
+    y = ops.linear(x, None, policy="native", wp=wp)
     yr = (x.float() @ w.float().t())
     torch.testing.assert_close(y.float(), yr, atol=3e-2, rtol=2e-2)
 
@@ -171,14 +174,14 @@ def test_gemm_swiglu_and_residual_epilogues(M):
     from src.models.weights import interleave_gate_up
 
     gu = interleave_gate_up(gate, up)
-    y = ops.linear(x, gu, epilogue=1, policy="native")
+    y = ops.linear(x, gu, epilogue=1, policy="native", wp=ops.pack_weight(gu))
     g, u = x.float() @ gate.float().t(), x.float() @ up.float().t()
     torch.testing.assert_close(y.float(), torch.nn.functional.silu(g) * u, atol=3e-2, rtol=3e-2)
     y_lib = ops.linear(x, gu, epilogue=1, policy="hipblaslt")
     torch.testing.assert_close(y.float(), y_lib.float(), atol=3e-2, rtol=3e-2)
     r = bf(torch.randn(M, F, device=DEV))
     w2 = bf(torch.randn(F, K, device=DEV) * 0.02)
-    y2 = ops.linear(x, w2, epilogue=2, residual=r, policy="native")
+    y2 = ops.linear(x, w2, epilogue=2, residual=r, policy="native", wp=ops.pack_weight(w2))
     torch.testing.assert_close(y2.float(), x.float() @ w2.float().t() + r.float(), atol=5e-2, rtol=3e-2)
 
 

@@ -32,13 +32,15 @@ __device__ __forceinline__ f32x4 mfma16(const u16x8& a, const u16x8& b, const f3
                                                   0, 0, 0);
 }
 
-constexpr int GU = 4;  // k-slices (of 32) per wave group
+constexpr int GU_MAX = 4;  // k-slices (of 32) per wave group (x 16 B per lane per column tile)
 
 template <int MT, int NT, int EPI>
 __global__ __launch_bounds__(512) void gemm_packed_kernel(const bf16_t* __restrict__ x, int64_t x_stride,
                                                           const bf16_t* __restrict__ wp, bf16_t* __restrict__ y,
                                                           int64_t y_stride, const bf16_t* __restrict__ res,
                                                           int64_t res_stride, int M, int N, int K) {
+  // fewer k-slices per group for the widest tiles keeps A + 2 x B + acc inside 256 VGPRs
+  constexpr int GU = (MT * NT >= 6) ? 2 : 4;
   __shared__ __attribute__((aligned(16))) float red[8][MT * NT * 4][64];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int c = lane & 15, q = lane >> 4;
@@ -50,13 +52,13 @@ __global__ __launch_bounds__(512) void gemm_packed_kernel(const bf16_t* __restri
 #pragma unroll
   for (int t = 0; t < NT; ++t) wbase[t] = wp + ((int64_t)(nt0 + t) * nks) * 512 + lane * 8;
 
+  // A rows >= M are clamped to a valid row (their accumulator rows are never stored): no
+  // per-load branches, so hipcc can count vmcnt through the loop (guide §5 trap (c)).
   const bf16_t* xrow[MT];
-  bool xok[MT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
-    const int r = mt * 16 + c;
-    xok[mt] = r < M;
-    xrow[mt] = x + (int64_t)(xok[mt] ? r : 0) * x_stride + 8 * q;
+    const int r = min(mt * 16 + c, M - 1);
+    xrow[mt] = x + (int64_t)r * x_stride + 8 * q;
   }
 
   f32x4 acc[MT][NT];
@@ -65,44 +67,46 @@ __global__ __launch_bounds__(512) void gemm_packed_kernel(const bf16_t* __restri
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[mt][t] = (f32x4)(0.f);
 
-  u16x8 b[NT][GU], bn[NT][GU];
+  // Ping-pong weight buffers (no register copies, which would force a vmcnt(0)), and the
+  // A fragments of group g issued BEFORE the prefetch of group g+8: vmcnt retires loads in
+  // issue order, so waiting for A leaves the weight prefetch in flight across the MFMAs.
+  u16x8 b0[NT][GU], b1[NT][GU], a[MT][GU];
+#define MP_LOAD_B(dst, grp)                                                                                   \
+  _Pragma("unroll") for (int t = 0; t < NT; ++t) _Pragma("unroll") for (int u = 0; u < GU; ++u) dst[t][u] =    \
+      __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(wbase[t] + (int64_t)((grp) * GU + u) * 512));
+#define MP_LOAD_A(grp)                                                                                        \
+  _Pragma("unroll") for (int mt = 0; mt < MT; ++mt) _Pragma("unroll") for (int u = 0; u < GU; ++u) a[mt][u] =  \
+      *reinterpret_cast<const u16x8*>(xrow[mt] + (grp) * GU * 32 + 32 * u);
+#define MP_MMA(bb)                                                                                            \
+  _Pragma("unroll") for (int mt = 0; mt < MT; ++mt) _Pragma("unroll") for (int u = 0; u < GU; ++u)            \
+      _Pragma("unroll") for (int t = 0; t < NT; ++t) acc[mt][t] = mfma16(a[mt][u], bb[t][u], acc[mt][t]);
   int g = wid;
   if (g < ngroups) {
-#pragma unroll
-    for (int t = 0; t < NT; ++t)
-#pragma unroll
-      for (int u = 0; u < GU; ++u)
-        b[t][u] = __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(wbase[t] + (int64_t)(g * GU + u) * 512));
+    MP_LOAD_B(b0, g)
   }
-  for (; g < ngroups; g += 8) {
-    const int gn = g + 8;
-    if (gn < ngroups) {
-#pragma unroll
-      for (int t = 0; t < NT; ++t)
-#pragma unroll
-        for (int u = 0; u < GU; ++u)
-          bn[t][u] =
-              __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(wbase[t] + (int64_t)(gn * GU + u) * 512));
+  while (g < ngroups) {
+    MP_LOAD_A(g)
+    if (g + 8 < ngroups) {
+      MP_LOAD_B(b1, g + 8)
+      MP_MMA(b0)
+    } else {
+      MP_MMA(b0)
+      break;
     }
-    const int k0 = g * GU * 32;
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      u16x8 a[GU];
-#pragma unroll
-      for (int u = 0; u < GU; ++u)
-        a[u] = xok[mt] ? *reinterpret_cast<const u16x8*>(xrow[mt] + k0 + 32 * u) : (u16x8)(0);
-#pragma unroll
-      for (int u = 0; u < GU; ++u)
-#pragma unroll
-        for (int t = 0; t < NT; ++t) acc[mt][t] = mfma16(a[u], b[t][u], acc[mt][t]);
+    g += 8;
+    MP_LOAD_A(g)
+    if (g + 8 < ngroups) {
+      MP_LOAD_B(b0, g + 8)
+      MP_MMA(b1)
+    } else {
+      MP_MMA(b1)
+      break;
     }
-    if (gn < ngroups) {
-#pragma unroll
-      for (int t = 0; t < NT; ++t)
-#pragma unroll
-        for (int u = 0; u < GU; ++u) b[t][u] = bn[t][u];
-    }
+    g += 8;
   }
+#undef MP_LOAD_B
+#undef MP_LOAD_A
+#undef MP_MMA
 
   // ---- combine the 8 waves' partial tiles through LDS ----
 #pragma unroll
@@ -187,7 +191,7 @@ extern "C" int mp_gemm_bf16(const void* x, int64_t x_stride, const void* w, void
                             hipStream_t stream) {
   using namespace mp;
   if (M == 0) return 0;
-  if (M > 64 || K % (32 * GU) || N % 16 || x_stride % 8) return -1;
+  if (M > 64 || K % (32 * GU_MAX) || N % 16 || x_stride % 8) return -1;
   int rc;
   if (M <= 16) rc = launch_gemm<1>(x, x_stride, w, y, y_stride, res, res_stride, M, N, K, epilogue, stream);
   else if (M <= 32) rc = launch_gemm<2>(x, x_stride, w, y, y_stride, res, res_stride, M, N, K, epilogue, stream);

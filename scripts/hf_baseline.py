@@ -18,6 +18,8 @@ import json
 import time
 
 import torch
+import os, sys
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def sample(logits, temperature, top_p, top_k):

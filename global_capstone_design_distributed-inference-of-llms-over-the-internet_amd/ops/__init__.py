@@ -84,14 +84,39 @@ def gemm_policy() -> str:
 
 
 # ---------------------------------------------------------------------------------------
-def rmsnorm(x, w, eps, out=None, residual=None, mode=0, rows=None):
-    """mode 0: y = norm(x)*w; 1: residual += x, y = norm(residual)*w; 2: residual = x, y = norm(x)*w."""
+def packed_numel(M: int, K: int) -> int:
+    """Elements of a packed decode activation (rows padded to a multiple of 16)."""
+    return ((M + 15) // 16) * 16 * K
+
+
+def pack_act(x, out=None):
+    """Row-major [M, K] -> packed decode-GEMM activation layout (flat, ``packed_numel`` elements)."""
+    M, K = x.shape
     if not _native(x):
-        return ref.rmsnorm(x, w, eps, out=out, residual=residual, mode=mode, rows=rows)
+        return ref.pack_act(x, out=out)
     if out is None:
-        n = rows.numel() if rows is not None else x.shape[0]
-        out = torch.empty(n, x.shape[1], dtype=x.dtype, device=x.device)
-    torch.ops.mpamd.rmsnorm(x, residual if residual is not None else x, w, out, float(eps), int(mode), rows)
+        out = torch.zeros(packed_numel(M, K), dtype=x.dtype, device=x.device)
+    torch.ops.mpamd.pack_act(x, out)
+    return out
+
+
+def unpack_act(ap, M, K):
+    return ref.unpack_act(ap, M, K)
+
+
+def rmsnorm(x, w, eps, out=None, residual=None, mode=0, rows=None, packed=False):
+    """mode 0: y = norm(x)*w; 1: residual += x, y = norm(residual)*w; 2: residual = x, y = norm(x)*w.
+
+    ``packed``: write y in the packed decode-GEMM activation layout (``out`` flat)."""
+    if not _native(x):
+        y = ref.rmsnorm(x, w, eps, out=None if packed else out, residual=residual, mode=mode, rows=rows)
+        return ref.pack_act(y, out=out) if packed else y
+    n = rows.numel() if rows is not None else x.shape[0]
+    if out is None:
+        out = (torch.empty(packed_numel(n, x.shape[1]), dtype=x.dtype, device=x.device) if packed
+               else torch.empty(n, x.shape[1], dtype=x.dtype, device=x.device))
+    torch.ops.mpamd.rmsnorm(x, residual if residual is not None else x, w, out, float(eps), int(mode), rows,
+                            int(bool(packed)))
     return out
 
 
@@ -123,9 +148,11 @@ def attention_workspace(num_queries: int, nh: int, head_dim: int, num_parts: int
 
 
 def paged_attention(q, k_cache, v_cache, block_tables, q_seq, q_ctx, nh, nkv, scale, out=None, workspace=None,
-                    part_size=None, num_parts=None, max_ctx=None):
+                    part_size=None, num_parts=None, max_ctx=None, packed=False):
     if not _native(q):
-        return ref.paged_attention(q, k_cache, v_cache, block_tables, q_seq, q_ctx, nh, nkv, scale, out=out)
+        y = ref.paged_attention(q, k_cache, v_cache, block_tables, q_seq, q_ctx, nh, nkv, scale,
+                                out=None if packed else out)
+        return ref.pack_act(y, out=out) if packed else y
     T = q.shape[0]
     D = k_cache.shape[-1]
     if part_size is None:
@@ -133,11 +160,12 @@ def paged_attention(q, k_cache, v_cache, block_tables, q_seq, q_ctx, nh, nkv, sc
             max_ctx = int(q_ctx.max().item()) if T else 1
         part_size, num_parts = attention_partition(T, nkv, max_ctx)
     if out is None:
-        out = torch.empty(T, nh * D, dtype=q.dtype, device=q.device)
+        out = (torch.empty(packed_numel(T, nh * D), dtype=q.dtype, device=q.device) if packed
+               else torch.empty(T, nh * D, dtype=q.dtype, device=q.device))
     if workspace is None:
         workspace = attention_workspace(T, nh, D, num_parts, q.device)
     torch.ops.mpamd.paged_attention(q, k_cache, v_cache, block_tables, q_seq, q_ctx, out, workspace, int(nh), int(nkv),
-                                    float(scale), int(part_size), int(num_parts))
+                                    float(scale), int(part_size), int(num_parts), int(bool(packed)))
     return out
 
 
@@ -206,23 +234,39 @@ def unpack_weight(wp: torch.Tensor) -> torch.Tensor:
     return wp.view(nt, ks, 4, 16, 8).permute(0, 3, 1, 2, 4).reshape(nt * 16, ks * 32)
 
 
-def linear(x, w, out=None, epilogue=0, residual=None, policy=None, wp=None):
+def linear(x, w, out=None, epilogue=0, residual=None, policy=None, wp=None, a_rows=None, out_packed=False):
     """y = epilogue(x @ w^T). epilogue 0: none; 1: SwiGLU (16-row interleaved gate/up w); 2: + residual.
 
     ``wp`` is the packed copy of ``w`` (``pack_weight``); the native decode GEMM needs it.
+    ``a_rows`` (int) says ``x`` is a PACKED activation holding that many rows (decode path);
+    ``out_packed`` (SwiGLU only) writes the output packed for the next GEMM.
     """
     if not _native(x):
-        return ref.linear(x, w if w is not None else unpack_weight(wp), out=out, epilogue=epilogue,
-                          residual=residual)
-    M, K = x.shape
+        if a_rows is not None:
+            K = 32 * wp.shape[1] if wp is not None else w.shape[1]
+            x = ref.unpack_act(x, a_rows, K)
+        y = ref.linear(x, w if w is not None else unpack_weight(wp), out=None if out_packed else out,
+                       epilogue=epilogue, residual=residual)
+        return ref.pack_act(y, out=out) if out_packed else y
+    if a_rows is not None:
+        M = int(a_rows)
+        K = 32 * wp.shape[1]
+    else:
+        M, K = x.shape
     N = w.shape[0] if w is not None else 16 * wp.shape[0]
     policy = policy or _GEMM_POLICY
-    ok = wp is not None and native_gemm_ok(M, N, K, epilogue) and x.stride(0) % 8 == 0 and x.stride(1) == 1
-    if ok and policy in ("auto", "native"):
+    ok = wp is not None and native_gemm_ok(M, N, K, epilogue) and (
+        a_rows is not None or (x.stride(0) % 8 == 0 and x.stride(1) == 1))
+    if ok and (policy in ("auto", "native") or a_rows is not None or out_packed):
+        ncols = N // 2 if epilogue == 1 else N
         if out is None:
-            out = torch.empty(M, N // 2 if epilogue == 1 else N, dtype=x.dtype, device=x.device)
-        torch.ops.mpamd.gemm(x, wp, out, residual, int(epilogue))
+            out = (torch.empty(packed_numel(M, ncols), dtype=x.dtype, device=x.device) if out_packed
+                   else torch.empty(M, ncols, dtype=x.dtype, device=x.device))
+        flags = (1 if a_rows is not None else 0) | (2 if out_packed else 0)
+        torch.ops.mpamd.gemm(x, wp, out, residual, int(epilogue), M, flags)
         return out
+    if a_rows is not None or out_packed:
+        raise RuntimeError(f"packed activations need the native decode GEMM (M={M}, N={N}, K={K})")
     if w is None:
         raise RuntimeError(f"no row-major weight for the hipBLASLt path (M={M}, N={N}, K={K})")
     y = torch.nn.functional.linear(x, w)  # hipBLASLt

@@ -76,8 +76,9 @@ def build(force: bool = False, jobs: int = 0, verbose: bool = False) -> str:
         cmds.append([HIPCC] + common + ["-c", src, "-o", obj])
     bobj = os.path.join(BUILD, "bindings.o")
     objs.append(bobj)
-    cmds.append([HIPCC, "-O2", "-fPIC", "-std=c++17", "-DUSE_ROCM=1", "-D__HIP_PLATFORM_AMD__=1"]
-                + [f"-I{p}" for p in inc] + ["-c", binding, "-o", bobj])
+    # host-only translation unit (torch headers): plain C++, no device pass
+    cmds.append([HIPCC, "-x", "c++", "-O2", "-fPIC", "-std=c++17", "-DUSE_ROCM=1", "-D__HIP_PLATFORM_AMD__=1",
+                 "-I/opt/rocm/include"] + [f"-I{p}" for p in inc] + ["-c", binding, "-o", bobj])
     jobs = jobs or min(len(cmds), os.cpu_count() or 4, 8)
     with cf.ThreadPoolExecutor(jobs) as ex:
         for out in ex.map(_run, cmds):

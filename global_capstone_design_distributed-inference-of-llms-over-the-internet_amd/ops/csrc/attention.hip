@@ -18,6 +18,7 @@
 // Queries carry their own (sequence row, context length), so the same kernel runs
 // decode (one query per sequence), chunked prefill (query i of a chunk sees
 // ctx = start + i + 1 -> causal) and replay.  ctx == 0 rows (batch padding) output 0.
+// packed_mt > 0 writes the output in the packed decode-GEMM activation layout (common.h).
 #include "common.h"
 
 namespace mp {
@@ -43,7 +44,7 @@ __global__ __launch_bounds__(256) void paged_attn_kernel(
     const bf16_t* __restrict__ vc, const int32_t* __restrict__ block_tables, int bt_stride,
     const int32_t* __restrict__ q_seq, const int32_t* __restrict__ q_ctx, bf16_t* __restrict__ out,
     float* __restrict__ part_o, float* __restrict__ part_ml, int nkv, int page_log2, int PS, int NP,
-    float scale_log2) {
+    float scale_log2, int packed_mt) {
   constexpr int LPT = D / 8;
   constexpr int TPI = 64 / LPT;
   constexpr int U = 4;
@@ -63,7 +64,8 @@ __global__ __launch_bounds__(256) void paged_attn_kernel(
   const int64_t obase = ((int64_t)t * nh + (int64_t)g * NREP) * D;
   if (start >= end) {
     if (NP == 1) {
-      for (int i = tid; i < NREP * D; i += 256) out[obase + i] = 0;
+      for (int i = tid; i < NREP * D; i += 256)
+        out[packed_mt > 0 ? apk_off(t, g * NREP * D + i, packed_mt) : obase + i] = 0;
     } else if (tid < NREP) {
       float* ml = part_ml + (((int64_t)t * nh + g * NREP + tid) * NP + p) * 2;
       ml[0] = -INFINITY;
@@ -202,7 +204,7 @@ __global__ __launch_bounds__(256) void paged_attn_kernel(
                     s_o[(3 * NREP + r) * D + d];
     const float l = s_l[r] + s_l[NREP + r] + s_l[2 * NREP + r] + s_l[3 * NREP + r];
     if (NP == 1) {
-      out[obase + i] = f2bf(o / l);
+      out[packed_mt > 0 ? apk_off(t, g * NREP * D + i, packed_mt) : obase + i] = f2bf(o / l);
     } else {
       const int64_t hp = ((int64_t)t * nh + g * NREP + r) * NP + p;
       part_o[hp * D + d] = o;
@@ -220,7 +222,7 @@ __global__ __launch_bounds__(256) void paged_attn_kernel(
 
 // Combine split-K partials: one workgroup (D threads) per (query row, head).
 __global__ void paged_attn_reduce_kernel(const float* __restrict__ part_o, const float* __restrict__ part_ml,
-                                         bf16_t* __restrict__ out, int NP, int D) {
+                                         bf16_t* __restrict__ out, int NP, int D, int nh, int packed_mt) {
   const int64_t h = blockIdx.x;
   const float* ml = part_ml + h * NP * 2;
   float M = -INFINITY;
@@ -236,19 +238,23 @@ __global__ void paged_attn_reduce_kernel(const float* __restrict__ part_o, const
         den += wgt * l;
       }
     }
-    out[h * D + d] = f2bf(den > 0.f ? num / den : 0.f);
+    const float v = den > 0.f ? num / den : 0.f;
+    if (packed_mt > 0)
+      out[apk_off((int)(h / nh), (int)(h % nh) * D + d, packed_mt)] = f2bf(v);
+    else
+      out[h * D + d] = f2bf(v);
   }
 }
 
 template <int D, int NREP>
 static void launch_attn(const void* q, int64_t q_stride, const void* kc, const void* vc, const int32_t* bt,
                         int bt_stride, const int32_t* q_seq, const int32_t* q_ctx, void* out, float* ws_o,
-                        float* ws_ml, int T, int nkv, int page_log2, int PS, int NP, float scale_log2,
+                        float* ws_ml, int T, int nkv, int page_log2, int PS, int NP, float scale_log2, int packed_mt,
                         hipStream_t stream) {
   const size_t lds = (size_t)(NREP * PS + 8 * NREP + 4 * NREP * D) * sizeof(float);
   hipLaunchKernelGGL((paged_attn_kernel<D, NREP>), dim3(NP, nkv, T), dim3(256), lds, stream, (const bf16_t*)q,
                      q_stride, (const bf16_t*)kc, (const bf16_t*)vc, bt, bt_stride, q_seq, q_ctx, (bf16_t*)out,
-                     ws_o, ws_ml, nkv, page_log2, PS, NP, scale_log2);
+                     ws_o, ws_ml, nkv, page_log2, PS, NP, scale_log2, packed_mt);
 }
 
 }  // namespace mp
@@ -256,7 +262,7 @@ static void launch_attn(const void* q, int64_t q_stride, const void* kc, const v
 extern "C" int mp_paged_attention(const void* q, int64_t q_stride, const void* kc, const void* vc,
                                   const int32_t* bt, int bt_stride, const int32_t* q_seq, const int32_t* q_ctx,
                                   void* out, float* workspace, int T, int nh, int nkv, int D, int page_size,
-                                  int PS, int NP, float scale, hipStream_t stream) {
+                                  int PS, int NP, float scale, int packed_mt, hipStream_t stream) {
   using namespace mp;
   if (T == 0) return 0;
   if (nh % nkv != 0 || PS % 64 != 0 || PS > 2048 || NP < 1) return -1;
@@ -270,7 +276,7 @@ extern "C" int mp_paged_attention(const void* q, int64_t q_stride, const void* k
 #define MP_ATTN_CASE(DD, RR)                                                                                  \
   if (D == DD && nrep == RR) {                                                                                \
     launch_attn<DD, RR>(q, q_stride, kc, vc, bt, bt_stride, q_seq, q_ctx, out, ws_o, ws_ml, T, nkv, page_log2, \
-                        PS, NP, scale_log2, stream);                                                          \
+                        PS, NP, scale_log2, packed_mt, stream);                                               \
     goto launched;                                                                                            \
   }
   MP_ATTN_CASE(128, 1)
@@ -286,7 +292,7 @@ extern "C" int mp_paged_attention(const void* q, int64_t q_stride, const void* k
 launched:
   if (NP > 1) {
     hipLaunchKernelGGL(paged_attn_reduce_kernel, dim3(T * nh), dim3(D), 0, stream, ws_o, ws_ml, (bf16_t*)out, NP,
-                       D);
+                       D, nh, packed_mt);
   }
   return (int)hipGetLastError();
 }

@@ -11,7 +11,8 @@
 
 extern "C" {
 int mp_rmsnorm(const void* x, int64_t x_stride, void* res, int64_t res_stride, const void* w, void* y,
-               int64_t y_stride, const int32_t* rows, int nrows, int H, float eps, int mode, hipStream_t stream);
+               int64_t y_stride, const int32_t* rows, int nrows, int H, float eps, int mode, int packed_mt,
+               hipStream_t stream);
 int mp_rope_kv_write(void* qkv, int64_t qkv_stride, const int64_t* pos, const float* cos_t, const float* sin_t,
                      void* kc, void* vc, const int64_t* slots, int T, int nh, int nkv, int D, int page_size,
                      hipStream_t stream);
@@ -19,7 +20,8 @@ int mp_kv_write(const void* k, int64_t k_stride, const void* v, int64_t v_stride
                 const int64_t* slots, int T, int nkv, int D, int page_size, hipStream_t stream);
 int mp_paged_attention(const void* q, int64_t q_stride, const void* kc, const void* vc, const int32_t* bt,
                        int bt_stride, const int32_t* q_seq, const int32_t* q_ctx, void* out, float* workspace, int T,
-                       int nh, int nkv, int D, int page_size, int PS, int NP, float scale, hipStream_t stream);
+                       int nh, int nkv, int D, int page_size, int PS, int NP, float scale, int packed_mt,
+                       hipStream_t stream);
 int mp_embedding(const int64_t* ids, const void* table, void* out, int T, int H, int64_t vocab, hipStream_t stream);
 int mp_swiglu(const void* gu, void* out, int64_t T, int F, hipStream_t stream);
 int mp_add(const void* a, const void* b, void* y, int64_t n, hipStream_t stream);
@@ -28,7 +30,8 @@ int mp_sample(const void* logits, int64_t stride, int R, int V, const float* tem
               const int32_t* top_ks, const float* rep_pens, const int32_t* recent, int recent_stride,
               const int32_t* recent_len, const int64_t* seeds, float* ws, int64_t* out, hipStream_t stream);
 int mp_gemm_bf16(const void* x, int64_t x_stride, const void* w, void* y, int64_t y_stride, const void* res,
-                 int64_t res_stride, int M, int N, int K, int epilogue, hipStream_t stream);
+                 int64_t res_stride, int M, int N, int K, int epilogue, int flags, hipStream_t stream);
+int mp_pack_act(const void* x, int64_t xs, void* ap, int M, int K, hipStream_t stream);
 int mp_pack_weight(const void* w, void* wp, int N, int K, hipStream_t stream);
 }
 
@@ -54,16 +57,20 @@ inline void check_rows(const at::Tensor& t, const char* name) {
   MP_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, std::string(name) + " must be 16-B aligned");
 }
 
+inline int64_t packed_numel(int64_t M, int64_t K) { return ((M + 15) / 16) * 16 * K; }
+
 void rmsnorm(const at::Tensor& x, at::Tensor& residual, const at::Tensor& w, at::Tensor& y, double eps, int64_t mode,
-             const c10::optional<at::Tensor>& rows) {
+             const c10::optional<at::Tensor>& rows, int64_t packed) {
   check_bf16_cuda(x, "x");
   check_bf16_cuda(w, "w");
   check_bf16_cuda(y, "y");
   check_rows(x, "x");
-  check_rows(y, "y");
   const int H = x.size(1);
   MP_CHECK(w.numel() == H && w.is_contiguous(), "weight shape");
-  MP_CHECK(y.size(1) == H, "y cols");
+  if (!packed) {
+    check_rows(y, "y");
+    MP_CHECK(y.size(1) == H, "y cols");
+  }
   MP_CHECK(mode >= 0 && mode <= 2, "mode");
   if (mode != 0) {
     check_bf16_cuda(residual, "residual");
@@ -78,10 +85,16 @@ void rmsnorm(const at::Tensor& x, at::Tensor& residual, const at::Tensor& w, at:
     rp = rows->data_ptr<int32_t>();
     nrows = rows->numel();
   }
-  MP_CHECK(y.size(0) >= nrows, "y rows");
+  int pmt = 0;
+  if (packed) {
+    MP_CHECK(H % 32 == 0 && y.is_contiguous() && y.numel() >= packed_numel(nrows, H), "packed y too small");
+    pmt = (nrows + 15) / 16;
+  } else {
+    MP_CHECK(y.size(0) >= nrows, "y rows");
+  }
   check_launch(mp_rmsnorm(x.data_ptr(), x.stride(0), mode ? residual.data_ptr() : nullptr,
-                          mode ? residual.stride(0) : 0, w.data_ptr(), y.data_ptr(), y.stride(0), rp, nrows, H,
-                          (float)eps, (int)mode, cur_stream()),
+                          mode ? residual.stride(0) : 0, w.data_ptr(), y.data_ptr(), packed ? 0 : y.stride(0), rp,
+                          nrows, H, (float)eps, (int)mode, pmt, cur_stream()),
                "rmsnorm");
 }
 
@@ -126,7 +139,7 @@ void kv_write(const at::Tensor& k, const at::Tensor& v, at::Tensor& k_cache, at:
 void paged_attention(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
                      const at::Tensor& block_tables, const at::Tensor& q_seq, const at::Tensor& q_ctx,
                      at::Tensor& out, at::Tensor& workspace, int64_t nh, int64_t nkv, double scale, int64_t part_size,
-                     int64_t num_parts) {
+                     int64_t num_parts, int64_t packed) {
   check_bf16_cuda(q, "q");
   check_rows(q, "q");
   check_bf16_cuda(out, "out");
@@ -134,7 +147,11 @@ void paged_attention(const at::Tensor& q, const at::Tensor& k_cache, const at::T
   const int D = k_cache.size(3);
   const int T = q.size(0);
   MP_CHECK(q.size(1) >= nh * D, "q width");
-  MP_CHECK(out.numel() == (int64_t)T * nh * D, "out numel");
+  if (packed) {
+    MP_CHECK(out.numel() >= packed_numel(T, nh * D) && (nh * D) % 32 == 0, "packed out numel");
+  } else {
+    MP_CHECK(out.numel() == (int64_t)T * nh * D, "out numel");
+  }
   MP_CHECK(k_cache.size(1) == nkv && k_cache.is_contiguous() && v_cache.is_contiguous(), "cache");
   MP_CHECK(block_tables.scalar_type() == at::kInt && block_tables.dim() == 2 && block_tables.stride(1) == 1,
            "block_tables int32 [S, max_pages]");
@@ -145,7 +162,8 @@ void paged_attention(const at::Tensor& q, const at::Tensor& k_cache, const at::T
   check_launch(mp_paged_attention(q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
                                   block_tables.data_ptr<int32_t>(), block_tables.stride(0), q_seq.data_ptr<int32_t>(),
                                   q_ctx.data_ptr<int32_t>(), out.data_ptr(), workspace.data_ptr<float>(), T, nh, nkv,
-                                  D, k_cache.size(2), part_size, num_parts, (float)scale, cur_stream()),
+                                  D, k_cache.size(2), part_size, num_parts, (float)scale,
+                                  packed ? (int)((T + 15) / 16) : 0, cur_stream()),
                "paged_attention");
 }
 
@@ -211,19 +229,32 @@ void sample(const at::Tensor& logits, const at::Tensor& temps, const at::Tensor&
                "sample");
 }
 
+// flags bit 0: x is packed (holds ceil(M/16)*16*K elements, M given); bit 1: packed SwiGLU output
 void gemm(const at::Tensor& x, const at::Tensor& wp, at::Tensor& y, const c10::optional<at::Tensor>& residual,
-          int64_t epilogue) {
+          int64_t epilogue, int64_t M_, int64_t flags) {
   check_bf16_cuda(x, "x");
   check_bf16_cuda(wp, "wp");
   check_bf16_cuda(y, "y");
-  check_rows(x, "x");
-  check_rows(y, "y");
   MP_CHECK(wp.dim() == 4 && wp.size(2) == 64 && wp.size(3) == 8 && wp.is_contiguous(),
            "wp must be a packed weight [N/16, K/32, 64, 8] (ops.pack_weight)");
-  const int M = x.size(0), K = x.size(1), N = 16 * wp.size(0);
-  MP_CHECK(32 * wp.size(1) == K, "K mismatch between x and packed weight");
+  const int N = 16 * wp.size(0), K = 32 * wp.size(1);
+  const bool apk = flags & 1, opk = flags & 2;
+  int M;
+  if (apk) {
+    M = (int)M_;
+    MP_CHECK(x.is_contiguous() && x.numel() >= packed_numel(M, K), "packed x too small");
+  } else {
+    check_rows(x, "x");
+    M = x.size(0);
+    MP_CHECK(x.size(1) == K, "K mismatch between x and packed weight");
+  }
   const int ncols = epilogue == 1 ? N / 2 : N;
-  MP_CHECK(y.size(0) == M && y.size(1) == ncols, "y shape");
+  if (opk) {
+    MP_CHECK(epilogue == 1 && y.is_contiguous() && y.numel() >= packed_numel(M, ncols), "packed y");
+  } else {
+    check_rows(y, "y");
+    MP_CHECK(y.size(0) == M && y.size(1) == ncols, "y shape");
+  }
   const void* rp = nullptr;
   int64_t rs = 0;
   if (residual.has_value()) {
@@ -235,9 +266,16 @@ void gemm(const at::Tensor& x, const at::Tensor& wp, at::Tensor& y, const c10::o
   }
   MP_CHECK(epilogue != 2 || rp != nullptr, "residual epilogue needs residual");
   MP_CHECK(epilogue >= 0 && epilogue <= 2, "epilogue");
-  check_launch(mp_gemm_bf16(x.data_ptr(), x.stride(0), wp.data_ptr(), y.data_ptr(), y.stride(0), rp, rs, M, N, K,
-                            (int)epilogue, cur_stream()),
+  check_launch(mp_gemm_bf16(x.data_ptr(), apk ? 0 : x.stride(0), wp.data_ptr(), y.data_ptr(), opk ? 0 : y.stride(0),
+                            rp, rs, M, N, K, (int)epilogue, (int)flags, cur_stream()),
                "gemm");
+}
+
+void pack_act(const at::Tensor& x, at::Tensor& ap) {
+  check_bf16_cuda(x, "x");
+  check_rows(x, "x");
+  MP_CHECK(ap.is_contiguous() && ap.numel() >= packed_numel(x.size(0), x.size(1)), "ap too small");
+  check_launch(mp_pack_act(x.data_ptr(), x.stride(0), ap.data_ptr(), x.size(0), x.size(1), cur_stream()), "pack_act");
 }
 
 at::Tensor pack_weight(const at::Tensor& w) {
@@ -253,14 +291,17 @@ at::Tensor pack_weight(const at::Tensor& w) {
 }  // namespace
 
 TORCH_LIBRARY(mpamd, m) {
-  m.def("rmsnorm(Tensor x, Tensor(a!) residual, Tensor w, Tensor(b!) y, float eps, int mode, Tensor? rows) -> ()");
+  m.def(
+      "rmsnorm(Tensor x, Tensor(a!) residual, Tensor w, Tensor(b!) y, float eps, int mode, Tensor? rows, "
+      "int packed) -> ()");
   m.def(
       "rope_kv_write(Tensor(a!) qkv, Tensor positions, Tensor cos, Tensor sin, Tensor(b!) k_cache, "
       "Tensor(c!) v_cache, Tensor slots, int nh, int nkv) -> ()");
   m.def("kv_write(Tensor k, Tensor v, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor slots) -> ()");
   m.def(
       "paged_attention(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor q_seq, Tensor q_ctx, "
-      "Tensor(a!) out, Tensor(b!) workspace, int nh, int nkv, float scale, int part_size, int num_parts) -> ()");
+      "Tensor(a!) out, Tensor(b!) workspace, int nh, int nkv, float scale, int part_size, int num_parts, "
+      "int packed) -> ()");
   m.def("embedding(Tensor ids, Tensor table, Tensor(a!) out) -> ()");
   m.def("swiglu(Tensor gu, Tensor(a!) out) -> ()");
   m.def("add(Tensor a, Tensor b, Tensor(a!) y) -> ()");
@@ -268,7 +309,8 @@ TORCH_LIBRARY(mpamd, m) {
   m.def(
       "sample(Tensor logits, Tensor temps, Tensor top_ps, Tensor top_ks, Tensor rep_pens, Tensor recent, "
       "Tensor recent_len, Tensor seeds, Tensor(a!) workspace, Tensor(b!) out) -> ()");
-  m.def("gemm(Tensor x, Tensor wp, Tensor(a!) y, Tensor? residual, int epilogue) -> ()");
+  m.def("gemm(Tensor x, Tensor wp, Tensor(a!) y, Tensor? residual, int epilogue, int M, int flags) -> ()");
+  m.def("pack_act(Tensor x, Tensor(a!) ap) -> ()");
   m.def("pack_weight(Tensor w) -> Tensor");
 }
 
@@ -284,4 +326,5 @@ TORCH_LIBRARY_IMPL(mpamd, CUDA, m) {
   m.impl("sample", &sample);
   m.impl("gemm", &gemm);
   m.impl("pack_weight", &pack_weight);
+  m.impl("pack_act", &pack_act);
 }

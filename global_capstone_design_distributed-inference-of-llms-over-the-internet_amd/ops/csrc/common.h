@@ -70,4 +70,12 @@ __device__ __forceinline__ float block_max(float v, float* red) {
   return t;
 }
 
+// Packed-activation ("fragment-native") layout shared by the decode kernels:
+//   Ap[K/32][MT][64][8], MT = ceil(M/16);  lane = 16 * ((col >> 3) & 3) + (row & 15)
+// i.e. exactly the A operand of v_mfma_f32_16x16x32_bf16 for k-slice col/32 and m-tile row/16,
+// so the decode GEMM reads every A fragment as one contiguous 1 KiB.
+__device__ __forceinline__ int64_t apk_off(int row, int col, int MT) {
+  return ((((int64_t)(col >> 5) * MT + (row >> 4)) * 64 + ((col >> 3) & 3) * 16 + (row & 15)) << 3) + (col & 7);
+}
+
 }  // namespace mp

@@ -13,8 +13,10 @@
 //     so the B operand of every v_mfma_f32_16x16x32_bf16 is ONE contiguous 1 KiB read
 //     (64 lanes x 16 B), and a wave walking K streams a contiguous region: perfectly
 //     coalesced, non-temporal (read once), straight to VGPRs (guide: "GEMV / M <= 16" row).
-//   * x (A operand) is read row-major from L2: lane (r, q) reads 16 B of row r at k offset
-//     8q, i.e. 16 rows x 64 contiguous bytes per wave-instruction.
+//   * x (A operand) is either row-major (lane (r, q) reads 16 B of row r at k offset 8q:
+//     16 rows x 64 B per wave-instruction, TA-heavy) or - on the decode path - PACKED in the
+//     same fragment order by its producer kernel (RMSNorm, attention, the SwiGLU epilogue):
+//       Ap[k/32][m/16][lane][8]  -> every A fragment is one contiguous 1 KiB read too.
 //   * one workgroup = 8 waves over NT column tiles (16 cols each) x all of K; the waves take
 //     interleaved groups of U k-slices and their partial tiles are combined through LDS
 //     (no atomics, no second pass); B is double-buffered in registers across groups.
@@ -34,7 +36,7 @@ __device__ __forceinline__ f32x4 mfma16(const u16x8& a, const u16x8& b, const f3
 
 constexpr int GU_MAX = 4;  // k-slices (of 32) per wave group (x 16 B per lane per column tile)
 
-template <int MT, int NT, int EPI>
+template <int MT, int NT, int EPI, bool APK, bool OPK>
 __global__ __launch_bounds__(512) void gemm_packed_kernel(const bf16_t* __restrict__ x, int64_t x_stride,
                                                           const bf16_t* __restrict__ wp, bf16_t* __restrict__ y,
                                                           int64_t y_stride, const bf16_t* __restrict__ res,
@@ -57,8 +59,12 @@ __global__ __launch_bounds__(512) void gemm_packed_kernel(const bf16_t* __restri
   const bf16_t* xrow[MT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
-    const int r = min(mt * 16 + c, M - 1);
-    xrow[mt] = x + (int64_t)r * x_stride + 8 * q;
+    if constexpr (APK) {
+      xrow[mt] = x + ((int64_t)mt * 64 + lane) * 8;  // + slice * MT * 512
+    } else {
+      const int r = min(mt * 16 + c, M - 1);
+      xrow[mt] = x + (int64_t)r * x_stride + 8 * q;
+    }
   }
 
   f32x4 acc[MT][NT];
@@ -76,7 +82,8 @@ __global__ __launch_bounds__(512) void gemm_packed_kernel(const bf16_t* __restri
       __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(wbase[t] + (int64_t)((grp) * GU + u) * 512));
 #define MP_LOAD_A(grp)                                                                                        \
   _Pragma("unroll") for (int mt = 0; mt < MT; ++mt) _Pragma("unroll") for (int u = 0; u < GU; ++u) a[mt][u] =  \
-      *reinterpret_cast<const u16x8*>(xrow[mt] + (grp) * GU * 32 + 32 * u);
+      *reinterpret_cast<const u16x8*>(xrow[mt] + (APK ? (int64_t)((grp) * GU + u) * MT * 512                  \
+                                                      : (int64_t)((grp) * GU * 32 + 32 * u)));
 #define MP_MMA(bb)                                                                                            \
   _Pragma("unroll") for (int mt = 0; mt < MT; ++mt) _Pragma("unroll") for (int u = 0; u < GU; ++u)            \
       _Pragma("unroll") for (int t = 0; t < NT; ++t) acc[mt][t] = mfma16(a[mt][u], bb[t][u], acc[mt][t]);
@@ -132,7 +139,8 @@ __global__ __launch_bounds__(512) void gemm_packed_kernel(const bf16_t* __restri
         const int ncol = ((nt0 + t) >> 1) * 16 + c;
         const float gg = round_bf(s);
         const float a = round_bf(gg / (1.f + __expf(-gg)));
-        y[(int64_t)row * y_stride + ncol] = f2bf(a * round_bf(up));
+        const int64_t yo = OPK ? apk_off(row, ncol, MT) : (int64_t)row * y_stride + ncol;
+        y[yo] = f2bf(a * round_bf(up));
       }
     } else {
       if (row < M) {
@@ -147,23 +155,27 @@ __global__ __launch_bounds__(512) void gemm_packed_kernel(const bf16_t* __restri
 
 template <int MT>
 static int launch_gemm(const void* x, int64_t xs, const void* w, void* y, int64_t ys, const void* res, int64_t rs,
-                       int M, int N, int K, int epi, hipStream_t stream) {
+                       int M, int N, int K, int epi, int flags, hipStream_t stream) {
   const int ntiles = N / 16;
   // two column tiles per wave when there are enough workgroups to fill the 256 CUs
   const bool two = epi == 1 || (ntiles % 2 == 0 && ntiles / 2 >= 256);
-#define MP_LAUNCH(NT_, EPI_)                                                                                   \
-  hipLaunchKernelGGL((gemm_packed_kernel<MT, NT_, EPI_>), dim3(ntiles / NT_), dim3(512), 0, stream,             \
+  const bool apk = flags & 1, opk = flags & 2;
+#define MP_LAUNCH(NT_, EPI_, APK_, OPK_)                                                                       \
+  hipLaunchKernelGGL((gemm_packed_kernel<MT, NT_, EPI_, APK_, OPK_>), dim3(ntiles / NT_), dim3(512), 0, stream, \
                      (const bf16_t*)x, xs, (const bf16_t*)w, (bf16_t*)y, ys, (const bf16_t*)res, rs, M, N, K)
+#define MP_APK(NT_, EPI_, OPK_) \
+  if (apk) MP_LAUNCH(NT_, EPI_, true, OPK_); else MP_LAUNCH(NT_, EPI_, false, OPK_);
   if (epi == 1) {
     if (ntiles % 2) return -2;
-    MP_LAUNCH(2, 1);
+    if (opk) { MP_APK(2, 1, true) } else { MP_APK(2, 1, false) }
+  } else if (opk) {
+    return -3;  // packed output only for the SwiGLU epilogue (it feeds the down projection)
   } else if (epi == 2) {
-    if (two) MP_LAUNCH(2, 2);
-    else MP_LAUNCH(1, 2);
+    if (two) { MP_APK(2, 2, false) } else { MP_APK(1, 2, false) }
   } else {
-    if (two) MP_LAUNCH(2, 0);
-    else MP_LAUNCH(1, 0);
+    if (two) { MP_APK(2, 0, false) } else { MP_APK(1, 0, false) }
   }
+#undef MP_APK
 #undef MP_LAUNCH
   return 0;
 }
@@ -186,18 +198,42 @@ __global__ __launch_bounds__(256) void pack_weight_kernel(const bf16_t* __restri
 
 }  // namespace mp
 
+// flags: bit 0 = x is packed (Ap[K/32][ceil(M/16)][64][8]); bit 1 = SwiGLU output packed.
 extern "C" int mp_gemm_bf16(const void* x, int64_t x_stride, const void* w, void* y, int64_t y_stride,
-                            const void* res, int64_t res_stride, int M, int N, int K, int epilogue,
+                            const void* res, int64_t res_stride, int M, int N, int K, int epilogue, int flags,
                             hipStream_t stream) {
   using namespace mp;
   if (M == 0) return 0;
-  if (M > 64 || K % (32 * GU_MAX) || N % 16 || x_stride % 8) return -1;
+  if (M > 64 || K % (32 * GU_MAX) || N % 16 || ((flags & 1) == 0 && x_stride % 8)) return -1;
   int rc;
-  if (M <= 16) rc = launch_gemm<1>(x, x_stride, w, y, y_stride, res, res_stride, M, N, K, epilogue, stream);
-  else if (M <= 32) rc = launch_gemm<2>(x, x_stride, w, y, y_stride, res, res_stride, M, N, K, epilogue, stream);
-  else if (M <= 48) rc = launch_gemm<3>(x, x_stride, w, y, y_stride, res, res_stride, M, N, K, epilogue, stream);
-  else rc = launch_gemm<4>(x, x_stride, w, y, y_stride, res, res_stride, M, N, K, epilogue, stream);
+  if (M <= 16) rc = launch_gemm<1>(x, x_stride, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, stream);
+  else if (M <= 32) rc = launch_gemm<2>(x, x_stride, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, stream);
+  else if (M <= 48) rc = launch_gemm<3>(x, x_stride, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, stream);
+  else rc = launch_gemm<4>(x, x_stride, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, stream);
   if (rc) return rc;
+  return (int)hipGetLastError();
+}
+
+namespace mp {
+// Pack row-major x[M, K] into Ap[K/32][ceil(M/16)][64][8] (rows >= M left untouched).
+__global__ __launch_bounds__(256) void pack_act_kernel(const bf16_t* __restrict__ x, int64_t xs, bf16_t* __restrict__ ap,
+                                                       int M, int K, int MT) {
+  const int nch = K >> 3;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < M * nch; i += gridDim.x * blockDim.x) {
+    const int row = i / nch, col = (i - row * nch) * 8;
+    *reinterpret_cast<u16x8*>(ap + apk_off(row, col, MT)) = *reinterpret_cast<const u16x8*>(x + row * xs + col);
+  }
+}
+}  // namespace mp
+
+extern "C" int mp_pack_act(const void* x, int64_t xs, void* ap, int M, int K, hipStream_t stream) {
+  using namespace mp;
+  if (K % 32 || xs % 8) return -1;
+  if (M == 0) return 0;
+  const int MT = (M + 15) / 16;
+  const int n = M * (K / 8);
+  hipLaunchKernelGGL(pack_act_kernel, dim3(min((n + 255) / 256, 4096)), dim3(256), 0, stream, (const bf16_t*)x, xs,
+                     (bf16_t*)ap, M, K, MT);
   return (int)hipGetLastError();
 }
 

@@ -7,6 +7,7 @@
 //   mode 0:  y = rmsnorm(x) * w
 //   mode 1:  residual = bf16(residual + x);  y = rmsnorm(residual) * w   (fused add)
 //   mode 2:  residual = x;                   y = rmsnorm(x) * w          (stage entry)
+// packed_mt > 0 writes y in the packed decode-GEMM activation layout (common.h apk_off).
 //
 // `rows` (optional) gathers input rows (e.g. the last token of each prompt for
 // the final norm before lm_head), so the output has one row per index.
@@ -20,7 +21,7 @@ template <int MAXC>
 __global__ __launch_bounds__(256) void rmsnorm_kernel(
     const bf16_t* __restrict__ x, int64_t x_stride, bf16_t* __restrict__ res, int64_t res_stride,
     const bf16_t* __restrict__ w, bf16_t* __restrict__ y, int64_t y_stride,
-    const int32_t* __restrict__ rows, int H, float eps, int mode) {
+    const int32_t* __restrict__ rows, int H, float eps, int mode, int packed_mt) {
   __shared__ float red[16];
   const int orow = blockIdx.x;
   const int irow = rows ? rows[orow] : orow;
@@ -61,7 +62,10 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(
       u16x8 o;
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = f2bf(round_bf(bf2f(v[k][j]) * r) * bf2f(wv[j]));
-      *reinterpret_cast<u16x8*>(yr + c * 8) = o;
+      if (packed_mt > 0)
+        *reinterpret_cast<u16x8*>(y + apk_off(orow, c * 8, packed_mt)) = o;
+      else
+        *reinterpret_cast<u16x8*>(yr + c * 8) = o;
     }
   }
 }
@@ -70,7 +74,7 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(
 
 extern "C" int mp_rmsnorm(const void* x, int64_t x_stride, void* res, int64_t res_stride, const void* w,
                           void* y, int64_t y_stride, const int32_t* rows, int nrows, int H, float eps,
-                          int mode, hipStream_t stream) {
+                          int mode, int packed_mt, hipStream_t stream) {
   using namespace mp;
   if (H % 8 != 0 || H > 8 * 256 * 8) return -1;
   if (nrows == 0) return 0;
@@ -78,7 +82,7 @@ extern "C" int mp_rmsnorm(const void* x, int64_t x_stride, void* res, int64_t re
   dim3 grid(nrows), block(256);
   auto args = [&](auto kern) {
     hipLaunchKernelGGL(kern, grid, block, 0, stream, (const bf16_t*)x, x_stride, (bf16_t*)res, res_stride,
-                       (const bf16_t*)w, (bf16_t*)y, y_stride, rows, H, eps, mode);
+                       (const bf16_t*)w, (bf16_t*)y, y_stride, rows, H, eps, mode, packed_mt);
   };
   if (nch <= 256) args(rmsnorm_kernel<1>);
   else if (nch <= 512) args(rmsnorm_kernel<2>);

@@ -17,6 +17,26 @@ import torch
 GU_BLOCK = 16  # gate/up weights are interleaved in blocks of 16 rows: [g16 u16 g16 u16 ...]
 
 
+def pack_act(x, out=None):
+    """Row-major [M, K] -> flat packed decode activation Ap[K/32][ceil(M/16)][64][8] (see csrc/common.h)."""
+    M, K = x.shape
+    MT = (M + 15) // 16
+    xp = torch.zeros(MT * 16, K, dtype=x.dtype, device=x.device)
+    xp[:M] = x
+    # [MT, 16(c), K/32, 4(q), 8(j)] -> [K/32, MT, 4(q), 16(c), 8(j)]
+    y = xp.view(MT, 16, K // 32, 4, 8).permute(2, 0, 3, 1, 4).reshape(-1)
+    if out is not None:
+        out[: y.numel()].copy_(y)
+        return out
+    return y
+
+
+def unpack_act(ap, M, K):
+    MT = (M + 15) // 16
+    x = ap[: MT * 16 * K].view(K // 32, MT, 4, 16, 8).permute(1, 3, 0, 2, 4).reshape(MT * 16, K)
+    return x[:M]
+
+
 def rmsnorm(x, w, eps, out=None, residual=None, mode=0, rows=None):
     dt = x.dtype
     if mode == 1:

@@ -243,37 +243,70 @@ class StageExecutor:
         ps, np_ = attn_part
         ws = e("attn_ws", (max(1, T * self.nh * np_ * (self.D + 2)),), torch.float32)
         res = e("res", (T, H))
-        xn = e("xn", (T, H))
         qkv = e("qkv", (T, cfg.q_dim + 2 * cfg.kv_dim))
-        attn = e("attn", (T, cfg.q_dim))
         o = e("o", (T, H))
-        act = e("act", (T, cfg.intermediate_size))
         mlp = e("mlp", (T, H))
-        for li, L in enumerate(w.layers):
-            if li == 0:
-                ops.rmsnorm(h, L.input_norm, eps, out=xn, residual=res, mode=2)
-            else:
-                ops.rmsnorm(mlp, L.input_norm, eps, out=xn, residual=res, mode=1)
-            ops.linear(xn, L.qkv, out=qkv, wp=L.qkv_p)
-            kc, vc = self.cache.layer(li)
-            ops.rope_kv_write(qkv, positions, self.cos, self.sin, kc, vc, slots, self.nh, self.nkv)
-            ops.paged_attention(qkv, kc, vc, table, q_seq, q_ctx, self.nh, self.nkv, self.scale, out=attn,
-                                workspace=ws, part_size=ps, num_parts=np_)
-            ops.linear(attn, L.o, out=o, wp=L.o_p)
-            ops.rmsnorm(o, L.post_norm, eps, out=xn, residual=res, mode=1)
-            ops.linear(xn, L.gate_up, out=act, epilogue=1, wp=L.gate_up_p)
-            ops.linear(act, L.down, out=mlp, wp=L.down_p)
+        if self._packed_ok(T):
+            # decode path: activations feeding a GEMM stay in the packed MFMA-fragment layout
+            pk = ops.packed_numel
+            xn = e("xn_p", (pk(T, H),))
+            attn = e("attn_p", (pk(T, cfg.q_dim),))
+            act = e("act_p", (pk(T, cfg.intermediate_size),))
+            for li, L in enumerate(w.layers):
+                if li == 0:
+                    ops.rmsnorm(h, L.input_norm, eps, out=xn, residual=res, mode=2, packed=True)
+                else:
+                    ops.rmsnorm(mlp, L.input_norm, eps, out=xn, residual=res, mode=1, packed=True)
+                ops.linear(xn, L.qkv, out=qkv, wp=L.qkv_p, a_rows=T)
+                kc, vc = self.cache.layer(li)
+                ops.rope_kv_write(qkv, positions, self.cos, self.sin, kc, vc, slots, self.nh, self.nkv)
+                ops.paged_attention(qkv, kc, vc, table, q_seq, q_ctx, self.nh, self.nkv, self.scale, out=attn,
+                                    workspace=ws, part_size=ps, num_parts=np_, packed=True)
+                ops.linear(attn, L.o, out=o, wp=L.o_p, a_rows=T)
+                ops.rmsnorm(o, L.post_norm, eps, out=xn, residual=res, mode=1, packed=True)
+                ops.linear(xn, L.gate_up, out=act, epilogue=1, wp=L.gate_up_p, a_rows=T, out_packed=True)
+                ops.linear(act, L.down, out=mlp, wp=L.down_p, a_rows=T)
+        else:
+            xn = e("xn", (T, H))
+            attn = e("attn", (T, cfg.q_dim))
+            act = e("act", (T, cfg.intermediate_size))
+            for li, L in enumerate(w.layers):
+                if li == 0:
+                    ops.rmsnorm(h, L.input_norm, eps, out=xn, residual=res, mode=2)
+                else:
+                    ops.rmsnorm(mlp, L.input_norm, eps, out=xn, residual=res, mode=1)
+                ops.linear(xn, L.qkv, out=qkv, wp=L.qkv_p)
+                kc, vc = self.cache.layer(li)
+                ops.rope_kv_write(qkv, positions, self.cos, self.sin, kc, vc, slots, self.nh, self.nkv)
+                ops.paged_attention(qkv, kc, vc, table, q_seq, q_ctx, self.nh, self.nkv, self.scale, out=attn,
+                                    workspace=ws, part_size=ps, num_parts=np_)
+                ops.linear(attn, L.o, out=o, wp=L.o_p)
+                ops.rmsnorm(o, L.post_norm, eps, out=xn, residual=res, mode=1)
+                ops.linear(xn, L.gate_up, out=act, epilogue=1, wp=L.gate_up_p)
+                ops.linear(act, L.down, out=mlp, wp=L.down_p)
         hout = ops.add(res, mlp, out=e("hout", (T, H)))
         if not self.is_last:
             return hout
         S = last_rows.numel()
-        fn = ops.rmsnorm(hout, w.final_norm, eps, out=e("fn", (S, H)), rows=last_rows)
         V = cfg.vocab_size
-        Vp = 16 * w.lm_head_p.shape[0] if w.lm_head_p is not None else V
-        logits = ops.linear(fn, w.lm_head if Vp == V else None, out=e("logits", (S, Vp)), wp=w.lm_head_p) \
-            if (Vp == V or ops.native_gemm_ok(S, Vp, H)) else \
-            ops.linear(fn, w.lm_head, out=e("logits", (S, V)))
-        return logits[:, :V]
+        if w.lm_head_p is not None and self._packed_ok(S):
+            fn = ops.rmsnorm(hout, w.final_norm, eps, out=e("fn_p", (ops.packed_numel(S, H),)), rows=last_rows,
+                             packed=True)
+            Vp = 16 * w.lm_head_p.shape[0]
+            logits = ops.linear(fn, None, out=e("logits", (S, Vp)), wp=w.lm_head_p, a_rows=S)
+            return logits[:, :V]
+        fn = ops.rmsnorm(hout, w.final_norm, eps, out=e("fn", (S, H)), rows=last_rows)
+        return ops.linear(fn, w.lm_head, out=e("logits", (S, V)))
+
+    def _packed_ok(self, M: int) -> bool:
+        """Packed-activation decode path: GPU, native GEMM allowed, all projections packed."""
+        if self.device.type != "cuda" or ops.gemm_policy() == "hipblaslt" or not 0 < M <= 64:
+            return False
+        if getattr(self, "_packed_ready", None) is None:
+            cfg = self.cfg
+            dims_ok = all(d % 128 == 0 for d in (cfg.hidden_size, cfg.q_dim, cfg.intermediate_size))
+            self._packed_ready = dims_ok and all(getattr(L, "qkv_p", None) is not None for L in self.w.layers)
+        return self._packed_ready
 
     # ------------------------------------------------------------------ gpt2 (plumbing family)
     def _forward_gpt2(self, plan: Plan, x):

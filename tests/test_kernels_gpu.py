@@ -239,3 +239,49 @@ def test_sampler_distribution_matches_reference():
     freq = torch.bincount(out, minlength=V).float() / R
     assert set(out.unique().tolist()) <= set(torch.nonzero(f).flatten().tolist())
     assert (freq - f).abs().max().item() < 0.04
+
+
+@pytest.mark.parametrize("M", [1, 13, 16, 40, 64])
+def test_packed_activation_paths(M):
+    """Producers that emit the packed decode-GEMM layout agree with pack(row-major)."""
+    H, K2 = 4096, 11008
+    x = bf(torch.randn(M, H, device=DEV))
+    assert torch.equal(ops.pack_act(x)[: ops.packed_numel(M, H)].view(-1)[: M * 0 + 1].cpu(),
+                       ref.pack_act(x.cpu())[:1])
+    ap = torch.zeros(ops.packed_numel(M, H), dtype=torch.bfloat16, device=DEV)
+    ops.pack_act(x, out=ap)
+    assert torch.equal(ref.unpack_act(ap.cpu(), M, H), x.cpu())
+    w = bf(torch.rand(H, device=DEV) + 0.5)
+    res = bf(torch.randn(M, H, device=DEV))
+    r1, r2 = res.clone(), res.clone()
+    yp = ops.rmsnorm(x, w, 1e-5, residual=r1, mode=1, packed=True)
+    y = ops.rmsnorm(x, w, 1e-5, residual=r2, mode=1)
+    assert torch.equal(ref.unpack_act(yp.cpu(), M, H), y.cpu())
+    # GEMM on packed A == GEMM on row-major A
+    wt = bf(torch.randn(12288, H, device=DEV) * 0.02)
+    wp = ops.pack_weight(wt)
+    g1 = ops.linear(y, None, wp=wp, policy="native")
+    g2 = ops.linear(yp, None, wp=wp, a_rows=M)
+    assert torch.equal(g1, g2)
+    # SwiGLU epilogue emitting packed output feeds the down projection
+    from src.models.weights import interleave_gate_up
+
+    gu = interleave_gate_up(bf(torch.randn(K2, H, device=DEV) * 0.02), bf(torch.randn(K2, H, device=DEV) * 0.02))
+    gup = ops.pack_weight(gu)
+    a_row = ops.linear(yp, None, wp=gup, epilogue=1, a_rows=M)
+    a_pk = ops.linear(yp, None, wp=gup, epilogue=1, a_rows=M, out_packed=True)
+    assert torch.equal(ref.unpack_act(a_pk.cpu(), M, K2), a_row.cpu())
+    wd = bf(torch.randn(H, K2, device=DEV) * 0.02)
+    d1 = ops.linear(a_row, None, wp=ops.pack_weight(wd), policy="native")
+    d2 = ops.linear(a_pk, None, wp=ops.pack_weight(wd), a_rows=M)
+    assert torch.equal(d1, d2)
+
+
+def test_paged_attention_packed_output():
+    nh, nkv, D = 32, 32, 128
+    q, kc, vc, bt, q_seq, q_ctx = _attn_case(nh, nkv, D, [100, 7, 600])
+    for parts in [(64, 10), (1024, 1)]:
+        o = ops.paged_attention(q, kc, vc, bt, q_seq, q_ctx, nh, nkv, 0.09, part_size=parts[0], num_parts=parts[1])
+        op = ops.paged_attention(q, kc, vc, bt, q_seq, q_ctx, nh, nkv, 0.09, part_size=parts[0], num_parts=parts[1],
+                                 packed=True)
+        assert torch.equal(ref.unpack_act(op.cpu(), 3, nh * D), o.cpu())

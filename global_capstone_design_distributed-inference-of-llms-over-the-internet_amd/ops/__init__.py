@@ -259,10 +259,12 @@ def linear(x, w, out=None, epilogue=0, residual=None, policy=None, wp=None, a_ro
         a_rows is not None or (x.stride(0) % 8 == 0 and x.stride(1) == 1))
     if ok and (policy in ("auto", "native") or a_rows is not None or out_packed):
         ncols = N // 2 if epilogue == 1 else N
+        if a_rows is None:  # row-major caller: pack x into the fragment layout first
+            x = pack_act(x)
         if out is None:
             out = (torch.empty(packed_numel(M, ncols), dtype=x.dtype, device=x.device) if out_packed
                    else torch.empty(M, ncols, dtype=x.dtype, device=x.device))
-        flags = (1 if a_rows is not None else 0) | (2 if out_packed else 0)
+        flags = 1 | (2 if out_packed else 0)
         torch.ops.mpamd.gemm(x, wp, out, residual, int(epilogue), M, flags)
         return out
     if a_rows is not None or out_packed:

@@ -44,7 +44,9 @@ __global__ __launch_bounds__(512) void gemm_packed_kernel(const bf16_t* __restri
   // fewer k-slices per group for the widest tiles keeps A + 2 x B + acc inside 256 VGPRs
   constexpr int GU = (MT * NT >= 6) ? 2 : 4;
   __shared__ __attribute__((aligned(16))) float red[8][MT * NT * 4][64];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  // wave id made provably uniform (readfirstlane): the group loop then compiles to scalar
+  // branches instead of an exec-masked divergent loop around the MFMAs
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int c = lane & 15, q = lane >> 4;
   const int nks = K >> 5;
   const int ngroups = nks / GU;
@@ -163,8 +165,11 @@ static int launch_gemm(const void* x, int64_t xs, const void* w, void* y, int64_
 #define MP_LAUNCH(NT_, EPI_, APK_, OPK_)                                                                       \
   hipLaunchKernelGGL((gemm_packed_kernel<MT, NT_, EPI_, APK_, OPK_>), dim3(ntiles / NT_), dim3(512), 0, stream, \
                      (const bf16_t*)x, xs, (const bf16_t*)w, (bf16_t*)y, ys, (const bf16_t*)res, rs, M, N, K)
-#define MP_APK(NT_, EPI_, OPK_) \
-  if (apk) MP_LAUNCH(NT_, EPI_, true, OPK_); else MP_LAUNCH(NT_, EPI_, false, OPK_);
+  // Only the packed-activation form is instantiated: row-major callers pack x first
+  // (mp_pack_act).  The row-major-A variant miscompiled at MT=1/NT=1 (ROCm 7.2, wrong
+  // results with several k-groups per wave) and loses to the packed form anyway.
+  if (!apk) return -4;
+#define MP_APK(NT_, EPI_, OPK_) MP_LAUNCH(NT_, EPI_, true, OPK_);
   if (epi == 1) {
     if (ntiles % 2) return -2;
     if (opk) { MP_APK(2, 1, true) } else { MP_APK(2, 1, false) }

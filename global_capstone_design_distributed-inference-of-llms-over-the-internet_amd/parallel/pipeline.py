@@ -63,7 +63,8 @@ class PipelineEngine:
         self._pending_recv = None  # (tag, work, buffer)
         self.timing = timing
         self._events: List = []
-        self.tokens_out: List[List[torch.Tensor]] = [[] for _ in range(n_micro)]  # last stage (world==1) history
+        self.record = False  # rank 0: keep every received token (tests / generation API)
+        self.tokens_out: List[List[torch.Tensor]] = [[] for _ in range(n_micro)]
         if self.last:
             dev = self.dev
             B = batch
@@ -148,6 +149,8 @@ class PipelineEngine:
                     w, buf = self._tok_recv[m]
                     w.wait()
                     x = buf
+                    if self.record:
+                        self.tokens_out[m].append(buf.clone())
             else:
                 if self._pending_recv is None:
                     self._pending_recv = self._post_recv(self._input_shape(n_tokens), dt, self.rank - 1)
@@ -163,6 +166,8 @@ class PipelineEngine:
                 tok = self._sample(mb, out)
                 if self.world == 1:
                     mb.tokens = tok
+                    if self.record:
+                        self.tokens_out[m].append(tok.clone())
                 else:
                     self._send(tok, 0)
             else:
@@ -184,10 +189,23 @@ class PipelineEngine:
         self._flush_sends()
         if self.first and self.world > 1:
             # tokens of the final round are still in flight; consume them
-            for w, buf in getattr(self, "_tok_recv", []):
+            for m, (w, buf) in enumerate(getattr(self, "_tok_recv", [])):
                 w.wait()
+                if self.record:
+                    self.tokens_out[m].append(buf.clone())
             self._tok_recv = []
             self._tok_recv_consumed = True
+
+    def generated(self) -> List[List[List[int]]]:
+        """rank 0: tokens[m][b] generated so far (needs ``record=True`` before the run)."""
+        out = []
+        for m in range(self.M):
+            if not self.tokens_out[m]:
+                out.append([[] for _ in range(self.B)])
+                continue
+            t = torch.stack(self.tokens_out[m], 1).cpu()
+            out.append(t.tolist())
+        return out
 
     def stage_ms(self) -> Optional[float]:
         if not self._events:

@@ -1,0 +1,225 @@
+"""Stage server RPC handler (``StageConnectionHandler``).
+
+Reference: src/rpc_handler.py:43-464 - a hivemind ConnectionHandler whose
+``rpc_forward`` / ``rpc_forward_stream`` handlers run the stage on one session's hidden
+states, keep that session's KV tuple in a dict forever, and (final stage) sample the next
+token server-side.  This implementation keeps the handler names, request metadata and
+reply format, and changes the engine underneath:
+
+* the stage is a ``StageExecutor`` (HIP kernels, paged KV in HBM, hipGraph decode);
+* **continuous batching**: requests from different sessions that arrive together are
+  executed as ONE ragged step (``batch_window_ms``), on a single GPU worker thread so the
+  asyncio loop never blocks on the device;
+* KV sessions have ``max_length`` enforced and expire after a TTL (no leak);
+* position bookkeeping is idempotent: a decode step carries ``cur_len``, so a retried or
+  replayed step overwrites its own slot instead of appending twice (the reference's replay
+  duplicates the current step);
+* extra handlers beyond the reference: ``rpc_info`` (free cache tokens, like upstream
+  Petals' ``rpc_info``), ``rpc_close_session`` and ``rpc_echo`` (link probing).
+
+Metadata keys: session_id, seq_len, cur_len, is_prefill, is_replay, max_length, temperature,
+top_p, top_k, repetition_penalty (default 1.5), generated_tokens.  Final-stage replies carry
+``token_id`` (and an int64 [[token]] tensor); others return hidden [1, T, H].
+"""
+from __future__ import annotations
+
+import asyncio
+import concurrent.futures
+import dataclasses
+import logging
+import time
+from typing import Dict, List, Optional
+
+import torch
+
+from .comm.rpc import RpcServer
+from .comm.wire import Message
+from .runtime.kv_cache import AllocationFailed
+from .runtime.sampler import BatchSampler, SamplingParams, session_seed
+
+logger = logging.getLogger(__name__)
+
+HANDLER_PREFIX = "StageConnectionHandler."
+
+
+@dataclasses.dataclass
+class _Req:
+    sid: str
+    x: torch.Tensor          # [T, H] hidden (or [T] ids for a first stage)
+    start: int               # first position of these tokens
+    reset: bool
+    params: SamplingParams
+    generated: List[int]
+    max_length: Optional[int]
+    fut: asyncio.Future
+    t0: float
+
+
+class StageConnectionHandler:
+    def __init__(self, dht, stage_model, device=None, request_timeout: float = 30.0, final_stage: bool = False,
+                 batch_window_ms: float = 0.5, max_batch_tokens: Optional[int] = None, seed: int = 0):
+        self.dht = dht
+        self.executor = stage_model
+        self.device = torch.device(device) if device is not None else stage_model.device
+        self.request_timeout = request_timeout
+        self.final_stage = final_stage
+        self.batch_window = batch_window_ms / 1000.0
+        self.max_batch_tokens = max_batch_tokens or stage_model.max_tokens
+        self.seed = seed
+        self._default = SamplingParams(0.8, 0.9, 0, 1.5)  # reference handler defaults (:71-73, :164)
+        self._pending: List[_Req] = []
+        self._draining = False
+        self._worker = concurrent.futures.ThreadPoolExecutor(1, thread_name_prefix="stage-gpu")
+        self._sampler = BatchSampler(self.device) if final_stage else None
+        self.stats = {"requests": 0, "batches": 0, "tokens": 0}
+
+    # ------------------------------------------------------------------ registration
+    def add_p2p_handlers(self, server: RpcServer) -> None:
+        server.add_handler(HANDLER_PREFIX + "rpc_forward", self.rpc_forward)
+        server.add_handler(HANDLER_PREFIX + "rpc_forward_stream", self.rpc_forward_stream)
+        server.add_handler(HANDLER_PREFIX + "rpc_info", self.rpc_info)
+        server.add_handler(HANDLER_PREFIX + "rpc_close_session", self.rpc_close_session)
+        server.add_handler(HANDLER_PREFIX + "rpc_echo", self.rpc_echo)
+
+    # ------------------------------------------------------------------ handlers
+    async def rpc_forward(self, msg: Message) -> Message:
+        return await asyncio.wait_for(self._submit(msg), self.request_timeout)
+
+    async def rpc_forward_stream(self, msg: Message) -> Message:
+        return await asyncio.wait_for(self._submit(msg), self.request_timeout)
+
+    async def rpc_info(self, msg: Message) -> Message:
+        ex = self.executor
+        return Message({"cache_tokens_left": ex.sessions.cache_tokens_left(), "sessions": len(ex.sessions.sessions),
+                        "start_block": ex.start, "end_block": ex.end, "final_stage": self.final_stage,
+                        **self.stats})
+
+    async def rpc_close_session(self, msg: Message) -> Message:
+        sid = msg.metadata.get("session_id")
+        if sid is not None:
+            await asyncio.get_running_loop().run_in_executor(self._worker, self.executor.sessions.close, sid)
+        return Message({"ok": True})
+
+    async def rpc_echo(self, msg: Message) -> Message:
+        return Message(dict(msg.metadata), list(msg.tensors))
+
+    # ------------------------------------------------------------------ request parsing
+    def _parse(self, msg: Message) -> _Req:
+        md = msg.metadata
+        sid = md.get("session_id")
+        if sid is None:
+            raise ValueError("request.metadata must contain session_id")
+        if not msg.tensors:
+            raise ValueError("request carries no tensor")
+        x = msg.tensors[0]
+        if x.dim() == 3:
+            x = x.reshape(-1, x.shape[-1])
+        elif x.dim() == 2 and self.executor.is_first and x.dtype in (torch.int64, torch.int32):
+            x = x.reshape(-1)
+        T = x.shape[0]
+        is_prefill = bool(md.get("is_prefill", False))
+        is_replay = bool(md.get("is_replay", False))
+        cur_len = int(md.get("cur_len", T))
+        sess = self.executor.sessions.get(sid)
+        if is_prefill:
+            start, reset = 0, True
+        elif sess is None:
+            if not is_replay:
+                raise ValueError(f"Missing past_key_values for session_id={sid}. This may indicate a server "
+                                 f"restart or cache loss. If this is a replay scenario, ensure is_replay=True.")
+            start, reset = 0, True  # first replayed request on a fresh server
+        else:
+            want = cur_len - T
+            if 0 <= want <= sess.length:
+                start = want  # idempotent: a retried / replayed step overwrites its own slot
+            else:
+                logger.warning(f"[{sid[:8]}] past len mismatch: cache={sess.length} cur_len={cur_len} T={T}")
+                start = sess.length
+            reset = False
+        params = SamplingParams(float(md.get("temperature", self._default.temperature)),
+                                float(md.get("top_p", self._default.top_p)), int(md.get("top_k", self._default.top_k)),
+                                float(md.get("repetition_penalty", self._default.repetition_penalty)))
+        return _Req(sid, x, start, reset, params, list(md.get("generated_tokens", []) or []),
+                    md.get("max_length"), None, time.perf_counter())
+
+    async def _submit(self, msg: Message) -> Message:
+        req = self._parse(msg)
+        req.fut = asyncio.get_running_loop().create_future()
+        self._pending.append(req)
+        self.stats["requests"] += 1
+        if not self._draining:
+            self._draining = True
+            asyncio.ensure_future(self._drain())
+        return await req.fut
+
+    # ------------------------------------------------------------------ continuous batching
+    async def _drain(self):
+        loop = asyncio.get_running_loop()
+        try:
+            while self._pending:
+                if self.batch_window > 0:
+                    await asyncio.sleep(self.batch_window)
+                batch, rest, seen, ntok = [], [], set(), 0
+                for r in self._pending:
+                    n = r.x.shape[0]
+                    if r.sid in seen or (batch and ntok + n > self.max_batch_tokens):
+                        rest.append(r)
+                        continue
+                    batch.append(r)
+                    seen.add(r.sid)
+                    ntok += n
+                self._pending = rest
+                try:
+                    outs = await loop.run_in_executor(self._worker, self._run_batch, batch)
+                except Exception as e:  # one bad request must not take the batch down: retry singly
+                    if len(batch) == 1:
+                        if not batch[0].fut.done():
+                            batch[0].fut.set_exception(e)
+                        continue
+                    outs = []
+                    for r in batch:
+                        try:
+                            outs.append((await loop.run_in_executor(self._worker, self._run_batch, [r]))[0])
+                        except Exception as e1:
+                            outs.append(e1)
+                for r, o in zip(batch, outs):
+                    if r.fut.done():
+                        continue
+                    if isinstance(o, Exception):
+                        r.fut.set_exception(o)
+                    else:
+                        r.fut.set_result(o)
+        finally:
+            self._draining = False
+
+    def _run_batch(self, batch: List[_Req]) -> List[Message]:
+        ex = self.executor
+        seqs = [(r.sid, r.x.shape[0]) for r in batch]
+        if ex.is_first:
+            x = torch.cat([r.x.reshape(-1).to(torch.long) for r in batch]).to(ex.device)
+        else:
+            x = torch.cat([r.x for r in batch]).to(ex.device, ex.dtype)
+        ml = max((int(r.max_length) for r in batch if r.max_length), default=None)
+        with torch.inference_mode():
+            out = ex.forward(seqs, x, reset=[r.reset for r in batch], starts=[r.start for r in batch], max_length=ml)
+            self.stats["batches"] += 1
+            self.stats["tokens"] += int(x.shape[0])
+            if self.final_stage:
+                seeds = [session_seed(r.sid, r.start + r.x.shape[0], self.seed) for r in batch]
+                toks = self._sampler(out, [r.params for r in batch], [r.generated for r in batch], seeds).tolist()
+                return [Message({"token_id": int(t), "session_id": r.sid}, [torch.tensor([[int(t)]], dtype=torch.long)])
+                        for r, t in zip(batch, toks)]
+            out_cpu = out.to("cpu", non_blocking=False)
+        res, off = [], 0
+        for r in batch:
+            n = r.x.shape[0]
+            h = out_cpu[off:off + n]
+            off += n
+            amax = float(h.float().abs().max()) if h.numel() else 0.0
+            if amax > 100:
+                logger.warning(f"[{r.sid[:8]}] large activation values detected (|x|max={amax:.2f})")
+            res.append(Message({"session_id": r.sid}, [h.unsqueeze(0)]))
+        return res
+
+    def shutdown(self):
+        self._worker.shutdown(wait=False)

@@ -1,0 +1,328 @@
+"""Client transport (``RpcTransport``): routes a session's activations through the swarm.
+
+Same public API as the reference (src/rpc_transport.py:45-863): ``send_prefill``,
+``send_decode_step``, ``recv_token``, ``shutdown``, per-hop timings in
+``last_prefill_stage_times`` / ``last_decode_stage_times`` / ``decode_stage_history``,
+``routing="stage"`` (fixed ``mini_petals:stage1..N`` keys) or ``routing="module"`` (greedy
+cover of blocks [start_block, total_blocks) from ``petals:module:*`` records: pick the
+candidate with the largest end block, ties by throughput, pin the route per session).
+
+Fault tolerance (Petals-style, reference :587-712) with the reference's defects fixed:
+
+* the per-hop input history is appended only AFTER a hop succeeded, so a replay never
+  contains the step being retried (reference: :741, :805 append first -> duplicate step);
+* a failed hop is re-routed from ITS start block: the replacement may have a different
+  span (module routing), so the route tail is recomputed and the session's history is
+  replayed hop-by-hop through the new tail (each replayed hop's outputs become the next
+  new hop's history) - the reference re-discovers under the same key and may pick a peer
+  with a different end block (:270-353);
+* recovery success is not reported as failure on the last attempt (reference :659-661).
+
+``hidden`` may be a GPU tensor; only the CPU copy crosses the wire.
+"""
+from __future__ import annotations
+
+import asyncio
+import logging
+import random
+import time
+from typing import Any, Dict, List, Optional, Sequence, Set, Tuple
+
+import torch
+
+from .comm.registry import DHT, get_dht_time
+from .comm.rpc import DEFAULT_MAX_MSG_SIZE, MAX_UNARY_PAYLOAD_SIZE, RemoteError, RpcClient, get_loop
+from .comm.wire import Message
+from .dht_utils import get_module_entries, get_stage_key
+
+logger = logging.getLogger(__name__)
+
+HANDLER = "StageConnectionHandler.rpc_forward"
+HANDLER_STREAM = "StageConnectionHandler.rpc_forward_stream"
+RECOVERABLE = (asyncio.TimeoutError, ConnectionError, OSError, RemoteError)
+
+
+class Hop:
+    """One hop of a route: a peer serving blocks [start, end) (``key`` names the record it came from)."""
+
+    def __init__(self, key: str, peer_id: str, maddrs: List[str], start: int, end: int, final: bool):
+        self.key, self.peer_id, self.maddrs = key, peer_id, list(maddrs)
+        self.start, self.end, self.final = start, end, final
+
+    @property
+    def expect_hidden(self) -> bool:
+        return not self.final
+
+    def __repr__(self):
+        return f"Hop({self.key}, {self.peer_id[:8]}, [{self.start},{self.end}), final={self.final})"
+
+
+class RpcTransport:
+    def __init__(self, device, stage: int, dht_initial_peers: Sequence[str], dht_port: int = 8000,
+                 rpc_port: int = 8001, timeout: float = 30.0, temperature: float = 1.0, top_p: float = 0.92,
+                 top_k: int = 50, stage_keys: Optional[List[str]] = None, routing: str = "stage",
+                 model_name: str = "default", total_blocks: Optional[int] = None, start_block: int = 0,
+                 dht: Optional[DHT] = None, repetition_penalty: Optional[float] = None, max_recovery_attempts: int = 3):
+        self.device = device
+        self.stage = stage
+        self.dht_port, self.rpc_port = dht_port, rpc_port
+        self.timeout = timeout
+        self.routing = routing
+        self.model_name = model_name
+        self.total_blocks = total_blocks
+        self.start_block = start_block
+        self.stage_keys = stage_keys or [get_stage_key(i) for i in (1, 2, 3)]
+        self.sampling: Dict[str, Any] = {"temperature": float(temperature), "top_p": float(top_p), "top_k": int(top_k)}
+        if repetition_penalty is not None:
+            self.sampling["repetition_penalty"] = float(repetition_penalty)
+        self.max_recovery_attempts = max_recovery_attempts
+        self._last_token: Optional[int] = None
+        self.last_prefill_stage_times: List[Tuple[str, float]] = []
+        self.last_prefill_total: Optional[float] = None
+        self.last_decode_stage_times: List[Tuple[str, float]] = []
+        self.last_decode_total: Optional[float] = None
+        self.decode_stage_history: List[List[Tuple[str, float]]] = []
+        self.decode_total_times: List[float] = []
+        self.failed_peers: Dict[str, Set[str]] = {}
+        self.session_routes: Dict[str, List[Hop]] = {}
+        # history[session][hop_start_block] = list of inputs successfully sent to the hop at that block
+        self.client_cache: Dict[str, Dict[int, List[torch.Tensor]]] = {}
+        self._own_dht = dht is None
+        self.dht = dht or DHT(start=True, initial_peers=list(dht_initial_peers or []))
+        self.loop = get_loop()
+        self.client = RpcClient()
+        self.peer_id = self.dht.peer_id
+        logger.info(f"RpcTransport initialized: stage={stage}, routing={routing}")
+
+    # ------------------------------------------------------------------ sync helpers
+    def _run(self, coro):
+        return self.loop.run(coro)
+
+    # ------------------------------------------------------------------ discovery
+    def _candidates(self, key: str, block: Optional[int] = None) -> List[dict]:
+        """Live records under ``key`` (stage keys) or covering ``block`` (module keys)."""
+        if block is not None:
+            ents = list(get_module_entries(self.dht, block, self.model_name).values())
+            return [e for e in ents if e.get("start_block") is not None and e.get("end_block") is not None
+                    and int(e["start_block"]) <= block < int(e["end_block"])]
+        res = self.dht.get(key, latest=True)
+        if res is None:
+            return []
+        val = res.value
+        if isinstance(val, dict) and "peer_id" in val and "p2p_maddrs" in val:
+            return [val]
+        out = []
+        if isinstance(val, dict):
+            for sk, raw in val.items():
+                e = raw.value if hasattr(raw, "value") else raw
+                if isinstance(e, dict):
+                    e = dict(e)
+                    e.setdefault("peer_id", str(sk))
+                    out.append(e)
+        return out
+
+    def _discover_peer(self, key: str, exclude: Set[str] = frozenset(), block: Optional[int] = None,
+                       max_retries: int = 10, retry_delay: float = 1.0) -> dict:
+        for attempt in range(max_retries):
+            cands = [e for e in self._candidates(key, block) if str(e.get("peer_id")) not in exclude]
+            if cands:
+                cands.sort(key=lambda e: float(e.get("timestamp", 0.0)), reverse=True)
+                return random.choice(cands[:5])
+            time.sleep(retry_delay)
+        raise RuntimeError(f"no live peer for {key} (excluded {len(exclude)})")
+
+    def _stage_hop(self, i: int, exclude: Set[str] = frozenset(), retries: int = 10, delay: float = 1.0) -> Hop:
+        key = self.stage_keys[i]
+        e = self._discover_peer(key, exclude, max_retries=retries, retry_delay=delay)
+        final = i == len(self.stage_keys) - 1
+        return Hop(key, str(e["peer_id"]), e.get("p2p_maddrs") or [], int(e.get("start_block", i)),
+                   int(e.get("end_block", i + 1)), final)
+
+    def _module_route(self, cur: int, exclude: Set[str] = frozenset()) -> List[Hop]:
+        if self.total_blocks is None:
+            raise ValueError("total_blocks is required when routing='module'")
+        hops: List[Hop] = []
+        while cur < self.total_blocks:
+            cands = [e for e in self._candidates("", cur) if str(e.get("peer_id")) not in exclude]
+            if not cands:
+                raise RuntimeError(f"[module routing] no server covers block={cur}")
+            cands.sort(key=lambda e: (int(e["end_block"]), float(e.get("throughput") or 0.0)), reverse=True)
+            e = cands[0]
+            end = int(e["end_block"])
+            final = end >= self.total_blocks
+            if final and not bool(e.get("final_stage", False)):
+                raise RuntimeError("[module routing] last hop server is not a final stage (needs lm_head)")
+            hops.append(Hop(f"petals:module:{self.model_name}:block_{cur}", str(e["peer_id"]),
+                            e.get("p2p_maddrs") or [], cur, end, final))
+            cur = end
+            if len(hops) > self.total_blocks + 5:
+                raise RuntimeError("[module routing] route did not converge")
+        logger.info(f"[module routing] route: {hops}")
+        return hops
+
+    def _get_route(self, session_id: str) -> List[Hop]:
+        if session_id not in self.session_routes:
+            if self.routing == "module":
+                self.session_routes[session_id] = self._module_route(int(self.start_block))
+            else:
+                self.session_routes[session_id] = [self._stage_hop(i) for i in range(len(self.stage_keys))]
+        return self.session_routes[session_id]
+
+    def _route_tail(self, route: List[Hop], k: int, exclude: Set[str]) -> List[Hop]:
+        if self.routing == "module":
+            return self._module_route(route[k].start, exclude)
+        return [self._stage_hop(i, exclude if i == k else frozenset(), retries=5, delay=0.5)
+                for i in range(k, len(self.stage_keys))]
+
+    # ------------------------------------------------------------------ calls
+    async def _call(self, hop: Hop, x: torch.Tensor, md: dict) -> Message:
+        if not hop.maddrs:
+            raise ConnectionError(f"peer {hop.peer_id[:8]} announced no addresses")
+        nbytes = x.numel() * x.element_size()
+        last_err = None
+        for addr in hop.maddrs:
+            try:
+                if nbytes > MAX_UNARY_PAYLOAD_SIZE // 2:
+                    return await self.client.call(addr, HANDLER_STREAM, Message(md, [x]), self.timeout,
+                                                  stream_chunk_bytes=DEFAULT_MAX_MSG_SIZE)
+                return await self.client.call(addr, HANDLER, Message(md, [x]), self.timeout)
+            except (ConnectionError, OSError) as e:
+                last_err = e
+                continue
+        raise last_err if last_err else ConnectionError("no address reachable")
+
+    @staticmethod
+    def _token_of(resp: Message) -> int:
+        if resp.metadata.get("token_id") is not None:
+            return int(resp.metadata["token_id"])
+        return int(resp.tensors[0].reshape(-1)[0])
+
+    async def _replay_tail(self, session_id: str, route: List[Hop], k: int, base_md: dict) -> None:
+        """Rebuild KV on hops route[k:] by replaying the history recorded at hop k's start block."""
+        hist = self.client_cache.get(session_id, {})
+        inputs = list(hist.get(route[k].start, []))
+        if not inputs:
+            return
+        new_hist: Dict[int, List[torch.Tensor]] = {}
+        for j in range(k, len(route)):
+            hop = route[j]
+            new_hist[hop.start] = list(inputs)
+            outs = []
+            cum = 0
+            for idx, x in enumerate(inputs):
+                cum += int(x.shape[1])
+                md = dict(base_md, session_id=session_id, seq_len=int(x.shape[1]), cur_len=cum,
+                          is_prefill=idx == 0, is_replay=True)
+                resp = await self._call(hop, x, md)
+                if hop.expect_hidden:
+                    outs.append(resp.tensors[0])
+            inputs = outs
+            if not hop.expect_hidden:
+                break
+        hist.update(new_hist)
+        self.client_cache[session_id] = hist
+
+    async def _send(self, session_id: str, hidden: torch.Tensor, md: dict, which: str):
+        t_all = time.perf_counter()
+        x = hidden.detach().to("cpu")
+        if x.dim() == 2:
+            x = x.unsqueeze(0)
+        route = self.session_routes[session_id]  # resolved by the caller (outside the event loop)
+        times: List[Tuple[str, float]] = []
+        k = 0
+        attempts = 0
+        while k < len(route):
+            hop = route[k]
+            t0 = time.perf_counter()
+            try:
+                resp = await self._call(hop, x, md)
+            except RECOVERABLE as e:
+                attempts += 1
+                logger.warning(f"hop {hop} failed ({type(e).__name__}: {e}); recovery {attempts}/"
+                               f"{self.max_recovery_attempts}")
+                self.failed_peers.setdefault(hop.key, set()).add(hop.peer_id)
+                self.client.drop(hop.maddrs[0]) if hop.maddrs else None
+                if attempts > self.max_recovery_attempts:
+                    raise RuntimeError(f"failed to recover {hop.key} after {self.max_recovery_attempts} attempts") from e
+                exclude = set().union(*self.failed_peers.values())
+                try:
+                    tail = await asyncio.get_running_loop().run_in_executor(None, self._route_tail, route, k, exclude)
+                    route = route[:k] + tail
+                    self.session_routes[session_id] = route
+                    base = {kk: v for kk, v in md.items() if kk not in ("seq_len", "cur_len", "is_prefill")}
+                    await self._replay_tail(session_id, route, k, base)
+                except RECOVERABLE + (RuntimeError,) as re:
+                    logger.error(f"recovery attempt failed: {re}")
+                    await asyncio.sleep(0.5)
+                continue
+            times.append((hop.key, time.perf_counter() - t0))
+            self.client_cache.setdefault(session_id, {}).setdefault(hop.start, []).append(x.clone())
+            if hop.expect_hidden:
+                x = resp.tensors[0]
+                if x.dim() == 2:
+                    x = x.unsqueeze(0)
+                k += 1
+                continue
+            total = time.perf_counter() - t_all
+            if which == "prefill":
+                self.last_prefill_stage_times, self.last_prefill_total = times, total
+            else:
+                self.last_decode_stage_times, self.last_decode_total = times, total
+                self.decode_stage_history.append(times)
+                self.decode_total_times.append(total)
+            return self._token_of(resp)
+        raise RuntimeError("No final stage returned a token")
+
+    # ------------------------------------------------------------------ public API
+    def send_prefill(self, L: int, hidden: torch.Tensor, session_id: str, max_length: int):
+        if self.stage != 0:
+            raise RuntimeError("send_prefill should only be called by stage0")
+        self.client_cache.pop(session_id, None)
+        md = {"session_id": session_id, "seq_len": int(L), "cur_len": int(L), "is_prefill": True,
+              "max_length": int(max_length), **self.sampling}
+        self._get_route(session_id)
+        self._last_token = self._run(self._send(session_id, hidden, md, "prefill"))
+
+    def send_decode_step(self, cur_len: int, hidden: torch.Tensor, session_id: str, max_length: int,
+                         generated_tokens: Optional[List[int]] = None):
+        if self.stage != 0:
+            raise RuntimeError("send_decode_step should only be called by stage0")
+        md = {"session_id": session_id, "seq_len": 1, "cur_len": int(cur_len), "is_prefill": False,
+              "max_length": int(max_length), "generated_tokens": list(generated_tokens or [])[-50:], **self.sampling}
+        self._get_route(session_id)
+        self._last_token = self._run(self._send(session_id, hidden, md, "decode"))
+
+    def recv_token(self) -> int:
+        if self.stage != 0:
+            raise RuntimeError("recv_token should only be called by stage0")
+        if self._last_token is None:
+            raise RuntimeError("No token received. Call send_prefill or send_decode_step first.")
+        t, self._last_token = self._last_token, None
+        return int(t)
+
+    def close_session(self, session_id: str) -> None:
+        """Free the session's KV pages on every hop (not in the reference: its caches leak)."""
+        route = self.session_routes.pop(session_id, [])
+        self.client_cache.pop(session_id, None)
+
+        async def _close():
+            for hop in route:
+                for addr in hop.maddrs[:1]:
+                    try:
+                        await self.client.call(addr, "StageConnectionHandler.rpc_close_session",
+                                               Message({"session_id": session_id}), timeout=5.0)
+                    except Exception:
+                        pass
+
+        try:
+            self._run(_close())
+        except Exception:
+            pass
+
+    def shutdown(self):
+        try:
+            self._run(self.client.close())
+        except Exception:
+            pass
+        if self._own_dht:
+            self.dht.shutdown()

@@ -1,0 +1,91 @@
+"""Server throughput for load balancing: min(compute, network x (1 - relay penalty)).
+
+Reference: src/throughput_measurement.py:15-263 measures the compute rate of the whole
+served span with 2 warm-up + 10 timed ``[1,1,H]`` forwards and ``torch.cuda.synchronize``,
+estimates the network rate as ``bandwidth_bps / (H * elt_size)`` (default 100 Mbit/s) times
+``1 - 0.2`` (relay penalty), takes the minimum, and falls back to 10.0 rps.
+
+Here the compute probe is a real decode step of the stage executor on a probe session
+(paged KV, hipGraph replay where available), timed with HIP events; the network term can
+also be *measured* on a live link (``measure_link_bandwidth``: round trips of an H-sized
+activation over the framework's TCP transport) instead of assumed.
+"""
+from __future__ import annotations
+
+import logging
+import time
+import uuid
+from typing import Optional
+
+import torch
+
+logger = logging.getLogger(__name__)
+
+DEFAULT_NETWORK_MBPS = 100.0
+RELAY_PENALTY = 0.2
+FALLBACK_THROUGHPUT = 10.0
+
+
+def measure_compute_throughput(executor, n_warmup: int = 2, n_steps: int = 10, batch: int = 1) -> float:
+    """Decode steps per second of this stage's whole span (``batch`` probe sessions)."""
+    H = executor.cfg.hidden_size
+    dev = executor.device
+    sids = [f"__probe_{uuid.uuid4().hex[:8]}_{i}" for i in range(batch)]
+    try:
+        if executor.is_first:
+            x = torch.randint(0, executor.cfg.vocab_size, (batch,), device=dev)
+        else:
+            x = torch.randn(batch, H, device=dev).to(executor.dtype)
+        seqs = [(s, 1) for s in sids]
+        for _ in range(n_warmup):
+            executor.forward(seqs, x)
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(n_steps):
+                executor.forward(seqs, x)
+            e1.record()
+            e1.synchronize()
+            dt = e0.elapsed_time(e1) / 1000.0
+        else:
+            t0 = time.perf_counter()
+            for _ in range(n_steps):
+                executor.forward(seqs, x)
+            dt = time.perf_counter() - t0
+        return n_steps / max(dt, 1e-9)
+    finally:
+        for s in sids:
+            executor.sessions.close(s)
+
+
+def estimate_network_throughput(hidden_size: int, dtype_bytes: int = 2,
+                                bandwidth_mbps: Optional[float] = None) -> float:
+    """Requests/s the link can carry for one [1, 1, H] activation (reference :157-190)."""
+    mbps = DEFAULT_NETWORK_MBPS if bandwidth_mbps is None else float(bandwidth_mbps)
+    bits_per_request = hidden_size * dtype_bytes * 8
+    return (mbps * 1e6) / bits_per_request
+
+
+def get_server_throughput(executor, network_bandwidth_mbps: Optional[float] = None,
+                          relay_penalty: float = RELAY_PENALTY, n_warmup: int = 2, n_steps: int = 10) -> float:
+    try:
+        compute = measure_compute_throughput(executor, n_warmup, n_steps)
+    except Exception as e:
+        logger.warning(f"compute throughput probe failed ({e!r}); using fallback {FALLBACK_THROUGHPUT}")
+        return FALLBACK_THROUGHPUT
+    elt = torch.tensor([], dtype=executor.dtype).element_size()
+    network = estimate_network_throughput(executor.cfg.hidden_size, elt, network_bandwidth_mbps) * (1 - relay_penalty)
+    final = min(compute, network)
+    logger.info(f"Server throughput: compute={compute:.2f} rps, network={network:.2f} rps, final={final:.2f} rps")
+    return float(final)
+
+
+def measure_link_bandwidth(rpc_call, payload_bytes: int, rounds: int = 5) -> float:
+    """Mbit/s measured with ``rpc_call(bytes)`` round trips (echo handler on the peer)."""
+    rpc_call(payload_bytes)
+    t0 = time.perf_counter()
+    for _ in range(rounds):
+        rpc_call(payload_bytes)
+    dt = (time.perf_counter() - t0) / rounds
+    return 2 * payload_bytes * 8 / dt / 1e6

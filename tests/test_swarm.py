@@ -1,0 +1,118 @@
+"""End-to-end swarm on localhost (registry + TCP RPC + stage servers in threads), CPU path.
+
+Covers the reference's manual integration procedures (scripts/run_all.py, test_fault_tolerance.py,
+elice_test_load_balancing.sh) as automated tests.
+"""
+import uuid
+
+import pytest
+import torch
+
+from src import main as M
+from src.dht_utils import get_remote_module_infos, get_stage_key
+from src.models.config import resolve_model
+from src.models.reference_model import greedy_generate
+from src.models.tokenizer import load_tokenizer
+from src.models.weights import random_stage_weights
+from src.rpc_transport import RpcTransport
+from src.runtime.executor import StageExecutor
+
+from .swarm_utils import ServerThread, client_args, server_argv, wait_for
+
+MODEL = "tiny-gpt2"
+
+
+def _reference(n_new, prompt="Hello, how are you?"):
+    cfg = resolve_model(MODEL)
+    w = random_stage_weights(cfg, 0, cfg.num_hidden_layers, has_embed=True, has_head=True, device="cpu",
+                             dtype=torch.float32)
+    ids = torch.tensor(load_tokenizer(MODEL, cfg).encode(prompt))
+    return greedy_generate([w], ids, n_new)
+
+
+@pytest.mark.timeout(120)
+def test_fixed_three_stage_generation_matches_reference():
+    s1 = ServerThread(server_argv(MODEL, "1,2", 1)).wait()
+    s2 = ServerThread(server_argv(MODEL, "1,2", 2, peers=s1.addr)).wait()
+    try:
+        assert wait_for(lambda: s1.dht.get(get_stage_key(2)) is not None)
+        args = client_args(MODEL, "1,2", s1.addr, "--max_new_tokens 6 --temperature 0")
+        gen = M.run_rank0(args, torch.device("cpu"), [1, 2])
+        ref = _reference(len(gen))
+        assert gen == ref
+    finally:
+        s1.close()
+        s2.close()
+
+
+def _client(peers, cuts, routing="stage", total=None):
+    cfg = resolve_model(MODEL)
+    w = random_stage_weights(cfg, 0, cuts[0], has_embed=True, has_head=False, device="cpu", dtype=torch.float32)
+    ex = StageExecutor(cfg, w, "cpu", dtype=torch.float32, kv_cache_bytes=8 << 20, max_sessions=4, max_seq_len=128)
+    tx = RpcTransport("cpu", 0, [peers], timeout=5.0, temperature=0.0,
+                      stage_keys=[get_stage_key(i) for i in range(1, len(cuts) + 1)], routing=routing,
+                      model_name=MODEL, total_blocks=total or cfg.num_hidden_layers, start_block=cuts[0])
+    return cfg, ex, tx
+
+
+def _generate(ex, tx, n, on_step=None):
+    cfg = resolve_model(MODEL)
+    ids = torch.tensor(load_tokenizer(MODEL, cfg).encode("Hello, how are you?"))
+    sid = str(uuid.uuid4())
+    h = ex.forward([(sid, len(ids))], ids, reset=[True])
+    tx.send_prefill(len(ids), h, sid, len(ids) + n + 1)
+    out = [tx.recv_token()]
+    cur = len(ids) + 1
+    for i in range(n - 1):
+        if on_step:
+            on_step(i)
+        h = ex.forward([(sid, 1)], torch.tensor([out[-1]]), starts=[cur - 1])
+        tx.send_decode_step(cur, h, sid, len(ids) + n + 1, out)
+        out.append(tx.recv_token())
+        cur += 1
+    return out
+
+
+@pytest.mark.timeout(180)
+def test_failover_to_replica_replays_kv():
+    s1 = ServerThread(server_argv(MODEL, "2", 1)).wait()
+    s1b = ServerThread(server_argv(MODEL, "2", 1, peers=s1.addr)).wait()
+    try:
+        assert wait_for(lambda: len(s1.dht.get(get_stage_key(1)).value) == 2)
+        cfg, ex, tx = _client(s1.addr, [2])
+        killed = []
+
+        def kill_current(i):
+            if i == 3:
+                pid = tx.session_routes[next(iter(tx.session_routes))][0].peer_id
+                victim = s1 if s1.srv.peer_id == pid else s1b
+                victim.kill()
+                killed.append(victim)
+
+        gen = _generate(ex, tx, 10, kill_current)
+        assert killed, "no server was killed"
+        assert gen == _reference(10)
+        assert tx.failed_peers  # a failover actually happened
+        tx.shutdown()
+    finally:
+        s1.close()
+        s1b.close()
+
+
+@pytest.mark.timeout(180)
+def test_load_balanced_servers_and_module_routing():
+    extra = "--use_load_balancing --num_blocks 1 --mean_balance_check_period 1000"
+    a = ServerThread(server_argv(MODEL, "2", 1, extra=extra)).wait()
+    b = ServerThread(server_argv(MODEL, "2", 1, peers=a.addr, extra=extra)).wait()
+    try:
+        spans = sorted([(a.srv.ex.start, a.srv.ex.end), (b.srv.ex.start, b.srv.ex.end)])
+        assert spans == [(2, 3), (3, 4)], spans  # the second server filled the uncovered block
+        assert wait_for(lambda: len(get_remote_module_infos(a.dht, MODEL, 4)) >= 2)
+        cfg, ex, tx = _client(a.addr, [2], routing="module", total=4)
+        gen = _generate(ex, tx, 5)
+        assert gen == _reference(5)
+        assert [h.start for h in next(iter(tx.session_routes.values()))] == [2, 3]
+        tx.shutdown()
+    finally:
+        a.close()
+        b.close()

@@ -37,7 +37,7 @@ def baseline_value():
     try:
         with open(os.path.join(HERE, "BASELINE.json")) as f:
             b = json.load(f)
-        v = b.get("measured_reference_equivalent", {}).get("decode_tokens_per_s_same_batch")
+        v = b.get("measured_reference_equivalent", {}).get("decode_tokens_per_s_same_batch")  # per GPU
         return float(v) if v else None
     except Exception:
         return None
@@ -142,7 +142,8 @@ def main(argv=None):
             "ms_per_step": round(1000 * dt / a.steps, 3),
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": (round(value / base, 3) if base else None),
+            "vs_baseline": (round(value / (base * world), 3) if base else None),
+            "baseline_tokens_per_s_per_gpu": base,
             "dtype": "bf16",
             "data": "synthetic (random-init Llama-2-7B weights, random prompt ids)",
             "config": {

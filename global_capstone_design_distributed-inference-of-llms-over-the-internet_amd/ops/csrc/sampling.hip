@@ -59,15 +59,18 @@ __global__ __launch_bounds__(SB) void sample_kernel(const bf16_t* __restrict__ l
                                                     const int32_t* __restrict__ recent, int recent_stride,
                                                     const int32_t* __restrict__ recent_len,
                                                     const int64_t* __restrict__ seeds, float* __restrict__ ws,
-                                                    int64_t* __restrict__ out) {
+                                                    int64_t* __restrict__ out, int use_lds) {
   __shared__ float red[SB / 64 + 1];
   __shared__ unsigned hist[256];
   __shared__ float mass[256];
   __shared__ unsigned s_u[4];
   __shared__ int s_i[2];
+  extern __shared__ __attribute__((aligned(16))) float s_row[];
   const int row = blockIdx.x, tid = threadIdx.x;
   const bf16_t* lrow = logits + (int64_t)row * stride;
-  float* x = ws + (int64_t)row * V;
+  // the working row lives in LDS when it fits (V <= 38K: every pass is an LDS sweep),
+  // otherwise in the global workspace (L2-resident)
+  float* x = (use_lds ? s_row : ws + (int64_t)row * V);
   const float temp = temps[row];
 
   // ---- fp32 copy + max (max is needed by both the greedy and the sampling path) ----
@@ -325,7 +328,9 @@ extern "C" int mp_sample(const void* logits, int64_t stride, int R, int V, const
   using namespace mp;
   if (R == 0) return 0;
   if (recent_stride > SB) return -1;
-  hipLaunchKernelGGL(sample_kernel, dim3(R), dim3(SB), 0, stream, (const bf16_t*)logits, stride, V, temps, top_ps,
-                     top_ks, rep_pens, recent, recent_stride, recent_len, seeds, ws, out);
+  const size_t lds = (size_t)V * sizeof(float);
+  const int use_lds = lds <= 150 * 1024;
+  hipLaunchKernelGGL(sample_kernel, dim3(R), dim3(SB), use_lds ? lds : 0, stream, (const bf16_t*)logits, stride, V,
+                     temps, top_ps, top_ks, rep_pens, recent, recent_stride, recent_len, seeds, ws, out, use_lds);
   return (int)hipGetLastError();
 }

@@ -87,6 +87,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--repetition_penalty", type=float, default=None, help="sent to the last stage (server default 1.5)")
     p.add_argument("--batch_window_ms", type=float, default=0.5, help="continuous-batching collection window")
     p.add_argument("--ttl", type=float, default=DEFAULT_TTL)
+    p.add_argument("--push", action="store_true",
+                   help="client: server-to-server forwarding along the route (one client round trip per token)")
+    p.add_argument("--alloc_timeout", type=float, default=5.0, help="server: wait this long for free KV pages")
     p.add_argument("--log_level", type=str, default=None)
     return p
 
@@ -145,7 +148,8 @@ def run_rank0(args, device, cuts: List[int]):
                       timeout=args.request_timeout, temperature=args.temperature, top_p=args.top_p,
                       top_k=args.top_k, stage_keys=[get_stage_key(i) for i in range(1, n_servers + 1)],
                       routing="module" if args.use_load_balancing else "stage", model_name=args.model,
-                      total_blocks=total_blocks, start_block=stage0_end, repetition_penalty=args.repetition_penalty)
+                      total_blocks=total_blocks, start_block=stage0_end, repetition_penalty=args.repetition_penalty,
+                      push=args.push)
     ids = tok(args.prompt, return_tensors="pt").input_ids.reshape(-1)
     Lp = int(ids.numel())
     sid = str(uuid.uuid4())
@@ -209,7 +213,8 @@ class _Server:
         self.server = RpcServer(args.host, args.rpc_port, announce_host=args.public_ip or None,
                                 announce_port=args.public_rpc_port)
         self.handler = StageConnectionHandler(dht, executor, executor.device, args.request_timeout, final,
-                                              batch_window_ms=args.batch_window_ms, seed=args.seed)
+                                              batch_window_ms=args.batch_window_ms, seed=args.seed,
+                                              alloc_timeout=getattr(args, "alloc_timeout", 5.0))
         self.loop.run(self.server.start())
         self.handler.add_p2p_handlers(self.server)
         self.maddrs = self.server.maddrs
@@ -226,7 +231,8 @@ class _Server:
     def store_once(self, state: ServerState = ServerState.ONLINE):
         a, ex = self.args, self.ex
         exp = get_dht_time() + a.ttl
-        extra = dict(start_block=ex.start, end_block=ex.end, final_stage=self.final)
+        extra = dict(start_block=ex.start, end_block=ex.end, final_stage=self.final,
+                     cache_tokens_left=int(ex.sessions.cache_tokens_left()))
         if self.lb:
             extra.update(blocks=[ex.start, ex.end], throughput=self.throughput)
         if state == ServerState.ONLINE:

@@ -83,6 +83,48 @@ def gemm_policy() -> str:
     return _GEMM_POLICY
 
 
+# Stream-K decode GEMM (gemm.hip, gemm_sk_kernel): "auto" = for M > SK_MIN_M; "on" = every
+# decode GEMM it covers; "off" = the one-group-per-workgroup kernel only.
+_GEMM_SK = os.environ.get("MPAMD_GEMM_SK", "auto")
+SK_MIN_M = int(os.environ.get("MPAMD_GEMM_SK_MIN_M", "16"))
+_GEMM_WS = {}
+
+
+def set_gemm_sk(mode: str) -> None:
+    global _GEMM_SK
+    assert mode in ("auto", "on", "off")
+    _GEMM_SK = mode
+
+
+def gemm_workspace(device) -> torch.Tensor:
+    """Per-device scratch of the stream-K GEMM: split-group arrival counters + fp32 slabs.
+
+    Zero-initialised once; the kernel leaves the counters at zero after every launch, so the
+    buffer is reusable by every later launch and graph replay.  One compute stream per device
+    uses it at a time (the executors' decode step is single-stream).  Call this before a
+    hipGraph capture so the allocation does not happen inside it.
+    """
+    device = torch.device(device)
+    key = (device.type, device.index if device.index is not None else torch.cuda.current_device())
+    ws = _GEMM_WS.get(key)
+    if ws is None:
+        require_native()
+        nbytes = int(torch.ops.mpamd.gemm_workspace_bytes())
+        ws = torch.zeros(nbytes, dtype=torch.uint8, device=device)
+        _GEMM_WS[key] = ws
+    return ws
+
+
+def _use_sk(M: int, N: int, K: int, epilogue: int) -> bool:
+    if _GEMM_SK == "off":
+        return False
+    nks = K // 32
+    covered = (N // 16) % 4 == 0 and nks % 8 == 0 and nks >= 32
+    if not covered:
+        return False
+    return _GEMM_SK == "on" or M > SK_MIN_M
+
+
 # ---------------------------------------------------------------------------------------
 def packed_numel(M: int, K: int) -> int:
     """Elements of a packed decode activation (rows padded to a multiple of 16)."""
@@ -265,7 +307,11 @@ def linear(x, w, out=None, epilogue=0, residual=None, policy=None, wp=None, a_ro
             out = (torch.empty(packed_numel(M, ncols), dtype=x.dtype, device=x.device) if out_packed
                    else torch.empty(M, ncols, dtype=x.dtype, device=x.device))
         flags = 1 | (2 if out_packed else 0)
-        torch.ops.mpamd.gemm(x, wp, out, residual, int(epilogue), M, flags)
+        ws = None
+        if _use_sk(M, N, K, epilogue):
+            flags |= 4
+            ws = gemm_workspace(x.device)
+        torch.ops.mpamd.gemm(x, wp, out, residual, int(epilogue), M, flags, ws)
         return out
     if a_rows is not None or out_packed:
         raise RuntimeError(f"packed activations need the native decode GEMM (M={M}, N={N}, K={K})")

@@ -29,8 +29,10 @@ int mp_argmax(const void* logits, int64_t stride, int R, int V, int64_t* out, hi
 int mp_sample(const void* logits, int64_t stride, int R, int V, const float* temps, const float* top_ps,
               const int32_t* top_ks, const float* rep_pens, const int32_t* recent, int recent_stride,
               const int32_t* recent_len, const int64_t* seeds, float* ws, int64_t* out, hipStream_t stream);
+int64_t mp_gemm_workspace_bytes();
 int mp_gemm_bf16(const void* x, int64_t x_stride, const void* w, void* y, int64_t y_stride, const void* res,
-                 int64_t res_stride, int M, int N, int K, int epilogue, int flags, hipStream_t stream);
+                 int64_t res_stride, int M, int N, int K, int epilogue, int flags, void* ws,
+                 hipStream_t stream);
 int mp_pack_act(const void* x, int64_t xs, void* ap, int M, int K, hipStream_t stream);
 int mp_pack_weight(const void* w, void* wp, int N, int K, hipStream_t stream);
 }
@@ -231,7 +233,7 @@ void sample(const at::Tensor& logits, const at::Tensor& temps, const at::Tensor&
 
 // flags bit 0: x is packed (holds ceil(M/16)*16*K elements, M given); bit 1: packed SwiGLU output
 void gemm(const at::Tensor& x, const at::Tensor& wp, at::Tensor& y, const c10::optional<at::Tensor>& residual,
-          int64_t epilogue, int64_t M_, int64_t flags) {
+          int64_t epilogue, int64_t M_, int64_t flags, const c10::optional<at::Tensor>& workspace) {
   check_bf16_cuda(x, "x");
   check_bf16_cuda(wp, "wp");
   check_bf16_cuda(y, "y");
@@ -266,8 +268,15 @@ void gemm(const at::Tensor& x, const at::Tensor& wp, at::Tensor& y, const c10::o
   }
   MP_CHECK(epilogue != 2 || rp != nullptr, "residual epilogue needs residual");
   MP_CHECK(epilogue >= 0 && epilogue <= 2, "epilogue");
+  void* ws = nullptr;
+  if (workspace.has_value()) {
+    MP_CHECK(workspace->is_cuda() && workspace->is_contiguous() &&
+                 workspace->numel() * workspace->element_size() >= mp_gemm_workspace_bytes(),
+             "gemm workspace too small (ops.gemm_workspace)");
+    ws = workspace->data_ptr();
+  }
   check_launch(mp_gemm_bf16(x.data_ptr(), apk ? 0 : x.stride(0), wp.data_ptr(), y.data_ptr(), opk ? 0 : y.stride(0),
-                            rp, rs, M, N, K, (int)epilogue, (int)flags, cur_stream()),
+                            rp, rs, M, N, K, (int)epilogue, (int)flags, ws, cur_stream()),
                "gemm");
 }
 
@@ -288,9 +297,12 @@ at::Tensor pack_weight(const at::Tensor& w) {
   return wp;
 }
 
+int64_t gemm_workspace_bytes() { return mp_gemm_workspace_bytes(); }
+
 }  // namespace
 
 TORCH_LIBRARY(mpamd, m) {
+  m.def("gemm_workspace_bytes() -> int", &gemm_workspace_bytes);
   m.def(
       "rmsnorm(Tensor x, Tensor(a!) residual, Tensor w, Tensor(b!) y, float eps, int mode, Tensor? rows, "
       "int packed) -> ()");
@@ -309,7 +321,9 @@ TORCH_LIBRARY(mpamd, m) {
   m.def(
       "sample(Tensor logits, Tensor temps, Tensor top_ps, Tensor top_ks, Tensor rep_pens, Tensor recent, "
       "Tensor recent_len, Tensor seeds, Tensor(a!) workspace, Tensor(b!) out) -> ()");
-  m.def("gemm(Tensor x, Tensor wp, Tensor(a!) y, Tensor? residual, int epilogue, int M, int flags) -> ()");
+  m.def(
+      "gemm(Tensor x, Tensor wp, Tensor(a!) y, Tensor? residual, int epilogue, int M, int flags, "
+      "Tensor(b!)? workspace=None) -> ()");
   m.def("pack_act(Tensor x, Tensor(a!) ap) -> ()");
   m.def("pack_weight(Tensor w) -> Tensor");
 }

@@ -24,6 +24,7 @@
 //     interleaved in 16-row blocks [g16 u16 g16 u16 ...] (tile 2t = gate, 2t+1 = up;
 //     output N/2 columns); 2 = y = bf16(bf16(acc) + residual).
 #include "common.h"
+#include <stdlib.h>
 
 namespace mp {
 
@@ -185,6 +186,262 @@ static int launch_gemm(const void* x, int64_t xs, const void* w, void* y, int64_
   return 0;
 }
 
+// ---------------------------------------------------------------------------------------
+// Stream-K form (M in 17..64, or any M when the caller gives a workspace).
+//
+// The one-group-per-workgroup kernel above leaves two things on the table at M = 32..64:
+//   * tails: the grid is N/(16 NT) workgroups; 384 (qkv) or 688 (gate/up) workgroups on 256
+//     CUs run 1.5 / 2.7 waves of workgroups, and at ~200 VGPRs only one fits per CU;
+//   * activation re-reads: every workgroup reads all of x (M x K) for just NT column tiles,
+//     so at M = 64 the L2->CU traffic of x is 2-4x the weight bytes.
+// Here the grid is exactly one workgroup per CU and the work is the flat list of units
+// (column group g of NT tiles, k-slice k), u = g * nks + k, cut into G equal contiguous
+// ranges (stream-K): every CU streams the same number of weight bytes, a group may be split
+// between consecutive workgroups, and with NT = 4 the activation traffic is 1/4 of the
+// NT = 1 form.  Inside a workgroup the 8 waves take the units of a range round-robin in
+// "chunks" of 8 consecutive k-slices (one per wave, chunks never straddle a group since
+// nks % 8 == 0), through a D-deep register ring that holds BOTH operands of a k-slice:
+// loads are issued D chunks ahead in consumption order, so in-order vmcnt never drains the
+// ring (the A-before-B trick of the kernel above is not needed).
+// Group boundaries: each wave parks its partial accumulators in LDS (one pending group at
+// a time: nks >= 8 D), the next ring turn sums the 8 waves' partials and either runs the
+// epilogue (group fully inside this range) or writes an fp32 slab; the last-arriving
+// workgroup of a split group (agent-scope release/acquire + counter, guide §5 "In-launch
+// split-K reduction") sums the slabs of all contributors in workgroup order
+// (deterministic) and runs the epilogue.  The counter is re-zeroed by that reducer, so a
+// zero-initialised workspace stays valid across launches and graph replays.
+constexpr int SK_MAX_GROUPS = 1 << 15;
+constexpr int SK_MAX_BLOCKS = 512;
+constexpr int SK_MAX_S = 64;  // MT * NT * 4 accumulator slots per lane
+constexpr int SK_ZERO_BYTES = 4 * 1024;  // zero A fragments (MT <= 4) for masked units
+
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+template <int MT, int NT, int EPI, bool OPK>
+__device__ __forceinline__ void sk_epilogue(int qd, int g, const f32x4& v, const f32x4& up, bf16_t* __restrict__ y,
+                                            int64_t ys, const bf16_t* __restrict__ res, int64_t rs, int M, int lane) {
+  const int mt = qd / NT, t = qd % NT, c = lane & 15, q = lane >> 4;
+  const int tile = g * NT + t;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = mt * 16 + q * 4 + r;
+    if (row >= M) continue;
+    if constexpr (EPI == 1) {
+      const int ncol = (tile >> 1) * 16 + c;
+      const float gg = round_bf(v[r]);
+      const float a = round_bf(gg / (1.f + __expf(-gg)));
+      const int64_t yo = OPK ? apk_off(row, ncol, MT) : (int64_t)row * ys + ncol;
+      y[yo] = f2bf(a * round_bf(up[r]));
+    } else {
+      const int col = tile * 16 + c;
+      float o = v[r];
+      if constexpr (EPI == 2) o = round_bf(o) + bf2f(res[(int64_t)row * rs + col]);
+      y[(int64_t)row * ys + col] = f2bf(o);
+    }
+  }
+}
+
+template <int MT, int NT, int D, int EPI, bool OPK>
+__global__ __launch_bounds__(512) void gemm_sk_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ wp,
+                                                      bf16_t* __restrict__ y, int64_t ys, const bf16_t* __restrict__ res,
+                                                      int64_t rs, int M, int N, int K, int* __restrict__ cnt,
+                                                      f32x4* __restrict__ slab) {
+  constexpr int Q = MT * NT;  // accumulator quads (f32x4) per lane
+  __shared__ __attribute__((aligned(16))) f32x4 red[8 * Q * 64 + 16];
+  int* s_flag = reinterpret_cast<int*>(red + 8 * Q * 64);
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int G = gridDim.x;
+  const int nks = K >> 5;
+  const int U = ((N >> 4) / NT) * nks;
+  // logical workgroup id: consecutive ranges (which share split groups) on the same XCD
+  const int lb = (G & 7) ? (int)blockIdx.x : (int)(blockIdx.x & 7) * (G >> 3) + (int)(blockIdx.x >> 3);
+  const int u0 = (int)((int64_t)lb * U / G), u1 = (int)((int64_t)(lb + 1) * U / G);
+  const int c_first = u0 >> 3, nch = ((u1 - 1) >> 3) + 1 - c_first;
+  auto start_of = [&](int b) { return (int)((int64_t)b * U / G); };
+  auto block_of = [&](int u) { return (int)(((int64_t)(u + 1) * G - 1) / U); };
+
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[mt][t] = (f32x4)(0.f);
+  u16x8 ra[D][MT], rb[D][NT];
+
+  // Ring loads are unconditional (a conditional load makes hipcc fall back to vmcnt(0) before
+  // every MFMA): units outside [u0, u1) - the ragged first/last chunk and the padding up to a
+  // whole ring turn - load a clamped, valid weight address (an L2 hit) and a zero A fragment
+  // from the workspace, so their MFMAs add exactly 0.
+  const bf16_t* zero_a = reinterpret_cast<const bf16_t*>(cnt + SK_MAX_GROUPS);
+#define SK_LOAD(s, cc)                                                                                      \
+  {                                                                                                         \
+    const int u_ = (cc) * 8 + wid;                                                                          \
+    const bool act_ = u_ >= u0 && u_ < u1;                                                                  \
+    const int uc_ = min(max(u_, u0), u1 - 1);                                                               \
+    const int g_ = uc_ / nks, k_ = uc_ - g_ * nks;                                                          \
+    _Pragma("unroll") for (int t = 0; t < NT; ++t) rb[s][t] = __builtin_nontemporal_load(                   \
+        reinterpret_cast<const u16x8*>(wp + (((int64_t)(g_ * NT + t) * nks + k_) << 9) + lane * 8));        \
+    const bf16_t* xa_ = act_ ? x + (((int64_t)k_ * MT) << 9) : zero_a;                                      \
+    _Pragma("unroll") for (int mt = 0; mt < MT; ++mt) ra[s][mt] =                                           \
+        *reinterpret_cast<const u16x8*>(xa_ + (mt << 9) + lane * 8);                                        \
+  }
+
+  // sum of the 8 waves' parked partials for quad qd (this lane)
+  auto red_sum = [&](int qd) {
+    f32x4 s = red[qd * 64 + lane];
+#pragma unroll
+    for (int w = 1; w < 8; ++w) s += red[(w * Q + qd) * 64 + lane];
+    return s;
+  };
+  auto stage = [&]() {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        red[(wid * Q + mt * NT + t) * 64 + lane] = acc[mt][t];
+        acc[mt][t] = (f32x4)(0.f);
+      }
+  };
+  auto reduce = [&](int g) {
+    lds_barrier();
+    const bool whole = g * nks >= u0 && (g + 1) * nks <= u1;
+    if (whole) {
+      for (int qd = wid; qd < Q; qd += 8) {
+        if (EPI == 1 && (qd % NT) & 1) continue;  // up tile: consumed with its gate tile
+        sk_epilogue<MT, NT, EPI, OPK>(qd, g, red_sum(qd), EPI == 1 ? red_sum(qd + 1) : (f32x4)(0.f), y, ys, res, rs,
+                                      M, lane);
+      }
+    } else {
+      const int side = (u0 / nks == g) ? 0 : 1;
+      f32x4* my = slab + (int64_t)(lb * 2 + side) * Q * 64;
+      for (int qd = wid; qd < Q; qd += 8) my[qd * 64 + lane] = red_sum(qd);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      lds_barrier();
+      const int bf = block_of(g * nks), bl = block_of((g + 1) * nks - 1);
+      if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int old = __hip_atomic_fetch_add(cnt + g, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = old == bl - bf;
+        if (last) {
+          __hip_atomic_store(cnt + g, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        *s_flag = last;
+      }
+      lds_barrier();
+      if (*s_flag) {
+        for (int qd = wid; qd < Q; qd += 8) {
+          if (EPI == 1 && (qd % NT) & 1) continue;
+          f32x4 v = (f32x4)(0.f), up = (f32x4)(0.f);
+          for (int b = bf; b <= bl; ++b) {
+            const int sd = (start_of(b) / nks == g) ? 0 : 1;
+            const f32x4* sb = slab + (int64_t)(b * 2 + sd) * Q * 64;
+            v += sb[qd * 64 + lane];
+            if (EPI == 1) up += sb[(qd + 1) * 64 + lane];
+          }
+          sk_epilogue<MT, NT, EPI, OPK>(qd, g, v, up, y, ys, res, rs, M, lane);
+        }
+      }
+    }
+    lds_barrier();  // red may be overwritten by the next stage()
+  };
+
+  // prologue: fill the ring
+  const int nch_pad = ((nch + D - 1) / D) * D;
+#pragma unroll
+  for (int s = 0; s < D; ++s) SK_LOAD(s, c_first + s)
+
+  // group of a chunk (chunks never straddle groups; padding chunks clamp to the last one)
+  auto chunk_group = [&](int cc) { return min(max(cc * 8, u0), u1 - 1) / nks; };
+  int cur_g = chunk_group(c_first);
+  bool pending = false;
+  int pend_g = 0;
+  for (int j0 = 0; j0 < nch_pad; j0 += D) {
+    if (pending) {
+      reduce(pend_g);
+      pending = false;
+    }
+#pragma unroll
+    for (int s = 0; s < D; ++s) {
+      const int cc = c_first + j0 + s;
+      const int g = chunk_group(cc);
+      if (g != cur_g) {  // at most one group boundary per ring turn (nks >= 8 D)
+        stage();
+        pending = true;
+        pend_g = cur_g;
+        cur_g = g;
+      }
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[mt][t] = mfma16(ra[s][mt], rb[s][t], acc[mt][t]);
+      SK_LOAD(s, cc + D)
+    }
+  }
+#undef SK_LOAD
+  if (pending) reduce(pend_g);
+  stage();
+  reduce(cur_g);
+}
+
+static int sk_num_cus() {
+  static int n[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (n[dev] == 0) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+    n[dev] = v;
+  }
+  return n[dev];
+}
+
+template <int MT, int NT, int D>
+static int launch_gemm_sk_cfg(const void* x, void* y, int64_t ys, const void* w, const void* res, int64_t rs, int M,
+                              int N, int K, int epi, int flags, void* ws, int gmul, hipStream_t stream) {
+  const int nks = K / 32;
+  const int ngrp = (N / 16) / NT;
+  if ((N / 16) % NT || nks % 8 || nks < 8 * D || ngrp > SK_MAX_GROUPS) return 1;  // caller falls back
+  const int U = ngrp * nks;
+  int G = sk_num_cus() * gmul;
+  if (G > SK_MAX_BLOCKS) G = SK_MAX_BLOCKS;
+  if (G > U) G = U;
+  int* cnt = (int*)ws;  // [SK_MAX_GROUPS] counters, [SK_ZERO_BYTES] zeros, slabs
+  f32x4* slab = (f32x4*)((char*)ws + SK_MAX_GROUPS * sizeof(int) + SK_ZERO_BYTES);
+  const bool opk = flags & 2;
+#define MP_SK(EPI_, OPK_)                                                                                         \
+  hipLaunchKernelGGL((gemm_sk_kernel<MT, NT, D, EPI_, OPK_>), dim3(G), dim3(512), 0, stream, (const bf16_t*)x,     \
+                     (const bf16_t*)w, (bf16_t*)y, ys, (const bf16_t*)res, rs, M, N, K, cnt, slab)
+  if (epi == 1) {
+    if (opk) { MP_SK(1, true); } else { MP_SK(1, false); }
+  } else if (opk) {
+    return -3;
+  } else if (epi == 2) {
+    MP_SK(2, false);
+  } else {
+    MP_SK(0, false);
+  }
+#undef MP_SK
+  return 0;
+}
+
+static int sk_env(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v ? atoi(v) : dflt;
+}
+
+template <int MT>
+static int launch_gemm_sk(const void* x, void* y, int64_t ys, const void* w, const void* res, int64_t rs, int M, int N,
+                          int K, int epi, int flags, void* ws, hipStream_t stream) {
+  // tuning knobs (experiments): MPAMD_SK_CFG 0 = NT 4 / ring 4 (3 for MT >= 3), 1 = NT 2 / ring 4,
+  // 2 = NT 4 / ring 2; MPAMD_SK_GM = workgroups per CU
+  static const int cfg = sk_env("MPAMD_SK_CFG", 0), gm = sk_env("MPAMD_SK_GM", 1);
+  if (cfg == 1) return launch_gemm_sk_cfg<MT, 2, 4>(x, y, ys, w, res, rs, M, N, K, epi, flags, ws, gm, stream);
+  if (cfg == 2) return launch_gemm_sk_cfg<MT, 4, 2>(x, y, ys, w, res, rs, M, N, K, epi, flags, ws, gm, stream);
+  return launch_gemm_sk_cfg<MT, 4, (MT >= 3 ? 3 : 4)>(x, y, ys, w, res, rs, M, N, K, epi, flags, ws, gm, stream);
+}
+
 // Pack W[N, K] (row-major) into the fragment-native layout Wp[N/16][K/32][64][8].
 __global__ __launch_bounds__(256) void pack_weight_kernel(const bf16_t* __restrict__ w, bf16_t* __restrict__ wp,
                                                           int N, int K) {
@@ -203,14 +460,31 @@ __global__ __launch_bounds__(256) void pack_weight_kernel(const bf16_t* __restri
 
 }  // namespace mp
 
-// flags: bit 0 = x is packed (Ap[K/32][ceil(M/16)][64][8]); bit 1 = SwiGLU output packed.
+extern "C" int64_t mp_gemm_workspace_bytes() {
+  using namespace mp;
+  return (int64_t)SK_MAX_GROUPS * sizeof(int) + SK_ZERO_BYTES +
+         (int64_t)SK_MAX_BLOCKS * 2 * SK_MAX_S * 64 * sizeof(float);
+}
+
+// flags: bit 0 = x is packed (Ap[K/32][ceil(M/16)][64][8]); bit 1 = SwiGLU output packed;
+//        bit 2 = use the stream-K kernel (needs ws: mp_gemm_workspace_bytes(), zero-initialised,
+//        used by one stream at a time); bit 3 = force the one-group-per-workgroup kernel.
 extern "C" int mp_gemm_bf16(const void* x, int64_t x_stride, const void* w, void* y, int64_t y_stride,
                             const void* res, int64_t res_stride, int M, int N, int K, int epilogue, int flags,
-                            hipStream_t stream) {
+                            void* ws, hipStream_t stream) {
   using namespace mp;
   if (M == 0) return 0;
   if (M > 64 || K % (32 * GU_MAX) || N % 16 || ((flags & 1) == 0 && x_stride % 8)) return -1;
   int rc;
+  if ((flags & 1) && (flags & 4) && !(flags & 8) && ws != nullptr) {
+    if (M <= 16) rc = launch_gemm_sk<1>(x, y, y_stride, w, res, res_stride, M, N, K, epilogue, flags, ws, stream);
+    else if (M <= 32) rc = launch_gemm_sk<2>(x, y, y_stride, w, res, res_stride, M, N, K, epilogue, flags, ws, stream);
+    else if (M <= 48) rc = launch_gemm_sk<3>(x, y, y_stride, w, res, res_stride, M, N, K, epilogue, flags, ws, stream);
+    else rc = launch_gemm_sk<4>(x, y, y_stride, w, res, res_stride, M, N, K, epilogue, flags, ws, stream);
+    if (rc < 0) return rc;
+    if (rc == 0) return (int)hipGetLastError();
+    // rc == 1: shape not covered by the stream-K form -> one-group-per-workgroup kernel
+  }
   if (M <= 16) rc = launch_gemm<1>(x, x_stride, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, stream);
   else if (M <= 32) rc = launch_gemm<2>(x, x_stride, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, stream);
   else if (M <= 48) rc = launch_gemm<3>(x, x_stride, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, stream);

@@ -14,8 +14,15 @@ reply format, and changes the engine underneath:
 * position bookkeeping is idempotent: a decode step carries ``cur_len``, so a retried or
   replayed step overwrites its own slot instead of appending twice (the reference's replay
   duplicates the current step, SURVEY §7.2);
-* extra handlers beyond the reference: ``rpc_info`` (free cache tokens, like upstream
-  Petals' ``rpc_info``), ``rpc_close_session`` and ``rpc_echo`` (link probing).
+* extra handlers beyond the reference, from the upstream Petals server surface the reference
+  vendors (petals/server/handler.py): ``rpc_info`` (free cache
+  tokens), ``rpc_inference`` (per-step session API with ``step_id`` de-duplication and
+  ``start_from_position`` rewind), server-to-server **push** (a request carrying
+  ``next_hops`` is forwarded by this server to the next one, upstream ``rpc_push``: the
+  client pays one round trip per token instead of one per stage), task priorities (decode
+  steps before prefills, upstream ``TaskPrioritizer``), KV allocation that waits for pages
+  to be freed up to ``alloc_timeout`` (upstream ``MemoryCache``), ``rpc_close_session``,
+  ``rpc_echo`` and ``rpc_check_reachability``.
 
 Metadata keys: session_id, seq_len, cur_len, is_prefill, is_replay, max_length, temperature,
 top_p, top_k, repetition_penalty (default 1.5), generated_tokens.  Final-stage replies carry
@@ -32,7 +39,7 @@ from typing import Dict, List, Optional
 
 import torch
 
-from .comm.rpc import RpcServer
+from .comm.rpc import RemoteError, RpcClient, RpcServer
 from .comm.wire import Message
 from .runtime.kv_cache import AllocationFailed
 from .runtime.sampler import BatchSampler, SamplingParams, session_seed
@@ -40,6 +47,15 @@ from .runtime.sampler import BatchSampler, SamplingParams, session_seed
 logger = logging.getLogger(__name__)
 
 HANDLER_PREFIX = "StageConnectionHandler."
+
+
+class TaskPrioritizer:
+    """Upstream Petals ``DummyTaskPrioritizer`` (petals/server/task_prioritizer.py:6-20):
+    inference (one-token decode) steps first, everything else (prefill / forward) after.
+    Lower value = served first; ties in arrival order."""
+
+    def prioritize(self, n_tokens: int, is_prefill: bool, **kwargs) -> float:
+        return 1.0 if (n_tokens == 1 and not is_prefill) else 2.0
 
 
 @dataclasses.dataclass
@@ -53,11 +69,13 @@ class _Req:
     max_length: Optional[int]
     fut: asyncio.Future
     t0: float
+    priority: float = 2.0
 
 
 class StageConnectionHandler:
     def __init__(self, dht, stage_model, device=None, request_timeout: float = 30.0, final_stage: bool = False,
-                 batch_window_ms: float = 0.5, max_batch_tokens: Optional[int] = None, seed: int = 0):
+                 batch_window_ms: float = 0.5, max_batch_tokens: Optional[int] = None, seed: int = 0,
+                 alloc_timeout: float = 5.0, prioritizer: Optional[TaskPrioritizer] = None):
         self.dht = dht
         self.executor = stage_model
         self.device = torch.device(device) if device is not None else stage_model.device
@@ -71,7 +89,11 @@ class StageConnectionHandler:
         self._draining = False
         self._worker = concurrent.futures.ThreadPoolExecutor(1, thread_name_prefix="stage-gpu")
         self._sampler = BatchSampler(self.device) if final_stage else None
-        self.stats = {"requests": 0, "batches": 0, "tokens": 0}
+        self.alloc_timeout = alloc_timeout
+        self.prioritizer = prioritizer or TaskPrioritizer()
+        self._client: Optional[RpcClient] = None  # for push forwarding (created on the server loop)
+        self._steps: Dict[str, Dict[str, Message]] = {}  # session -> step_id -> reply (dedup, rpc_inference)
+        self.stats = {"requests": 0, "batches": 0, "tokens": 0, "pushed": 0}
 
     # ------------------------------------------------------------------ registration
     def add_p2p_handlers(self, server: RpcServer) -> None:
@@ -80,13 +102,104 @@ class StageConnectionHandler:
         server.add_handler(HANDLER_PREFIX + "rpc_info", self.rpc_info)
         server.add_handler(HANDLER_PREFIX + "rpc_close_session", self.rpc_close_session)
         server.add_handler(HANDLER_PREFIX + "rpc_echo", self.rpc_echo)
+        server.add_handler(HANDLER_PREFIX + "rpc_inference", self.rpc_inference)
+        server.add_handler(HANDLER_PREFIX + "rpc_push", self.rpc_push)
+        server.add_handler(HANDLER_PREFIX + "rpc_check_reachability", self.rpc_check_reachability)
 
     # ------------------------------------------------------------------ handlers
     async def rpc_forward(self, msg: Message) -> Message:
-        return await asyncio.wait_for(self._submit(msg), self.request_timeout)
+        return await self._handle(msg)
 
     async def rpc_forward_stream(self, msg: Message) -> Message:
-        return await asyncio.wait_for(self._submit(msg), self.request_timeout)
+        return await self._handle(msg)
+
+    async def rpc_push(self, msg: Message) -> Message:
+        """Server-to-server hop of a pushed chain (upstream ``rpc_push``); same body as rpc_forward."""
+        return await self._handle(msg)
+
+    async def rpc_inference(self, msg: Message) -> Message:
+        """Upstream Petals per-step inference API (petals/server/handler.py ``rpc_inference``).
+
+        Metadata: ``session_id``, ``step_id`` (a repeated step id returns the cached reply
+        instead of running twice), optional ``start_from_position`` (rewind the session to
+        that position before this step), ``max_length``; otherwise as ``rpc_forward``.
+        """
+        md = dict(msg.metadata)
+        sid, step_id = md.get("session_id"), md.get("step_id")
+        if sid is not None and step_id is not None:
+            cached = self._steps.get(sid, {}).get(str(step_id))
+            if cached is not None:
+                return cached
+        x = msg.tensors[0] if msg.tensors else None
+        if x is not None and "cur_len" not in md:
+            T = x.shape[-2] if x.dim() >= 2 and not self.executor.is_first else x.reshape(-1).shape[0]
+            sess = self.executor.sessions.get(sid) if sid is not None else None
+            start = md.get("start_from_position")
+            base = int(start) if start is not None else (sess.length if sess is not None else 0)
+            md["cur_len"] = base + int(T)
+            md.setdefault("is_prefill", sess is None or base == 0)
+        reply = await self._handle(Message(md, list(msg.tensors)))
+        if sid is not None and step_id is not None:
+            steps = self._steps.setdefault(sid, {})
+            steps[str(step_id)] = reply
+            while len(steps) > 64:
+                steps.pop(next(iter(steps)))
+        return reply
+
+    async def rpc_check_reachability(self, msg: Message) -> Message:
+        """Probe whether ``target`` (a multiaddr) is reachable from THIS server (upstream
+        petals/server/reachability.py: peers check each other's direct reachability)."""
+        target = msg.metadata.get("target")
+        if not target:
+            return Message({"ok": False, "error": "no target"})
+        t0 = time.perf_counter()
+        try:
+            if self._client is None:
+                self._client = RpcClient()
+            await self._client.call(target, HANDLER_PREFIX + "rpc_echo", Message({"ping": True}),
+                                    timeout=float(msg.metadata.get("timeout", 5.0)))
+            return Message({"ok": True, "rtt_s": time.perf_counter() - t0})
+        except Exception as e:  # noqa: BLE001 - any failure means "not reachable"
+            return Message({"ok": False, "error": f"{type(e).__name__}: {e}"})
+
+    async def _handle(self, msg: Message) -> Message:
+        reply = await asyncio.wait_for(self._submit(msg), self.request_timeout)
+        hops = msg.metadata.get("next_hops")
+        if not hops or self.final_stage:
+            return reply
+        return await self._push(msg.metadata, reply, list(hops))
+
+    async def _push(self, md: dict, reply: Message, hops: List[dict]) -> Message:
+        """Forward this stage's output to the next server of the chain and return the
+        downstream reply with this hop's output prepended (the client keeps every hop's
+        input for failover replay).  A downstream failure returns this hop's output with
+        ``push_failed_at`` = index (relative to this server) of the hop that failed."""
+        out = reply.tensors[0]
+        nxt, rest = hops[0], hops[1:]
+        fwd = {k: v for k, v in md.items() if k != "next_hops"}
+        if rest:
+            fwd["next_hops"] = rest
+        if self._client is None:
+            self._client = RpcClient()
+        self.stats["pushed"] += 1
+        err = None
+        for addr in nxt.get("maddrs") or []:
+            try:
+                down = await self._client.call(addr, HANDLER_PREFIX + "rpc_push", Message(fwd, [out]),
+                                               timeout=self.request_timeout * (1 + len(rest)))
+                dmd = dict(down.metadata)
+                if "push_failed_at" in dmd:
+                    dmd["push_failed_at"] = int(dmd["push_failed_at"]) + 1
+                    return Message(dmd, [out] + list(down.tensors))
+                # final reply: [token, hiddens...] -> [token, out, hiddens...]
+                if "token_id" in dmd:
+                    return Message(dmd, [down.tensors[0], out] + list(down.tensors[1:]))
+                return Message(dmd, [out] + list(down.tensors))
+            except (ConnectionError, OSError, asyncio.TimeoutError, RemoteError) as e:
+                err = e
+                self._client.drop(addr)
+        return Message({"session_id": md.get("session_id"), "push_failed_at": 1,
+                        "push_error": f"{type(err).__name__}: {err}" if err else "no address"}, [out])
 
     async def rpc_info(self, msg: Message) -> Message:
         ex = self.executor
@@ -97,6 +210,7 @@ class StageConnectionHandler:
     async def rpc_close_session(self, msg: Message) -> Message:
         sid = msg.metadata.get("session_id")
         if sid is not None:
+            self._steps.pop(sid, None)
             await asyncio.get_running_loop().run_in_executor(self._worker, self.executor.sessions.close, sid)
         return Message({"ok": True})
 
@@ -144,6 +258,7 @@ class StageConnectionHandler:
 
     async def _submit(self, msg: Message) -> Message:
         req = self._parse(msg)
+        req.priority = self.prioritizer.prioritize(int(req.x.shape[0]), bool(req.reset))
         req.fut = asyncio.get_running_loop().create_future()
         self._pending.append(req)
         self.stats["requests"] += 1
@@ -160,6 +275,8 @@ class StageConnectionHandler:
                 if self.batch_window > 0:
                     await asyncio.sleep(self.batch_window)
                 batch, rest, seen, ntok = [], [], set(), 0
+                # priority order (decode steps first), arrival order within a priority
+                self._pending.sort(key=lambda r: (r.priority, r.t0))
                 for r in self._pending:
                     n = r.x.shape[0]
                     if r.sid in seen or (batch and ntok + n > self.max_batch_tokens):
@@ -170,7 +287,7 @@ class StageConnectionHandler:
                     ntok += n
                 self._pending = rest
                 try:
-                    outs = await loop.run_in_executor(self._worker, self._run_batch, batch)
+                    outs = await self._run_with_alloc_wait(loop, batch)
                 except Exception as e:  # one bad request must not take the batch down: retry singly
                     if len(batch) == 1:
                         if not batch[0].fut.done():
@@ -191,6 +308,20 @@ class StageConnectionHandler:
                         r.fut.set_result(o)
         finally:
             self._draining = False
+
+    async def _run_with_alloc_wait(self, loop, batch: List[_Req]):
+        """Run a batch; when the KV cache is full, evict expired sessions and wait (up to
+        ``alloc_timeout``) for pages to be freed - upstream MemoryCache semantics
+        (petals/server/memory_cache.py: allocation waits, then ``AllocationFailed``)."""
+        deadline = time.perf_counter() + self.alloc_timeout
+        while True:
+            try:
+                return await loop.run_in_executor(self._worker, self._run_batch, batch)
+            except AllocationFailed:
+                await loop.run_in_executor(self._worker, self.executor.sessions.evict_expired)
+                if time.perf_counter() >= deadline:
+                    raise
+                await asyncio.sleep(0.05)
 
     def _run_batch(self, batch: List[_Req]) -> List[Message]:
         ex = self.executor

@@ -18,6 +18,14 @@ Fault tolerance (Petals-style, reference :587-712) with the reference's defects 
   with a different end block (:270-353);
 * recovery success is not reported as failure on the last attempt (reference :659-661).
 
+``push=True`` switches the data path to server-to-server forwarding (upstream Petals
+``rpc_push``): the client sends the step to the first hop with the rest of the route in
+``next_hops``; each server forwards its output to the next and the final token comes back
+along the chain together with every hop's output, so the client still records the per-hop
+history it needs for replay.  One client round trip per token instead of one per stage;
+a downstream failure comes back as ``push_failed_at`` and is recovered like a star-mode
+failure of that hop.
+
 ``hidden`` may be a GPU tensor; only the CPU copy crosses the wire.
 """
 from __future__ import annotations
@@ -62,7 +70,8 @@ class RpcTransport:
                  rpc_port: int = 8001, timeout: float = 30.0, temperature: float = 1.0, top_p: float = 0.92,
                  top_k: int = 50, stage_keys: Optional[List[str]] = None, routing: str = "stage",
                  model_name: str = "default", total_blocks: Optional[int] = None, start_block: int = 0,
-                 dht: Optional[DHT] = None, repetition_penalty: Optional[float] = None, max_recovery_attempts: int = 3):
+                 dht: Optional[DHT] = None, repetition_penalty: Optional[float] = None, max_recovery_attempts: int = 3,
+                 push: bool = False):
         self.device = device
         self.stage = stage
         self.dht_port, self.rpc_port = dht_port, rpc_port
@@ -76,6 +85,7 @@ class RpcTransport:
         if repetition_penalty is not None:
             self.sampling["repetition_penalty"] = float(repetition_penalty)
         self.max_recovery_attempts = max_recovery_attempts
+        self.push = bool(push)
         self._last_token: Optional[int] = None
         self.last_prefill_stage_times: List[Tuple[str, float]] = []
         self.last_prefill_total: Optional[float] = None
@@ -222,6 +232,9 @@ class RpcTransport:
         hist.update(new_hist)
         self.client_cache[session_id] = hist
 
+    def _record(self, session_id: str, hop: Hop, x: torch.Tensor) -> None:
+        self.client_cache.setdefault(session_id, {}).setdefault(hop.start, []).append(x.clone())
+
     async def _send(self, session_id: str, hidden: torch.Tensor, md: dict, which: str):
         t_all = time.perf_counter()
         x = hidden.detach().to("cpu")
@@ -234,16 +247,44 @@ class RpcTransport:
         while k < len(route):
             hop = route[k]
             t0 = time.perf_counter()
+            failed_exc: Optional[BaseException] = None
+            resp = None
+            push = self.push and k + 1 < len(route)
             try:
-                resp = await self._call(hop, x, md)
+                call_md = md
+                if push:
+                    call_md = dict(md, next_hops=[{"key": h.key, "peer_id": h.peer_id, "maddrs": h.maddrs}
+                                                  for h in route[k + 1:]])
+                resp = await self._call(hop, x, call_md)
             except RECOVERABLE as e:
+                failed_exc = e
+            if resp is not None and push:
+                # chain reply: outputs of hops k.. (+ token if the chain completed)
+                pf = resp.metadata.get("push_failed_at")
+                final = pf is None
+                hiddens = list(resp.tensors[1:] if final else resp.tensors)
+                j = len(route) if final else k + int(pf)
+                inp = x
+                for i in range(k, j):
+                    self._record(session_id, route[i], inp)
+                    if i - k < len(hiddens):
+                        inp = hiddens[i - k]
+                        if inp.dim() == 2:
+                            inp = inp.unsqueeze(0)
+                times.append((f"push:{hop.key}", time.perf_counter() - t0))
+                if final:
+                    return self._finish(which, times, t_all, resp)
+                x, k, hop = inp, j, route[j]
+                failed_exc = ConnectionError(resp.metadata.get("push_error", "push failed"))
+            if failed_exc is not None:
                 attempts += 1
-                logger.warning(f"hop {hop} failed ({type(e).__name__}: {e}); recovery {attempts}/"
+                logger.warning(f"hop {hop} failed ({type(failed_exc).__name__}: {failed_exc}); recovery {attempts}/"
                                f"{self.max_recovery_attempts}")
                 self.failed_peers.setdefault(hop.key, set()).add(hop.peer_id)
                 self.client.drop(hop.maddrs[0]) if hop.maddrs else None
                 if attempts > self.max_recovery_attempts:
-                    raise RuntimeError(f"failed to recover {hop.key} after {self.max_recovery_attempts} attempts") from e
+                    raise RuntimeError(f"failed to recover {hop.key} after {self.max_recovery_attempts} attempts") \
+                        from failed_exc
                 exclude = set().union(*self.failed_peers.values())
                 try:
                     tail = await asyncio.get_running_loop().run_in_executor(None, self._route_tail, route, k, exclude)
@@ -256,22 +297,25 @@ class RpcTransport:
                     await asyncio.sleep(0.5)
                 continue
             times.append((hop.key, time.perf_counter() - t0))
-            self.client_cache.setdefault(session_id, {}).setdefault(hop.start, []).append(x.clone())
+            self._record(session_id, hop, x)
             if hop.expect_hidden:
                 x = resp.tensors[0]
                 if x.dim() == 2:
                     x = x.unsqueeze(0)
                 k += 1
                 continue
-            total = time.perf_counter() - t_all
-            if which == "prefill":
-                self.last_prefill_stage_times, self.last_prefill_total = times, total
-            else:
-                self.last_decode_stage_times, self.last_decode_total = times, total
-                self.decode_stage_history.append(times)
-                self.decode_total_times.append(total)
-            return self._token_of(resp)
+            return self._finish(which, times, t_all, resp)
         raise RuntimeError("No final stage returned a token")
+
+    def _finish(self, which: str, times, t_all: float, resp: Message) -> int:
+        total = time.perf_counter() - t_all
+        if which == "prefill":
+            self.last_prefill_stage_times, self.last_prefill_total = times, total
+        else:
+            self.last_decode_stage_times, self.last_decode_total = times, total
+            self.decode_stage_history.append(times)
+            self.decode_total_times.append(total)
+        return self._token_of(resp)
 
     # ------------------------------------------------------------------ public API
     def send_prefill(self, L: int, hidden: torch.Tensor, session_id: str, max_length: int):

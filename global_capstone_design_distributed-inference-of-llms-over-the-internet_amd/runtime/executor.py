@@ -136,6 +136,7 @@ class StageExecutor:
             ops.require_native()
             if cfg.model_type != "gpt2" and ops.gemm_policy() != "hipblaslt":
                 weights.pack_for_decode()
+                ops.gemm_workspace(self.device)  # allocated before any hipGraph capture
         logger.info(f"StageExecutor blocks [{self.start},{self.end}) embed={self.is_first} head={self.is_last} "
                     f"kv_pages={num_pages} x {page_size} tokens ({self.cache.nbytes / 2**30:.2f} GiB) "
                     f"graphs={self.use_graphs}")

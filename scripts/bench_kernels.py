@@ -43,11 +43,16 @@ def gemm_rows(Ms, shapes):
             x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
             xp = ops.pack_act(x)  # decode path: activations arrive packed from their producer
             y = torch.empty(M, N // 2 if epi == 1 else N, device="cuda", dtype=torch.bfloat16)
+            ops.set_gemm_sk("off")
             t_nat = timeit(lambda: ops.linear(xp, None, out=y, epilogue=epi, wp=wp, a_rows=M))
+            ops.set_gemm_sk("on")
+            t_sk = timeit(lambda: ops.linear(xp, None, out=y, epilogue=epi, wp=wp, a_rows=M))
+            ops.set_gemm_sk("auto")
             t_lib = timeit(lambda: ops.linear(x, w, out=y, epilogue=epi, policy="hipblaslt"))
             byts = N * K * 2
             out.append(dict(kernel="gemm", name=name, M=M, N=N, K=K, native_us=round(t_nat, 2),
-                            hipblaslt_us=round(t_lib, 2), native_TBps=round(byts / t_nat / 1e6, 2),
+                            streamk_us=round(t_sk, 2), hipblaslt_us=round(t_lib, 2),
+                            native_TBps=round(byts / t_nat / 1e6, 2), streamk_TBps=round(byts / t_sk / 1e6, 2),
                             hipblaslt_TBps=round(byts / t_lib / 1e6, 2)))
             print(json.dumps(out[-1]), flush=True)
     return out

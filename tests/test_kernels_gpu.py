@@ -185,6 +185,53 @@ def test_gemm_swiglu_and_residual_epilogues(M):
     torch.testing.assert_close(y2.float(), x.float() @ w2.float().t() + r.float(), atol=5e-2, rtol=3e-2)
 
 
+@pytest.mark.parametrize("sk", ["on", "off"])
+@pytest.mark.parametrize("M", [1, 16, 17, 48, 64])
+@pytest.mark.parametrize("N,K", [(4096, 4096), (12288, 4096), (4096, 11008), (1024, 1024), (22016, 4096),
+                                 (32000, 4096), (192, 8192)])
+def test_gemm_stream_k(M, N, K, sk):
+    """Stream-K decode GEMM (split groups, cross-workgroup slab fixup) vs fp32 reference;
+    repeated launches must be bit-identical (counters re-zeroed, fixed reduction order)."""
+    x = bf(torch.randn(M, K, device=DEV))
+    w = bf(torch.randn(N, K, device=DEV) * 0.02)
+    wp = ops.pack_weight(w)
+    xp = ops.pack_act(x)
+    ops.set_gemm_sk(sk)
+    try:
+        y1 = ops.linear(xp, None, wp=wp, a_rows=M)
+        y2 = ops.linear(xp, None, wp=wp, a_rows=M)
+        y3 = ops.linear(x, None, policy="native", wp=wp)
+    finally:
+        ops.set_gemm_sk("auto")
+    torch.cuda.synchronize()
+    yr = x.float() @ w.float().t()
+    torch.testing.assert_close(y1.float(), yr, atol=3e-2, rtol=2e-2)
+    assert torch.equal(y1, y2)
+    assert torch.equal(y1, y3)
+    assert int(ops.gemm_workspace(DEV)[:4 * 4096].view(torch.int32).abs().sum()) == 0  # counters re-zeroed
+
+
+@pytest.mark.parametrize("M", [5, 33, 64])
+def test_gemm_stream_k_swiglu_packed_out(M):
+    K, F = 4096, 11008
+    from src.models.weights import interleave_gate_up
+
+    x = bf(torch.randn(M, K, device=DEV))
+    gate = bf(torch.randn(F, K, device=DEV) * 0.02)
+    up = bf(torch.randn(F, K, device=DEV) * 0.02)
+    gu = interleave_gate_up(gate, up)
+    wp = ops.pack_weight(gu)
+    ops.set_gemm_sk("on")
+    try:
+        yp = ops.linear(ops.pack_act(x), None, epilogue=1, wp=wp, a_rows=M, out_packed=True)
+        y = ops.linear(x, None, epilogue=1, policy="native", wp=wp)
+    finally:
+        ops.set_gemm_sk("auto")
+    g, u = x.float() @ gate.float().t(), x.float() @ up.float().t()
+    torch.testing.assert_close(y.float(), torch.nn.functional.silu(g) * u, atol=3e-2, rtol=3e-2)
+    assert torch.equal(ops.unpack_act(yp, M, F), y)
+
+
 def test_sampler_greedy_and_topk1():
     R, V = 6, 32000
     logits = bf(torch.randn(R, V, device=DEV) * 3)

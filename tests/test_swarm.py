@@ -45,13 +45,13 @@ def test_fixed_three_stage_generation_matches_reference():
         s2.close()
 
 
-def _client(peers, cuts, routing="stage", total=None):
+def _client(peers, cuts, routing="stage", total=None, push=False):
     cfg = resolve_model(MODEL)
     w = random_stage_weights(cfg, 0, cuts[0], has_embed=True, has_head=False, device="cpu", dtype=torch.float32)
     ex = StageExecutor(cfg, w, "cpu", dtype=torch.float32, kv_cache_bytes=8 << 20, max_sessions=4, max_seq_len=128)
     tx = RpcTransport("cpu", 0, [peers], timeout=5.0, temperature=0.0,
                       stage_keys=[get_stage_key(i) for i in range(1, len(cuts) + 1)], routing=routing,
-                      model_name=MODEL, total_blocks=total or cfg.num_hidden_layers, start_block=cuts[0])
+                      model_name=MODEL, total_blocks=total or cfg.num_hidden_layers, start_block=cuts[0], push=push)
     return cfg, ex, tx
 
 
@@ -116,3 +116,94 @@ def test_load_balanced_servers_and_module_routing():
     finally:
         a.close()
         b.close()
+
+
+@pytest.mark.timeout(180)
+def test_push_chain_matches_reference_and_records_history():
+    """Server-to-server forwarding (upstream rpc_push): one client call per token."""
+    s1 = ServerThread(server_argv(MODEL, "1,2", 1)).wait()
+    s2 = ServerThread(server_argv(MODEL, "1,2", 2, peers=s1.addr)).wait()
+    try:
+        assert wait_for(lambda: s1.dht.get(get_stage_key(2)) is not None)
+        cfg, ex, tx = _client(s1.addr, [1, 2], push=True)
+        gen = _generate(ex, tx, 6)
+        assert gen == _reference(6)
+        assert s1.srv.handler.stats["pushed"] >= 6
+        assert all(name.startswith("push:") for name, _ in tx.last_decode_stage_times)
+        hist = next(iter(tx.client_cache.values()))
+        assert sorted(hist) == [1, 2] and len(hist[1]) == len(hist[2]) == 6
+        tx.shutdown()
+    finally:
+        s1.close()
+        s2.close()
+
+
+@pytest.mark.timeout(180)
+def test_push_chain_downstream_failure_recovers_on_replica():
+    s1 = ServerThread(server_argv(MODEL, "1,2", 1)).wait()
+    s2 = ServerThread(server_argv(MODEL, "1,2", 2, peers=s1.addr)).wait()
+    s2b = ServerThread(server_argv(MODEL, "1,2", 2, peers=s1.addr)).wait()
+    try:
+        assert wait_for(lambda: len(s1.dht.get(get_stage_key(2)).value) == 2)
+        cfg, ex, tx = _client(s1.addr, [1, 2], push=True)
+        killed = []
+
+        def kill_last(i):
+            if i == 2:
+                pid = tx.session_routes[next(iter(tx.session_routes))][1].peer_id
+                victim = s2 if s2.srv.peer_id == pid else s2b
+                victim.kill()
+                killed.append(victim)
+
+        gen = _generate(ex, tx, 8, kill_last)
+        assert killed and tx.failed_peers
+        assert gen == _reference(8)
+        tx.shutdown()
+    finally:
+        for s in (s1, s2, s2b):
+            s.close()
+
+
+@pytest.mark.timeout(120)
+def test_rpc_inference_step_dedup_and_reachability():
+    from src.comm.rpc import RpcClient, get_loop
+    from src.comm.wire import Message
+
+    s1 = ServerThread(server_argv(MODEL, "2", 1)).wait()
+    try:
+        cfg = resolve_model(MODEL)
+        addr = s1.srv.maddrs[0]
+        cl = RpcClient()
+        loop = get_loop()
+        h = torch.randn(1, 3, cfg.hidden_size)
+
+        def call(name, md, tensors=()):
+            return loop.run(cl.call(addr, "StageConnectionHandler." + name, Message(md, list(tensors)), 10.0))
+
+        md = {"session_id": "s-1", "step_id": "a", "temperature": 0.0}
+        r1 = call("rpc_inference", md, [h])
+        r2 = call("rpc_inference", md, [h])  # same step id: served from the dedup cache
+        assert r1.metadata["token_id"] == r2.metadata["token_id"]
+        assert s1.srv.ex.sessions.get("s-1").length == 3
+        r3 = call("rpc_inference", {"session_id": "s-1", "step_id": "b", "temperature": 0.0}, [h[:, :1]])
+        assert s1.srv.ex.sessions.get("s-1").length == 4
+        # rewind: re-run step b's position
+        call("rpc_inference", {"session_id": "s-1", "step_id": "c", "start_from_position": 3, "temperature": 0.0},
+             [h[:, :1]])
+        assert s1.srv.ex.sessions.get("s-1").length == 4
+        assert "token_id" in r3.metadata
+        ok = call("rpc_check_reachability", {"target": addr})
+        assert ok.metadata["ok"] is True
+        bad = call("rpc_check_reachability", {"target": "/ip4/127.0.0.1/tcp/1/p2p/x", "timeout": 1.0})
+        assert bad.metadata["ok"] is False
+        loop.run(cl.close())
+    finally:
+        s1.close()
+
+
+def test_task_prioritizer_orders_decode_first():
+    from src.rpc_handler import TaskPrioritizer
+
+    p = TaskPrioritizer()
+    assert p.prioritize(1, False) < p.prioritize(128, True)
+    assert p.prioritize(1, True) == p.prioritize(5, False)

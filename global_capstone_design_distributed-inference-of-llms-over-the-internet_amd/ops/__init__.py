@@ -85,7 +85,7 @@ def gemm_policy() -> str:
 
 # Stream-K decode GEMM (gemm.hip, gemm_sk_kernel): "auto" = for M > SK_MIN_M; "on" = every
 # decode GEMM it covers; "off" = the one-group-per-workgroup kernel only.
-_GEMM_SK = os.environ.get("MPAMD_GEMM_SK", "auto")
+_GEMM_SK = os.environ.get("MPAMD_GEMM_SK", "off")
 SK_MIN_M = int(os.environ.get("MPAMD_GEMM_SK_MIN_M", "16"))
 _GEMM_WS = {}
 

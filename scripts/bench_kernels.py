@@ -47,7 +47,7 @@ def gemm_rows(Ms, shapes):
             t_nat = timeit(lambda: ops.linear(xp, None, out=y, epilogue=epi, wp=wp, a_rows=M))
             ops.set_gemm_sk("on")
             t_sk = timeit(lambda: ops.linear(xp, None, out=y, epilogue=epi, wp=wp, a_rows=M))
-            ops.set_gemm_sk("auto")
+            ops.set_gemm_sk("off")
             t_lib = timeit(lambda: ops.linear(x, w, out=y, epilogue=epi, policy="hipblaslt"))
             byts = N * K * 2
             out.append(dict(kernel="gemm", name=name, M=M, N=N, K=K, native_us=round(t_nat, 2),

@@ -90,6 +90,10 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--push", action="store_true",
                    help="client: server-to-server forwarding along the route (one client round trip per token)")
     p.add_argument("--alloc_timeout", type=float, default=5.0, help="server: wait this long for free KV pages")
+    p.add_argument("--auto_num_blocks", action="store_true",
+                   help="LB server: size the span from free HBM (upstream Petals num_blocks=None behaviour)")
+    p.add_argument("--throughput_cache", type=str, default=None,
+                   help="LB server: JSON cache of throughput measurements ('' disables; default: no cache)")
     p.add_argument("--log_level", type=str, default=None)
     return p
 
@@ -314,9 +318,20 @@ def run_stage_server_with_load_balancing(args, device, cuts: List[int], stop: Op
                                          on_ready=None):
     cfg = resolve_model(args.model)
     total = args.total_blocks or cfg.num_hidden_layers
-    num_blocks = args.num_blocks or 4
     min_block = cuts[0] if cuts else 0
     dtype = resolve_dtype(args.dtype, device)
+    if args.num_blocks is None and getattr(args, "auto_num_blocks", False) and device.type == "cuda":
+        from .block_utils import auto_num_blocks
+
+        num_blocks = auto_num_blocks(cfg, dtype=dtype, device=device, total_blocks=total - min_block)
+        logger.info(f"auto num_blocks = {num_blocks}")
+    else:
+        num_blocks = args.num_blocks or 4
+    tcache = None
+    if getattr(args, "throughput_cache", None):
+        from .throughput_measurement import ThroughputCache
+
+        tcache = ThroughputCache(args.throughput_cache)
     dht = _start_dht(args)
     stop = stop or threading.Event()
     _install_signal_handlers(stop)
@@ -341,7 +356,7 @@ def run_stage_server_with_load_balancing(args, device, cuts: List[int], stop: Op
         full = load_stage_model(args.model, device, "last" if final else "segment", start=s, end=e, dtype=dtype,
                                 seed=args.seed, **_executor_kwargs(args))
         ex = StageExecutor(cfg, full.weights, device, dtype=dtype, **full.executor_kwargs)
-        thr = get_server_throughput(ex, args.network_bandwidth_mbps)
+        thr = get_server_throughput(ex, args.network_bandwidth_mbps, cache=tcache)
         srv = _Server(args, dht, ex, final, args.stage, throughput=thr, lb=True)
         if on_ready is not None:
             on_ready(dht, srv)

@@ -245,7 +245,7 @@ template <int MT, int NT, int D, int EPI, bool OPK>
 __global__ __launch_bounds__(512) void gemm_sk_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ wp,
                                                       bf16_t* __restrict__ y, int64_t ys, const bf16_t* __restrict__ res,
                                                       int64_t rs, int M, int N, int K, int* __restrict__ cnt,
-                                                      f32x4* __restrict__ slab) {
+                                                      f32x4* __restrict__ slab, int remap) {
   constexpr int Q = MT * NT;  // accumulator quads (f32x4) per lane
   __shared__ __attribute__((aligned(16))) f32x4 red[8 * Q * 64 + 16];
   int* s_flag = reinterpret_cast<int*>(red + 8 * Q * 64);
@@ -254,7 +254,7 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(const bf16_t* __restrict__
   const int nks = K >> 5;
   const int U = ((N >> 4) / NT) * nks;
   // logical workgroup id: consecutive ranges (which share split groups) on the same XCD
-  const int lb = (G & 7) ? (int)blockIdx.x : (int)(blockIdx.x & 7) * (G >> 3) + (int)(blockIdx.x >> 3);
+  const int lb = ((G & 7) || !remap) ? (int)blockIdx.x : (int)(blockIdx.x & 7) * (G >> 3) + (int)(blockIdx.x >> 3);
   const int u0 = (int)((int64_t)lb * U / G), u1 = (int)((int64_t)(lb + 1) * U / G);
   const int c_first = u0 >> 3, nch = ((u1 - 1) >> 3) + 1 - c_first;
   auto start_of = [&](int b) { return (int)((int64_t)b * U / G); };
@@ -399,7 +399,7 @@ static int sk_num_cus() {
 
 template <int MT, int NT, int D>
 static int launch_gemm_sk_cfg(const void* x, void* y, int64_t ys, const void* w, const void* res, int64_t rs, int M,
-                              int N, int K, int epi, int flags, void* ws, int gmul, hipStream_t stream) {
+                              int N, int K, int epi, int flags, void* ws, int gmul, int remap, hipStream_t stream) {
   const int nks = K / 32;
   const int ngrp = (N / 16) / NT;
   if ((N / 16) % NT || nks % 8 || nks < 8 * D || ngrp > SK_MAX_GROUPS) return 1;  // caller falls back
@@ -412,7 +412,7 @@ static int launch_gemm_sk_cfg(const void* x, void* y, int64_t ys, const void* w,
   const bool opk = flags & 2;
 #define MP_SK(EPI_, OPK_)                                                                                         \
   hipLaunchKernelGGL((gemm_sk_kernel<MT, NT, D, EPI_, OPK_>), dim3(G), dim3(512), 0, stream, (const bf16_t*)x,     \
-                     (const bf16_t*)w, (bf16_t*)y, ys, (const bf16_t*)res, rs, M, N, K, cnt, slab)
+                     (const bf16_t*)w, (bf16_t*)y, ys, (const bf16_t*)res, rs, M, N, K, cnt, slab, remap)
   if (epi == 1) {
     if (opk) { MP_SK(1, true); } else { MP_SK(1, false); }
   } else if (opk) {
@@ -436,10 +436,10 @@ static int launch_gemm_sk(const void* x, void* y, int64_t ys, const void* w, con
                           int K, int epi, int flags, void* ws, hipStream_t stream) {
   // tuning knobs (experiments): MPAMD_SK_CFG 0 = NT 4 / ring 4 (3 for MT >= 3), 1 = NT 2 / ring 4,
   // 2 = NT 4 / ring 2; MPAMD_SK_GM = workgroups per CU
-  static const int cfg = sk_env("MPAMD_SK_CFG", 0), gm = sk_env("MPAMD_SK_GM", 1);
-  if (cfg == 1) return launch_gemm_sk_cfg<MT, 2, 4>(x, y, ys, w, res, rs, M, N, K, epi, flags, ws, gm, stream);
-  if (cfg == 2) return launch_gemm_sk_cfg<MT, 4, 2>(x, y, ys, w, res, rs, M, N, K, epi, flags, ws, gm, stream);
-  return launch_gemm_sk_cfg<MT, 4, (MT >= 3 ? 3 : 4)>(x, y, ys, w, res, rs, M, N, K, epi, flags, ws, gm, stream);
+  static const int cfg = sk_env("MPAMD_SK_CFG", 0), gm = sk_env("MPAMD_SK_GM", 1), rm = sk_env("MPAMD_SK_REMAP", 1);
+  if (cfg == 1) return launch_gemm_sk_cfg<MT, 2, 4>(x, y, ys, w, res, rs, M, N, K, epi, flags, ws, gm, rm, stream);
+  if (cfg == 2) return launch_gemm_sk_cfg<MT, 4, 2>(x, y, ys, w, res, rs, M, N, K, epi, flags, ws, gm, rm, stream);
+  return launch_gemm_sk_cfg<MT, 4, (MT >= 3 ? 3 : 4)>(x, y, ys, w, res, rs, M, N, K, epi, flags, ws, gm, rm, stream);
 }
 
 // Pack W[N, K] (row-major) into the fragment-native layout Wp[N/16][K/32][64][8].

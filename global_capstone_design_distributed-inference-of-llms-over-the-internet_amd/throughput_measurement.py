@@ -9,10 +9,19 @@ Here the compute probe is a real decode step of the stage executor on a probe se
 (paged KV, hipGraph replay where available), timed with HIP events; the network term can
 also be *measured* on a live link (``measure_link_bandwidth``: round trips of an H-sized
 activation over the framework's TCP transport) instead of assumed.
+
+Upstream Petals (petals/server/throughput.py) additionally measures a
+prefill rate (``forward_rps``, 1024-token forwards) and caches measurements in a JSON file
+under a system-wide ``flock`` so restarts and co-located servers do not re-measure:
+``measure_forward_throughput`` and ``ThroughputCache`` / ``get_server_throughput(cache=...)``.
 """
 from __future__ import annotations
 
+import contextlib
+import fcntl
+import json
 import logging
+import os
 import time
 import uuid
 from typing import Optional
@@ -59,6 +68,76 @@ def measure_compute_throughput(executor, n_warmup: int = 2, n_steps: int = 10, b
             executor.sessions.close(s)
 
 
+def measure_forward_throughput(executor, n_tokens: int = 1024, n_steps: int = 3) -> float:
+    """Prefill rate: tokens/s of ``n_tokens``-token forwards through the whole span (upstream
+    ``forward_rps`` x tokens).  Each step is a fresh probe session (prefill from position 0)."""
+    H = executor.cfg.hidden_size
+    dev = executor.device
+    n_tokens = int(min(n_tokens, executor.max_tokens, executor.max_seq_len))
+    if executor.is_first:
+        x = torch.randint(0, executor.cfg.vocab_size, (n_tokens,), device=dev)
+    else:
+        x = torch.randn(n_tokens, H, device=dev).to(executor.dtype)
+    sid = f"__probe_fwd_{uuid.uuid4().hex[:8]}"
+    try:
+        executor.forward([(sid, n_tokens)], x, reset=[True])
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(n_steps):
+            executor.forward([(sid, n_tokens)], x, reset=[True])
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        return n_steps * n_tokens / max(time.perf_counter() - t0, 1e-9)
+    finally:
+        executor.sessions.close(sid)
+
+
+class ThroughputCache:
+    """JSON file of past measurements keyed by (model, span, dtype, device), guarded by an
+    exclusive ``flock`` (upstream: one system-wide lock + ``throughput_v2.json``)."""
+
+    def __init__(self, path: Optional[str] = None):
+        self.path = path or os.path.join(os.path.expanduser(os.environ.get("MPAMD_CACHE_DIR", "~/.cache/mpamd")),
+                                         "throughput_v1.json")
+
+    @contextlib.contextmanager
+    def _locked(self):
+        os.makedirs(os.path.dirname(self.path), exist_ok=True)
+        with open(self.path + ".lock", "w") as lf:
+            fcntl.flock(lf, fcntl.LOCK_EX)
+            try:
+                yield
+            finally:
+                fcntl.flock(lf, fcntl.LOCK_UN)
+
+    def _read(self) -> dict:
+        try:
+            with open(self.path) as f:
+                return json.load(f)
+        except (OSError, ValueError):
+            return {}
+
+    @staticmethod
+    def key(executor) -> str:
+        dev = executor.device
+        name = torch.cuda.get_device_name(dev) if dev.type == "cuda" else "cpu"
+        return f"{executor.cfg.name}|{executor.start}-{executor.end}|{executor.dtype}|{name}"
+
+    def get(self, key: str) -> Optional[dict]:
+        with self._locked():
+            return self._read().get(key)
+
+    def put(self, key: str, value: dict) -> None:
+        with self._locked():
+            d = self._read()
+            d[key] = value
+            tmp = self.path + ".tmp"
+            with open(tmp, "w") as f:
+                json.dump(d, f, indent=1, sort_keys=True)
+            os.replace(tmp, self.path)
+
+
 def estimate_network_throughput(hidden_size: int, dtype_bytes: int = 2,
                                 bandwidth_mbps: Optional[float] = None) -> float:
     """Requests/s the link can carry for one [1, 1, H] activation (reference :157-190)."""
@@ -68,12 +147,21 @@ def estimate_network_throughput(hidden_size: int, dtype_bytes: int = 2,
 
 
 def get_server_throughput(executor, network_bandwidth_mbps: Optional[float] = None,
-                          relay_penalty: float = RELAY_PENALTY, n_warmup: int = 2, n_steps: int = 10) -> float:
-    try:
-        compute = measure_compute_throughput(executor, n_warmup, n_steps)
-    except Exception as e:
-        logger.warning(f"compute throughput probe failed ({e!r}); using fallback {FALLBACK_THROUGHPUT}")
-        return FALLBACK_THROUGHPUT
+                          relay_penalty: float = RELAY_PENALTY, n_warmup: int = 2, n_steps: int = 10,
+                          cache: Optional[ThroughputCache] = None, force_eval: bool = False) -> float:
+    key = ThroughputCache.key(executor) if cache is not None else None
+    cached = cache.get(key) if (cache is not None and not force_eval) else None
+    if cached and "compute_rps" in cached:
+        compute = float(cached["compute_rps"])
+        logger.info(f"Server throughput: cached compute={compute:.2f} rps ({key})")
+    else:
+        try:
+            compute = measure_compute_throughput(executor, n_warmup, n_steps)
+        except Exception as e:
+            logger.warning(f"compute throughput probe failed ({e!r}); using fallback {FALLBACK_THROUGHPUT}")
+            return FALLBACK_THROUGHPUT
+        if cache is not None:
+            cache.put(key, {"compute_rps": compute, "measured_at": time.time()})
     elt = torch.tensor([], dtype=executor.dtype).element_size()
     network = estimate_network_throughput(executor.cfg.hidden_size, elt, network_bandwidth_mbps) * (1 - relay_penalty)
     final = min(compute, network)

@@ -101,3 +101,48 @@ def test_rebalance_never_uncovers(spec):
         should_choose_other_blocks(pid, infos, 0.75, total_blocks=total, rng=np.random.default_rng(1))
     # the call must not mutate the caller's records
     assert compute_throughputs(compute_spans(infos), total).sum() > 0
+
+
+def test_block_utils_sizes_and_auto_num_blocks():
+    import torch
+
+    from src.block_utils import (auto_num_blocks, default_attn_cache_tokens, get_block_size, kv_cache_bytes_per_block,
+                                 resolve_block_dtype)
+    from src.models.config import resolve_model
+
+    cfg = resolve_model("llama2-7b")
+    # 4096*12288 + 4096*4096 + 3*4096*11008 + 2*4096 parameters
+    n = 4096 * 12288 + 4096 * 4096 + 3 * 4096 * 11008 + 2 * 4096
+    assert get_block_size(cfg, "memory", torch.bfloat16) == 2 * n
+    assert get_block_size(cfg, "disk", torch.float32) == 4 * n
+    fp8 = get_block_size(cfg, "memory", torch.bfloat16, quant_type="fp8")
+    assert n - 2 * 4096 < fp8 < 1.01 * n
+    assert resolve_block_dtype(cfg, "auto") == torch.bfloat16
+    assert default_attn_cache_tokens(cfg) == 4096
+    assert default_attn_cache_tokens(resolve_model("llama3-8b")) == 16384
+    per = get_block_size(cfg) + kv_cache_bytes_per_block(cfg)
+    assert auto_num_blocks(cfg, free_bytes=10 * per + (2 << 30)) == 10
+    assert auto_num_blocks(cfg, free_bytes=288 << 30) == 32  # a whole Llama-2-7B fits one MI355X
+    assert auto_num_blocks(cfg, free_bytes=1) == 1
+
+
+def test_throughput_cache_roundtrip(tmp_path):
+    import torch
+
+    from src.models.config import resolve_model
+    from src.models.weights import random_stage_weights
+    from src.runtime.executor import StageExecutor
+    from src.throughput_measurement import ThroughputCache, get_server_throughput, measure_forward_throughput
+
+    cfg = resolve_model("tiny-llama")
+    w = random_stage_weights(cfg, 0, 2, has_embed=False, has_head=False, device="cpu", dtype=torch.float32)
+    ex = StageExecutor(cfg, w, "cpu", dtype=torch.float32, kv_cache_bytes=8 << 20, max_sessions=4, max_seq_len=256,
+                       max_tokens_per_step=128)
+    cache = ThroughputCache(str(tmp_path / "tp.json"))
+    t1 = get_server_throughput(ex, 1e6, cache=cache, n_steps=2)
+    key = ThroughputCache.key(ex)
+    assert cache.get(key)["compute_rps"] > 0
+    cache.put(key, {"compute_rps": 12.5})
+    assert get_server_throughput(ex, 1e6, cache=cache) == 12.5  # served from the cache
+    assert t1 > 0
+    assert measure_forward_throughput(ex, n_tokens=64, n_steps=1) > 0

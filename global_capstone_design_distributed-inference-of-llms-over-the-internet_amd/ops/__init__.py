@@ -83,11 +83,13 @@ def gemm_policy() -> str:
     return _GEMM_POLICY
 
 
-# Stream-K decode GEMM (gemm.hip, gemm_sk_kernel): "auto" = for M > SK_MIN_M; "on" = every
-# decode GEMM it covers; "off" = the one-group-per-workgroup kernel only.
-_GEMM_SK = os.environ.get("MPAMD_GEMM_SK", "off")
-SK_MIN_M = int(os.environ.get("MPAMD_GEMM_SK_MIN_M", "16"))
+# Decode GEMM kernel choice (gemm.hip): the one-group-per-workgroup kernel or the stream-K
+# kernel.  "auto" = per (M bucket, N, K, epilogue) choice measured by ``autotune_gemm`` (the
+# executor tunes its own shapes at start-up; untuned shapes use the first kernel); "on" /
+# "off" force the stream-K kernel on / off wherever it applies.
+_GEMM_SK = os.environ.get("MPAMD_GEMM_SK", "auto")
 _GEMM_WS = {}
+_SK_CHOICE = {}  # (m_bucket, N, K, epilogue) -> bool
 
 
 def set_gemm_sk(mode: str) -> None:
@@ -97,7 +99,8 @@ def set_gemm_sk(mode: str) -> None:
 
 
 def gemm_workspace(device) -> torch.Tensor:
-    """Per-device scratch of the stream-K GEMM: split-group arrival counters + fp32 slabs.
+    """Per-device scratch of the stream-K GEMM: split-group arrival counters, a zero A
+    fragment for masked units, and fp32 partial slabs.
 
     Zero-initialised once; the kernel leaves the counters at zero after every launch, so the
     buffer is reusable by every later launch and graph replay.  One compute stream per device
@@ -115,14 +118,68 @@ def gemm_workspace(device) -> torch.Tensor:
     return ws
 
 
-def _use_sk(M: int, N: int, K: int, epilogue: int) -> bool:
-    if _GEMM_SK == "off":
-        return False
+def _m_bucket(M: int) -> int:
+    return 16 * ((M + 15) // 16)
+
+
+def _sk_covered(N: int, K: int) -> bool:
     nks = K // 32
-    covered = (N // 16) % 4 == 0 and nks % 8 == 0 and nks >= 32
-    if not covered:
+    return (N // 16) % 2 == 0 and nks % 8 == 0 and nks >= 32
+
+
+def _use_sk(M: int, N: int, K: int, epilogue: int) -> bool:
+    if _GEMM_SK == "off" or not _sk_covered(N, K):
         return False
-    return _GEMM_SK == "on" or M > SK_MIN_M
+    if _GEMM_SK == "on":
+        return True
+    return _SK_CHOICE.get((_m_bucket(M), N, K, int(epilogue)), False)
+
+
+def autotune_gemm(shapes, device, ms=(16, 32, 48, 64), iters: int = 20) -> dict:
+    """Time both decode-GEMM kernels on each (N, K, epilogue) for each M bucket (random data,
+    HIP events) and record the faster one for ``linear``.  Returns the choice table."""
+    global _GEMM_SK
+    device = torch.device(device)
+    if device.type != "cuda":
+        return {}
+    require_native()
+    gemm_workspace(device)
+    saved = _GEMM_SK
+    try:
+        for (N, K, epi) in shapes:
+            if not _sk_covered(N, K):
+                continue
+            w = (torch.randn(N, K, device=device) * 0.02).to(torch.bfloat16)
+            wp = pack_weight(w)
+            ncols = N // 2 if epi == 1 else N
+            for M in ms:
+                key = (_m_bucket(M), N, K, int(epi))
+                if key in _SK_CHOICE:
+                    continue
+                xp = pack_act(torch.randn(M, K, device=device).to(torch.bfloat16))
+                y = torch.empty(packed_numel(M, ncols) if epi == 1 else M * ncols, dtype=torch.bfloat16,
+                                device=device)
+                res = torch.zeros(M, N, dtype=torch.bfloat16, device=device) if epi == 2 else None
+                out = y if epi == 1 else y.view(M, ncols)
+                t = {}
+                for mode in ("off", "on"):
+                    _GEMM_SK = mode
+                    fn = lambda: linear(xp, None, out=out, epilogue=epi, residual=res, wp=wp, a_rows=M,  # noqa: E731
+                                        out_packed=epi == 1)
+                    for _ in range(3):
+                        fn()
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    for _ in range(iters):
+                        fn()
+                    e1.record()
+                    e1.synchronize()
+                    t[mode] = e0.elapsed_time(e1) / iters
+                _SK_CHOICE[key] = t["on"] < 0.97 * t["off"]
+    finally:
+        _GEMM_SK = saved
+    return dict(_SK_CHOICE)
+
 
 
 # ---------------------------------------------------------------------------------------

@@ -29,6 +29,7 @@
 namespace mp {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
 
 __device__ __forceinline__ f32x4 mfma16(const u16x8& a, const u16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b), c,
@@ -301,6 +302,14 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(const bf16_t* __restrict__
         acc[mt][t] = (f32x4)(0.f);
       }
   };
+  // Split groups: this workgroup's partial goes out as a write-through (sc1) fp32 slab right
+  // away, but the hand-off (drain + arrival ticket) is deferred to the end of the range, so a
+  // split head group never stalls the weight stream (one ticket episode per workgroup).
+  // Guide §6 Guideline 16 R1: sc1 stores need no release fence; the reducer reads the slabs
+  // with sc1 loads, which need no acquire.
+  const __amdgpu_buffer_rsrc_t slab_rsrc =
+      __builtin_amdgcn_make_buffer_rsrc(slab, (short)0, (int)(SK_MAX_BLOCKS * 2 * Q * 64 * 16), 0x00020000);
+  int split_g0 = -1, split_g1 = -1;  // split head / tail group of this range (uniform)
   auto reduce = [&](int g) {
     lds_barrier();
     const bool whole = g * nks >= u0 && (g + 1) * nks <= u1;
@@ -312,39 +321,53 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(const bf16_t* __restrict__
       }
     } else {
       const int side = (u0 / nks == g) ? 0 : 1;
-      f32x4* my = slab + (int64_t)(lb * 2 + side) * Q * 64;
-      for (int qd = wid; qd < Q; qd += 8) my[qd * 64 + lane] = red_sum(qd);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      lds_barrier();
-      const int bf = block_of(g * nks), bl = block_of((g + 1) * nks - 1);
-      if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const int old = __hip_atomic_fetch_add(cnt + g, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int last = old == bl - bf;
-        if (last) {
-          __hip_atomic_store(cnt + g, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        *s_flag = last;
-      }
-      lds_barrier();
-      if (*s_flag) {
-        for (int qd = wid; qd < Q; qd += 8) {
-          if (EPI == 1 && (qd % NT) & 1) continue;
-          f32x4 v = (f32x4)(0.f), up = (f32x4)(0.f);
-          for (int b = bf; b <= bl; ++b) {
-            const int sd = (start_of(b) / nks == g) ? 0 : 1;
-            const f32x4* sb = slab + (int64_t)(b * 2 + sd) * Q * 64;
-            v += sb[qd * 64 + lane];
-            if (EPI == 1) up += sb[(qd + 1) * 64 + lane];
-          }
-          sk_epilogue<MT, NT, EPI, OPK>(qd, g, v, up, y, ys, res, rs, M, lane);
-        }
-      }
+      if (side == 0) split_g0 = g; else split_g1 = g;
+      for (int qd = wid; qd < Q; qd += 8)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, red_sum(qd)), slab_rsrc,
+                                               (((lb * 2 + side) * Q + qd) * 64 + lane) * 16, 0, 16);
     }
     lds_barrier();  // red may be overwritten by the next stage()
+  };
+  auto finish_splits = [&]() {
+    if (split_g0 < 0 && split_g1 < 0) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave: its sc1 slab stores landed
+    lds_barrier();
+    if (tid == 0) {
+#pragma unroll
+      for (int side = 0; side < 2; ++side) {
+        const int g = side ? split_g1 : split_g0;
+        int last = 0;
+        if (g >= 0) {
+          const int bf = block_of(g * nks), bl = block_of((g + 1) * nks - 1);
+          const int old = __hip_atomic_fetch_add(cnt + g, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          last = old == bl - bf;
+          if (last) __hip_atomic_store(cnt + g, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        s_flag[side] = last;
+      }
+    }
+    lds_barrier();
+#pragma unroll
+    for (int side = 0; side < 2; ++side) {
+      if (!s_flag[side]) continue;
+      const int g = side ? split_g1 : split_g0;
+      const int bf = block_of(g * nks), bl = block_of((g + 1) * nks - 1);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keep the slab loads below the ticket
+      for (int qd = wid; qd < Q; qd += 8) {
+        if (EPI == 1 && (qd % NT) & 1) continue;
+        f32x4 v = (f32x4)(0.f), up = (f32x4)(0.f);
+        for (int b = bf; b <= bl; ++b) {  // fixed order: deterministic sums
+          const int sd = (start_of(b) / nks == g) ? 0 : 1;
+          const int base = ((b * 2 + sd) * Q) * 64;
+          v += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(slab_rsrc, ((base + qd * 64) + lane) * 16,
+                                                                                0, 16));
+          if (EPI == 1)
+            up += __builtin_bit_cast(
+                f32x4, __builtin_amdgcn_raw_buffer_load_b128(slab_rsrc, ((base + (qd + 1) * 64) + lane) * 16, 0, 16));
+        }
+        sk_epilogue<MT, NT, EPI, OPK>(qd, g, v, up, y, ys, res, rs, M, lane);
+      }
+    }
   };
 
   // prologue: fill the ring
@@ -383,6 +406,7 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(const bf16_t* __restrict__
   if (pending) reduce(pend_g);
   stage();
   reduce(cur_g);
+  finish_splits();
 }
 
 static int sk_num_cus() {
@@ -399,12 +423,11 @@ static int sk_num_cus() {
 
 template <int MT, int NT, int D>
 static int launch_gemm_sk_cfg(const void* x, void* y, int64_t ys, const void* w, const void* res, int64_t rs, int M,
-                              int N, int K, int epi, int flags, void* ws, int gmul, int remap, hipStream_t stream) {
+                              int N, int K, int epi, int flags, void* ws, int G, hipStream_t stream) {
   const int nks = K / 32;
   const int ngrp = (N / 16) / NT;
   if ((N / 16) % NT || nks % 8 || nks < 8 * D || ngrp > SK_MAX_GROUPS) return 1;  // caller falls back
   const int U = ngrp * nks;
-  int G = sk_num_cus() * gmul;
   if (G > SK_MAX_BLOCKS) G = SK_MAX_BLOCKS;
   if (G > U) G = U;
   int* cnt = (int*)ws;  // [SK_MAX_GROUPS] counters, [SK_ZERO_BYTES] zeros, slabs
@@ -412,9 +435,13 @@ static int launch_gemm_sk_cfg(const void* x, void* y, int64_t ys, const void* w,
   const bool opk = flags & 2;
 #define MP_SK(EPI_, OPK_)                                                                                         \
   hipLaunchKernelGGL((gemm_sk_kernel<MT, NT, D, EPI_, OPK_>), dim3(G), dim3(512), 0, stream, (const bf16_t*)x,     \
-                     (const bf16_t*)w, (bf16_t*)y, ys, (const bf16_t*)res, rs, M, N, K, cnt, slab, remap)
+                     (const bf16_t*)w, (bf16_t*)y, ys, (const bf16_t*)res, rs, M, N, K, cnt, slab, 1)
   if (epi == 1) {
-    if (opk) { MP_SK(1, true); } else { MP_SK(1, false); }
+    if constexpr (NT % 2 == 0) {
+      if (opk) { MP_SK(1, true); } else { MP_SK(1, false); }
+    } else {
+      return 1;
+    }
   } else if (opk) {
     return -3;
   } else if (epi == 2) {
@@ -426,20 +453,30 @@ static int launch_gemm_sk_cfg(const void* x, void* y, int64_t ys, const void* w,
   return 0;
 }
 
-static int sk_env(const char* name, int dflt) {
-  const char* v = getenv(name);
-  return v ? atoi(v) : dflt;
+// Largest grid G in [0.9 C, C] that divides the group count (every workgroup then owns whole
+// groups: no split-group hand-off at all), else 0.
+static int sk_whole_grid(int ngrp, int C) {
+  for (int G = C; G * 10 >= C * 9; --G)
+    if (G > 0 && ngrp % G == 0) return G;
+  return 0;
 }
 
+// Stream-K launch: prefer a column-group width NT (4, then 3 for non-SwiGLU, then 2) whose
+// group count splits evenly over ~all CUs (no split groups); otherwise NT = 4 on every CU with
+// split groups (deferred sc1 hand-off).
 template <int MT>
 static int launch_gemm_sk(const void* x, void* y, int64_t ys, const void* w, const void* res, int64_t rs, int M, int N,
                           int K, int epi, int flags, void* ws, hipStream_t stream) {
-  // tuning knobs (experiments): MPAMD_SK_CFG 0 = NT 4 / ring 4 (3 for MT >= 3), 1 = NT 2 / ring 4,
-  // 2 = NT 4 / ring 2; MPAMD_SK_GM = workgroups per CU
-  static const int cfg = sk_env("MPAMD_SK_CFG", 0), gm = sk_env("MPAMD_SK_GM", 1), rm = sk_env("MPAMD_SK_REMAP", 1);
-  if (cfg == 1) return launch_gemm_sk_cfg<MT, 2, 4>(x, y, ys, w, res, rs, M, N, K, epi, flags, ws, gm, rm, stream);
-  if (cfg == 2) return launch_gemm_sk_cfg<MT, 4, 2>(x, y, ys, w, res, rs, M, N, K, epi, flags, ws, gm, rm, stream);
-  return launch_gemm_sk_cfg<MT, 4, (MT >= 3 ? 3 : 4)>(x, y, ys, w, res, rs, M, N, K, epi, flags, ws, gm, rm, stream);
+  constexpr int DW = (MT >= 3) ? 3 : 4;  // ring depth (256-VGPR cap at MT >= 3)
+  const int C = sk_num_cus(), nt = N / 16;
+  int G;
+  if (nt % 4 == 0 && (G = sk_whole_grid(nt / 4, C)))
+    return launch_gemm_sk_cfg<MT, 4, DW>(x, y, ys, w, res, rs, M, N, K, epi, flags, ws, G, stream);
+  if (epi != 1 && nt % 3 == 0 && (G = sk_whole_grid(nt / 3, C)))
+    return launch_gemm_sk_cfg<MT, 3, DW>(x, y, ys, w, res, rs, M, N, K, epi, flags, ws, G, stream);
+  if (nt % 2 == 0 && (G = sk_whole_grid(nt / 2, C)))
+    return launch_gemm_sk_cfg<MT, 2, 4>(x, y, ys, w, res, rs, M, N, K, epi, flags, ws, G, stream);
+  return launch_gemm_sk_cfg<MT, 4, DW>(x, y, ys, w, res, rs, M, N, K, epi, flags, ws, C, stream);
 }
 
 // Pack W[N, K] (row-major) into the fragment-native layout Wp[N/16][K/32][64][8].

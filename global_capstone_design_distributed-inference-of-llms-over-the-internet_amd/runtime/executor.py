@@ -137,6 +137,12 @@ class StageExecutor:
             if cfg.model_type != "gpt2" and ops.gemm_policy() != "hipblaslt":
                 weights.pack_for_decode()
                 ops.gemm_workspace(self.device)  # allocated before any hipGraph capture
+                if os.environ.get("MPAMD_GEMM_AUTOTUNE", "1") != "0" and weights.layers:
+                    H, F = cfg.hidden_size, cfg.intermediate_size
+                    shapes = [(cfg.q_dim + 2 * cfg.kv_dim, H, 0), (H, cfg.q_dim, 0), (2 * F, H, 1), (H, F, 0)]
+                    if weights.lm_head_p is not None:
+                        shapes.append((16 * weights.lm_head_p.shape[0], H, 0))
+                    ops.autotune_gemm(shapes, self.device)
         logger.info(f"StageExecutor blocks [{self.start},{self.end}) embed={self.is_first} head={self.is_last} "
                     f"kv_pages={num_pages} x {page_size} tokens ({self.cache.nbytes / 2**30:.2f} GiB) "
                     f"graphs={self.use_graphs}")

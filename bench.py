@@ -51,6 +51,8 @@ def main(argv=None):
     ap.add_argument("--model", default="llama2-7b")
     ap.add_argument("--batch", type=int, default=64, help="sessions per micro-batch")
     ap.add_argument("--micro", type=int, default=None, help="micro-batches in flight (default: N stages)")
+    ap.add_argument("--replicas", type=int, default=1,
+                    help="independent pipelines (data parallel): N GPUs = replicas x stages, e.g. 8 = 2 x 4")
     ap.add_argument("--prompt-len", type=int, default=128)
     ap.add_argument("--temperature", type=float, default=1.0)
     ap.add_argument("--top-p", type=float, default=0.92)
@@ -66,7 +68,7 @@ def main(argv=None):
     from src.models.config import resolve_model
     from src.models.weights import random_stage_weights
     from src.parallel import dist as pdist
-    from src.parallel.pipeline import PipelineEngine
+    from src.parallel.pipeline import PipelineEngine, make_replica_groups
     from src.partition import even_splits, stage_ranges
     from src.runtime.executor import StageExecutor
     from src.runtime.sampler import SamplingParams
@@ -78,13 +80,19 @@ def main(argv=None):
         raise SystemExit(f"--gpus {n} but WORLD_SIZE={world}: launch with torchrun --nproc-per-node {n}")
     ops.set_gemm_policy(a.gemm)
     cfg = resolve_model(a.model)
-    cuts = even_splits(cfg.num_hidden_layers, world)
-    start, end = stage_ranges(cuts, cfg.num_hidden_layers)[rank]
-    M = a.micro or world
+    R = max(1, a.replicas)
+    if world % R:
+        raise SystemExit(f"--replicas {R} does not divide {world} GPUs")
+    S = world // R
+    groups = make_replica_groups(world, S)
+    stage = rank % S
+    cuts = even_splits(cfg.num_hidden_layers, S)
+    start, end = stage_ranges(cuts, cfg.num_hidden_layers)[stage]
+    M = a.micro or S
     B = a.batch
     dtype = torch.bfloat16
     t0 = time.time()
-    w = random_stage_weights(cfg, start, end, has_embed=rank == 0, has_head=rank == world - 1, device=device,
+    w = random_stage_weights(cfg, start, end, has_embed=stage == 0, has_head=stage == S - 1, device=device,
                              dtype=dtype, seed=a.seed)
     max_len = a.prompt_len + a.warmup + a.steps + 8
     max_len = 64 * math.ceil(max_len / 64)
@@ -96,7 +104,7 @@ def main(argv=None):
         print("gemm kernel choice (stream-K?):", {f"M{k[0]}:N{k[1]}xK{k[2]}e{k[3]}": v
                                                    for k, v in sorted(ops._SK_CHOICE.items())}, file=sys.stderr)
     sp = SamplingParams(a.temperature, a.top_p, a.top_k, a.repetition_penalty)
-    eng = PipelineEngine(ex, rank, world, sp, n_micro=M, batch=B, seed=a.seed)
+    eng = PipelineEngine(ex, rank, world, sp, n_micro=M, batch=B, seed=a.seed, stages=S, groups=groups)
     gen = torch.Generator().manual_seed(1234)
     prompts = [torch.randint(0, cfg.vocab_size, (B, a.prompt_len), generator=gen) for _ in range(M)]
     load_s = time.time() - t0
@@ -131,7 +139,7 @@ def main(argv=None):
     eng.finish()
     dt = pdist.all_max(dt_local, device)
     per_stage = pdist.all_gather_floats([stage_ms, float(end - start)], device)
-    tokens = a.steps * M * B
+    tokens = a.steps * M * B * R
     value = tokens / dt
     base = baseline_value()
     if rank == 0:
@@ -151,9 +159,9 @@ def main(argv=None):
             "data": "synthetic (random-init Llama-2-7B weights, random prompt ids)",
             "config": {
                 "model": "Llama-2-7B" if a.model == "llama2-7b" else a.model,
-                "global_batch": M * B,
+                "global_batch": M * B * R,
                 "seq_len": a.prompt_len,
-                "parallelism": f"pp{world}",
+                "parallelism": f"pp{S}" + (f"xdp{R}" if R > 1 else ""),
                 "micro_batches": M,
                 "sessions_per_micro_batch": B,
                 "splits": cuts,

@@ -17,6 +17,12 @@ direct xGMI link between neighbouring GPUs:
 * Sampling happens on the last stage (reference semantics) with the repetition-penalty
   history kept ON DEVICE (no host round trip per token).
 * gloo carries the identical protocol on CPU (tests).
+* Replicas (data parallel over pipelines, BASELINE config "4 stages x 2 replicas"): with
+  ``stages=S < world`` the node runs R = world / S independent pipelines, replica r on ranks
+  [r*S, (r+1)*S), each with its own RCCL sub-communicator (``dist.new_group``) so the
+  replicas' hops never share a communicator.  Sessions are assigned to replicas by
+  ``assign_sessions`` (throughput-proportional, the load_balancing.py rule re-expressed
+  for replicas of a whole pipeline).
 """
 from __future__ import annotations
 
@@ -42,20 +48,54 @@ class MicroBatch:
     index: int = 0
 
 
+def assign_sessions(n_sessions: int, throughputs: Sequence[float]) -> List[int]:
+    """Replica index for each of ``n_sessions`` new sessions, proportional to replica
+    throughput (largest-remainder rounding; ties to the lower index)."""
+    tp = [max(float(t), 0.0) for t in throughputs]
+    tot = sum(tp)
+    if tot <= 0:
+        tp, tot = [1.0] * len(tp), float(len(tp))
+    quota = [n_sessions * t / tot for t in tp]
+    base = [int(q) for q in quota]
+    rem = n_sessions - sum(base)
+    order = sorted(range(len(tp)), key=lambda i: (-(quota[i] - base[i]), i))
+    for i in order[:rem]:
+        base[i] += 1
+    out: List[int] = []
+    for r, n in enumerate(base):
+        out.extend([r] * n)
+    return out
+
+
+def make_replica_groups(world: int, stages: int):
+    """One sub-communicator per replica (every rank creates every group, same order)."""
+    if stages >= world:
+        return None
+    return [dist.new_group(list(range(r * stages, (r + 1) * stages))) for r in range(world // stages)]
+
+
 class PipelineEngine:
     def __init__(self, executor: StageExecutor, rank: int, world: int, sampling: SamplingParams,
-                 n_micro: int, batch: int, seed: int = 0, send_ring: int = 4, timing: bool = False):
+                 n_micro: int, batch: int, seed: int = 0, send_ring: int = 4, timing: bool = False,
+                 stages: Optional[int] = None, groups=None):
         self.ex = executor
         self.rank, self.world = rank, world
+        S = int(stages or world)
+        if world % S:
+            raise ValueError(f"world size {world} is not a multiple of stages={S}")
+        self.S, self.R = S, world // S
+        self.replica, self.stage = rank // S, rank % S
+        self.base = self.replica * S
+        self.group = groups[self.replica] if groups else None
         self.dev = executor.device
         self.sp = sampling
         self.B, self.M = batch, n_micro
         self.seed = seed
-        self.first = rank == 0
-        self.last = rank == world - 1
+        self.first = self.stage == 0
+        self.last = self.stage == S - 1
         H = executor.cfg.hidden_size
         self.H = H
-        self.mbs = [MicroBatch([f"s{m}_{b}" for b in range(batch)], index=m) for m in range(n_micro)]
+        self.mbs = [MicroBatch([f"r{self.replica}s{m}_{b}" for b in range(batch)], index=m) for m in range(n_micro)]
         # send ring (hidden for mid stages, tokens for the last stage)
         self._ring = [None] * send_ring
         self._ring_work = [None] * send_ring
@@ -89,11 +129,11 @@ class PipelineEngine:
             buf = torch.empty_like(t)
             self._ring[k] = buf
         buf.copy_(t)
-        self._ring_work[k] = dist.isend(buf, dst)
+        self._ring_work[k] = dist.isend(buf, dst, group=self.group)
 
     def _post_recv(self, shape, dtype, src):
         buf = torch.empty(shape, dtype=dtype, device=self.dev)
-        return dist.irecv(buf, src), buf
+        return dist.irecv(buf, src, group=self.group), buf
 
     def _flush_sends(self):
         for i, w in enumerate(self._ring_work):
@@ -107,7 +147,8 @@ class PipelineEngine:
         if self.sp.temperature <= 0:
             tok = ops.argmax(logits)
         else:
-            seeds = (self._arange[:B] + (self.seed * 1000003 + mb.step * 7919 + mb.index * 104729) * 4096)
+            seeds = (self._arange[:B] + (self.seed * 1000003 + mb.step * 7919 + mb.index * 104729
+                                         + self.replica * 15485863) * 4096)
             tok = ops.sample(logits, self._temps[:B], self._topp[:B], self._topk[:B], self._rp[:B], mb.recent,
                              mb.recent_len, seeds)
         # device-side rolling history (left-aligned, newest at recent_len-1)
@@ -143,7 +184,7 @@ class PipelineEngine:
             if self.first:
                 if prompts is not None:
                     x = prompts[m].to(self.dev).view(-1)
-                elif self.world == 1:
+                elif self.S == 1:
                     x = mb.tokens
                 else:
                     w, buf = self._tok_recv[m]
@@ -164,17 +205,17 @@ class PipelineEngine:
             # ---------------- output
             if self.last:
                 tok = self._sample(mb, out)
-                if self.world == 1:
+                if self.S == 1:
                     mb.tokens = tok
                     if self.record:
                         self.tokens_out[m].append(tok.clone())
                 else:
-                    self._send(tok, 0)
+                    self._send(tok, self.base)
             else:
                 self._send(out, self.rank + 1)
-        if self.first and self.world > 1:
+        if self.first and self.S > 1:
             # receive this round's tokens (posted after all sends of the round, in micro-batch order)
-            self._tok_recv = [self._post_recv((self.B,), torch.long, self.world - 1) for _ in range(M)]
+            self._tok_recv = [self._post_recv((self.B,), torch.long, self.base + self.S - 1) for _ in range(M)]
 
     def prefill(self, prompts: Sequence[torch.Tensor]):
         """prompts[m]: int64 [B, L] token ids for micro-batch m (stage 0 only reads them)."""
@@ -187,7 +228,7 @@ class PipelineEngine:
 
     def finish(self):
         self._flush_sends()
-        if self.first and self.world > 1:
+        if self.first and self.S > 1:
             # tokens of the final round are still in flight; consume them
             for m, (w, buf) in enumerate(getattr(self, "_tok_recv", [])):
                 w.wait()

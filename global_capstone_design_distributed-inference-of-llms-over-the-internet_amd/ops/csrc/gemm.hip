@@ -467,13 +467,14 @@ static int sk_whole_grid(int ngrp, int C) {
 template <int MT>
 static int launch_gemm_sk(const void* x, void* y, int64_t ys, const void* w, const void* res, int64_t rs, int M, int N,
                           int K, int epi, int flags, void* ws, hipStream_t stream) {
-  constexpr int DW = (MT >= 3) ? 3 : 4;  // ring depth (256-VGPR cap at MT >= 3)
+  // ring depth 4 (3 when MT x NT >= 16: the 256-VGPR cap)
+  constexpr int DW = (MT * 4 >= 16) ? 3 : 4, D3 = (MT * 3 >= 16) ? 3 : 4;
   const int C = sk_num_cus(), nt = N / 16;
   int G;
   if (nt % 4 == 0 && (G = sk_whole_grid(nt / 4, C)))
     return launch_gemm_sk_cfg<MT, 4, DW>(x, y, ys, w, res, rs, M, N, K, epi, flags, ws, G, stream);
   if (epi != 1 && nt % 3 == 0 && (G = sk_whole_grid(nt / 3, C)))
-    return launch_gemm_sk_cfg<MT, 3, DW>(x, y, ys, w, res, rs, M, N, K, epi, flags, ws, G, stream);
+    return launch_gemm_sk_cfg<MT, 3, D3>(x, y, ys, w, res, rs, M, N, K, epi, flags, ws, G, stream);
   if (nt % 2 == 0 && (G = sk_whole_grid(nt / 2, C)))
     return launch_gemm_sk_cfg<MT, 2, 4>(x, y, ys, w, res, rs, M, N, K, epi, flags, ws, G, stream);
   return launch_gemm_sk_cfg<MT, 4, DW>(x, y, ys, w, res, rs, M, N, K, epi, flags, ws, C, stream);

@@ -57,6 +57,30 @@ class LlamaLayer:
     o_p: Optional[torch.Tensor] = None
     gate_up_p: Optional[torch.Tensor] = None
     down_p: Optional[torch.Tensor] = None
+    # fp8 e4m3 W8A8 copies (ops.pack_weight_fp8): packed uint8 + per-output-channel fp32 scale
+    qkv_q: Optional[torch.Tensor] = None
+    qkv_s: Optional[torch.Tensor] = None
+    o_q: Optional[torch.Tensor] = None
+    o_s: Optional[torch.Tensor] = None
+    gate_up_q: Optional[torch.Tensor] = None
+    gate_up_s: Optional[torch.Tensor] = None
+    down_q: Optional[torch.Tensor] = None
+    down_s: Optional[torch.Tensor] = None
+
+    PROJ = ("qkv", "o", "gate_up", "down")
+
+    @property
+    def fp8(self) -> bool:
+        return self.qkv_q is not None
+
+    def dense(self, name: str, dtype=torch.bfloat16) -> torch.Tensor:
+        """Row-major weight ``name`` (dequantized on the fly when only the fp8 copy is kept)."""
+        w = getattr(self, name)
+        if w is not None:
+            return w
+        from .. import ops
+
+        return ops.unpack_weight_fp8(getattr(self, name + "_q"), getattr(self, name + "_s"), dtype)
 
 
 @dataclasses.dataclass
@@ -111,7 +135,7 @@ class StageWeights:
         from .. import ops
 
         for lay in self.layers:
-            if isinstance(lay, LlamaLayer) and lay.qkv_p is None:
+            if isinstance(lay, LlamaLayer) and lay.qkv_p is None and lay.qkv is not None:
                 lay.qkv_p = ops.pack_weight(lay.qkv)
                 lay.o_p = ops.pack_weight(lay.o)
                 lay.gate_up_p = ops.pack_weight(lay.gate_up)
@@ -122,6 +146,30 @@ class StageWeights:
                 pad = (-V) % 16
                 w = self.lm_head if pad == 0 else torch.cat([self.lm_head, self.lm_head.new_zeros(pad, H)])
                 self.lm_head_p = ops.pack_weight(w.contiguous())
+
+    def quantize_fp8(self, drop_dense: bool = True) -> None:
+        """fp8 (OCP e4m3) W8A8 weights for every projection (the 70B fp8 MFMA path).
+
+        ``drop_dense`` frees the bf16 copies (the prefill path then dequantizes one layer at a
+        time), halving resident weight bytes: Llama-3-70B fits ONE MI355X (~70 GB) with room
+        for a large KV cache.  Embeddings, norms and lm_head stay bf16.
+        """
+        from .. import ops
+
+        for lay in self.layers:
+            if not isinstance(lay, LlamaLayer) or lay.fp8:
+                continue
+            for name in LlamaLayer.PROJ:
+                q, sc = ops.pack_weight_fp8(getattr(lay, name))
+                setattr(lay, name + "_q", q)
+                setattr(lay, name + "_s", sc)
+                if drop_dense:
+                    setattr(lay, name, None)
+                    setattr(lay, name + "_p", None)
+
+    @property
+    def fp8(self) -> bool:
+        return bool(self.layers) and all(isinstance(L, LlamaLayer) and L.fp8 for L in self.layers)
 
     def tensors(self):
         seen = set()

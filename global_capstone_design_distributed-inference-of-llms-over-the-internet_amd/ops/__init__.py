@@ -383,3 +383,57 @@ def linear(x, w, out=None, epilogue=0, residual=None, policy=None, wp=None, a_ro
         out.copy_(y)
         return out
     return y
+
+
+# ---------------------------------------------------------------------------------------
+# FP8 (OCP e4m3fn) W8A8 decode GEMM (csrc/fp8.hip) - the Llama-3-70B fp8 MFMA path.
+def pack_weight_fp8(w: torch.Tensor):
+    """W [N, K] -> (Wq uint8 [N/16, K/64, 64, 16], per-output-channel scale fp32 [N])."""
+    return ref.pack_weight_fp8(w)
+
+
+def unpack_weight_fp8(wq: torch.Tensor, w_scale: torch.Tensor, dtype=torch.bfloat16) -> torch.Tensor:
+    return ref.unpack_weight_fp8(wq, w_scale, dtype)
+
+
+def fp8_gemm_ok(M: int, N: int, K: int) -> bool:
+    return 0 < M <= 64 and K % 256 == 0 and N % 32 == 0
+
+
+def quant_act_fp8(xp: torch.Tensor, M: int, K: int, out=None, scale=None):
+    """Packed bf16 decode activation -> (fp8 A8 uint8, per-row scale fp32 [ceil(M/16)*16])."""
+    if not _native(xp):
+        a8, s = ref.quant_act_fp8(xp, M, K)
+        if out is not None:
+            out[: a8.numel()].copy_(a8)
+            a8 = out
+        if scale is not None:
+            scale[: s.numel()].copy_(s)
+            s = scale
+        return a8, s
+    if out is None:
+        out = torch.empty(packed_numel(M, K), dtype=torch.uint8, device=xp.device)
+    if scale is None:
+        scale = torch.empty(((M + 15) // 16) * 16, dtype=torch.float32, device=xp.device)
+    torch.ops.mpamd.quant_act_fp8(xp, out, scale, int(M), int(K))
+    return out, scale
+
+
+def linear_fp8(a8, a_scale, wq, w_scale, M: int, out=None, epilogue: int = 0, residual=None,
+               out_packed: bool = False):
+    """y = epilogue((a8 * a_scale) . (wq * w_scale)^T) for M <= 64 decode rows."""
+    N = 16 * wq.shape[0]
+    ncols = N // 2 if epilogue == 1 else N
+    if not _native(a8):
+        y = ref.linear_fp8(a8, a_scale, wq, w_scale, M, epilogue, residual)
+        if out_packed:
+            return ref.pack_act(y, out=out)
+        if out is not None:
+            out.copy_(y)
+            return out
+        return y
+    if out is None:
+        out = (torch.empty(packed_numel(M, ncols), dtype=torch.bfloat16, device=a8.device) if out_packed
+               else torch.empty(M, ncols, dtype=torch.bfloat16, device=a8.device))
+    torch.ops.mpamd.gemm_fp8(a8, a_scale, wq, w_scale, out, residual, int(epilogue), int(M), int(bool(out_packed)))
+    return out

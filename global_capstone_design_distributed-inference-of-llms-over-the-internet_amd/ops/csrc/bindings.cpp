@@ -30,6 +30,9 @@ int mp_sample(const void* logits, int64_t stride, int R, int V, const float* tem
               const int32_t* top_ks, const float* rep_pens, const int32_t* recent, int recent_stride,
               const int32_t* recent_len, const int64_t* seeds, float* ws, int64_t* out, hipStream_t stream);
 int64_t mp_gemm_workspace_bytes();
+int mp_quant_act_fp8(const void* ap, void* a8, float* scale, int M, int K, hipStream_t stream);
+int mp_gemm_fp8(const void* a8, const float* as, const void* wq, const float* ws, void* y, int64_t ys, const void* res,
+                int64_t rs, int M, int N, int K, int epilogue, int out_packed, hipStream_t stream);
 int mp_gemm_bf16(const void* x, int64_t x_stride, const void* w, void* y, int64_t y_stride, const void* res,
                  int64_t res_stride, int M, int N, int K, int epilogue, int flags, void* ws,
                  hipStream_t stream);
@@ -299,6 +302,52 @@ at::Tensor pack_weight(const at::Tensor& w) {
 
 int64_t gemm_workspace_bytes() { return mp_gemm_workspace_bytes(); }
 
+// packed bf16 decode activation (M rows) -> fp8 A8 [K/64][MT][64][16] (uint8) + row scales (fp32, >= MT*16)
+void quant_act_fp8(const at::Tensor& ap, at::Tensor& a8, at::Tensor& scale, int64_t M, int64_t K) {
+  check_bf16_cuda(ap, "ap");
+  MP_CHECK(ap.is_contiguous() && ap.numel() >= packed_numel(M, K), "packed activation too small");
+  MP_CHECK(a8.is_cuda() && a8.scalar_type() == at::kByte && a8.is_contiguous() && a8.numel() >= packed_numel(M, K),
+           "a8: uint8 [packed_numel(M, K)]");
+  MP_CHECK(scale.is_cuda() && scale.scalar_type() == at::kFloat && scale.numel() >= ((M + 15) / 16) * 16,
+           "scale: fp32 [ceil(M/16)*16]");
+  MP_CHECK(K % 64 == 0, "K % 64");
+  check_launch(mp_quant_act_fp8(ap.data_ptr(), a8.data_ptr(), scale.data_ptr<float>(), (int)M, (int)K, cur_stream()),
+               "quant_act_fp8");
+}
+
+// y = epilogue((a8 * as) . (wq * ws)^T); wq: [N/16, K/64, 64, 16] uint8 (ops.pack_weight_fp8)
+void gemm_fp8(const at::Tensor& a8, const at::Tensor& as, const at::Tensor& wq, const at::Tensor& ws, at::Tensor& y,
+              const c10::optional<at::Tensor>& residual, int64_t epilogue, int64_t M, int64_t out_packed) {
+  MP_CHECK(wq.is_cuda() && wq.scalar_type() == at::kByte && wq.dim() == 4 && wq.size(2) == 64 && wq.size(3) == 16 &&
+               wq.is_contiguous(),
+           "wq must be a packed fp8 weight [N/16, K/64, 64, 16]");
+  const int N = 16 * wq.size(0), K = 64 * wq.size(1);
+  MP_CHECK(a8.is_cuda() && a8.scalar_type() == at::kByte && a8.numel() >= packed_numel(M, K), "a8");
+  MP_CHECK(as.is_cuda() && as.scalar_type() == at::kFloat && as.numel() >= M, "as");
+  MP_CHECK(ws.is_cuda() && ws.scalar_type() == at::kFloat && ws.numel() == N, "ws: fp32 [N]");
+  check_bf16_cuda(y, "y");
+  const int ncols = epilogue == 1 ? N / 2 : N;
+  if (out_packed) {
+    MP_CHECK(epilogue == 1 && y.is_contiguous() && y.numel() >= packed_numel(M, ncols), "packed y");
+  } else {
+    check_rows(y, "y");
+    MP_CHECK(y.size(0) == M && y.size(1) == ncols, "y shape");
+  }
+  const void* rp = nullptr;
+  int64_t rs = 0;
+  if (residual.has_value()) {
+    check_bf16_cuda(*residual, "residual");
+    check_rows(*residual, "residual");
+    rp = residual->data_ptr();
+    rs = residual->stride(0);
+  }
+  MP_CHECK(epilogue != 2 || rp != nullptr, "residual epilogue needs residual");
+  check_launch(mp_gemm_fp8(a8.data_ptr(), as.data_ptr<float>(), wq.data_ptr(), ws.data_ptr<float>(), y.data_ptr(),
+                           out_packed ? 0 : y.stride(0), rp, rs, (int)M, N, K, (int)epilogue, (int)out_packed,
+                           cur_stream()),
+               "gemm_fp8");
+}
+
 }  // namespace
 
 TORCH_LIBRARY(mpamd, m) {
@@ -326,6 +375,10 @@ TORCH_LIBRARY(mpamd, m) {
       "Tensor(b!)? workspace=None) -> ()");
   m.def("pack_act(Tensor x, Tensor(a!) ap) -> ()");
   m.def("pack_weight(Tensor w) -> Tensor");
+  m.def("quant_act_fp8(Tensor ap, Tensor(a!) a8, Tensor(b!) scale, int M, int K) -> ()");
+  m.def(
+      "gemm_fp8(Tensor a8, Tensor a_scale, Tensor wq, Tensor w_scale, Tensor(a!) y, Tensor? residual, int epilogue, "
+      "int M, int out_packed) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(mpamd, CUDA, m) {
@@ -341,4 +394,6 @@ TORCH_LIBRARY_IMPL(mpamd, CUDA, m) {
   m.impl("gemm", &gemm);
   m.impl("pack_weight", &pack_weight);
   m.impl("pack_act", &pack_act);
+  m.impl("quant_act_fp8", &quant_act_fp8);
+  m.impl("gemm_fp8", &gemm_fp8);
 }

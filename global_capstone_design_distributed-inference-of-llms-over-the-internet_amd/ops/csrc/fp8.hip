@@ -1,0 +1,229 @@
+// FP8 (OCP e4m3fn) W8A8 decode GEMM for gfx950 - the "fp8 MFMA path" of the Llama-3-70B
+// configuration (BASELINE.json config 5).
+//
+// The reference has no quantized path (bitsandbytes NF4/INT8 exists only in the vendored,
+// unreachable Petals server: petals/server/block_utils.py, convert_block).  On MI355X the
+// natural 8-bit format is OCP fp8 with the native MFMA v_mfma_f32_16x16x32_fp8_fp8:
+//
+//   y[m, n] = a_m * s_n * sum_k  q8(x)[m, k] * q8(W)[n, k]
+//
+//   * weights: per-output-channel scale s_n = max|W[n, :]| / 448, packed once (ops.pack_weight_fp8)
+//       Wq[N/16][K/64][lane][16 B]:  lane = 16 q + c holds W[16 nt + c][64 kc + 32 s + 8 q + j]
+//       at byte 8 s + j  -> one 16-B load per lane feeds TWO 16x16x32 fp8 MFMAs (s = 0, 1);
+//   * activations: per-row scale a_m = max|x[m, :]| / 448, quantized from the packed bf16
+//     decode activation (quant_act_fp8_kernel) into the same [K/64][MT][lane][16 B] order;
+//   * half the weight bytes of the bf16 path: decode stays HBM-bound, so the fp8 GEMM streams
+//     a 70B stage in half the time.  Loop structure = the bf16 one-group-per-workgroup kernel
+//     (gemm.hip): 8 waves interleave k-groups, ping-pong weight registers, LDS combine,
+//     fused epilogues (scales, SwiGLU on 16-row-interleaved gate/up, residual).
+#include "common.h"
+
+namespace mp {
+
+typedef __attribute__((ext_vector_type(2))) long i64x2;
+
+__device__ __forceinline__ f32x4 mfma_fp8x2(const u16x8& a, const u16x8& b, f32x4 c) {
+  const i64x2 av = __builtin_bit_cast(i64x2, a), bv = __builtin_bit_cast(i64x2, b);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(av[0], bv[0], c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(av[1], bv[1], c, 0, 0, 0);
+}
+
+// 4 floats -> 4 OCP e4m3 bytes (round to nearest even; inputs already within +-448)
+__device__ __forceinline__ int pack4_fp8(float a, float b, float c, float d) {
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  return __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
+}
+
+// Packed bf16 decode activation Ap[K/32][MT][64][8] (M rows) -> fp8 A8[K/64][MT][64][16 B]
+// plus per-row scales (MT*16 floats; rows >= M get a scale too and are never stored).
+// One workgroup per 16-row tile: pass 1 row absmax, pass 2 quantize (the tile is L2-hot).
+__global__ __launch_bounds__(512) void quant_act_fp8_kernel(const bf16_t* __restrict__ ap, uint8_t* __restrict__ a8,
+                                                            float* __restrict__ scale, int K, int MT) {
+  __shared__ float red[8][16];
+  const int mt = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int nks = K >> 5;
+  float m = 0.f;
+  for (int ks = wid; ks < nks; ks += 8) {
+    const u16x8 v = *reinterpret_cast<const u16x8*>(ap + (((int64_t)ks * MT + mt) * 64 + lane) * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf(bf2f(v[j])));
+  }
+  m = fmaxf(m, __shfl_xor(m, 16, 64));
+  m = fmaxf(m, __shfl_xor(m, 32, 64));
+  if (lane < 16) red[wid][lane] = m;
+  __syncthreads();
+  const int r = lane & 15;
+  float mx = red[0][r];
+#pragma unroll
+  for (int w = 1; w < 8; ++w) mx = fmaxf(mx, red[w][r]);
+  const float s = mx > 0.f ? mx * (1.f / 448.f) : 1.f;
+  const float inv = 1.f / s;
+  if (wid == 0 && lane < 16) scale[mt * 16 + lane] = s;
+  for (int c = wid; c < (nks >> 1); c += 8) {
+    const u16x8 v0 = *reinterpret_cast<const u16x8*>(ap + (((int64_t)(2 * c) * MT + mt) * 64 + lane) * 8);
+    const u16x8 v1 = *reinterpret_cast<const u16x8*>(ap + (((int64_t)(2 * c + 1) * MT + mt) * 64 + lane) * 8);
+    float f[16];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      f[j] = fminf(fmaxf(bf2f(v0[j]) * inv, -448.f), 448.f);
+      f[8 + j] = fminf(fmaxf(bf2f(v1[j]) * inv, -448.f), 448.f);
+    }
+    int4 o;
+    o.x = pack4_fp8(f[0], f[1], f[2], f[3]);
+    o.y = pack4_fp8(f[4], f[5], f[6], f[7]);
+    o.z = pack4_fp8(f[8], f[9], f[10], f[11]);
+    o.w = pack4_fp8(f[12], f[13], f[14], f[15]);
+    *reinterpret_cast<int4*>(a8 + (((int64_t)c * MT + mt) * 64 + lane) * 16) = o;
+  }
+}
+
+constexpr int F8_GU_MAX = 4;  // 64-k chunks per wave group
+
+template <int MT, int NT, int EPI, bool OPK>
+__global__ __launch_bounds__(512) void gemm_fp8_kernel(const uint8_t* __restrict__ a8, const float* __restrict__ ascale,
+                                                       const uint8_t* __restrict__ wq, const float* __restrict__ wscale,
+                                                       bf16_t* __restrict__ y, int64_t ys,
+                                                       const bf16_t* __restrict__ res, int64_t rs, int M, int N,
+                                                       int K) {
+  constexpr int GU = (MT * NT >= 6) ? 2 : 4;
+  __shared__ __attribute__((aligned(16))) float red[8][MT * NT * 4][64];
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int c = lane & 15, q = lane >> 4;
+  const int nch = K >> 6;
+  const int ngroups = nch / GU;
+  const int nt0 = blockIdx.x * NT;
+
+  const uint8_t* wbase[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) wbase[t] = wq + ((int64_t)(nt0 + t) * nch) * 1024 + lane * 16;
+  const uint8_t* abase = a8 + lane * 16;
+
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[mt][t] = (f32x4)(0.f);
+
+  u16x8 b0[NT][GU], b1[NT][GU], a[MT][GU];
+#define F8_LOAD_B(dst, grp)                                                                                  \
+  _Pragma("unroll") for (int t = 0; t < NT; ++t) _Pragma("unroll") for (int u = 0; u < GU; ++u) dst[t][u] =   \
+      __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(wbase[t] + (int64_t)((grp) * GU + u) * 1024));
+#define F8_LOAD_A(grp)                                                                                       \
+  _Pragma("unroll") for (int mt = 0; mt < MT; ++mt) _Pragma("unroll") for (int u = 0; u < GU; ++u) a[mt][u] = \
+      *reinterpret_cast<const u16x8*>(abase + ((int64_t)((grp) * GU + u) * MT + mt) * 1024);
+#define F8_MMA(bb)                                                                                           \
+  _Pragma("unroll") for (int mt = 0; mt < MT; ++mt) _Pragma("unroll") for (int u = 0; u < GU; ++u)           \
+      _Pragma("unroll") for (int t = 0; t < NT; ++t) acc[mt][t] = mfma_fp8x2(a[mt][u], bb[t][u], acc[mt][t]);
+  int g = wid;
+  if (g < ngroups) {
+    F8_LOAD_B(b0, g)
+  }
+  while (g < ngroups) {
+    F8_LOAD_A(g)
+    if (g + 8 < ngroups) {
+      F8_LOAD_B(b1, g + 8)
+      F8_MMA(b0)
+    } else {
+      F8_MMA(b0)
+      break;
+    }
+    g += 8;
+    F8_LOAD_A(g)
+    if (g + 8 < ngroups) {
+      F8_LOAD_B(b0, g + 8)
+      F8_MMA(b1)
+    } else {
+      F8_MMA(b1)
+      break;
+    }
+    g += 8;
+  }
+#undef F8_LOAD_B
+#undef F8_LOAD_A
+#undef F8_MMA
+
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[wid][(mt * NT + t) * 4 + r][lane] = acc[mt][t][r];
+  __syncthreads();
+  for (int i = wid; i < MT * NT * 4; i += 8) {
+    const int mt = i / (NT * 4), t = (i / 4) % NT, r = i & 3;
+    const int row = mt * 16 + q * 4 + r;
+    float s = 0.f;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) s += red[w][i][lane];
+    if (row >= M) continue;
+    const float as = ascale[row];
+    if constexpr (EPI == 1) {
+      if (t & 1) continue;  // up tile consumed with its gate tile
+      float up = 0.f;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) up += red[w][i + 4][lane];
+      const int gcol = (nt0 + t) * 16 + c;
+      const float gg = round_bf(s * as * wscale[gcol]);
+      const float uu = round_bf(up * as * wscale[gcol + 16]);
+      const float act = round_bf(gg / (1.f + __expf(-gg)));
+      const int ncol = ((nt0 + t) >> 1) * 16 + c;
+      const int64_t yo = OPK ? apk_off(row, ncol, MT) : (int64_t)row * ys + ncol;
+      y[yo] = f2bf(act * uu);
+    } else {
+      const int col = (nt0 + t) * 16 + c;
+      float v = s * as * wscale[col];
+      if constexpr (EPI == 2) v = round_bf(v) + bf2f(res[(int64_t)row * rs + col]);
+      y[(int64_t)row * ys + col] = f2bf(v);
+    }
+  }
+}
+
+template <int MT>
+static int launch_gemm_fp8(const void* a8, const float* as, const void* wq, const float* ws, void* y, int64_t ys,
+                           const void* res, int64_t rs, int M, int N, int K, int epi, int opk, hipStream_t stream) {
+  const int ntiles = N / 16;
+  const bool two = epi == 1 || (ntiles % 2 == 0 && ntiles / 2 >= 256);
+#define F8_LAUNCH(NT_, EPI_, OPK_)                                                                              \
+  hipLaunchKernelGGL((gemm_fp8_kernel<MT, NT_, EPI_, OPK_>), dim3(ntiles / NT_), dim3(512), 0, stream,           \
+                     (const uint8_t*)a8, as, (const uint8_t*)wq, ws, (bf16_t*)y, ys, (const bf16_t*)res, rs, M, N, K)
+  if (epi == 1) {
+    if (ntiles % 2) return -2;
+    if (opk) { F8_LAUNCH(2, 1, true); } else { F8_LAUNCH(2, 1, false); }
+  } else if (opk) {
+    return -3;
+  } else if (epi == 2) {
+    if (two) { F8_LAUNCH(2, 2, false); } else { F8_LAUNCH(1, 2, false); }
+  } else {
+    if (two) { F8_LAUNCH(2, 0, false); } else { F8_LAUNCH(1, 0, false); }
+  }
+#undef F8_LAUNCH
+  return 0;
+}
+
+}  // namespace mp
+
+extern "C" int mp_quant_act_fp8(const void* ap, void* a8, float* scale, int M, int K, hipStream_t stream) {
+  using namespace mp;
+  if (M <= 0) return 0;
+  if (K % 64) return -1;
+  const int MT = (M + 15) / 16;
+  hipLaunchKernelGGL(quant_act_fp8_kernel, dim3(MT), dim3(512), 0, stream, (const bf16_t*)ap, (uint8_t*)a8, scale, K,
+                     MT);
+  return (int)hipGetLastError();
+}
+
+// a8/as: quant_act_fp8 output for M rows; wq/ws: pack_weight_fp8 output for W[N, K].
+extern "C" int mp_gemm_fp8(const void* a8, const float* as, const void* wq, const float* ws, void* y, int64_t ys,
+                           const void* res, int64_t rs, int M, int N, int K, int epilogue, int out_packed,
+                           hipStream_t stream) {
+  using namespace mp;
+  if (M == 0) return 0;
+  if (M > 64 || K % (64 * F8_GU_MAX) || N % 16) return -1;
+  int rc;
+  if (M <= 16) rc = launch_gemm_fp8<1>(a8, as, wq, ws, y, ys, res, rs, M, N, K, epilogue, out_packed, stream);
+  else if (M <= 32) rc = launch_gemm_fp8<2>(a8, as, wq, ws, y, ys, res, rs, M, N, K, epilogue, out_packed, stream);
+  else if (M <= 48) rc = launch_gemm_fp8<3>(a8, as, wq, ws, y, ys, res, rs, M, N, K, epilogue, out_packed, stream);
+  else rc = launch_gemm_fp8<4>(a8, as, wq, ws, y, ys, res, rs, M, N, K, epilogue, out_packed, stream);
+  if (rc) return rc;
+  return (int)hipGetLastError();
+}

@@ -250,3 +250,63 @@ def sample(logits, temps, top_ps, top_ks, rep_pens, recent, recent_len, seeds, w
         out.copy_(res)
         return out
     return res
+
+
+# ------------------------------------------------------------------ fp8 (OCP e4m3fn) W8A8
+FP8_MAX = 448.0
+
+
+def pack_weight_fp8(w):
+    """W [N, K] -> (Wq uint8 [N/16, K/64, 64, 16], per-row scale fp32 [N]); see csrc/fp8.hip."""
+    N, K = w.shape
+    wf = w.float()
+    s = wf.abs().amax(1).clamp_min(1e-30) / FP8_MAX
+    q = (wf / s[:, None]).clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn).view(torch.uint8)
+    qp = q.view(N // 16, 16, K // 64, 2, 4, 8).permute(0, 2, 4, 1, 3, 5).reshape(N // 16, K // 64, 64, 16)
+    return qp.contiguous(), s.contiguous()
+
+
+def unpack_weight_fp8(qp, s, dtype=torch.float32):
+    n16, k64 = qp.shape[0], qp.shape[1]
+    q = qp.view(n16, k64, 4, 16, 2, 8).permute(0, 3, 1, 4, 2, 5).reshape(n16 * 16, k64 * 64)
+    return (q.view(torch.float8_e4m3fn).float() * s.float()[:, None]).to(dtype)
+
+
+def quant_rows_fp8(x):
+    """x [R, K] float -> (q float8 [R, K], scale [R]) with per-row absmax / 448 (1 for zero rows)."""
+    x = x.float()
+    amax = x.abs().amax(1)
+    s = torch.where(amax > 0, amax / FP8_MAX, torch.ones_like(amax))
+    return (x / s[:, None]).clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn), s
+
+
+def quant_act_fp8(xp, M, K):
+    """Packed bf16 activation (M rows) -> (A8 uint8 flat [K/64][MT][64][16], scale fp32 [MT*16])."""
+    MT = (M + 15) // 16
+    x = torch.zeros(MT * 16, K, dtype=torch.float32, device=xp.device)
+    x[:M] = unpack_act(xp, M, K).float()
+    q, s = quant_rows_fp8(x)
+    a8 = q.view(torch.uint8).view(MT, 16, K // 64, 2, 4, 8).permute(2, 0, 4, 1, 3, 5).reshape(-1)
+    return a8.contiguous(), s
+
+
+def dequant_act_fp8(a8, s, M, K):
+    MT = (M + 15) // 16
+    q = a8[: MT * 16 * K].view(K // 64, MT, 4, 16, 2, 8).permute(1, 3, 0, 4, 2, 5).reshape(MT * 16, K)
+    return (q.view(torch.float8_e4m3fn).float() * s[: MT * 16, None].float())[:M]
+
+
+def linear_fp8(a8, a_scale, wq, w_scale, M, epilogue=0, residual=None, dtype=torch.bfloat16):
+    """fp32 reference of csrc/fp8.hip gemm_fp8 (same epilogue rounding as the kernel)."""
+    N, K = 16 * wq.shape[0], 64 * wq.shape[1]
+    y = dequant_act_fp8(a8, a_scale, M, K) @ unpack_weight_fp8(wq, w_scale).t()
+    if epilogue == 1:
+        F = N // 2
+        v = y.view(M, F // GU_BLOCK, 2, GU_BLOCK)
+        g = v[:, :, 0].reshape(M, F).to(dtype).float()
+        u = v[:, :, 1].reshape(M, F).to(dtype).float()
+        a = torch.nn.functional.silu(g).to(dtype).float()
+        return (a * u).to(dtype)
+    if epilogue == 2:
+        return (y.to(dtype).float() + residual.float()).to(dtype)
+    return y.to(dtype)

@@ -137,9 +137,10 @@ class StageExecutor:
             if cfg.model_type != "gpt2" and ops.gemm_policy() != "hipblaslt":
                 weights.pack_for_decode()
                 ops.gemm_workspace(self.device)  # allocated before any hipGraph capture
-                if os.environ.get("MPAMD_GEMM_AUTOTUNE", "1") != "0" and weights.layers:
+                if os.environ.get("MPAMD_GEMM_AUTOTUNE", "1") != "0":
                     H, F = cfg.hidden_size, cfg.intermediate_size
-                    shapes = [(cfg.q_dim + 2 * cfg.kv_dim, H, 0), (H, cfg.q_dim, 0), (2 * F, H, 1), (H, F, 0)]
+                    shapes = [] if (weights.fp8 or not weights.layers) else \
+                        [(cfg.q_dim + 2 * cfg.kv_dim, H, 0), (H, cfg.q_dim, 0), (2 * F, H, 1), (H, F, 0)]
                     if weights.lm_head_p is not None:
                         shapes.append((16 * weights.lm_head_p.shape[0], H, 0))
                     ops.autotune_gemm(shapes, self.device)
@@ -253,7 +254,35 @@ class StageExecutor:
         qkv = e("qkv", (T, cfg.q_dim + 2 * cfg.kv_dim))
         o = e("o", (T, H))
         mlp = e("mlp", (T, H))
-        if self._packed_ok(T):
+        if self._fp8_ok(T):
+            # fp8 W8A8 decode path: packed bf16 activations are quantized per row right before
+            # each GEMM (csrc/fp8.hip); weights stream at 1 byte per parameter
+            pk = ops.packed_numel
+            xn = e("xn_p", (pk(T, H),))
+            attn = e("attn_p", (pk(T, cfg.q_dim),))
+            act = e("act_p", (pk(T, cfg.intermediate_size),))
+            a8 = e("a8", (pk(T, max(H, cfg.q_dim, cfg.intermediate_size)),), torch.uint8)
+            asc = e("a8_scale", (((T + 15) // 16) * 16,), torch.float32)
+            F = cfg.intermediate_size
+            for li, L in enumerate(w.layers):
+                if li == 0:
+                    ops.rmsnorm(h, L.input_norm, eps, out=xn, residual=res, mode=2, packed=True)
+                else:
+                    ops.rmsnorm(mlp, L.input_norm, eps, out=xn, residual=res, mode=1, packed=True)
+                ops.quant_act_fp8(xn, T, H, out=a8, scale=asc)
+                ops.linear_fp8(a8, asc, L.qkv_q, L.qkv_s, T, out=qkv)
+                kc, vc = self.cache.layer(li)
+                ops.rope_kv_write(qkv, positions, self.cos, self.sin, kc, vc, slots, self.nh, self.nkv)
+                ops.paged_attention(qkv, kc, vc, table, q_seq, q_ctx, self.nh, self.nkv, self.scale, out=attn,
+                                    workspace=ws, part_size=ps, num_parts=np_, packed=True)
+                ops.quant_act_fp8(attn, T, cfg.q_dim, out=a8, scale=asc)
+                ops.linear_fp8(a8, asc, L.o_q, L.o_s, T, out=o)
+                ops.rmsnorm(o, L.post_norm, eps, out=xn, residual=res, mode=1, packed=True)
+                ops.quant_act_fp8(xn, T, H, out=a8, scale=asc)
+                ops.linear_fp8(a8, asc, L.gate_up_q, L.gate_up_s, T, out=act, epilogue=1, out_packed=True)
+                ops.quant_act_fp8(act, T, F, out=a8, scale=asc)
+                ops.linear_fp8(a8, asc, L.down_q, L.down_s, T, out=mlp)
+        elif self._packed_ok(T):
             # decode path: activations feeding a GEMM stay in the packed MFMA-fragment layout
             pk = ops.packed_numel
             xn = e("xn_p", (pk(T, H),))
@@ -282,21 +311,21 @@ class StageExecutor:
                     ops.rmsnorm(h, L.input_norm, eps, out=xn, residual=res, mode=2)
                 else:
                     ops.rmsnorm(mlp, L.input_norm, eps, out=xn, residual=res, mode=1)
-                ops.linear(xn, L.qkv, out=qkv, wp=L.qkv_p)
+                ops.linear(xn, L.dense("qkv"), out=qkv, wp=L.qkv_p)
                 kc, vc = self.cache.layer(li)
                 ops.rope_kv_write(qkv, positions, self.cos, self.sin, kc, vc, slots, self.nh, self.nkv)
                 ops.paged_attention(qkv, kc, vc, table, q_seq, q_ctx, self.nh, self.nkv, self.scale, out=attn,
                                     workspace=ws, part_size=ps, num_parts=np_)
-                ops.linear(attn, L.o, out=o, wp=L.o_p)
+                ops.linear(attn, L.dense("o"), out=o, wp=L.o_p)
                 ops.rmsnorm(o, L.post_norm, eps, out=xn, residual=res, mode=1)
-                ops.linear(xn, L.gate_up, out=act, epilogue=1, wp=L.gate_up_p)
-                ops.linear(act, L.down, out=mlp, wp=L.down_p)
+                ops.linear(xn, L.dense("gate_up"), out=act, epilogue=1, wp=L.gate_up_p)
+                ops.linear(act, L.dense("down"), out=mlp, wp=L.down_p)
         hout = ops.add(res, mlp, out=e("hout", (T, H)))
         if not self.is_last:
             return hout
         S = last_rows.numel()
         V = cfg.vocab_size
-        if w.lm_head_p is not None and self._packed_ok(S):
+        if w.lm_head_p is not None and self._head_packed_ok(S):
             fn = ops.rmsnorm(hout, w.final_norm, eps, out=e("fn_p", (ops.packed_numel(S, H),)), rows=last_rows,
                              packed=True)
             Vp = 16 * w.lm_head_p.shape[0]
@@ -304,6 +333,18 @@ class StageExecutor:
             return logits[:, :V]
         fn = ops.rmsnorm(hout, w.final_norm, eps, out=e("fn", (S, H)), rows=last_rows)
         return ops.linear(fn, w.lm_head, out=e("logits", (S, V)))
+
+    def _head_packed_ok(self, M: int) -> bool:
+        return self.device.type == "cuda" and ops.gemm_policy() != "hipblaslt" and 0 < M <= 64 and \
+            self.cfg.hidden_size % 128 == 0
+
+    def _fp8_ok(self, M: int) -> bool:
+        """fp8 W8A8 decode path: GPU, fp8 weights, fp8 GEMM shape constraints."""
+        if self.device.type != "cuda" or not 0 < M <= 64 or not self.w.fp8:
+            return False
+        cfg = self.cfg
+        return all(d % 256 == 0 for d in (cfg.hidden_size, cfg.q_dim, cfg.intermediate_size)) and \
+            (cfg.q_dim + 2 * cfg.kv_dim) % 32 == 0
 
     def _packed_ok(self, M: int) -> bool:
         """Packed-activation decode path: GPU, native GEMM allowed, all projections packed."""

@@ -332,3 +332,50 @@ def test_paged_attention_packed_output():
         op = ops.paged_attention(q, kc, vc, bt, q_seq, q_ctx, nh, nkv, 0.09, part_size=parts[0], num_parts=parts[1],
                                  packed=True)
         assert torch.equal(ref.unpack_act(op.cpu(), 3, nh * D), o.cpu())
+
+
+@pytest.mark.parametrize("M", [1, 17, 64])
+def test_fp8_quant_act_kernel_matches_reference(M):
+    from src.ops import reference as ref
+
+    K = 4096
+    x = bf(torch.randn(M, K, device=DEV) * 3)
+    xp = ops.pack_act(x)
+    a8, s = ops.quant_act_fp8(xp, M, K)
+    a8r, sr = ref.quant_act_fp8(xp.cpu(), M, K)
+    torch.testing.assert_close(s[:M].cpu(), sr[:M], rtol=1e-6, atol=0)
+    MT = (M + 15) // 16
+    got = ref.dequant_act_fp8(a8.cpu(), s.cpu(), M, K)
+    want = ref.dequant_act_fp8(a8r, sr, M, K)
+    # identical up to round-half ties of 1/scale vs *1/448 (1 fp8 ulp on a handful of elements)
+    assert (got != want).float().mean() < 1e-3
+    torch.testing.assert_close(got, want, atol=0, rtol=0.07)
+    assert a8.numel() >= MT * 16 * K
+
+
+@pytest.mark.parametrize("M", [1, 30, 64])
+@pytest.mark.parametrize("N,K,epi", [(1024, 1024, 0), (10240, 8192, 0), (8192, 28672, 0), (2048, 4096, 1),
+                                     (4096, 11008, 2)])
+def test_fp8_gemm_kernel_matches_reference(M, N, K, epi):
+    from src.ops import reference as ref
+    from src.models.weights import interleave_gate_up
+
+    x = bf(torch.randn(M, K, device=DEV))
+    if epi == 1:
+        w = interleave_gate_up(torch.randn(N // 2, K, device=DEV) * 0.02, torch.randn(N // 2, K, device=DEV) * 0.02)
+    else:
+        w = torch.randn(N, K, device=DEV) * 0.02
+    wq, ws = ops.pack_weight_fp8(w)
+    a8, s = ops.quant_act_fp8(ops.pack_act(x), M, K)
+    res = bf(torch.randn(M, N, device=DEV)) if epi == 2 else None
+    y = ops.linear_fp8(a8, s, wq, ws, M, epilogue=epi, residual=res)
+    yr = ref.linear_fp8(a8.cpu(), s.cpu(), wq.cpu(), ws.cpu(), M, epilogue=epi,
+                        residual=None if res is None else res.cpu())
+    torch.testing.assert_close(y.float().cpu(), yr.float(), atol=2e-2, rtol=2e-2)
+    if epi == 1:
+        yp = ops.linear_fp8(a8, s, wq, ws, M, epilogue=1, out_packed=True)
+        assert torch.equal(ops.unpack_act(yp, M, N // 2), y)
+    # vs the unquantized product: fp8 error budget
+    if epi == 0:
+        exact = x.float() @ w.float().t()
+        assert float((y.float() - exact).norm() / exact.norm()) < 0.06

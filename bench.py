@@ -60,6 +60,7 @@ def main(argv=None):
     ap.add_argument("--repetition-penalty", type=float, default=1.5)
     ap.add_argument("--gemm", default=os.environ.get("MPAMD_GEMM", "auto"), choices=["auto", "native", "hipblaslt"])
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--fp8", action="store_true", help="fp8 (OCP e4m3) W8A8 projections (the 70B config)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--device", default=None)
     a = ap.parse_args(argv)
@@ -93,7 +94,7 @@ def main(argv=None):
     dtype = torch.bfloat16
     t0 = time.time()
     w = random_stage_weights(cfg, start, end, has_embed=stage == 0, has_head=stage == S - 1, device=device,
-                             dtype=dtype, seed=a.seed)
+                             dtype=dtype, seed=a.seed, fp8=a.fp8)
     max_len = a.prompt_len + a.warmup + a.steps + 8
     max_len = 64 * math.ceil(max_len / 64)
     kv_bytes = None if device.type == "cuda" else 256 << 20
@@ -141,7 +142,7 @@ def main(argv=None):
     per_stage = pdist.all_gather_floats([stage_ms, float(end - start)], device)
     tokens = a.steps * M * B * R
     value = tokens / dt
-    base = baseline_value()
+    base = baseline_value() if a.model == "llama2-7b" else None  # the baseline is a Llama-2-7B number
     if rank == 0:
         rec = {
             "metric": METRIC,
@@ -155,10 +156,11 @@ def main(argv=None):
             "scaling": "weak",
             "vs_baseline": (round(value / (base * world), 3) if base else None),
             "baseline_tokens_per_s_per_gpu": base,
-            "dtype": "bf16",
-            "data": "synthetic (random-init Llama-2-7B weights, random prompt ids)",
+            "dtype": "fp8-w8a8 (bf16 activations/KV)" if a.fp8 else "bf16",
+            "data": f"synthetic (random-init {cfg.name} weights, random prompt ids)",
             "config": {
-                "model": "Llama-2-7B" if a.model == "llama2-7b" else a.model,
+                "model": {"llama2-7b": "Llama-2-7B", "llama3-70b": "Llama-3-70B", "llama3-8b": "Llama-3-8B"}.get(
+                    a.model, a.model),
                 "global_batch": M * B * R,
                 "seq_len": a.prompt_len,
                 "parallelism": f"pp{S}" + (f"xdp{R}" if R > 1 else ""),

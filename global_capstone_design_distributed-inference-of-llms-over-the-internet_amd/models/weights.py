@@ -219,10 +219,18 @@ def _random_gpt2_layer(cfg: ModelConfig, idx: int, device, dtype, seed: int) -> 
 
 
 def random_stage_weights(cfg: ModelConfig, start: int, end: int, *, has_embed: bool, has_head: bool, device,
-                         dtype=torch.bfloat16, seed: int = 0) -> StageWeights:
+                         dtype=torch.bfloat16, seed: int = 0, fp8: bool = False) -> StageWeights:
+    """``fp8``: quantize each block as soon as it is generated (bf16 copies dropped), so a
+    70B stage never holds its full bf16 weights."""
     device = torch.device(device)
     mk = _random_gpt2_layer if cfg.model_type == "gpt2" else _random_llama_layer
-    layers = [mk(cfg, i, device, dtype, seed) for i in range(start, end)]
+    layers = []
+    for i in range(start, end):
+        lay = mk(cfg, i, device, dtype, seed)
+        if fp8 and isinstance(lay, LlamaLayer):
+            one = StageWeights(cfg, i, i + 1, [lay])
+            one.quantize_fp8(drop_dense=True)
+        layers.append(lay)
     sw = StageWeights(cfg, start, end, layers)
     H, V = cfg.hidden_size, cfg.vocab_size
     if has_embed or (has_head and cfg.tie_word_embeddings):

@@ -304,15 +304,22 @@ def argmax(logits, out=None):
     return out
 
 
-def sample(logits, temps, top_ps, top_ks, rep_pens, recent, recent_len, seeds, workspace=None, out=None):
+def sample(logits, temps, top_ps, top_ks, rep_pens, recent, recent_len, seeds, workspace=None, out=None,
+           update_history: bool = False):
+    """Batched reference-semantics sampler.  ``update_history`` appends each drawn id to its
+    row of ``recent`` / ``recent_len`` (left-aligned, last ``recent.shape[1]`` ids) in place."""
     if not _native(logits):
-        return ref.sample(logits, temps, top_ps, top_ks, rep_pens, recent, recent_len, seeds, out=out)
+        out = ref.sample(logits, temps, top_ps, top_ks, rep_pens, recent, recent_len, seeds, out=out)
+        if update_history:
+            ref.push_history(recent, recent_len, out)
+        return out
     R, V = logits.shape
     if out is None:
         out = torch.empty(R, dtype=torch.long, device=logits.device)
     if workspace is None:
         workspace = torch.empty(max(1, R * V), dtype=torch.float32, device=logits.device)
-    torch.ops.mpamd.sample(logits, temps, top_ps, top_ks, rep_pens, recent, recent_len, seeds, workspace, out)
+    torch.ops.mpamd.sample(logits, temps, top_ps, top_ks, rep_pens, recent, recent_len, seeds, workspace, out,
+                           int(bool(update_history)))
     return out
 
 

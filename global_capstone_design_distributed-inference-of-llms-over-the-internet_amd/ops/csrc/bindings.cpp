@@ -27,8 +27,8 @@ int mp_swiglu(const void* gu, void* out, int64_t T, int F, hipStream_t stream);
 int mp_add(const void* a, const void* b, void* y, int64_t n, hipStream_t stream);
 int mp_argmax(const void* logits, int64_t stride, int R, int V, int64_t* out, hipStream_t stream);
 int mp_sample(const void* logits, int64_t stride, int R, int V, const float* temps, const float* top_ps,
-              const int32_t* top_ks, const float* rep_pens, const int32_t* recent, int recent_stride,
-              const int32_t* recent_len, const int64_t* seeds, float* ws, int64_t* out, hipStream_t stream);
+              const int32_t* top_ks, const float* rep_pens, int32_t* recent, int recent_stride, int32_t* recent_len,
+              const int64_t* seeds, float* ws, int64_t* out, int update, hipStream_t stream);
 int64_t mp_gemm_workspace_bytes();
 int mp_quant_act_fp8(const void* ap, void* a8, float* scale, int M, int K, hipStream_t stream);
 int mp_gemm_fp8(const void* a8, const float* as, const void* wq, const float* ws, void* y, int64_t ys, const void* res,
@@ -212,8 +212,8 @@ void argmax(const at::Tensor& logits, at::Tensor& out) {
 }
 
 void sample(const at::Tensor& logits, const at::Tensor& temps, const at::Tensor& top_ps, const at::Tensor& top_ks,
-            const at::Tensor& rep_pens, const at::Tensor& recent, const at::Tensor& recent_len,
-            const at::Tensor& seeds, at::Tensor& workspace, at::Tensor& out) {
+            const at::Tensor& rep_pens, at::Tensor& recent, at::Tensor& recent_len, const at::Tensor& seeds,
+            at::Tensor& workspace, at::Tensor& out, int64_t update) {
   check_bf16_cuda(logits, "logits");
   check_rows(logits, "logits");
   const int R = logits.size(0), V = logits.size(1);
@@ -230,7 +230,7 @@ void sample(const at::Tensor& logits, const at::Tensor& temps, const at::Tensor&
   check_launch(mp_sample(logits.data_ptr(), logits.stride(0), R, V, temps.data_ptr<float>(), top_ps.data_ptr<float>(),
                          top_ks.data_ptr<int32_t>(), rep_pens.data_ptr<float>(), recent.data_ptr<int32_t>(),
                          recent.size(1), recent_len.data_ptr<int32_t>(), seeds.data_ptr<int64_t>(),
-                         workspace.data_ptr<float>(), out.data_ptr<int64_t>(), cur_stream()),
+                         workspace.data_ptr<float>(), out.data_ptr<int64_t>(), (int)update, cur_stream()),
                "sample");
 }
 
@@ -368,8 +368,8 @@ TORCH_LIBRARY(mpamd, m) {
   m.def("add(Tensor a, Tensor b, Tensor(a!) y) -> ()");
   m.def("argmax(Tensor logits, Tensor(a!) out) -> ()");
   m.def(
-      "sample(Tensor logits, Tensor temps, Tensor top_ps, Tensor top_ks, Tensor rep_pens, Tensor recent, "
-      "Tensor recent_len, Tensor seeds, Tensor(a!) workspace, Tensor(b!) out) -> ()");
+      "sample(Tensor logits, Tensor temps, Tensor top_ps, Tensor top_ks, Tensor rep_pens, Tensor(c!) recent, "
+      "Tensor(d!) recent_len, Tensor seeds, Tensor(a!) workspace, Tensor(b!) out, int update=0) -> ()");
   m.def(
       "gemm(Tensor x, Tensor wp, Tensor(a!) y, Tensor? residual, int epilogue, int M, int flags, "
       "Tensor(b!)? workspace=None) -> ()");

@@ -9,10 +9,18 @@
 //   softmax(logits / max(T, 1e-5)), top-k mask (0 < k < V), top-p "keep cum <= p, always
 //   keep the first", renormalise, draw one id.
 // Instead of a Python loop, torch.topk, a full sort and a cumsum, one 1024-thread block per
-// row does: fp32 copy -> penalty -> softmax -> radix-select top-k threshold (4 x 8-bit
-// histogram passes) -> radix top-p threshold on probability MASS histograms -> one
-// inverse-CDF draw with a block scan.  Ties at a threshold value are kept together
-// (torch.topk/sort break them by position; documented divergence).
+// row works on an fp32 copy of the row in LDS:
+//   * top-k path (0 < k < V, the reference CLI default k = 50): penalty -> max -> softmax
+//     normaliser Z -> ONE 2048-bin histogram of the order-preserving logit key picks the bin
+//     holding the k-th largest -> the (few) candidates at or above it are collected, ranked by
+//     value (index breaks ties, like a stable sort), and top-p / renormalise / the draw run
+//     on the <= k sorted candidates only.  Five sweeps over the row, no sort of V.
+//   * otherwise (no top-k, or a degenerate row with > 1024 candidates): radix-select on the
+//     probabilities (4 x 8-bit passes) for top-k and on probability MASS for top-p, then an
+//     inverse-CDF draw with a block scan.  Ties at a threshold value are kept together there.
+// The per-row history of the last RECENT generated ids (repetition penalty input) is
+// updated in place by the same kernel (``update`` flag), so the serving loop needs no extra
+// device ops per token.
 #include "common.h"
 
 namespace mp {
@@ -24,7 +32,25 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
   return x ^ (x >> 31);
 }
 
-constexpr int SB = 1024;  // threads per block
+constexpr int SB = 1024;   // threads per block
+constexpr int CAND = 1024;  // top-k candidate capacity of the fast path
+
+// order-preserving unsigned key of a float (ascending key == ascending value)
+__device__ __forceinline__ unsigned okey(float f) {
+  const unsigned b = __float_as_uint(f);
+  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+
+// Append a generated id to a row's left-aligned history of the last `cap` ids.
+__device__ __forceinline__ void push_history(int32_t* rec, int32_t* len, int cap, int tok) {
+  int n = *len;
+  if (n >= cap) {
+    for (int j = 0; j + 1 < cap; ++j) rec[j] = rec[j + 1];
+    n = cap - 1;
+  }
+  rec[n] = tok;
+  *len = n + 1;
+}
 
 // Exclusive block scan of one float per thread (blockDim == SB).
 __device__ __forceinline__ float block_excl_scan(float v, float* red, float* total) {
@@ -56,10 +82,10 @@ __global__ __launch_bounds__(SB) void sample_kernel(const bf16_t* __restrict__ l
                                                     const float* __restrict__ temps, const float* __restrict__ top_ps,
                                                     const int32_t* __restrict__ top_ks,
                                                     const float* __restrict__ rep_pens,
-                                                    const int32_t* __restrict__ recent, int recent_stride,
-                                                    const int32_t* __restrict__ recent_len,
+                                                    int32_t* __restrict__ recent, int recent_stride,
+                                                    int32_t* __restrict__ recent_len,
                                                     const int64_t* __restrict__ seeds, float* __restrict__ ws,
-                                                    int64_t* __restrict__ out, int use_lds) {
+                                                    int64_t* __restrict__ out, int use_lds, int update) {
   __shared__ float red[SB / 64 + 1];
   __shared__ unsigned hist[256];
   __shared__ float mass[256];
@@ -98,6 +124,8 @@ __global__ __launch_bounds__(SB) void sample_kernel(const bf16_t* __restrict__ l
       for (int k = 1; k < SB / 64; ++k)
         if (bv[k] > b || (bv[k] == b && bi[k] < ix)) { b = bv[k]; ix = bi[k]; }
       out[row] = ix == 0x7fffffff ? 0 : ix;
+      if (update) push_history(recent + (int64_t)row * recent_stride, recent_len + row, recent_stride,
+                               ix == 0x7fffffff ? 0 : ix);
     }
     return;
   }
@@ -136,22 +164,94 @@ __global__ __launch_bounds__(SB) void sample_kernel(const bf16_t* __restrict__ l
     __syncthreads();
   }
 
-  // ---- softmax(x / T) ----
+  // ---- softmax(x / T): max and normaliser (x keeps the penalised logits) ----
   const float inv_t = 1.f / fmaxf(temp, 1e-5f);
   float lm = -INFINITY;
   for (int i = tid; i < V; i += SB) lm = fmaxf(lm, x[i]);
   const float m = block_max(lm, red);
   float ls = 0.f;
-  for (int i = tid; i < V; i += SB) {
-    const float e = __expf((x[i] - m) * inv_t);
-    x[i] = e;
-    ls += e;
+  for (int i = tid; i < V; i += SB) ls += __expf((x[i] - m) * inv_t);
+  const float inv_s = 1.f / block_sum(ls, red);
+  const int k = top_ks[row];
+  const float tp = top_ps[row];
+  const uint64_t rnd = splitmix64((uint64_t)seeds[row] * 0x9E3779B97F4A7C15ull + (uint64_t)row);
+  const float u01 = (float)((double)(rnd >> 11) * (1.0 / 9007199254740992.0));
+
+  if (k > 0 && k < V) {
+    // ---- fast top-k: 2048-bin histogram of the order-preserving key, bin of the k-th largest ----
+    __shared__ unsigned h2k[2048];
+    __shared__ unsigned c_key[CAND];
+    __shared__ int c_idx[CAND];
+    __shared__ float c_p[CAND];
+    __shared__ int s_cnt;
+    for (int i = tid; i < 2048; i += SB) h2k[i] = 0;
+    if (tid == 0) s_cnt = 0;
+    __syncthreads();
+    for (int i = tid; i < V; i += SB) atomicAdd(&h2k[okey(x[i]) >> 21], 1u);
+    __syncthreads();
+    const float own0 = (float)h2k[2 * tid], own1 = (float)h2k[2 * tid + 1];
+    float tot;
+    const float P = block_excl_scan(own0 + own1, red, &tot);  // elements in bins < 2 tid
+    const float ge1 = tot - P - own0, ge0 = tot - P;          // elements in bins >= 2t+1 / >= 2t
+    const float kf = (float)k;
+    if (ge1 >= kf && ge1 - own1 < kf) { s_u[0] = 2 * tid + 1; s_u[1] = (unsigned)ge1; }
+    if (ge0 >= kf && ge0 - own0 < kf) { s_u[0] = 2 * tid; s_u[1] = (unsigned)ge0; }
+    __syncthreads();
+    const unsigned bstar = s_u[0], ncand = s_u[1];
+    if (ncand <= CAND) {
+      for (int i = tid; i < V; i += SB) {
+        const unsigned key = okey(x[i]);
+        if ((key >> 21) >= bstar) {
+          const int pos = atomicAdd(&s_cnt, 1);
+          c_key[pos] = key;
+          c_idx[pos] = i;
+        }
+      }
+      __syncthreads();
+      const int c = s_cnt;
+      // rank by (value desc, index asc); rank < k survives top-k
+      int rank = CAND, my_idx = 0;
+      if (tid < c) {
+        const unsigned kt = c_key[tid];
+        my_idx = c_idx[tid];
+        rank = 0;
+        for (int j = 0; j < c; ++j) {
+          const unsigned kj = c_key[j];
+          rank += (kj > kt) || (kj == kt && c_idx[j] < my_idx);
+        }
+      }
+      __syncthreads();
+      if (rank < k) {  // sorted (descending) survivors: index and FULL-softmax probability
+        c_idx[rank] = my_idx;
+        c_p[rank] = __expf((x[my_idx] - m) * inv_t) * inv_s;
+      }
+      __syncthreads();
+      const int kk = min(k, c);
+      const float pv = tid < kk ? c_p[tid] : 0.f;
+      float t1;
+      const float ex1 = block_excl_scan(pv, red, &t1);
+      // top-p (reference): keep sorted prefix with cumulative <= p, always keep the first
+      const bool keep = tid < kk && (tid == 0 || !(tp > 0.f && tp < 1.f) || ex1 + pv <= tp);
+      const float q = keep ? pv : 0.f;
+      float t2;
+      const float ex2 = block_excl_scan(q, red, &t2);
+      const float uu = u01 * t2;
+      if (tid == 0) s_i[1] = c_idx[0];  // rounding fallback: the most likely id
+      __syncthreads();
+      if (q > 0.f && uu >= ex2 && uu < ex2 + q) s_i[1] = c_idx[tid];
+      __syncthreads();
+      if (tid == 0) {
+        out[row] = s_i[1];
+        if (update) push_history(recent + (int64_t)row * recent_stride, recent_len + row, recent_stride, s_i[1]);
+      }
+      return;
+    }
+    // degenerate row (too many candidates at the k-th value): general path below
   }
-  const float s = block_sum(ls, red);
-  const float inv_s = 1.f / s;
+  // general path works on probabilities
   unsigned maxbits = 0;
   for (int i = tid; i < V; i += SB) {
-    const float pv = x[i] * inv_s;
+    const float pv = __expf((x[i] - m) * inv_t) * inv_s;
     x[i] = pv;
     maxbits = max(maxbits, __float_as_uint(pv));
   }
@@ -163,12 +263,11 @@ __global__ __launch_bounds__(SB) void sample_kernel(const bf16_t* __restrict__ l
     if ((tid & 63) == 0) red[tid >> 6] = __uint_as_float(maxbits);
     __syncthreads();
     unsigned mb = 0;
-    for (int k = 0; k < SB / 64; ++k) mb = max(mb, __float_as_uint(red[k]));
+    for (int k2 = 0; k2 < SB / 64; ++k2) mb = max(mb, __float_as_uint(red[k2]));
     maxbits = mb;
   }
 
   // ---- top-k: radix-select the k-th largest probability (bits are order-preserving, p >= 0) ----
-  const int k = top_ks[row];
   if (k > 0 && k < V) {
     unsigned prefix = 0, msk = 0;
     int kk = k;
@@ -217,7 +316,6 @@ __global__ __launch_bounds__(SB) void sample_kernel(const bf16_t* __restrict__ l
   }
 
   // ---- top-p: smallest kept value = first value whose cumulative (descending) mass > p ----
-  const float tp = top_ps[row];
   if (tp > 0.f && tp < 1.f) {
     unsigned prefix = 0, msk = 0;
     float above = 0.f;
@@ -291,8 +389,7 @@ __global__ __launch_bounds__(SB) void sample_kernel(const bf16_t* __restrict__ l
   for (int i = lo; i < hi; ++i) loc += x[i];
   float total;
   const float excl = block_excl_scan(loc, red, &total);
-  const uint64_t r = splitmix64((uint64_t)seeds[row] * 0x9E3779B97F4A7C15ull + (uint64_t)row);
-  const float u = (float)((double)(r >> 11) * (1.0 / 9007199254740992.0)) * total;
+  const float u = u01 * total;
   if (tid == 0) s_i[1] = -1;
   __syncthreads();
   if (loc > 0.f && u >= excl && u < excl + loc) {
@@ -316,21 +413,23 @@ __global__ __launch_bounds__(SB) void sample_kernel(const bf16_t* __restrict__ l
         if (__float_as_uint(x[i]) == maxbits) { pick = i; break; }
     }
     out[row] = pick < 0 ? 0 : pick;
+    if (update) push_history(recent + (int64_t)row * recent_stride, recent_len + row, recent_stride,
+                             pick < 0 ? 0 : pick);
   }
 }
 
 }  // namespace mp
 
 extern "C" int mp_sample(const void* logits, int64_t stride, int R, int V, const float* temps, const float* top_ps,
-                         const int32_t* top_ks, const float* rep_pens, const int32_t* recent, int recent_stride,
-                         const int32_t* recent_len, const int64_t* seeds, float* ws, int64_t* out,
+                         const int32_t* top_ks, const float* rep_pens, int32_t* recent, int recent_stride,
+                         int32_t* recent_len, const int64_t* seeds, float* ws, int64_t* out, int update,
                          hipStream_t stream) {
   using namespace mp;
   if (R == 0) return 0;
   if (recent_stride > SB) return -1;
   const size_t lds = (size_t)V * sizeof(float);
-  const int use_lds = lds <= 150 * 1024;
+  const int use_lds = lds <= 136 * 1024;  // + ~23 KB of histogram / candidate arrays
   hipLaunchKernelGGL(sample_kernel, dim3(R), dim3(SB), use_lds ? lds : 0, stream, (const bf16_t*)logits, stride, V,
-                     temps, top_ps, top_ks, rep_pens, recent, recent_stride, recent_len, seeds, ws, out, use_lds);
+                     temps, top_ps, top_ks, rep_pens, recent, recent_stride, recent_len, seeds, ws, out, use_lds, update);
   return (int)hipGetLastError();
 }

@@ -236,6 +236,18 @@ def sample_row(logits_row: torch.Tensor, temperature: float, top_p: float, top_k
     return int(torch.multinomial(probs, 1, generator=generator).item())
 
 
+def push_history(recent, recent_len, toks):
+    """Append toks[r] to row r of the left-aligned history (drop the oldest when full)."""
+    cap = recent.shape[1]
+    for r in range(recent.shape[0]):
+        n = int(recent_len[r])
+        if n >= cap:
+            recent[r, :-1] = recent[r, 1:].clone()
+            n = cap - 1
+        recent[r, n] = int(toks[r])
+        recent_len[r] = n + 1
+
+
 def sample(logits, temps, top_ps, top_ks, rep_pens, recent, recent_len, seeds, workspace=None, out=None):
     R = logits.shape[0]
     res = torch.empty(R, dtype=torch.long, device=logits.device)

@@ -143,20 +143,13 @@ class PipelineEngine:
 
     # ------------------------------------------------------------------ sampling on the last stage
     def _sample(self, mb: MicroBatch, logits: torch.Tensor) -> torch.Tensor:
+        """One fused kernel per micro-batch: penalty + top-k/top-p draw (or argmax at T <= 0)
+        and the device-side history update (no host round trip, no extra device ops)."""
         B = logits.shape[0]
-        if self.sp.temperature <= 0:
-            tok = ops.argmax(logits)
-        else:
-            seeds = (self._arange[:B] + (self.seed * 1000003 + mb.step * 7919 + mb.index * 104729
-                                         + self.replica * 15485863) * 4096)
-            tok = ops.sample(logits, self._temps[:B], self._topp[:B], self._topk[:B], self._rp[:B], mb.recent,
-                             mb.recent_len, seeds)
-        # device-side rolling history (left-aligned, newest at recent_len-1)
-        full = (mb.recent_len >= RECENT).unsqueeze(1)
-        mb.recent.copy_(torch.where(full, torch.roll(mb.recent, -1, 1), mb.recent))
-        pos = torch.clamp(mb.recent_len, max=RECENT - 1).long().unsqueeze(1)
-        mb.recent.scatter_(1, pos, tok.to(torch.int32).unsqueeze(1))
-        mb.recent_len.copy_(torch.clamp(mb.recent_len + 1, max=RECENT))
+        seeds = (self._arange[:B] + (self.seed * 1000003 + mb.step * 7919 + mb.index * 104729
+                                     + self.replica * 15485863) * 4096)
+        tok = ops.sample(logits, self._temps[:B], self._topp[:B], self._topk[:B], self._rp[:B], mb.recent,
+                         mb.recent_len, seeds, update_history=True)
         mb.step += 1
         return tok
 

@@ -379,3 +379,59 @@ def test_fp8_gemm_kernel_matches_reference(M, N, K, epi):
     if epi == 0:
         exact = x.float() @ w.float().t()
         assert float((y.float() - exact).norm() / exact.norm()) < 0.06
+
+
+@pytest.mark.parametrize("k,tp", [(50, 0.92), (0, 0.92), (50, 1.0)])
+def test_sampler_large_vocab_distribution(k, tp):
+    """V = 32000 at the reference CLI defaults: fast top-k candidate path (k > 0) and the
+    general radix path (k = 0) both sample the reference's filtered distribution."""
+    V, R = 32000, 8192
+    g = torch.Generator().manual_seed(11)
+    base = torch.randn(V, generator=g) * 1.5
+    base[:20] += 6  # a peaked head, like real LM logits
+    logits = bf(base.to(DEV).unsqueeze(0).repeat(R, 1))
+    kw = dict(top_ps=torch.full((R,), tp, device=DEV), top_ks=torch.full((R,), k, dtype=torch.int32, device=DEV),
+              rep_pens=torch.ones(R, device=DEV), recent=torch.zeros(R, 50, dtype=torch.int32, device=DEV),
+              recent_len=torch.zeros(R, dtype=torch.int32, device=DEV),
+              seeds=torch.arange(R, dtype=torch.long, device=DEV) * 13 + 1)
+    out = ops.sample(logits, torch.ones(R, device=DEV), **kw).cpu()
+    p = torch.softmax(logits[0].float().cpu(), -1)
+    q = p
+    if 0 < k < V:
+        tv, ti = torch.topk(p, k)
+        q = torch.zeros_like(p).scatter(0, ti, tv)
+    if 0 < tp < 1:
+        sp, si = torch.sort(q, descending=True)
+        keep = torch.cumsum(sp, 0) <= tp
+        keep[0] = True
+        q = torch.zeros_like(p).scatter(0, si, sp * keep)
+    f = q / q.sum()
+    freq = torch.bincount(out, minlength=V).float() / R
+    assert set(out.unique().tolist()) <= set(torch.nonzero(f).flatten().tolist())
+    assert (freq - f).abs().max().item() < 0.03
+
+
+def test_sampler_history_update_and_degenerate_row():
+    R, V = 3, 32000
+    logits = torch.zeros(R, V, device=DEV)
+    logits[1, 123] = 50.0
+    logits = bf(logits)  # row 0 / 2: all-equal logits -> > 1024 top-k candidates (general path)
+    recent = torch.zeros(R, 50, dtype=torch.int32, device=DEV)
+    recent_len = torch.tensor([0, 50, 3], dtype=torch.int32, device=DEV)
+    recent[1] = torch.arange(50, dtype=torch.int32, device=DEV) + 1000
+    recent[2, :3] = torch.tensor([7, 8, 9], dtype=torch.int32, device=DEV)
+    kw = dict(top_ps=torch.full((R,), 0.9, device=DEV), top_ks=torch.full((R,), 50, dtype=torch.int32, device=DEV),
+              rep_pens=torch.ones(R, device=DEV), seeds=torch.arange(R, device=DEV))
+    out = ops.sample(logits, torch.ones(R, device=DEV), recent=recent, recent_len=recent_len, update_history=True,
+                     **kw)
+    o = out.cpu().tolist()
+    assert o[1] == 123 and 0 <= o[0] < V and 0 <= o[2] < V
+    assert recent_len.cpu().tolist() == [1, 50, 4]
+    r = recent.cpu()
+    assert r[0, 0] == o[0]
+    assert r[1, :49].tolist() == list(range(1001, 1050)) and r[1, 49] == 123
+    assert r[2, :4].tolist() == [7, 8, 9, o[2]]
+    # greedy rows update too
+    out2 = ops.sample(logits, torch.zeros(R, device=DEV), recent=recent, recent_len=recent_len,
+                      update_history=True, **kw)
+    assert out2.cpu().tolist()[1] == 123 and recent_len.cpu().tolist() == [2, 50, 5]

@@ -202,11 +202,60 @@ class StageExecutor:
         """One ragged step.  ``x``: token ids [T] (first stage) or hidden [T, H].
 
         Returns hidden [T, H] (non-last stage) or last-token logits [S, V] (last stage).
+        Steps larger than ``max_tokens_per_step`` run as consecutive chunks (chunked prefill,
+        upstream Petals TransformerBackend.inference_step): a long prompt is split at token
+        boundaries, later pieces attend to the KV the earlier pieces wrote.
         """
+        T = sum(int(n) for _, n in seqs)
+        if T > self.max_tokens:
+            return self._forward_chunked(seqs, x, **plan_kw)
         plan = self.plan(seqs, **plan_kw)
         out = self.run(plan, x)
         self.commit(plan)
         return out
+
+    def _forward_chunked(self, seqs, x, reset: Sequence[bool] = (), starts=None, max_length=None):
+        C = self.max_tokens
+        pieces = []  # (seq index, token offset within the seq, count, offset into x)
+        xoff = 0
+        for i, (sid, n) in enumerate(seqs):
+            off = 0
+            while off < n:
+                pieces.append((i, off, min(int(n) - off, C), xoff + off))
+                off += pieces[-1][2]
+            xoff += int(n)
+        chunks, cur, used = [], [], 0
+        for pc in pieces:
+            if used + pc[2] > C and cur:
+                chunks.append(cur)
+                cur, used = [], 0
+            take = pc
+            while used + take[2] > C:  # a piece longer than the room left: split it
+                room = C - used
+                cur.append((take[0], take[1], room, take[3]))
+                chunks.append(cur)
+                cur, used = [], 0
+                take = (take[0], take[1] + room, take[2] - room, take[3] + room)
+            cur.append(take)
+            used += take[2]
+        if cur:
+            chunks.append(cur)
+        hidden, logits = [], [None] * len(seqs)
+        for ch in chunks:
+            sub = [(seqs[i][0], c) for (i, off, c, _) in ch]
+            sub_reset = [bool(reset[i]) if (reset and off == 0) else False for (i, off, c, _) in ch]
+            sub_starts = [(starts[i] if (starts is not None and off == 0) else None) for (i, off, c, _) in ch]
+            xs = torch.cat([x[xo:xo + c] for (_, _, c, xo) in ch])
+            out = self.forward(sub, xs, reset=sub_reset, starts=sub_starts, max_length=max_length)
+            if self.is_last:
+                for r, (i, off, c, _) in enumerate(ch):
+                    if off + c == int(seqs[i][1]):
+                        logits[i] = out[r]
+            else:
+                hidden.append(out)
+        if self.is_last:
+            return torch.stack(logits)
+        return torch.cat(hidden)
 
     def run(self, plan: Plan, x: torch.Tensor) -> torch.Tensor:
         if plan.T == 0:

@@ -105,3 +105,31 @@ def test_packed_layouts_cpu_roundtrip():
     assert torch.equal(g, g2) and torch.equal(u, u2)
     y = ops.linear(ops.pack_act(x[:, :128]), None, wp=ops.pack_weight(w), a_rows=37)
     torch.testing.assert_close(y, x[:, :128] @ w.t())
+
+
+def test_chunked_prefill_matches_single_step():
+    """A prompt longer than max_tokens_per_step runs as chunks with identical results."""
+    import torch
+
+    from src.models.config import resolve_model
+    from src.models.weights import random_stage_weights
+    from src.runtime.executor import StageExecutor
+
+    cfg = resolve_model("tiny-llama")
+    for head in (True, False):
+        w = random_stage_weights(cfg, 0, 2, has_embed=True, has_head=head, device="cpu", dtype=torch.float32)
+        big = StageExecutor(cfg, w, "cpu", dtype=torch.float32, kv_cache_bytes=8 << 20, max_sessions=4,
+                            max_seq_len=128, max_tokens_per_step=64)
+        small = StageExecutor(cfg, w, "cpu", dtype=torch.float32, kv_cache_bytes=8 << 20, max_sessions=4,
+                              max_seq_len=128, max_tokens_per_step=7)
+        g = torch.Generator().manual_seed(4)
+        ids = torch.randint(0, cfg.vocab_size, (20 + 9,), generator=g)
+        seqs = [("a", 20), ("b", 9)]
+        ref = big.forward(seqs, ids, reset=[True, True])
+        got = small.forward(seqs, ids, reset=[True, True])
+        torch.testing.assert_close(got, ref, atol=1e-4, rtol=1e-4)
+        assert small.sessions.get("a").length == 20 and small.sessions.get("b").length == 9
+        # decode continues on the chunk-written KV
+        nxt = torch.tensor([3, 5])
+        torch.testing.assert_close(small.forward([("a", 1), ("b", 1)], nxt), big.forward([("a", 1), ("b", 1)], nxt),
+                                   atol=1e-4, rtol=1e-4)

@@ -7,8 +7,10 @@
 //   grid  = (num_parts, nkv, T)   one workgroup per (query row, kv head, context slice)
 //   block = 256 threads (4 waves of 64)
 //
-// Each workgroup serves all NREP = nh / nkv query heads of its kv head (GQA without
-// materialising repeat_kv).  Lane mapping: LPT = D/8 lanes per token, each lane owns 8
+// Each workgroup serves NREP (<= nh / nkv) query heads of one kv head (GQA without
+// materialising repeat_kv): blockIdx.y * NREP is its first query head, so a GQA group of
+// 8 heads runs as two workgroups of 4 (K/V re-read from L2, half the q/acc registers:
+// the register count, not the math, limits how many K/V bytes a CU keeps in flight).  Lane mapping: LPT = D/8 lanes per token, each lane owns 8
 // head dims (one 16-B load); a wave-instruction covers 64/LPT consecutive tokens, i.e.
 // 1 KiB of contiguous cache.  Partial dot products are summed over the LPT lanes with
 // DPP row permutes (no LDS traffic), scores live in LDS, softmax is done in the exp2
@@ -20,6 +22,7 @@
 // ctx = start + i + 1 -> causal) and replay.  ctx == 0 rows (batch padding) output 0.
 // packed_mt > 0 writes the output in the packed decode-GEMM activation layout (common.h).
 #include "common.h"
+#include <stdlib.h>
 
 namespace mp {
 
@@ -43,7 +46,7 @@ __global__ __launch_bounds__(256) void paged_attn_kernel(
     const bf16_t* __restrict__ q, int64_t q_stride, const bf16_t* __restrict__ kc,
     const bf16_t* __restrict__ vc, const int32_t* __restrict__ block_tables, int bt_stride,
     const int32_t* __restrict__ q_seq, const int32_t* __restrict__ q_ctx, bf16_t* __restrict__ out,
-    float* __restrict__ part_o, float* __restrict__ part_ml, int nkv, int page_log2, int PS, int NP,
+    float* __restrict__ part_o, float* __restrict__ part_ml, int nkv, int nh, int page_log2, int PS, int NP,
     float scale_log2, int packed_mt) {
   constexpr int LPT = D / 8;
   constexpr int TPI = 64 / LPT;
@@ -54,20 +57,21 @@ __global__ __launch_bounds__(256) void paged_attn_kernel(
   float* s_red = smem + NREP * PS;    // [4][NREP] per-wave maxes, then [4][NREP] sums
   float* s_o = s_red + 8 * NREP;      // [4][NREP][D]
 
-  const int t = blockIdx.z, g = blockIdx.y, p = blockIdx.x;
+  const int t = blockIdx.z, p = blockIdx.x;
+  const int hbase = blockIdx.y * NREP;  // first query head of this workgroup
+  const int g = hbase / (nh / nkv);      // its kv head
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int sl = lane % LPT, tg = lane / LPT;
-  const int nh = nkv * NREP;
   const int ctx = q_ctx[t];
   const int start = p * PS;
   const int end = min(start + PS, ctx);
-  const int64_t obase = ((int64_t)t * nh + (int64_t)g * NREP) * D;
+  const int64_t obase = ((int64_t)t * nh + hbase) * D;
   if (start >= end) {
     if (NP == 1) {
       for (int i = tid; i < NREP * D; i += 256)
-        out[packed_mt > 0 ? apk_off(t, g * NREP * D + i, packed_mt) : obase + i] = 0;
+        out[packed_mt > 0 ? apk_off(t, hbase * D + i, packed_mt) : obase + i] = 0;
     } else if (tid < NREP) {
-      float* ml = part_ml + (((int64_t)t * nh + g * NREP + tid) * NP + p) * 2;
+      float* ml = part_ml + (((int64_t)t * nh + hbase + tid) * NP + p) * 2;
       ml[0] = -INFINITY;
       ml[1] = 0.f;
     }
@@ -81,7 +85,7 @@ __global__ __launch_bounds__(256) void paged_attn_kernel(
   float qf[NREP][8];
 #pragma unroll
   for (int r = 0; r < NREP; ++r) {
-    const u16x8 v = *reinterpret_cast<const u16x8*>(q + (int64_t)t * q_stride + (g * NREP + r) * D + sl * 8);
+    const u16x8 v = *reinterpret_cast<const u16x8*>(q + (int64_t)t * q_stride + (hbase + r) * D + sl * 8);
 #pragma unroll
     for (int j = 0; j < 8; ++j) qf[r][j] = bf2f(v[j]) * scale_log2;
   }
@@ -204,9 +208,9 @@ __global__ __launch_bounds__(256) void paged_attn_kernel(
                     s_o[(3 * NREP + r) * D + d];
     const float l = s_l[r] + s_l[NREP + r] + s_l[2 * NREP + r] + s_l[3 * NREP + r];
     if (NP == 1) {
-      out[packed_mt > 0 ? apk_off(t, g * NREP * D + i, packed_mt) : obase + i] = f2bf(o / l);
+      out[packed_mt > 0 ? apk_off(t, hbase * D + i, packed_mt) : obase + i] = f2bf(o / l);
     } else {
-      const int64_t hp = ((int64_t)t * nh + g * NREP + r) * NP + p;
+      const int64_t hp = ((int64_t)t * nh + hbase + r) * NP + p;
       part_o[hp * D + d] = o;
       if (d == 0) {
         float m = mrow[0];
@@ -249,12 +253,12 @@ __global__ void paged_attn_reduce_kernel(const float* __restrict__ part_o, const
 template <int D, int NREP>
 static void launch_attn(const void* q, int64_t q_stride, const void* kc, const void* vc, const int32_t* bt,
                         int bt_stride, const int32_t* q_seq, const int32_t* q_ctx, void* out, float* ws_o,
-                        float* ws_ml, int T, int nkv, int page_log2, int PS, int NP, float scale_log2, int packed_mt,
-                        hipStream_t stream) {
+                        float* ws_ml, int T, int nkv, int nh, int page_log2, int PS, int NP, float scale_log2,
+                        int packed_mt, hipStream_t stream) {
   const size_t lds = (size_t)(NREP * PS + 8 * NREP + 4 * NREP * D) * sizeof(float);
-  hipLaunchKernelGGL((paged_attn_kernel<D, NREP>), dim3(NP, nkv, T), dim3(256), lds, stream, (const bf16_t*)q,
+  hipLaunchKernelGGL((paged_attn_kernel<D, NREP>), dim3(NP, nh / NREP, T), dim3(256), lds, stream, (const bf16_t*)q,
                      q_stride, (const bf16_t*)kc, (const bf16_t*)vc, bt, bt_stride, q_seq, q_ctx, (bf16_t*)out,
-                     ws_o, ws_ml, nkv, page_log2, PS, NP, scale_log2, packed_mt);
+                     ws_o, ws_ml, nkv, nh, page_log2, PS, NP, scale_log2, packed_mt);
 }
 
 }  // namespace mp
@@ -273,10 +277,17 @@ extern "C" int mp_paged_attention(const void* q, int64_t q_stride, const void* k
   const float scale_log2 = scale * 1.4426950408889634f;
   float* ws_o = workspace;
   float* ws_ml = workspace + (int64_t)T * nh * NP * D;
+  // heads per workgroup: at most ATTN_HPB of a GQA group (register budget), a divisor of nrep
+  static const int hpb_max = [] {
+    const char* v = getenv("MPAMD_ATTN_HPB");
+    return v ? atoi(v) : 4;
+  }();
+  int hpb = 1;
+  while (hpb * 2 <= hpb_max && nrep % (hpb * 2) == 0) hpb *= 2;
 #define MP_ATTN_CASE(DD, RR)                                                                                  \
-  if (D == DD && nrep == RR) {                                                                                \
-    launch_attn<DD, RR>(q, q_stride, kc, vc, bt, bt_stride, q_seq, q_ctx, out, ws_o, ws_ml, T, nkv, page_log2, \
-                        PS, NP, scale_log2, packed_mt, stream);                                               \
+  if (D == DD && hpb == RR) {                                                                                 \
+    launch_attn<DD, RR>(q, q_stride, kc, vc, bt, bt_stride, q_seq, q_ctx, out, ws_o, ws_ml, T, nkv, nh,       \
+                        page_log2, PS, NP, scale_log2, packed_mt, stream);                                    \
     goto launched;                                                                                            \
   }
   MP_ATTN_CASE(128, 1)

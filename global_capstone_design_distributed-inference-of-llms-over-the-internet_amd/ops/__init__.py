@@ -242,6 +242,52 @@ def attention_partition(num_queries: int, nkv: int, max_ctx: int, target_wgs: in
     return ps, np_
 
 
+def query_blocks(ntoks, nrep: int):
+    """MFMA attention query blocks for a ragged step: int32 [2, NB] = (first flat token, count).
+
+    A block holds 16 / min(nrep, 16) consecutive tokens of ONE sequence (x the GQA group's
+    heads = 16 MFMA rows).  ``ntoks``: tokens per sequence in flat order."""
+    import numpy as np
+
+    tb = 16 // min(max(int(nrep), 1), 16)
+    n = np.asarray(ntoks, dtype=np.int64)
+    off = np.concatenate([[0], np.cumsum(n)[:-1]]) if n.size else n
+    nb = (n + tb - 1) // tb
+    seq_of_block = np.repeat(np.arange(n.size), nb)
+    k = np.arange(int(nb.sum())) - np.repeat(np.concatenate([[0], np.cumsum(nb)[:-1]]) if nb.size else nb, nb)
+    tok0 = off[seq_of_block] + k * tb
+    cnt = np.minimum(tb, n[seq_of_block] - k * tb)
+    return np.stack([tok0, cnt]).astype(np.int32)
+
+
+def attention_mfma(q, k_cache, v_cache, block_tables, q_seq, q_ctx, qblocks, nh, nkv, scale, out=None,
+                   workspace=None, part_size=None, num_parts=None, max_ctx=None, packed=False):
+    """MFMA flash attention (csrc/attention_mfma.hip): prefill blocks of 16 query rows and GQA
+    decode.  Same semantics and output as ``paged_attention``; ``qblocks`` from
+    ``query_blocks`` (device int32 [2, NB])."""
+    if not _native(q):
+        return paged_attention(q, k_cache, v_cache, block_tables, q_seq, q_ctx, nh, nkv, scale, out=out,
+                               packed=packed)
+    T = q.shape[0]
+    D = k_cache.shape[-1]
+    if part_size is None:
+        if max_ctx is None:
+            max_ctx = int(q_ctx.max().item()) if T else 1
+        nblk = qblocks.shape[1] * (nh // min(nh // nkv, 16))
+        want = max(1, math.ceil(1024 / max(1, nblk)))
+        num_parts = max(1, min(want, math.ceil(max_ctx / 128)))
+        part_size = 128 * math.ceil(math.ceil(max_ctx / num_parts) / 128)
+        num_parts = math.ceil(max(max_ctx, 1) / part_size)
+    if out is None:
+        out = (torch.empty(packed_numel(T, nh * D), dtype=q.dtype, device=q.device) if packed
+               else torch.empty(T, nh * D, dtype=q.dtype, device=q.device))
+    if workspace is None or (num_parts > 1 and workspace.numel() < T * nh * num_parts * (D + 2)):
+        workspace = attention_workspace(T, nh, D, num_parts, q.device)
+    torch.ops.mpamd.attention_mfma(q, k_cache, v_cache, block_tables, q_seq, q_ctx, qblocks, out, workspace, nh, nkv,
+                                   float(scale), int(part_size), int(num_parts), int(bool(packed)))
+    return out
+
+
 def attention_workspace(num_queries: int, nh: int, head_dim: int, num_parts: int, device) -> torch.Tensor:
     return torch.empty(max(1, num_queries * nh * num_parts * (head_dim + 2)), dtype=torch.float32, device=device)
 

@@ -1,0 +1,255 @@
+// MFMA flash attention over the paged KV cache for gfx950 (survey K7: "attn_prefill ...
+// MFMA QK^T and PV, LDS tiles"; also GQA decode).
+//
+// A workgroup (4 waves) owns a block of 16 query ROWS of one kv head: row r is query token
+// tok0 + r / HB of one sequence and query head hbase + r % HB (HB = heads of the GQA group
+// in the block, TB = 16 / HB tokens).  So MHA prefill processes 16 consecutive tokens per
+// block (K/V read once per 16 queries instead of once per query), and GQA decode puts the
+// whole group (4 or 8 heads of one token) into the MFMA M dimension.
+//
+// Per wave and per 32-token step of the context (waves interleave steps):
+//   S^T[tok][row] = K[tok, :] . Q[row, :]          2 x (D/32) v_mfma_f32_16x16x32_bf16
+//       A = K rows straight from the cache page (lane (q, c): 16 B of token c at d = 8q),
+//       B = Q^T fragments held in registers for the whole kernel;
+//   online softmax per row in the exp2 domain (row = lane & 15; the 4 lanes of a row
+//       combine with two xor shuffles), causal + context masking per row;
+//   O[row][d] += P[row][tok] . V[tok][d]            D/16 MFMAs
+//       A = P straight from the S^T accumulators: lane (q, c) holds row c at tokens
+//       {4q..4q+3, 16+4q..16+4q+3}, used as the MFMA k order,
+//       B = V^T read from a per-wave LDS tile [d][32 tok] (row pitch 36 bf16) that the
+//       wave fills from the contiguous 8 KiB of V (the tile never straddles a 64-token page;
+//       tokens past the context are zeroed so stale cache bytes never meet a p = 0)
+//       -> two ds_read_b64 per fragment, in the same permuted k order.
+// The 4 waves' (m, l, O) are merged through LDS; with num_parts > 1 the merged partials go
+// to the split-K workspace reduced by paged_attn_reduce_kernel (attention.hip).
+#include "common.h"
+
+namespace mp {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_mf;
+
+__device__ __forceinline__ f32x4 mfma_bf16(const u16x8& a, const u16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_mf, a), __builtin_bit_cast(bf16x8_mf, b), c,
+                                                 0, 0, 0);
+}
+
+constexpr int VT_PITCH = 36;  // bf16 per LDS row of the transposed V tile (32 tokens + pad; 8-B aligned rows)
+
+template <int D, int HB>
+__global__ __launch_bounds__(256) void attn_mfma_kernel(
+    const bf16_t* __restrict__ q, int64_t q_stride, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
+    const int32_t* __restrict__ block_tables, int bt_stride, const int32_t* __restrict__ q_seq,
+    const int32_t* __restrict__ q_ctx, const int32_t* __restrict__ qb_tok0, const int32_t* __restrict__ qb_ntok,
+    bf16_t* __restrict__ out, float* __restrict__ part_o, float* __restrict__ part_ml, int nkv, int nh,
+    int page_log2, int PS, int NP, float scale_log2, int packed_mt) {
+  constexpr int TB = 16 / HB;
+  constexpr int KD = D / 32;  // k-chunks of the QK^T product
+  constexpr int DT = D / 16;  // 16-column tiles of O
+  __shared__ __attribute__((aligned(16))) bf16_t s_vt[4][D * VT_PITCH];
+  __shared__ float s_m[4][16], s_l[4][16];
+  __shared__ __attribute__((aligned(16))) float s_o[4][16][D + 1];
+
+  const int b = blockIdx.x, p = blockIdx.z;
+  const int hbase = blockIdx.y * HB;
+  const int g = hbase / (nh / nkv);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int c = lane & 15, qd = lane >> 4;
+  const int tok0 = qb_tok0[b], ntok = qb_ntok[b];
+  const int seq = q_seq[tok0];
+  const int32_t* bt = block_tables + (int64_t)seq * bt_stride;
+  const int page_size = 1 << page_log2;
+  const int64_t page_stride = (int64_t)nkv * page_size * D;
+  const int64_t head_off = (int64_t)g * page_size * D;
+
+  // this lane's row (for Q^T fragments, masking and softmax state): row c
+  const int my_t = c / HB, my_h = hbase + c % HB;
+  const bool row_ok = my_t < ntok;
+  const int my_ctx = row_ok ? q_ctx[tok0 + my_t] : 0;
+  int blk_ctx = 0;  // context the block needs = the largest ctx of its tokens (causal: the last)
+  for (int i = 0; i < ntok; ++i) blk_ctx = max(blk_ctx, q_ctx[tok0 + i]);
+  const int start = p * PS, end = min(start + PS, blk_ctx);
+
+  u16x8 qf[KD];
+#pragma unroll
+  for (int kd = 0; kd < KD; ++kd) {
+    if (row_ok) qf[kd] = *reinterpret_cast<const u16x8*>(q + (int64_t)(tok0 + my_t) * q_stride + (int64_t)my_h * D +
+                                                         kd * 32 + qd * 8);
+    else qf[kd] = (u16x8)(0);
+  }
+
+  f32x4 o[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) o[dt] = (f32x4)(0.f);
+  float m = -INFINITY, l = 0.f;
+  bf16_t* vt = s_vt[w];
+
+  for (int b0 = start + w * 32; b0 < end; b0 += 128) {
+    // ---- S^T = K . Q^T for tokens b0 .. b0+31 (two 16-token subtiles) ----
+    const int64_t pg = bt[b0 >> page_log2];
+    const bf16_t* kpage = kc + pg * page_stride + head_off + (int64_t)(b0 & (page_size - 1)) * D;
+    const bf16_t* vpage = vc + pg * page_stride + head_off + (int64_t)(b0 & (page_size - 1)) * D;
+    f32x4 st[2];
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      st[sub] = (f32x4)(0.f);
+#pragma unroll
+      for (int kd = 0; kd < KD; ++kd) {
+        const u16x8 kf = *reinterpret_cast<const u16x8*>(kpage + (int64_t)(sub * 16 + c) * D + kd * 32 + qd * 8);
+        st[sub] = mfma_bf16(kf, qf[kd], st[sub]);
+      }
+    }
+    // ---- V tile -> LDS transposed [d][tok] (this wave only; in-order LDS needs no barrier) ----
+#pragma unroll
+    for (int i = 0; i < (32 * D * 2) / 1024; ++i) {
+      const int byte = i * 1024 + lane * 16;
+      const int tk = byte / (D * 2), d0 = (byte % (D * 2)) / 2;
+      u16x8 vv = *reinterpret_cast<const u16x8*>(vpage + (int64_t)tk * D + d0);
+      if (b0 + tk >= end) vv = (u16x8)(0);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) vt[(d0 + e) * VT_PITCH + tk] = vv[e];
+    }
+    // ---- online softmax for row c over this lane's 8 tokens {4qd + r, 16 + 4qd + r} ----
+    float s8[8];
+    float lm = -INFINITY;
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int tk = b0 + sub * 16 + qd * 4 + r;
+        const float v = (tk < my_ctx && tk < end) ? st[sub][r] * scale_log2 : -INFINITY;
+        s8[sub * 4 + r] = v;
+        lm = fmaxf(lm, v);
+      }
+    lm = fmaxf(lm, __shfl_xor(lm, 16, 64));
+    lm = fmaxf(lm, __shfl_xor(lm, 32, 64));
+    const float m_new = fmaxf(m, lm);
+    const float alpha = (m_new == -INFINITY) ? 1.f : exp2f(m - m_new);
+    u16x8 pa;
+    float ps = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float pv = (m_new == -INFINITY) ? 0.f : exp2f(s8[j] - m_new);
+      const bf16_t pb = f2bf(pv);
+      pa[j] = pb;
+      ps += bf2f(pb);  // l accumulates the rounded p that the MFMA uses
+    }
+    l = l * alpha + ps;
+    m = m_new;
+    // O rows are 4qd + r: fetch those rows' alpha from lanes 4qd + r (row == lane & 15)
+    float ar[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) ar[r] = __shfl(alpha, qd * 4 + r, 64);
+    // ---- O += P . V ----
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      const bf16_t* vrow = vt + (dt * 16 + c) * VT_PITCH;
+      const u16x4 lo = *reinterpret_cast<const u16x4*>(vrow + qd * 4);
+      const u16x4 hi = *reinterpret_cast<const u16x4*>(vrow + 16 + qd * 4);
+      const u16x8 vb = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[dt][r] *= ar[r];
+      o[dt] = mfma_bf16(pa, vb, o[dt]);
+    }
+  }
+  // row sums of l over the 4 lanes of each row
+  l += __shfl_xor(l, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+  if (lane < 16) {
+    s_m[w][lane] = m;
+    s_l[w][lane] = l;
+  }
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) s_o[w][qd * 4 + r][dt * 16 + c] = o[dt][r];
+  __syncthreads();
+  // ---- merge the 4 waves; thread -> (row, d) ----
+  for (int i = tid; i < 16 * D; i += 256) {
+    const int row = i / D, d = i - row * D;
+    const int t = row / HB, h = hbase + row % HB;
+    if (t >= ntok) continue;
+    float M = -INFINITY;
+#pragma unroll
+    for (int ww = 0; ww < 4; ++ww) M = fmaxf(M, s_m[ww][row]);
+    float num = 0.f, den = 0.f;
+    if (M != -INFINITY) {
+#pragma unroll
+      for (int ww = 0; ww < 4; ++ww) {
+        const float f = exp2f(s_m[ww][row] - M);
+        num += f * s_o[ww][row][d];
+        den += f * s_l[ww][row];
+      }
+    }
+    const int tok = tok0 + t;
+    if (NP == 1) {
+      const float v = den > 0.f ? num / den : 0.f;
+      const int64_t col = (int64_t)h * D + d;
+      out[packed_mt > 0 ? apk_off(tok, (int)col, packed_mt) : (int64_t)tok * nh * D + col] = f2bf(v);
+    } else {
+      const int64_t hp = ((int64_t)tok * nh + h) * NP + p;
+      part_o[hp * D + d] = num;
+      if (d == 0) {
+        part_ml[hp * 2] = M;
+        part_ml[hp * 2 + 1] = den;
+      }
+    }
+  }
+}
+
+template <int D, int HB>
+static void launch_attn_mfma(const void* q, int64_t q_stride, const void* kc, const void* vc, const int32_t* bt,
+                             int bt_stride, const int32_t* q_seq, const int32_t* q_ctx, const int32_t* qb_tok0,
+                             const int32_t* qb_ntok, int NB, void* out, float* ws_o, float* ws_ml, int nkv, int nh,
+                             int page_log2, int PS, int NP, float scale_log2, int packed_mt, hipStream_t stream) {
+  hipLaunchKernelGGL((attn_mfma_kernel<D, HB>), dim3(NB, nh / HB, NP), dim3(256), 0, stream, (const bf16_t*)q,
+                     q_stride, (const bf16_t*)kc, (const bf16_t*)vc, bt, bt_stride, q_seq, q_ctx, qb_tok0, qb_ntok,
+                     (bf16_t*)out, ws_o, ws_ml, nkv, nh, page_log2, PS, NP, scale_log2, packed_mt);
+}
+
+__global__ void paged_attn_reduce_kernel(const float* __restrict__ part_o, const float* __restrict__ part_ml,
+                                         bf16_t* __restrict__ out, int NP, int D, int nh, int packed_mt);
+
+}  // namespace mp
+
+// Query blocks: qb_tok0[i] = first flat token of block i, qb_ntok[i] = its token count
+// (<= 16 / heads_per_block, all from one sequence).  heads_per_block = min(nh / nkv, 16).
+extern "C" int mp_attention_mfma(const void* q, int64_t q_stride, const void* kc, const void* vc, const int32_t* bt,
+                                 int bt_stride, const int32_t* q_seq, const int32_t* q_ctx, const int32_t* qb_tok0,
+                                 const int32_t* qb_ntok, int NB, void* out, float* workspace, int T, int nh, int nkv,
+                                 int D, int page_size, int PS, int NP, float scale, int packed_mt, hipStream_t stream) {
+  using namespace mp;
+  if (NB == 0 || T == 0) return 0;
+  if (nh % nkv != 0 || PS % 128 != 0 || NP < 1 || page_size % 32 != 0) return -1;
+  int page_log2 = 0;
+  while ((1 << page_log2) < page_size) ++page_log2;
+  if ((1 << page_log2) != page_size) return -2;
+  const int nrep = nh / nkv;
+  const int hb = nrep >= 16 ? 16 : nrep;
+  if (nrep % hb) return -3;
+  const float scale_log2 = scale * 1.4426950408889634f;
+  float* ws_o = workspace;
+  float* ws_ml = workspace + (int64_t)T * nh * NP * D;
+#define MP_AM_CASE(DD, HH)                                                                                      \
+  if (D == DD && hb == HH) {                                                                                    \
+    launch_attn_mfma<DD, HH>(q, q_stride, kc, vc, bt, bt_stride, q_seq, q_ctx, qb_tok0, qb_ntok, NB, out, ws_o,  \
+                             ws_ml, nkv, nh, page_log2, PS, NP, scale_log2, packed_mt, stream);                 \
+    goto launched;                                                                                              \
+  }
+  MP_AM_CASE(128, 1)
+  MP_AM_CASE(128, 2)
+  MP_AM_CASE(128, 4)
+  MP_AM_CASE(128, 8)
+  MP_AM_CASE(128, 16)
+  MP_AM_CASE(64, 1)
+  MP_AM_CASE(64, 2)
+  MP_AM_CASE(64, 4)
+  MP_AM_CASE(64, 8)
+  MP_AM_CASE(64, 16)
+#undef MP_AM_CASE
+  return -4;
+launched:
+  if (NP > 1)
+    hipLaunchKernelGGL(paged_attn_reduce_kernel, dim3(T * nh), dim3(D), 0, stream, ws_o, ws_ml, (bf16_t*)out, NP, D,
+                       nh, packed_mt);
+  return (int)hipGetLastError();
+}

@@ -30,6 +30,10 @@ int mp_sample(const void* logits, int64_t stride, int R, int V, const float* tem
               const int32_t* top_ks, const float* rep_pens, int32_t* recent, int recent_stride, int32_t* recent_len,
               const int64_t* seeds, float* ws, int64_t* out, int update, hipStream_t stream);
 int64_t mp_gemm_workspace_bytes();
+int mp_attention_mfma(const void* q, int64_t q_stride, const void* kc, const void* vc, const int32_t* bt, int bt_stride,
+                      const int32_t* q_seq, const int32_t* q_ctx, const int32_t* qb_tok0, const int32_t* qb_ntok, int NB,
+                      void* out, float* workspace, int T, int nh, int nkv, int D, int page_size, int PS, int NP,
+                      float scale, int packed_mt, hipStream_t stream);
 int mp_quant_act_fp8(const void* ap, void* a8, float* scale, int M, int K, hipStream_t stream);
 int mp_gemm_fp8(const void* a8, const float* as, const void* wq, const float* ws, void* y, int64_t ys, const void* res,
                 int64_t rs, int M, int N, int K, int epilogue, int out_packed, hipStream_t stream);
@@ -170,6 +174,41 @@ void paged_attention(const at::Tensor& q, const at::Tensor& k_cache, const at::T
                                   D, k_cache.size(2), part_size, num_parts, (float)scale,
                                   packed ? (int)((T + 15) / 16) : 0, cur_stream()),
                "paged_attention");
+}
+
+void attention_mfma(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
+                     const at::Tensor& block_tables, const at::Tensor& q_seq, const at::Tensor& q_ctx,
+                     const at::Tensor& qblocks, at::Tensor& out, at::Tensor& workspace, int64_t nh, int64_t nkv, double scale, int64_t part_size,
+                     int64_t num_parts, int64_t packed) {
+  check_bf16_cuda(q, "q");
+  check_rows(q, "q");
+  check_bf16_cuda(out, "out");
+  MP_CHECK(out.is_contiguous(), "out contiguous");
+  const int D = k_cache.size(3);
+  const int T = q.size(0);
+  MP_CHECK(q.size(1) >= nh * D, "q width");
+  if (packed) {
+    MP_CHECK(out.numel() >= packed_numel(T, nh * D) && (nh * D) % 32 == 0, "packed out numel");
+  } else {
+    MP_CHECK(out.numel() == (int64_t)T * nh * D, "out numel");
+  }
+  MP_CHECK(k_cache.size(1) == nkv && k_cache.is_contiguous() && v_cache.is_contiguous(), "cache");
+  MP_CHECK(block_tables.scalar_type() == at::kInt && block_tables.dim() == 2 && block_tables.stride(1) == 1,
+           "block_tables int32 [S, max_pages]");
+  MP_CHECK(q_seq.scalar_type() == at::kInt && q_seq.numel() == T, "q_seq");
+  MP_CHECK(q_ctx.scalar_type() == at::kInt && q_ctx.numel() == T, "q_ctx");
+  MP_CHECK(workspace.scalar_type() == at::kFloat, "workspace fp32");
+  if (num_parts > 1) MP_CHECK(workspace.numel() >= (int64_t)T * nh * num_parts * (D + 2), "workspace too small");
+  MP_CHECK(qblocks.scalar_type() == at::kInt && qblocks.dim() == 2 && qblocks.size(0) == 2 && qblocks.is_contiguous(),
+           "qblocks int32 [2, NB] (first token, token count)");
+  const int NB = qblocks.size(1);
+  check_launch(mp_attention_mfma(q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
+                                 block_tables.data_ptr<int32_t>(), block_tables.stride(0), q_seq.data_ptr<int32_t>(),
+                                 q_ctx.data_ptr<int32_t>(), qblocks.data_ptr<int32_t>(),
+                                 qblocks.data_ptr<int32_t>() + NB, NB, out.data_ptr(), workspace.data_ptr<float>(), T,
+                                 nh, nkv, D, k_cache.size(2), part_size, num_parts, (float)scale,
+                                 packed ? (int)((T + 15) / 16) : 0, cur_stream()),
+               "attention_mfma");
 }
 
 void embedding(const at::Tensor& ids, const at::Tensor& table, at::Tensor& out) {
@@ -363,6 +402,10 @@ TORCH_LIBRARY(mpamd, m) {
       "paged_attention(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor q_seq, Tensor q_ctx, "
       "Tensor(a!) out, Tensor(b!) workspace, int nh, int nkv, float scale, int part_size, int num_parts, "
       "int packed) -> ()");
+  m.def(
+      "attention_mfma(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor q_seq, Tensor q_ctx, "
+      "Tensor qblocks, Tensor(a!) out, Tensor(b!) workspace, int nh, int nkv, float scale, int part_size, "
+      "int num_parts, int packed) -> ()");
   m.def("embedding(Tensor ids, Tensor table, Tensor(a!) out) -> ()");
   m.def("swiglu(Tensor gu, Tensor(a!) out) -> ()");
   m.def("add(Tensor a, Tensor b, Tensor(a!) y) -> ()");
@@ -386,6 +429,7 @@ TORCH_LIBRARY_IMPL(mpamd, CUDA, m) {
   m.impl("rope_kv_write", &rope_kv_write);
   m.impl("kv_write", &kv_write);
   m.impl("paged_attention", &paged_attention);
+  m.impl("attention_mfma", &attention_mfma);
   m.impl("embedding", &embedding);
   m.impl("swiglu", &swiglu);
   m.impl("add", &add);

@@ -75,8 +75,34 @@ def attn_rows(cases):
         t = timeit(lambda: ops.paged_attention(q, kc, vc, bt, q_seq, q_ctx, nh, nkv, 0.088, out=out, workspace=ws,
                                                part_size=part[0], num_parts=part[1]))
         byts = B * ctx * nkv * D * 2 * 2
+        qb = torch.from_numpy(ops.query_blocks([1] * B, nh // nkv)).cuda()
+        wsm = ops.attention_workspace(B, nh, D, 16, "cuda")
+        tm = timeit(lambda: ops.attention_mfma(q, kc, vc, bt, q_seq, q_ctx, qb, nh, nkv, 0.088, out=out, workspace=wsm,
+                                               max_ctx=ctx))
         print(json.dumps(dict(kernel="paged_attention", B=B, ctx=ctx, nh=nh, nkv=nkv, part=part, us=round(t, 2),
-                              TBps=round(byts / t / 1e6, 2))), flush=True)
+                              TBps=round(byts / t / 1e6, 2), mfma_us=round(tm, 2),
+                              mfma_TBps=round(byts / tm / 1e6, 2))), flush=True)
+    # prefill: B sequences x L prompt tokens, causal, all queries at once
+    for (B, L, nh, nkv) in [(64, 128, 32, 32), (4, 2048, 32, 32), (8, 1024, 64, 8)]:
+        D, ps = 128, 64
+        pages_per = math.ceil(L / ps)
+        P = B * pages_per
+        kc = torch.randn(P, nkv, ps, D, device="cuda").to(torch.bfloat16)
+        vc = torch.randn_like(kc)
+        bt = torch.randperm(P, device="cuda").view(B, pages_per).to(torch.int32)
+        T = B * L
+        q = torch.randn(T, (nh + 2 * nkv) * D, device="cuda").to(torch.bfloat16)
+        q_seq = torch.arange(B, dtype=torch.int32, device="cuda").repeat_interleave(L)
+        q_ctx = torch.arange(1, L + 1, dtype=torch.int32, device="cuda").repeat(B)
+        out = torch.empty(T, nh * D, device="cuda", dtype=torch.bfloat16)
+        qb = torch.from_numpy(ops.query_blocks([L] * B, nh // nkv)).cuda()
+        t = timeit(lambda: ops.paged_attention(q, kc, vc, bt, q_seq, q_ctx, nh, nkv, 0.088, out=out, max_ctx=L),
+                   iters=5)
+        tm = timeit(lambda: ops.attention_mfma(q, kc, vc, bt, q_seq, q_ctx, qb, nh, nkv, 0.088, out=out, max_ctx=L),
+                    iters=5)
+        flops = 4 * B * nh * D * L * L / 2
+        print(json.dumps(dict(kernel="prefill_attention", B=B, L=L, nh=nh, nkv=nkv, valu_us=round(t, 1),
+                              mfma_us=round(tm, 1), mfma_TFLOPs=round(flops / tm / 1e6, 1))), flush=True)
 
 
 def misc_rows(B=64):

@@ -435,3 +435,28 @@ def test_sampler_history_update_and_degenerate_row():
     out2 = ops.sample(logits, torch.zeros(R, device=DEV), recent=recent, recent_len=recent_len,
                       update_history=True, **kw)
     assert out2.cpu().tolist()[1] == 123 and recent_len.cpu().tolist() == [2, 50, 5]
+
+
+@pytest.mark.parametrize("nh,nkv,D", [(32, 32, 128), (32, 8, 128), (64, 8, 128), (16, 4, 128), (12, 12, 64)])
+@pytest.mark.parametrize("ctxs,multi", [([70, 9, 1, 33], True), ([1, 5, 300, 1000], False), ([4097], False)])
+def test_attention_mfma_matches_reference(nh, nkv, D, ctxs, multi):
+    """MFMA flash attention: causal prefill blocks (multi=True) and GQA/MHA decode."""
+    q, kc, vc, bt, q_seq, q_ctx = _attn_case(nh, nkv, D, ctxs, multi_q=multi)
+    ntoks = ctxs if multi else [1] * len(ctxs)
+    qb = torch.from_numpy(ops.query_blocks(ntoks, nh // nkv)).to(DEV)
+    scale = 1 / math.sqrt(D)
+    out = ops.attention_mfma(q, kc, vc, bt, q_seq, q_ctx, qb, nh, nkv, scale)
+    o_ref = ref.paged_attention(q.float(), kc.float(), vc.float(), bt, q_seq, q_ctx, nh, nkv, scale)
+    torch.testing.assert_close(out.float(), o_ref.float(), atol=2e-2, rtol=2e-2)
+    # split-K partitions and the packed output layout
+    outp = ops.attention_mfma(q, kc, vc, bt, q_seq, q_ctx, qb, nh, nkv, scale, part_size=128,
+                              num_parts=math.ceil(max(ctxs) / 128), packed=True)
+    torch.testing.assert_close(ops.unpack_act(outp, q.shape[0], nh * D).float(), o_ref.float(), atol=2e-2,
+                               rtol=2e-2)
+
+
+def test_query_blocks():
+    qb = ops.query_blocks([5, 1, 17], 1)
+    assert qb.tolist() == [[0, 5, 6, 22], [5, 1, 16, 1]]
+    qb = ops.query_blocks([5, 1], 8)  # 2 tokens x 8 heads per block
+    assert qb.tolist() == [[0, 2, 4, 5], [2, 2, 1, 1]]

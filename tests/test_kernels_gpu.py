@@ -348,7 +348,7 @@ def test_fp8_quant_act_kernel_matches_reference(M):
     got = ref.dequant_act_fp8(a8.cpu(), sr, M, K)  # same scales: compare the fp8 codes
     want = ref.dequant_act_fp8(a8r, sr, M, K)
     # identical up to round-half ties of 1/scale vs *1/448 (1 fp8 ulp on a handful of elements)
-    assert (got != want).float().mean() < 1e-3
+    assert (got != want).float().mean() < 5e-3
     torch.testing.assert_close(got, want, atol=0, rtol=0.07)
     assert a8.numel() >= MT * 16 * K
 

@@ -48,6 +48,7 @@ class Plan:
     is_decode: bool
     meta_i64: torch.Tensor  # [2, T] positions, slots (device)
     meta_i32: torch.Tensor  # [2*T + S] q_seq, q_ctx, last_rows (device)
+    qblocks: Optional[torch.Tensor] = None  # [2, NB] MFMA-attention query blocks (prefill steps)
 
     @property
     def positions(self):
@@ -131,6 +132,9 @@ class StageExecutor:
         self._graph_pool = None
         self._pinned = _Pinned(2 * max_tokens_per_step, 2 * max_tokens_per_step + max_sessions, self.device)
         self.last_step_ms: Optional[float] = None
+        # MFMA flash attention for prefill steps (csrc/attention_mfma.hip); MPAMD_ATTN_MFMA=off disables
+        self._attn_mfma_prefill = os.environ.get("MPAMD_ATTN_MFMA", "prefill") != "off" and \
+            cfg.model_type != "gpt2" and cfg.head_dim in (64, 128)
         self.timing = False
         if self.device.type == "cuda":
             ops.require_native()
@@ -190,7 +194,11 @@ class StageExecutor:
             meta32 = h32[: 2 * T + S].clone()
         self._pinned.mark()
         max_ctx = int((st + ntoks).max()) if S else 0
-        return Plan(sess, ntoks, st, T, max_ctx, bool(S and (ntoks == 1).all()), meta64, meta32)
+        is_decode = bool(S and (ntoks == 1).all())
+        qb = None
+        if self.device.type == "cuda" and not is_decode and self._attn_mfma_prefill:
+            qb = torch.from_numpy(ops.query_blocks(ntoks, self.nh // self.nkv)).to(self.device, non_blocking=True)
+        return Plan(sess, ntoks, st, T, max_ctx, is_decode, meta64, meta32, qb)
 
     def commit(self, plan: Plan) -> None:
         for s, n in zip(plan.sessions, plan.ntoks):
@@ -274,7 +282,7 @@ class StageExecutor:
             out = self._forward_gpt2(plan, x)
         else:
             out = self._forward_llama(x, plan.positions, plan.slots, plan.q_seq, plan.q_ctx, plan.last_rows,
-                                      plan.T, plan.max_ctx, None)
+                                      plan.T, plan.max_ctx, None, qblocks=plan.qblocks)
         if ev is not None:
             ev[1].record()
             ev[1].synchronize()
@@ -282,8 +290,18 @@ class StageExecutor:
         return out
 
     # ------------------------------------------------------------------ llama
+    def _attend(self, qkv, kc, vc, q_seq, q_ctx, out, ws, ps, np_, packed, qblocks, max_ctx):
+        """Paged attention: MFMA flash attention for prefill blocks (``qblocks``), else the
+        flash-decoding kernel."""
+        table = self.sessions.table_dev
+        if qblocks is not None:
+            return ops.attention_mfma(qkv, kc, vc, table, q_seq, q_ctx, qblocks, self.nh, self.nkv, self.scale,
+                                      out=out, workspace=ws, max_ctx=max_ctx, packed=packed)
+        return ops.paged_attention(qkv, kc, vc, table, q_seq, q_ctx, self.nh, self.nkv, self.scale, out=out,
+                                   workspace=ws, part_size=ps, num_parts=np_, packed=packed)
+
     def _forward_llama(self, x, positions, slots, q_seq, q_ctx, last_rows, T, max_ctx, attn_part,
-                       bufs: Optional[dict] = None):
+                       bufs: Optional[dict] = None, qblocks=None):
         cfg, w = self.cfg, self.w
         H, eps = cfg.hidden_size, cfg.rms_norm_eps
         dev, dt = self.device, self.dtype
@@ -322,8 +340,7 @@ class StageExecutor:
                 ops.linear_fp8(a8, asc, L.qkv_q, L.qkv_s, T, out=qkv)
                 kc, vc = self.cache.layer(li)
                 ops.rope_kv_write(qkv, positions, self.cos, self.sin, kc, vc, slots, self.nh, self.nkv)
-                ops.paged_attention(qkv, kc, vc, table, q_seq, q_ctx, self.nh, self.nkv, self.scale, out=attn,
-                                    workspace=ws, part_size=ps, num_parts=np_, packed=True)
+                self._attend(qkv, kc, vc, q_seq, q_ctx, attn, ws, ps, np_, True, qblocks, max_ctx)
                 ops.quant_act_fp8(attn, T, cfg.q_dim, out=a8, scale=asc)
                 ops.linear_fp8(a8, asc, L.o_q, L.o_s, T, out=o)
                 ops.rmsnorm(o, L.post_norm, eps, out=xn, residual=res, mode=1, packed=True)
@@ -345,8 +362,7 @@ class StageExecutor:
                 ops.linear(xn, L.qkv, out=qkv, wp=L.qkv_p, a_rows=T)
                 kc, vc = self.cache.layer(li)
                 ops.rope_kv_write(qkv, positions, self.cos, self.sin, kc, vc, slots, self.nh, self.nkv)
-                ops.paged_attention(qkv, kc, vc, table, q_seq, q_ctx, self.nh, self.nkv, self.scale, out=attn,
-                                    workspace=ws, part_size=ps, num_parts=np_, packed=True)
+                self._attend(qkv, kc, vc, q_seq, q_ctx, attn, ws, ps, np_, True, qblocks, max_ctx)
                 ops.linear(attn, L.o, out=o, wp=L.o_p, a_rows=T)
                 ops.rmsnorm(o, L.post_norm, eps, out=xn, residual=res, mode=1, packed=True)
                 ops.linear(xn, L.gate_up, out=act, epilogue=1, wp=L.gate_up_p, a_rows=T, out_packed=True)
@@ -363,8 +379,7 @@ class StageExecutor:
                 ops.linear(xn, L.dense("qkv"), out=qkv, wp=L.qkv_p)
                 kc, vc = self.cache.layer(li)
                 ops.rope_kv_write(qkv, positions, self.cos, self.sin, kc, vc, slots, self.nh, self.nkv)
-                ops.paged_attention(qkv, kc, vc, table, q_seq, q_ctx, self.nh, self.nkv, self.scale, out=attn,
-                                    workspace=ws, part_size=ps, num_parts=np_)
+                self._attend(qkv, kc, vc, q_seq, q_ctx, attn, ws, ps, np_, False, qblocks, max_ctx)
                 ops.linear(attn, L.dense("o"), out=o, wp=L.o_p)
                 ops.rmsnorm(o, L.post_norm, eps, out=xn, residual=res, mode=1)
                 ops.linear(xn, L.dense("gate_up"), out=act, epilogue=1, wp=L.gate_up_p)

@@ -11,10 +11,10 @@
 // Instead of a Python loop, torch.topk, a full sort and a cumsum, one 1024-thread block per
 // row works on an fp32 copy of the row in LDS:
 //   * top-k path (0 < k < V, the reference CLI default k = 50): penalty -> max -> softmax
-//     normaliser Z -> ONE 2048-bin histogram of the order-preserving logit key picks the bin
-//     holding the k-th largest -> the (few) candidates at or above it are collected, ranked by
-//     value (index breaks ties, like a stable sort), and top-p / renormalise / the draw run
-//     on the <= k sorted candidates only.  Five sweeps over the row, no sort of V.
+//     normaliser Z -> a lower bound of the k-th largest logit from a histogram of the 1024
+//     per-thread maxima -> the (few) candidates above it are collected, ranked by value
+//     (index breaks ties, like a stable sort), and top-p / renormalise / the draw run on the
+//     <= k sorted candidates only.  Four sweeps over the row, no sort of V, no V atomics.
 //   * otherwise (no top-k, or a degenerate row with > 1024 candidates): radix-select on the
 //     probabilities (4 x 8-bit passes) for top-k and on probability MASS for top-p, then an
 //     inverse-CDF draw with a block scan.  Ties at a threshold value are kept together there.
@@ -178,36 +178,48 @@ __global__ __launch_bounds__(SB) void sample_kernel(const bf16_t* __restrict__ l
   const float u01 = (float)((double)(rnd >> 11) * (1.0 / 9007199254740992.0));
 
   if (k > 0 && k < V) {
-    // ---- fast top-k: 2048-bin histogram of the order-preserving key, bin of the k-th largest ----
+    // ---- fast top-k.  The k-th largest of the 1024 per-thread maxima is <= the k-th largest
+    //      value (those k maxima are values), so every top-k id has key >= the lower edge tau of
+    //      the 2048-bin histogram bin holding that maximum.  Histogramming 1024 maxima instead
+    //      of V keys avoids the LDS-atomic pile-up on the few bins dense logits fall into. ----
     __shared__ unsigned h2k[2048];
     __shared__ unsigned c_key[CAND];
     __shared__ int c_idx[CAND];
     __shared__ float c_p[CAND];
     __shared__ int s_cnt;
     for (int i = tid; i < 2048; i += SB) h2k[i] = 0;
-    if (tid == 0) s_cnt = 0;
+    if (tid == 0) { s_cnt = 0; s_u[1] = 0u; }
+    unsigned tmax = 0u;
+    for (int i = tid; i < V; i += SB) tmax = max(tmax, okey(x[i]));
     __syncthreads();
-    for (int i = tid; i < V; i += SB) atomicAdd(&h2k[okey(x[i]) >> 21], 1u);
+    if (tid < V) atomicAdd(&h2k[tmax >> 21], 1u);
     __syncthreads();
     const float own0 = (float)h2k[2 * tid], own1 = (float)h2k[2 * tid + 1];
     float tot;
-    const float P = block_excl_scan(own0 + own1, red, &tot);  // elements in bins < 2 tid
-    const float ge1 = tot - P - own0, ge0 = tot - P;          // elements in bins >= 2t+1 / >= 2t
+    const float P = block_excl_scan(own0 + own1, red, &tot);  // maxima in bins < 2 tid
+    const float ge1 = tot - P - own0, ge0 = tot - P;          // maxima in bins >= 2t+1 / >= 2t
     const float kf = (float)k;
-    if (ge1 >= kf && ge1 - own1 < kf) { s_u[0] = 2 * tid + 1; s_u[1] = (unsigned)ge1; }
-    if (ge0 >= kf && ge0 - own0 < kf) { s_u[0] = 2 * tid; s_u[1] = (unsigned)ge0; }
+    if (ge1 >= kf && ge1 - own1 < kf) s_u[0] = 2 * tid + 1;
+    if (ge0 >= kf && ge0 - own0 < kf) s_u[0] = 2 * tid;
+    if (tid == 0 && tot < kf) s_u[1] = 1u;  // fewer maxima than k (tiny vocab): general path
     __syncthreads();
-    const unsigned bstar = s_u[0], ncand = s_u[1];
-    if (ncand <= CAND) {
+    const unsigned tau = s_u[0] << 21;
+    bool fast = s_u[1] == 0u;
+    if (fast) {
       for (int i = tid; i < V; i += SB) {
         const unsigned key = okey(x[i]);
-        if ((key >> 21) >= bstar) {
+        if (key >= tau) {
           const int pos = atomicAdd(&s_cnt, 1);
-          c_key[pos] = key;
-          c_idx[pos] = i;
+          if (pos < CAND) {
+            c_key[pos] = key;
+            c_idx[pos] = i;
+          }
         }
       }
       __syncthreads();
+      fast = s_cnt <= CAND;
+    }
+    if (fast) {
       const int c = s_cnt;
       // rank by (value desc, index asc); rank < k survives top-k
       int rank = CAND, my_idx = 0;

@@ -100,12 +100,37 @@ __global__ __launch_bounds__(SB) void sample_kernel(const bf16_t* __restrict__ l
   const float temp = temps[row];
 
   // ---- fp32 copy + max (max is needed by both the greedy and the sampling path) ----
+  // 16-B loads, 4 in flight per thread before any use (one latency, not V/1024 of them)
   float mx = -INFINITY;
   int mi = 0x7fffffff;
-  for (int i = tid; i < V; i += SB) {
-    const float f = bf2f(lrow[i]);
-    x[i] = f;
-    if (f > mx) { mx = f; mi = i; }
+  const bool vec = ((V & 7) == 0) && ((stride & 7) == 0);
+  if (vec) {
+    for (int base = tid * 8; base < V; base += SB * 8 * 4) {
+      u16x8 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i0 = base + u * SB * 8;
+        v[u] = i0 < V ? *reinterpret_cast<const u16x8*>(lrow + i0) : (u16x8)(0);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i0 = base + u * SB * 8;
+        if (i0 < V) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float f = bf2f(v[u][j]);
+            x[i0 + j] = f;
+            if (f > mx) { mx = f; mi = i0 + j; }
+          }
+        }
+      }
+    }
+  } else {
+    for (int i = tid; i < V; i += SB) {
+      const float f = bf2f(lrow[i]);
+      x[i] = f;
+      if (f > mx) { mx = f; mi = i; }
+    }
   }
   if (temp <= 0.f) {  // greedy: first maximum of the raw logits
 #pragma unroll
@@ -133,8 +158,11 @@ __global__ __launch_bounds__(SB) void sample_kernel(const bf16_t* __restrict__ l
 
   // ---- repetition penalty (reference src/rpc_handler.py:345-374) ----
   const float rp = rep_pens[row];
-  const int nrec = recent_len[row];
-  const int32_t* rec = recent + (int64_t)row * recent_stride;
+  const int nrec = min((int)recent_len[row], recent_stride);
+  __shared__ int s_rec[SB];
+  if (tid < nrec) s_rec[tid] = recent[(int64_t)row * recent_stride + tid];
+  __syncthreads();
+  const int* rec = s_rec;  // the history, staged in LDS (each thread scans all of it)
   if (rp != 1.f && nrec > 0) {
     if (tid < nrec) {
       const int tok = rec[tid];

@@ -349,7 +349,7 @@ def test_fp8_quant_act_kernel_matches_reference(M):
     want = ref.dequant_act_fp8(a8r, sr, M, K)
     # identical up to round-half ties of 1/scale vs *1/448 (1 fp8 ulp on a handful of elements)
     assert (got != want).float().mean() < 2e-2
-    torch.testing.assert_close(got, want, atol=0, rtol=0.07)
+    torch.testing.assert_close(got, want, atol=0, rtol=0.13)  # <= 1 e4m3 ulp
     assert a8.numel() >= MT * 16 * K
 
 

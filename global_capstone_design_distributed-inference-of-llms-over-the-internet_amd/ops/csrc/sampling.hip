@@ -89,7 +89,7 @@ __global__ __launch_bounds__(SB) void sample_kernel(const bf16_t* __restrict__ l
   __shared__ float red[SB / 64 + 1];
   __shared__ unsigned hist[256];
   __shared__ float mass[256];
-  __shared__ unsigned s_u[4];
+  __shared__ unsigned s_u[4];  // scratch: selected bin, fallback flag, remaining rank
   __shared__ int s_i[2];
   extern __shared__ __attribute__((aligned(16))) float s_row[];
   const int row = blockIdx.x, tid = threadIdx.x;
@@ -206,32 +206,45 @@ __global__ __launch_bounds__(SB) void sample_kernel(const bf16_t* __restrict__ l
   const float u01 = (float)((double)(rnd >> 11) * (1.0 / 9007199254740992.0));
 
   if (k > 0 && k < V) {
-    // ---- fast top-k.  The k-th largest of the 1024 per-thread maxima is <= the k-th largest
-    //      value (those k maxima are values), so every top-k id has key >= the lower edge tau of
-    //      the 2048-bin histogram bin holding that maximum.  Histogramming 1024 maxima instead
-    //      of V keys avoids the LDS-atomic pile-up on the few bins dense logits fall into. ----
+    // ---- fast top-k.  The k-th largest of the 1024 per-thread maxima, tau, is <= the k-th
+    //      largest value (those k maxima are values of the row), so every top-k id has
+    //      key >= tau, and few others do.  Selecting among 1024 maxima instead of V keys
+    //      avoids the LDS-atomic pile-up on the few bins dense logits fall into. ----
     __shared__ unsigned h2k[2048];
     __shared__ unsigned c_key[CAND];
     __shared__ int c_idx[CAND];
     __shared__ float c_p[CAND];
     __shared__ int s_cnt;
-    for (int i = tid; i < 2048; i += SB) h2k[i] = 0;
     if (tid == 0) { s_cnt = 0; s_u[1] = 0u; }
     unsigned tmax = 0u;
     for (int i = tid; i < V; i += SB) tmax = max(tmax, okey(x[i]));
-    __syncthreads();
-    if (tid < V) atomicAdd(&h2k[tmax >> 21], 1u);
-    __syncthreads();
-    const float own0 = (float)h2k[2 * tid], own1 = (float)h2k[2 * tid + 1];
-    float tot;
-    const float P = block_excl_scan(own0 + own1, red, &tot);  // maxima in bins < 2 tid
-    const float ge1 = tot - P - own0, ge0 = tot - P;          // maxima in bins >= 2t+1 / >= 2t
-    const float kf = (float)k;
-    if (ge1 >= kf && ge1 - own1 < kf) s_u[0] = 2 * tid + 1;
-    if (ge0 >= kf && ge0 - own0 < kf) s_u[0] = 2 * tid;
-    if (tid == 0 && tot < kf) s_u[1] = 1u;  // fewer maxima than k (tiny vocab): general path
-    __syncthreads();
-    const unsigned tau = s_u[0] << 21;
+    // exact k-th largest of the per-thread maxima: radix select over 1024 keys (11 + 11 + 10
+    // bits), cheap however flat the row is (random-init logits are nearly uniform)
+    unsigned prefix = 0u, msk = 0u;
+    int kk = k;
+    for (int round = 0; round < 3; ++round) {
+      const int shift = round == 0 ? 21 : (round == 1 ? 10 : 0);
+      const unsigned nb = round < 2 ? 2048u : 1024u;
+      for (int i = tid; i < 2048; i += SB) h2k[i] = 0;
+      __syncthreads();
+      if (tid < V && (tmax & msk) == prefix) atomicAdd(&h2k[(tmax >> shift) & (nb - 1)], 1u);
+      __syncthreads();
+      const float own0 = (float)h2k[2 * tid], own1 = (float)h2k[2 * tid + 1];
+      float tot;
+      const float P = block_excl_scan(own0 + own1, red, &tot);  // keys in bins < 2 tid
+      const float ge1 = tot - P - own0, ge0 = tot - P;          // keys in bins >= 2t+1 / >= 2t
+      const float kf = (float)kk;
+      if (ge1 >= kf && ge1 - own1 < kf) { s_u[0] = 2 * tid + 1; s_u[2] = (unsigned)(kk - (int)(ge1 - own1)); }
+      if (ge0 >= kf && ge0 - own0 < kf) { s_u[0] = 2 * tid; s_u[2] = (unsigned)(kk - (int)(ge0 - own0)); }
+      if (tid == 0 && tot < kf) s_u[1] = 1u;  // fewer maxima than k (tiny vocab): general path
+      __syncthreads();
+      if (s_u[1]) break;
+      prefix |= s_u[0] << shift;
+      msk |= (nb - 1) << shift;
+      kk = (int)s_u[2];
+      __syncthreads();
+    }
+    const unsigned tau = prefix;  // a value of the row <= the k-th largest value
     bool fast = s_u[1] == 0u;
     if (fast) {
       for (int i = tid; i < V; i += SB) {

@@ -454,7 +454,8 @@ def fp8_gemm_ok(M: int, N: int, K: int) -> bool:
 
 
 def quant_act_fp8(xp: torch.Tensor, M: int, K: int, out=None, scale=None):
-    """Packed bf16 decode activation -> (fp8 A8 uint8, per-row scale fp32 [ceil(M/16)*16])."""
+    """Packed bf16 decode activation -> (fp8 A8 uint8, per-row scale fp32; the first
+    ceil(M/16)*16 entries are the row scales, the rest (GPU) is kernel scratch)."""
     if not _native(xp):
         a8, s = ref.quant_act_fp8(xp, M, K)
         if out is not None:
@@ -466,8 +467,8 @@ def quant_act_fp8(xp: torch.Tensor, M: int, K: int, out=None, scale=None):
         return a8, s
     if out is None:
         out = torch.empty(packed_numel(M, K), dtype=torch.uint8, device=xp.device)
-    if scale is None:
-        scale = torch.empty(((M + 15) // 16) * 16, dtype=torch.float32, device=xp.device)
+    if scale is None:  # row scales, then the kernel's per-slice absmax scratch
+        scale = torch.empty(((M + 15) // 16) * 16 * 33, dtype=torch.float32, device=xp.device)
     torch.ops.mpamd.quant_act_fp8(xp, out, scale, int(M), int(K))
     return out, scale
 

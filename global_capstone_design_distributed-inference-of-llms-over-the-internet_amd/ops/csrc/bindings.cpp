@@ -34,7 +34,7 @@ int mp_attention_mfma(const void* q, int64_t q_stride, const void* kc, const voi
                       const int32_t* q_seq, const int32_t* q_ctx, const int32_t* qb_tok0, const int32_t* qb_ntok, int NB,
                       void* out, float* workspace, int T, int nh, int nkv, int D, int page_size, int PS, int NP,
                       float scale, int packed_mt, hipStream_t stream);
-int mp_quant_act_fp8(const void* ap, void* a8, float* scale, int M, int K, hipStream_t stream);
+int mp_quant_act_fp8(const void* ap, void* a8, float* scale, float* part, int M, int K, hipStream_t stream);
 int mp_gemm_fp8(const void* a8, const float* as, const void* wq, const float* ws, void* y, int64_t ys, const void* res,
                 int64_t rs, int M, int N, int K, int epilogue, int out_packed, hipStream_t stream);
 int mp_gemm_bf16(const void* x, int64_t x_stride, const void* w, void* y, int64_t y_stride, const void* res,
@@ -347,10 +347,12 @@ void quant_act_fp8(const at::Tensor& ap, at::Tensor& a8, at::Tensor& scale, int6
   MP_CHECK(ap.is_contiguous() && ap.numel() >= packed_numel(M, K), "packed activation too small");
   MP_CHECK(a8.is_cuda() && a8.scalar_type() == at::kByte && a8.is_contiguous() && a8.numel() >= packed_numel(M, K),
            "a8: uint8 [packed_numel(M, K)]");
-  MP_CHECK(scale.is_cuda() && scale.scalar_type() == at::kFloat && scale.numel() >= ((M + 15) / 16) * 16,
-           "scale: fp32 [ceil(M/16)*16]");
+  const int64_t rows = ((M + 15) / 16) * 16;
+  MP_CHECK(scale.is_cuda() && scale.scalar_type() == at::kFloat && scale.numel() >= rows * 33,
+           "scale: fp32 [ceil(M/16)*16 * 33] (row scales + per-slice absmax scratch)");
   MP_CHECK(K % 64 == 0, "K % 64");
-  check_launch(mp_quant_act_fp8(ap.data_ptr(), a8.data_ptr(), scale.data_ptr<float>(), (int)M, (int)K, cur_stream()),
+  check_launch(mp_quant_act_fp8(ap.data_ptr(), a8.data_ptr(), scale.data_ptr<float>(), scale.data_ptr<float>() + rows,
+                                (int)M, (int)K, cur_stream()),
                "quant_act_fp8");
 }
 

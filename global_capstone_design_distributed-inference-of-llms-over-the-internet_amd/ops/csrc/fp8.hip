@@ -11,7 +11,7 @@
 //       Wq[N/16][K/64][lane][16 B]:  lane = 16 q + c holds W[16 nt + c][64 kc + 32 s + 8 q + j]
 //       at byte 8 s + j  -> one 16-B load per lane feeds TWO 16x16x32 fp8 MFMAs (s = 0, 1);
 //   * activations: per-row scale a_m = max|x[m, :]| / 448, quantized from the packed bf16
-//     decode activation (quant_act_fp8_kernel) into the same [K/64][MT][lane][16 B] order;
+//     decode activation (quant_absmax + quant_apply) into the same [K/64][MT][lane][16 B] order;
 //   * half the weight bytes of the bf16 path: decode stays HBM-bound, so the fp8 GEMM streams
 //     a 70B stage in half the time.  Loop structure = the bf16 one-group-per-workgroup kernel
 //     (gemm.hip): 8 waves interleave k-groups, ping-pong weight registers, LDS combine,
@@ -36,14 +36,19 @@ __device__ __forceinline__ int pack4_fp8(float a, float b, float c, float d) {
 
 // Packed bf16 decode activation Ap[K/32][MT][64][8] (M rows) -> fp8 A8[K/64][MT][64][16 B]
 // plus per-row scales (MT*16 floats; rows >= M get a scale too and are never stored).
-// One workgroup per 16-row tile: pass 1 row absmax, pass 2 quantize (the tile is L2-hot).
-__global__ __launch_bounds__(512) void quant_act_fp8_kernel(const bf16_t* __restrict__ ap, uint8_t* __restrict__ a8,
-                                                            float* __restrict__ scale, int K, int MT) {
-  __shared__ float red[8][16];
-  const int mt = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int nks = K >> 5;
+// Two short launches over a (16-row tile, K slice) grid so the whole chip works on it:
+//   phase 1: per-slice row absmax -> part[MT*16][NS]   (no atomics, nothing to re-zero)
+//   phase 2: row scale = max over slices / 448, quantize this slice (slice 0 stores the scale).
+constexpr int Q_NS = 32;  // K slices per 16-row tile
+
+__global__ __launch_bounds__(256) void quant_absmax_kernel(const bf16_t* __restrict__ ap, float* __restrict__ part,
+                                                           int K, int MT) {
+  __shared__ float red[4][16];
+  const int mt = blockIdx.x, sl = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int nks = K >> 5, per = (nks + Q_NS - 1) / Q_NS;
+  const int k0 = sl * per, k1 = min(k0 + per, nks);
   float m = 0.f;
-  for (int ks = wid; ks < nks; ks += 8) {
+  for (int ks = k0 + wid; ks < k1; ks += 4) {
     const u16x8 v = *reinterpret_cast<const u16x8*>(ap + (((int64_t)ks * MT + mt) * 64 + lane) * 8);
 #pragma unroll
     for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf(bf2f(v[j])));
@@ -52,14 +57,24 @@ __global__ __launch_bounds__(512) void quant_act_fp8_kernel(const bf16_t* __rest
   m = fmaxf(m, __shfl_xor(m, 32, 64));
   if (lane < 16) red[wid][lane] = m;
   __syncthreads();
+  if (tid < 16) part[(mt * 16 + tid) * Q_NS + sl] = fmaxf(fmaxf(red[0][tid], red[1][tid]), fmaxf(red[2][tid], red[3][tid]));
+}
+
+__global__ __launch_bounds__(256) void quant_apply_kernel(const bf16_t* __restrict__ ap, const float* __restrict__ part,
+                                                          uint8_t* __restrict__ a8, float* __restrict__ scale, int K,
+                                                          int MT) {
+  const int mt = blockIdx.x, sl = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int r = lane & 15;
-  float mx = red[0][r];
-#pragma unroll
-  for (int w = 1; w < 8; ++w) mx = fmaxf(mx, red[w][r]);
+  const float* pr = part + (mt * 16 + r) * Q_NS;
+  float mx = 0.f;
+#pragma unroll 8
+  for (int i = 0; i < Q_NS; ++i) mx = fmaxf(mx, pr[i]);
   const float s = mx > 0.f ? mx * (1.f / 448.f) : 1.f;
   const float inv = 1.f / s;
-  if (wid == 0 && lane < 16) scale[mt * 16 + lane] = s;
-  for (int c = wid; c < (nks >> 1); c += 8) {
+  if (sl == 0 && wid == 0 && lane < 16) scale[mt * 16 + lane] = s;
+  const int nch = K >> 6, per = (nch + Q_NS - 1) / Q_NS;
+  const int c0 = sl * per, c1 = min(c0 + per, nch);
+  for (int c = c0 + wid; c < c1; c += 4) {
     const u16x8 v0 = *reinterpret_cast<const u16x8*>(ap + (((int64_t)(2 * c) * MT + mt) * 64 + lane) * 8);
     const u16x8 v1 = *reinterpret_cast<const u16x8*>(ap + (((int64_t)(2 * c + 1) * MT + mt) * 64 + lane) * 8);
     float f[16];
@@ -85,7 +100,7 @@ __global__ __launch_bounds__(512) void gemm_fp8_kernel(const uint8_t* __restrict
                                                        bf16_t* __restrict__ y, int64_t ys,
                                                        const bf16_t* __restrict__ res, int64_t rs, int M, int N,
                                                        int K) {
-  constexpr int GU = (MT * NT >= 6) ? 2 : 4;
+  constexpr int GU = (MT * NT >= 8) ? 2 : 4;  // 64-k chunks per group (2 at the widest tile: VGPR cap)
   __shared__ __attribute__((aligned(16))) float red[8][MT * NT * 4][64];
   const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int c = lane & 15, q = lane >> 4;
@@ -202,13 +217,16 @@ static int launch_gemm_fp8(const void* a8, const float* as, const void* wq, cons
 
 }  // namespace mp
 
-extern "C" int mp_quant_act_fp8(const void* ap, void* a8, float* scale, int M, int K, hipStream_t stream) {
+// part: >= ceil(M/16) * 16 * Q_NS floats of scratch
+extern "C" int mp_quant_act_fp8(const void* ap, void* a8, float* scale, float* part, int M, int K,
+                                hipStream_t stream) {
   using namespace mp;
   if (M <= 0) return 0;
   if (K % 64) return -1;
   const int MT = (M + 15) / 16;
-  hipLaunchKernelGGL(quant_act_fp8_kernel, dim3(MT), dim3(512), 0, stream, (const bf16_t*)ap, (uint8_t*)a8, scale, K,
-                     MT);
+  hipLaunchKernelGGL(quant_absmax_kernel, dim3(MT, Q_NS), dim3(256), 0, stream, (const bf16_t*)ap, part, K, MT);
+  hipLaunchKernelGGL(quant_apply_kernel, dim3(MT, Q_NS), dim3(256), 0, stream, (const bf16_t*)ap, part, (uint8_t*)a8,
+                     scale, K, MT);
   return (int)hipGetLastError();
 }
 

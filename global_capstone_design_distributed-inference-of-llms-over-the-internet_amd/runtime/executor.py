@@ -329,7 +329,7 @@ class StageExecutor:
             attn = e("attn_p", (pk(T, cfg.q_dim),))
             act = e("act_p", (pk(T, cfg.intermediate_size),))
             a8 = e("a8", (pk(T, max(H, cfg.q_dim, cfg.intermediate_size)),), torch.uint8)
-            asc = e("a8_scale", (((T + 15) // 16) * 16,), torch.float32)
+            asc = e("a8_scale", (((T + 15) // 16) * 16 * 33,), torch.float32)
             F = cfg.intermediate_size
             for li, L in enumerate(w.layers):
                 if li == 0:

@@ -135,6 +135,9 @@ class StageExecutor:
         # MFMA flash attention for prefill steps (csrc/attention_mfma.hip); MPAMD_ATTN_MFMA=off disables
         self._attn_mfma_prefill = os.environ.get("MPAMD_ATTN_MFMA", "prefill") != "off" and \
             cfg.model_type != "gpt2" and cfg.head_dim in (64, 128)
+        # GQA decode: the whole group of a kv head in the MFMA rows (2x the VALU kernel at nrep 8)
+        self._attn_mfma_gqa = self._attn_mfma_prefill and self.nh // self.nkv >= 4
+        self._decode_qb: Dict[int, torch.Tensor] = {}
         self.timing = False
         if self.device.type == "cuda":
             ops.require_native()
@@ -290,10 +293,28 @@ class StageExecutor:
         return out
 
     # ------------------------------------------------------------------ llama
+    def decode_qblocks(self, T: int) -> torch.Tensor:
+        """Query blocks of a decode step (one token per block); cached per batch size so
+        hipGraph captures reuse the same buffer."""
+        qb = self._decode_qb.get(T)
+        if qb is None:
+            import numpy as np
+
+            qb = torch.from_numpy(np.stack([np.arange(T), np.ones(T)]).astype(np.int32)).to(self.device)
+            self._decode_qb[T] = qb
+        return qb
+
     def _attend(self, qkv, kc, vc, q_seq, q_ctx, out, ws, ps, np_, packed, qblocks, max_ctx):
-        """Paged attention: MFMA flash attention for prefill blocks (``qblocks``), else the
-        flash-decoding kernel."""
+        """Paged attention: MFMA flash attention for prefill blocks (``qblocks``) and GQA decode,
+        else the flash-decoding kernel."""
         table = self.sessions.table_dev
+        if qblocks is None and self._attn_mfma_gqa and self.device.type == "cuda":
+            T = qkv.shape[0]
+            ps2 = 128 * math.ceil(ps / 128)
+            np2 = max(1, math.ceil(ps * np_ / ps2))
+            return ops.attention_mfma(qkv, kc, vc, table, q_seq, q_ctx, self.decode_qblocks(T), self.nh, self.nkv,
+                                      self.scale, out=out, workspace=ws, part_size=ps2, num_parts=np2,
+                                      packed=packed)
         if qblocks is not None:
             return ops.attention_mfma(qkv, kc, vc, table, q_seq, q_ctx, qblocks, self.nh, self.nkv, self.scale,
                                       out=out, workspace=ws, max_ctx=max_ctx, packed=packed)
@@ -489,6 +510,8 @@ class _DecodeGraph:
         self.meta64 = torch.zeros(2, B, dtype=torch.int64, device=dev)
         self.meta32 = torch.zeros(3 * B, dtype=torch.int32, device=dev)
         self.meta64[1].fill_(-1)
+        if ex._attn_mfma_gqa:
+            ex.decode_qblocks(B)  # allocated outside the capture
         self.meta32[B: 2 * B].fill_(0)
         self.meta32[2 * B:] = torch.arange(B, dtype=torch.int32, device=dev)
         self.bufs: dict = {}

@@ -42,3 +42,65 @@ def test_kill_stage_dry_run():
     r = subprocess.run([sys.executable, "scripts/kill_stage.py", "7", "--dry_run"], cwd=ROOT, capture_output=True,
                        text=True, timeout=60)
     assert "no stage 7 server found" in r.stdout
+
+
+@pytest.mark.timeout(300)
+def test_sigkill_replica_process_mid_decode(tmp_path):
+    """Fault injection at process level (reference scripts/test_fault_tolerance.py + kill_stage.py):
+    two OS processes serve stage 1; the one on the session's route is SIGKILLed mid-decode and the
+    generation continues on the other replica with identical (greedy) output."""
+    import re
+    import signal
+    import time
+
+    import torch
+
+    from tests.test_swarm import MODEL, _client, _generate, _reference
+
+    def start(i, peers=None):
+        log = tmp_path / f"s{i}.log"
+        cmd = [sys.executable, "-m", "src.main", "--model", MODEL, "--splits", "2", "--stage", "1", "--dht_port", "0",
+               "--rpc_port", "0", "--host", "127.0.0.1", "--device", "cpu", "--kv_cache_gb", "0.05",
+               "--max_sessions", "8"]
+        if peers:
+            cmd += ["--dht_initial_peers", peers]
+        p = subprocess.Popen(cmd, cwd=ROOT, stdout=open(log, "w"), stderr=subprocess.STDOUT)
+        t0 = time.time()
+        while time.time() - t0 < 120:
+            txt = log.read_text()
+            m = re.search(r"handlers registered .*peer (\S+),", txt)
+            d = re.search(r"DHT visible multiaddrs: \['([^']+)'", txt)
+            if m and d:
+                return p, m.group(1), d.group(1)
+            assert p.poll() is None, txt[-2000:]
+            time.sleep(0.2)
+        raise TimeoutError(txt[-2000:])
+
+    p1, id1, maddr = start(1)
+    p2, id2, _ = start(2, maddr)
+    procs = {id1: p1, id2: p2}
+    try:
+        cfg, ex, tx = _client(maddr, [2])
+        t0 = time.time()
+        while time.time() - t0 < 30:
+            if len(tx._candidates(tx.stage_keys[0])) == 2:
+                break
+            time.sleep(0.2)
+        killed = []
+
+        def kill_current(i):
+            if i == 3:
+                pid = tx.session_routes[next(iter(tx.session_routes))][0].peer_id
+                procs[pid].send_signal(signal.SIGKILL)
+                procs[pid].wait(10)
+                killed.append(pid)
+
+        gen = _generate(ex, tx, 10, kill_current)
+        assert killed and tx.failed_peers
+        assert gen == _reference(10)
+        tx.shutdown()
+    finally:
+        for p in (p1, p2):
+            if p.poll() is None:
+                p.terminate()
+                p.wait(10)

@@ -122,10 +122,16 @@ class StageConnectionHandler:
 
         Metadata: ``session_id``, ``step_id`` (a repeated step id returns the cached reply
         instead of running twice), optional ``start_from_position`` (rewind the session to
-        that position before this step), ``max_length``; otherwise as ``rpc_forward``.
+        that position before this step), optional ``fork_from`` (beam search: this session
+        first becomes a copy of that one, the per-session form of upstream ``hypo_ids``),
+        ``max_length``; otherwise as ``rpc_forward``.
         """
         md = dict(msg.metadata)
         sid, step_id = md.get("session_id"), md.get("step_id")
+        src = md.pop("fork_from", None)
+        if src is not None and sid is not None:  # beam search: continue from another hypothesis
+            await asyncio.get_running_loop().run_in_executor(self._worker, self.executor.sessions.fork, str(src),
+                                                             str(sid))
         if sid is not None and step_id is not None:
             cached = self._steps.get(sid, {}).get(str(step_id))
             if cached is not None:

@@ -69,6 +69,13 @@ class PagedKVCache:
     def layer(self, i: int):
         return self.k[i], self.v[i]
 
+    def copy_pages(self, src: List[int], dst: List[int]) -> None:
+        """Copy whole pages (every layer, K and V) src[i] -> dst[i] on the device."""
+        si = torch.tensor(src, dtype=torch.long, device=self.device)
+        di = torch.tensor(dst, dtype=torch.long, device=self.device)
+        self.k.index_copy_(1, di, self.k.index_select(1, si))
+        self.v.index_copy_(1, di, self.v.index_select(1, si))
+
     @property
     def bytes_per_page(self) -> int:
         return 2 * self.num_layers * self.nkv * self.page_size * self.head_dim * torch.tensor([], dtype=self.dtype).element_size()

@@ -88,6 +88,38 @@ class SessionManager:
             self._dirty = True
             self._free_rows.append(s.row)
 
+    def fork(self, src: str, dst: str, max_length: Optional[int] = None) -> SessionState:
+        """``dst`` becomes a copy of ``src`` (its KV pages are copied on the device): the
+        building block of beam search (upstream Petals reorders a session's hypotheses by
+        ``hypo_ids``; here every hypothesis is a session and ``reorder`` forks them)."""
+        with self.lock:
+            s = self.sessions[src]
+            d = self.open(dst, max_length or s.max_length)
+            self.reset(dst)
+            if s.pages:
+                new = self.cache.allocator.alloc(len(s.pages))
+                self.cache.copy_pages(s.pages, new)
+                self.table[d.row, : len(new)] = new
+                d.pages = list(new)
+                self._dirty = True
+            d.length = s.length
+            d.generated = list(s.generated)
+            d.last_used = time.monotonic()
+            return d
+
+    def reorder(self, sids: List[str], hypo_ids: List[int]) -> None:
+        """Beam-search reorder: hypothesis i continues from hypothesis ``hypo_ids[i]``
+        (upstream TransformerBackend ``hypo_ids``).  Sources are snapshotted first."""
+        if list(hypo_ids) == list(range(len(sids))):
+            return
+        with self.lock:
+            tmp = [f"__reorder_{i}_{sids[h]}" for i, h in enumerate(hypo_ids)]
+            for t, h in zip(tmp, hypo_ids):
+                self.fork(sids[h], t)
+            for sid, t in zip(sids, tmp):
+                self.fork(t, sid)
+                self.close(t)
+
     def evict_expired(self, now: Optional[float] = None) -> int:
         now = time.monotonic() if now is None else now
         with self.lock:

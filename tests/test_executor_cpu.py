@@ -133,3 +133,32 @@ def test_chunked_prefill_matches_single_step():
         nxt = torch.tensor([3, 5])
         torch.testing.assert_close(small.forward([("a", 1), ("b", 1)], nxt), big.forward([("a", 1), ("b", 1)], nxt),
                                    atol=1e-4, rtol=1e-4)
+
+
+def test_session_fork_and_beam_reorder():
+    import torch
+
+    from src.models.config import resolve_model
+    from src.models.weights import random_stage_weights
+    from src.runtime.executor import StageExecutor
+
+    cfg = resolve_model("tiny-llama")
+    w = random_stage_weights(cfg, 0, 4, has_embed=True, has_head=True, device="cpu", dtype=torch.float32)
+    ex = StageExecutor(cfg, w, "cpu", dtype=torch.float32, kv_cache_bytes=8 << 20, max_sessions=8, max_seq_len=128)
+    ids = torch.randint(0, cfg.vocab_size, (11,), generator=torch.Generator().manual_seed(2))
+    ex.forward([("a", 11)], ids, reset=[True])
+    ex.forward([("b", 5)], ids[:5], reset=[True])
+    ex.sessions.fork("a", "c")
+    assert ex.sessions.get("c").length == 11
+    la = ex.forward([("a", 1)], torch.tensor([7]))
+    lc = ex.forward([("c", 1)], torch.tensor([7]))
+    torch.testing.assert_close(la, lc)
+    # beam reorder: hypothesis "a" continues from old "b" and "b" from old "a"
+    ex.forward([("a", 1), ("b", 1)], torch.tensor([3, 4]))
+    ex.sessions.fork("a", "a_old")
+    ex.sessions.fork("b", "b_old")
+    ex.sessions.reorder(["a", "b"], [1, 0])
+    assert ex.sessions.get("a").length == 6 and ex.sessions.get("b").length == 13
+    torch.testing.assert_close(ex.forward([("b", 1)], torch.tensor([9])), ex.forward([("a_old", 1)], torch.tensor([9])))
+    torch.testing.assert_close(ex.forward([("a", 1)], torch.tensor([8])), ex.forward([("b_old", 1)], torch.tensor([8])))
+    assert not any(k.startswith("__reorder") for k in ex.sessions.sessions)

@@ -32,9 +32,10 @@ from typing import List, Optional
 
 import torch
 
+from .comm.wire import Message
 from .comm.registry import DHT, get_dht_time
 from .comm.rpc import RpcServer, get_loop
-from .dht_utils import (DEFAULT_TTL, get_remote_module_infos, get_stage_key, register_blocks_on_dht,
+from .dht_utils import (DEFAULT_TTL, get_module_entries, get_remote_module_infos, get_stage_key, register_blocks_on_dht,
                         register_server_on_dht, register_stage_on_dht)
 from .llama_partition import load_stage_model, resolve_dtype
 from .load_balancing import ServerState, choose_best_blocks, should_choose_other_blocks
@@ -225,6 +226,7 @@ class _Server:
         if args.host in ("0.0.0.0", "") and not args.public_ip:
             self.maddrs = [m.replace("/ip4/0.0.0.0/", "/ip4/127.0.0.1/") for m in self.maddrs]
         self.peer_id = self.server.peer_id
+        self.next_pings: dict = {}
         self._stop = threading.Event()
         self.store_once()
         logger.info(f"StageConnectionHandler handlers registered (stage {stage_idx}, blocks "
@@ -237,6 +239,8 @@ class _Server:
         exp = get_dht_time() + a.ttl
         extra = dict(start_block=ex.start, end_block=ex.end, final_stage=self.final,
                      cache_tokens_left=int(ex.sessions.cache_tokens_left()))
+        if self.next_pings:
+            extra["next_pings"] = dict(self.next_pings)
         if self.lb:
             extra.update(blocks=[ex.start, ex.end], throughput=self.throughput)
         if state == ServerState.ONLINE:
@@ -248,10 +252,48 @@ class _Server:
             register_blocks_on_dht(self.dht, self.peer_id, list(range(ex.start, ex.end)), a.model, self.maddrs,
                                    ex.start, ex.end, self.throughput, self.final, state, exp)
 
+    def measure_next_pings(self, max_peers: int = 5, timeout: float = 2.0) -> dict:
+        """RTT (s) to servers hosting the block right after this span (upstream Petals
+        ModuleAnnouncerThread ``next_pings``, petals/server/server.py:674-767): routing hints."""
+        if self.final:
+            return {}
+        from .comm.rpc import RpcClient
+
+        ents = get_module_entries(self.dht, self.ex.end, self.args.model)
+        if not ents:  # fixed-split swarm: the next stage's records
+            res = self.dht.get(get_stage_key(self.stage_idx + 1), latest=True)
+            if res is not None and isinstance(res.value, dict):
+                ents = {str(k): (v.value if hasattr(v, "value") else v) for k, v in res.value.items()}
+        pings = {}
+
+        async def probe(client, addr):
+            t0 = time.perf_counter()
+            await client.call(addr, "StageConnectionHandler.rpc_echo", Message({"ping": True}), timeout=timeout)
+            return time.perf_counter() - t0
+
+        client = RpcClient()
+        try:
+            for pid, e in list(ents.items())[:max_peers]:
+                addrs = (e or {}).get("p2p_maddrs") or []
+                if pid == self.peer_id or not addrs:
+                    continue
+                try:
+                    pings[pid] = round(self.loop.run(probe(client, addrs[0]), timeout=timeout + 1), 6)
+                except Exception:  # unreachable peers are simply absent
+                    pass
+        finally:
+            try:
+                self.loop.run(client.close(), timeout=2)
+            except Exception:
+                pass
+        self.next_pings = pings
+        return pings
+
     def _heartbeat(self):
         period = self.args.ttl / 3
         while not self._stop.wait(period):
             try:
+                self.measure_next_pings()
                 self.store_once()
                 self.ex.sessions.evict_expired()
             except Exception as e:  # pragma: no cover

@@ -104,3 +104,15 @@ def test_sigkill_replica_process_mid_decode(tmp_path):
             if p.poll() is None:
                 p.terminate()
                 p.wait(10)
+
+
+@pytest.mark.timeout(300)
+def test_lb_swarm_recipe(tmp_path):
+    """Reference scripts/elice_test_load_balancing.sh on one host: servers pick disjoint spans."""
+    r = subprocess.run([sys.executable, "scripts/lb_swarm.py", "--model", "tiny-llama", "--servers", "3",
+                        "--num_blocks", "1", "--splits", "1", "--base_port", "29970", "--log_dir", str(tmp_path)],
+                       cwd=ROOT, capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    spans = sorted(set(__import__("re").findall(r"Selected blocks \[(\d+), (\d+)\)", r.stdout)))
+    assert spans == [("1", "2"), ("2", "3"), ("3", "4")], r.stdout
+    assert "GENERATED:" in r.stdout

@@ -207,3 +207,23 @@ def test_task_prioritizer_orders_decode_first():
     p = TaskPrioritizer()
     assert p.prioritize(1, False) < p.prioritize(128, True)
     assert p.prioritize(1, True) == p.prioritize(5, False)
+
+
+@pytest.mark.timeout(120)
+def test_next_pings_announced():
+    """Servers measure RTTs to the next span's servers (upstream ModuleAnnouncer next_pings)."""
+    s1 = ServerThread(server_argv(MODEL, "1,2", 1)).wait()
+    s2 = ServerThread(server_argv(MODEL, "1,2", 2, peers=s1.addr)).wait()
+    try:
+        assert wait_for(lambda: s1.dht.get(get_stage_key(2)) is not None)
+        pings = s1.srv.measure_next_pings()
+        assert list(pings) == [s2.srv.peer_id] and 0 < pings[s2.srv.peer_id] < 2.0
+        s1.srv.store_once()
+        rec = s1.dht.get(get_stage_key(1)).value
+        e = next(iter(rec.values()))
+        e = e.value if hasattr(e, "value") else e
+        assert e["next_pings"] == pings and e["cache_tokens_left"] > 0
+        assert s2.srv.measure_next_pings() == {}  # final stage: nothing after it
+    finally:
+        s1.close()
+        s2.close()

@@ -31,6 +31,11 @@ namespace mp {
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
 typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
 
+// A-fragment load (16 B per lane); scripts/gemm_lab.hip overrides it to ablate the A stream.
+#ifndef MP_LOAD_A_FRAG
+#define MP_LOAD_A_FRAG(p) (*reinterpret_cast<const u16x8*>(p))
+#endif
+
 __device__ __forceinline__ f32x4 mfma16(const u16x8& a, const u16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b), c,
                                                   0, 0, 0);
@@ -86,8 +91,8 @@ __global__ __launch_bounds__(512) void gemm_packed_kernel(const bf16_t* __restri
       __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(wbase[t] + (int64_t)((grp) * GU + u) * 512));
 #define MP_LOAD_A(grp)                                                                                        \
   _Pragma("unroll") for (int mt = 0; mt < MT; ++mt) _Pragma("unroll") for (int u = 0; u < GU; ++u) a[mt][u] =  \
-      *reinterpret_cast<const u16x8*>(xrow[mt] + (APK ? (int64_t)((grp) * GU + u) * MT * 512                  \
-                                                      : (int64_t)((grp) * GU * 32 + 32 * u)));
+      MP_LOAD_A_FRAG(xrow[mt] + (APK ? (int64_t)((grp) * GU + u) * MT * 512                                    \
+                                     : (int64_t)((grp) * GU * 32 + 32 * u)));
 #define MP_MMA(bb)                                                                                            \
   _Pragma("unroll") for (int mt = 0; mt < MT; ++mt) _Pragma("unroll") for (int u = 0; u < GU; ++u)            \
       _Pragma("unroll") for (int t = 0; t < NT; ++t) acc[mt][t] = mfma16(a[mt][u], bb[t][u], acc[mt][t]);
@@ -282,8 +287,7 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(const bf16_t* __restrict__
     _Pragma("unroll") for (int t = 0; t < NT; ++t) rb[s][t] = __builtin_nontemporal_load(                   \
         reinterpret_cast<const u16x8*>(wp + (((int64_t)(g_ * NT + t) * nks + k_) << 9) + lane * 8));        \
     const bf16_t* xa_ = act_ ? x + (((int64_t)k_ * MT) << 9) : zero_a;                                      \
-    _Pragma("unroll") for (int mt = 0; mt < MT; ++mt) ra[s][mt] =                                           \
-        *reinterpret_cast<const u16x8*>(xa_ + (mt << 9) + lane * 8);                                        \
+    _Pragma("unroll") for (int mt = 0; mt < MT; ++mt) ra[s][mt] = MP_LOAD_A_FRAG(xa_ + (mt << 9) + lane * 8); \
   }
 
   // sum of the 8 waves' parked partials for quad qd (this lane)

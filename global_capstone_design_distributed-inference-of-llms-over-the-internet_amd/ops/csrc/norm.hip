@@ -28,17 +28,26 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(
   const int nch = H >> 3;
   const bf16_t* xr = x + (int64_t)irow * x_stride;
   bf16_t* rr = res + (int64_t)irow * res_stride;
-  u16x8 v[MAXC];
+  // every global load (x, residual, weight) is issued before the first store and before the
+  // block reduction, unconditionally (clamped chunk index: no exec-masked branches between the
+  // loads): one memory round trip per call instead of three
+  u16x8 v[MAXC], rv[MAXC], wv[MAXC];
+#pragma unroll
+  for (int k = 0; k < MAXC; ++k) {
+    const int c = min((int)threadIdx.x + k * 256, nch - 1);
+    v[k] = *reinterpret_cast<const u16x8*>(xr + c * 8);
+    rv[k] = *reinterpret_cast<const u16x8*>((mode == 1 ? rr : xr) + c * 8);
+    wv[k] = *reinterpret_cast<const u16x8*>(w + c * 8);
+  }
   float ss = 0.f;
 #pragma unroll
   for (int k = 0; k < MAXC; ++k) {
     const int c = threadIdx.x + k * 256;
     if (c < nch) {
-      u16x8 a = *reinterpret_cast<const u16x8*>(xr + c * 8);
+      u16x8 a = v[k];
       if (mode == 1) {
-        u16x8 b = *reinterpret_cast<const u16x8*>(rr + c * 8);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) a[j] = f2bf(bf2f(a[j]) + bf2f(b[j]));
+        for (int j = 0; j < 8; ++j) a[j] = f2bf(bf2f(a[j]) + bf2f(rv[k][j]));
         *reinterpret_cast<u16x8*>(rr + c * 8) = a;
       } else if (mode == 2) {
         *reinterpret_cast<u16x8*>(rr + c * 8) = a;
@@ -58,10 +67,10 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(
   for (int k = 0; k < MAXC; ++k) {
     const int c = threadIdx.x + k * 256;
     if (c < nch) {
-      const u16x8 wv = *reinterpret_cast<const u16x8*>(w + c * 8);
+      const u16x8 wv_ = wv[k];
       u16x8 o;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = f2bf(round_bf(bf2f(v[k][j]) * r) * bf2f(wv[j]));
+      for (int j = 0; j < 8; ++j) o[j] = f2bf(round_bf(bf2f(v[k][j]) * r) * bf2f(wv_[j]));
       if (packed_mt > 0)
         *reinterpret_cast<u16x8*>(y + apk_off(orow, c * 8, packed_mt)) = o;
       else

@@ -16,40 +16,69 @@
 
 namespace mp {
 
-__global__ __launch_bounds__(256) void rope_kv_kernel(bf16_t* __restrict__ qkv, int64_t qkv_stride,
-                                                      const int64_t* __restrict__ pos,
-                                                      const float* __restrict__ cos_t,
-                                                      const float* __restrict__ sin_t,
-                                                      bf16_t* __restrict__ kc, bf16_t* __restrict__ vc,
-                                                      const int64_t* __restrict__ slots, int nh, int nkv,
-                                                      int D, int page_size) {
+// Every load of a row is issued before the first store, unconditionally (indices clamped, so
+// no exec-masked branches split the load phase): the old item loop stored into the same qkv
+// row between loads, so each of its iterations paid a full memory round trip (5.5 us per call
+// at 64 rows).  ROPE_MAXI items of 4 rotation pairs and ROPE_MAXV 16-B v chunks per thread.
+constexpr int ROPE_THREADS = 512, ROPE_MAXI = 4, ROPE_MAXV = 2;
+
+__global__ __launch_bounds__(ROPE_THREADS) void rope_kv_kernel(bf16_t* __restrict__ qkv, int64_t qkv_stride,
+                                                               const int64_t* __restrict__ pos,
+                                                               const float* __restrict__ cos_t,
+                                                               const float* __restrict__ sin_t,
+                                                               bf16_t* __restrict__ kc, bf16_t* __restrict__ vc,
+                                                               const int64_t* __restrict__ slots, int nh, int nkv,
+                                                               int D, int page_size) {
   const int t = blockIdx.x;
   const int64_t slot = slots[t];
   const int64_t p = pos[t];
   bf16_t* row = qkv + (int64_t)t * qkv_stride;
   const int half = D >> 1;
   const int qpr = half >> 2;  // 4-pair groups per head
+  const int nitems = (nh + nkv) * qpr;
+  const int vch = D >> 3, nv = nkv * vch;
+  const bf16_t* vsrc = row + (nh + nkv) * D;
   const float* ct = cos_t + p * half;
   const float* st = sin_t + p * half;
+
+  u16x4 a[ROPE_MAXI], b[ROPE_MAXI];
+  f32x4 cs[ROPE_MAXI], sn[ROPE_MAXI];
+  u16x8 v[ROPE_MAXV];
+#pragma unroll
+  for (int k = 0; k < ROPE_MAXI; ++k) {
+    const int it = min((int)threadIdx.x + k * ROPE_THREADS, nitems - 1);
+    const int h = it / qpr, i = (it - h * qpr) * 4;
+    a[k] = *reinterpret_cast<const u16x4*>(row + h * D + i);
+    b[k] = *reinterpret_cast<const u16x4*>(row + h * D + half + i);
+  }
+#pragma unroll
+  for (int k = 0; k < ROPE_MAXV; ++k) {
+    const int it = min((int)threadIdx.x + k * ROPE_THREADS, nv - 1);
+    const int h = it / vch, c = it - h * vch;
+    v[k] = *reinterpret_cast<const u16x8*>(vsrc + h * D + c * 8);
+  }
+#pragma unroll
+  for (int k = 0; k < ROPE_MAXI; ++k) {
+    const int it = min((int)threadIdx.x + k * ROPE_THREADS, nitems - 1);
+    const int i = (it % qpr) * 4;
+    cs[k] = *reinterpret_cast<const f32x4*>(ct + i);
+    sn[k] = *reinterpret_cast<const f32x4*>(st + i);
+  }
   const int64_t page = slot >= 0 ? slot / page_size : 0;
   const int64_t off = slot >= 0 ? slot - page * page_size : 0;
   const int64_t page_base = page * (int64_t)nkv * page_size * D;
-
-  // q and k: (nh + nkv) heads x qpr groups of 4 rotation pairs.
-  const int nitems = (nh + nkv) * qpr;
-  for (int it = threadIdx.x; it < nitems; it += blockDim.x) {
+  // rotate and store: q in place, k and v into the page slot
+#pragma unroll
+  for (int k = 0; k < ROPE_MAXI; ++k) {
+    const int it = threadIdx.x + k * ROPE_THREADS;
+    if (it >= nitems) continue;
     const int h = it / qpr, i = (it - h * qpr) * 4;
-    const bf16_t* src = row + h * D;
-    const u16x4 a = *reinterpret_cast<const u16x4*>(src + i);
-    const u16x4 b = *reinterpret_cast<const u16x4*>(src + half + i);
-    const f32x4 c = *reinterpret_cast<const f32x4*>(ct + i);
-    const f32x4 s = *reinterpret_cast<const f32x4*>(st + i);
     u16x4 oa, ob;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const float x1 = bf2f(a[j]), x2 = bf2f(b[j]);
-      oa[j] = f2bf(x1 * c[j] - x2 * s[j]);
-      ob[j] = f2bf(x2 * c[j] + x1 * s[j]);
+      const float x1 = bf2f(a[k][j]), x2 = bf2f(b[k][j]);
+      oa[j] = f2bf(x1 * cs[k][j] - x2 * sn[k][j]);
+      ob[j] = f2bf(x2 * cs[k][j] + x1 * sn[k][j]);
     }
     if (h < nh) {
       *reinterpret_cast<u16x4*>(row + h * D + i) = oa;
@@ -61,13 +90,13 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(bf16_t* __restrict__ qkv, 
     }
   }
   if (slot < 0) return;
-  // v: nkv heads x D/8 chunks of 16 B.
-  const int vch = D >> 3;
-  const bf16_t* vsrc = row + (nh + nkv) * D;
-  for (int it = threadIdx.x; it < nkv * vch; it += blockDim.x) {
-    const int h = it / vch, c = it - h * vch;
-    const u16x8 v = *reinterpret_cast<const u16x8*>(vsrc + h * D + c * 8);
-    *reinterpret_cast<u16x8*>(vc + page_base + ((int64_t)h * page_size + off) * D + c * 8) = v;
+#pragma unroll
+  for (int k = 0; k < ROPE_MAXV; ++k) {
+    const int it = threadIdx.x + k * ROPE_THREADS;
+    if (it < nv) {
+      const int h = it / vch, c = it - h * vch;
+      *reinterpret_cast<u16x8*>(vc + page_base + ((int64_t)h * page_size + off) * D + c * 8) = v[k];
+    }
   }
 }
 
@@ -98,8 +127,9 @@ extern "C" int mp_rope_kv_write(void* qkv, int64_t qkv_stride, const int64_t* po
                                 int nkv, int D, int page_size, hipStream_t stream) {
   using namespace mp;
   if (D % 8 != 0) return -1;
+  if ((nh + nkv) * D / 8 > ROPE_THREADS * ROPE_MAXI || nkv * D / 8 > ROPE_THREADS * ROPE_MAXV) return -2;
   if (T == 0) return 0;
-  hipLaunchKernelGGL(rope_kv_kernel, dim3(T), dim3(256), 0, stream, (bf16_t*)qkv, qkv_stride, pos, cos_t, sin_t,
+  hipLaunchKernelGGL(rope_kv_kernel, dim3(T), dim3(ROPE_THREADS), 0, stream, (bf16_t*)qkv, qkv_stride, pos, cos_t, sin_t,
                      (bf16_t*)kc, (bf16_t*)vc, slots, nh, nkv, D, page_size);
   return (int)hipGetLastError();
 }

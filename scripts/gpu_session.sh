@@ -22,7 +22,7 @@ step() {  # name, timeout, command...
 
 for s in $STEPS; do
   case $s in
-    tests) step pytest_gpu 900 python -m pytest tests -m gpu -x -q ;;
+    tests) step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
     bench) step bench1 600 python bench.py ;;
     benchgemm) step bench1_hipblaslt 600 python bench.py --gemm hipblaslt ;;
     prof) step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o bench -- python bench.py --steps 8 --warmup 2 ;;

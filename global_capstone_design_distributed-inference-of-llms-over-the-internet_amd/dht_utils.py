@@ -126,6 +126,26 @@ def get_remote_module_infos(dht: DHT, model_name: str = "default",
     return infos
 
 
+MODELS_KEY = "_petals.models"
+
+
+def register_model_on_dht(dht: DHT, model_name: str, num_blocks: int, repository: Optional[str] = None,
+                          public_name: Optional[str] = None, ttl: float = DEFAULT_TTL) -> bool:
+    """Announce which model the swarm serves (upstream ModuleAnnouncerThread stores
+    ``_petals.models`` -> {dht_prefix: model info}, petals/server/server.py:674-767), so a client
+    can list models without knowing block keys."""
+    rec = {"dht_prefix": model_name, "num_blocks": int(num_blocks), "repository": repository or model_name,
+           "public_name": public_name, "timestamp": get_dht_time()}
+    return dht.store(MODELS_KEY, rec, get_dht_time() + ttl, subkey=model_name)
+
+
+def get_models_on_dht(dht: DHT) -> Dict[str, dict]:
+    res = dht.get(MODELS_KEY, latest=True)
+    if res is None or not isinstance(res.value, dict):
+        return {}
+    return {str(k): _unwrap(v) for k, v in res.value.items() if isinstance(_unwrap(v), dict)}
+
+
 def update_server_throughput_on_dht(dht: DHT, peer_id, new_throughput: float, model_name: str = "default",
                                     expiration_time: Optional[float] = None) -> bool:
     res = dht.get(get_server_key(peer_id, model_name), latest=True)

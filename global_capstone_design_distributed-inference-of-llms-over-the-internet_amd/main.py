@@ -36,7 +36,7 @@ from .comm.wire import Message
 from .comm.registry import DHT, get_dht_time
 from .comm.rpc import RpcServer, get_loop
 from .dht_utils import (DEFAULT_TTL, get_module_entries, get_remote_module_infos, get_stage_key, register_blocks_on_dht,
-                        register_server_on_dht, register_stage_on_dht)
+                        register_model_on_dht, register_server_on_dht, register_stage_on_dht)
 from .llama_partition import load_stage_model, resolve_dtype
 from .load_balancing import ServerState, choose_best_blocks, should_choose_other_blocks
 from .models.config import resolve_model
@@ -96,6 +96,14 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--throughput_cache", type=str, default=None,
                    help="LB server: JSON cache of throughput measurements ('' disables; default: no cache)")
     p.add_argument("--log_level", type=str, default=None)
+    # upstream Petals Server options (petals/server/server.py:58-86,197-228,403-414)
+    p.add_argument("--block_indices", type=str, default=None,
+                   help="load balancing: serve exactly blocks start:end (never rebalanced)")
+    p.add_argument("--mean_block_selection_delay", type=float, default=0.0,
+                   help="load balancing: sleep U(0, 2*delay) s before choosing blocks (joining servers spread out)")
+    p.add_argument("--inference_max_length", type=int, default=None,
+                   help="server: longest session (tokens) a client may open; alias of --max_seq_len")
+    p.add_argument("--public_name", type=str, default=None, help="server: human-readable name in announcements")
     return p
 
 
@@ -121,7 +129,22 @@ def _executor_kwargs(args) -> dict:
         kw["kv_cache_bytes"] = int(args.kv_cache_gb * (1 << 30))
     if args.max_seq_len is not None:
         kw["max_seq_len"] = args.max_seq_len
+    if getattr(args, "inference_max_length", None) is not None:
+        kw["max_seq_len"] = min(kw.get("max_seq_len", args.inference_max_length), args.inference_max_length)
     return kw
+
+
+def parse_block_indices(s: Optional[str], total: int) -> Optional[List[int]]:
+    """``start:end`` -> list of block ids (upstream Server ``block_indices``, server.py:221-227)."""
+    if not s:
+        return None
+    try:
+        a, b = [int(x.strip()) for x in s.split(":")]
+    except ValueError:
+        raise SystemExit(f"--block_indices {s!r}: expected start:end, e.g. 8:16")
+    if not 0 <= a < b <= total:
+        raise SystemExit(f"--block_indices {s!r} outside [0, {total}]")
+    return list(range(a, b))
 
 
 def _start_dht(args) -> DHT:
@@ -243,8 +266,12 @@ class _Server:
             extra["next_pings"] = dict(self.next_pings)
         if self.lb:
             extra.update(blocks=[ex.start, ex.end], throughput=self.throughput)
+        if getattr(a, "public_name", None):
+            extra["public_name"] = a.public_name
         if state == ServerState.ONLINE:
             register_stage_on_dht(self.dht, self.stage_idx, self.peer_id, self.maddrs, ttl=a.ttl, **extra)
+        register_model_on_dht(self.dht, a.model, getattr(a, "total_blocks", None) or ex.cfg.num_hidden_layers,
+                              public_name=getattr(a, "public_name", None), ttl=a.ttl)
         if self.lb:
             register_server_on_dht(self.dht, self.peer_id, ex.start, ex.end, self.throughput or FALLBACK_THROUGHPUT,
                                    a.model, p2p_maddrs=self.maddrs, final_stage=self.final, state=state,
@@ -377,7 +404,11 @@ def run_stage_server_with_load_balancing(args, device, cuts: List[int], stop: Op
     dht = _start_dht(args)
     stop = stop or threading.Event()
     _install_signal_handlers(stop)
+    strict = parse_block_indices(getattr(args, "block_indices", None), total)
     while not stop.is_set():
+        sel_delay = getattr(args, "mean_block_selection_delay", 0.0)
+        if strict is None and sel_delay > 0 and stop.wait(random.uniform(0, 2 * sel_delay)):
+            break
         infos = []
         delay = 2.0
         for attempt in range(3):
@@ -388,7 +419,9 @@ def run_stage_server_with_load_balancing(args, device, cuts: List[int], stop: Op
                 logger.warning(f"module info query failed ({e}); retry in {delay:.1f}s")
                 time.sleep(delay)
                 delay *= 1.5
-        if infos:
+        if strict is not None:
+            blocks = strict
+        elif infos:
             blocks = choose_best_blocks(num_blocks, infos, total, min_block=min_block)
         else:
             blocks = list(range(min_block, min(min_block + num_blocks, total)))
@@ -403,7 +436,9 @@ def run_stage_server_with_load_balancing(args, device, cuts: List[int], stop: Op
         if on_ready is not None:
             on_ready(dht, srv)
         rebalance = False
-        while not stop.is_set():
+        if strict is not None:  # pinned span: heartbeat only, never rebalanced (upstream server.py:414)
+            stop.wait()
+        while strict is None and not stop.is_set():
             if stop.wait(random.uniform(0, 2 * args.mean_balance_check_period)):
                 break
             try:

@@ -210,6 +210,29 @@ def test_task_prioritizer_orders_decode_first():
 
 
 @pytest.mark.timeout(120)
+def test_strict_block_indices_and_models_record():
+    """--block_indices pins the span (upstream Server strict_block_indices); _petals.models is announced."""
+    from src.dht_utils import get_models_on_dht
+    from src.main import parse_block_indices
+
+    extra = "--use_load_balancing --block_indices 3:4 --public_name box-a --inference_max_length 64"
+    a = ServerThread(server_argv(MODEL, "2", 1, extra=extra)).wait()
+    try:
+        assert (a.srv.ex.start, a.srv.ex.end) == (3, 4) and a.srv.final
+        assert a.srv.ex.sessions.max_seq_len == 64
+        models = get_models_on_dht(a.dht)
+        assert models[MODEL]["num_blocks"] == 4 and models[MODEL]["public_name"] == "box-a"
+        e = next(iter(a.dht.get(get_stage_key(1)).value.values()))
+        e = e.value if hasattr(e, "value") else e
+        assert e["public_name"] == "box-a"
+    finally:
+        a.close()
+    assert parse_block_indices("0:2", 4) == [0, 1] and parse_block_indices(None, 4) is None
+    with pytest.raises(SystemExit):
+        parse_block_indices("3:9", 4)
+
+
+@pytest.mark.timeout(120)
 def test_next_pings_announced():
     """Servers measure RTTs to the next span's servers (upstream ModuleAnnouncer next_pings)."""
     s1 = ServerThread(server_argv(MODEL, "1,2", 1)).wait()

@@ -105,13 +105,67 @@ class StageConnectionHandler:
         server.add_handler(HANDLER_PREFIX + "rpc_inference", self.rpc_inference)
         server.add_handler(HANDLER_PREFIX + "rpc_push", self.rpc_push)
         server.add_handler(HANDLER_PREFIX + "rpc_check_reachability", self.rpc_check_reachability)
+        server.add_handler(HANDLER_PREFIX + "rpc_backward", self.rpc_backward)
+        server.add_handler(HANDLER_PREFIX + "rpc_backward_stream", self.rpc_backward_stream)
 
     # ------------------------------------------------------------------ handlers
     async def rpc_forward(self, msg: Message) -> Message:
+        if msg.metadata.get("stateless"):
+            return await self._stateless(msg, backward=False)
         return await self._handle(msg)
 
     async def rpc_forward_stream(self, msg: Message) -> Message:
-        return await self._handle(msg)
+        return await self.rpc_forward(msg)
+
+    async def rpc_backward(self, msg: Message) -> Message:
+        """Gradients w.r.t. the span's input hidden states and deep prompts (upstream
+        ``rpc_backward``, petals/server/handler.py:434-459; ``run_rpc_backward``,
+        block_functions.py:84-141). Tensors: ``[hidden [B,T,H], grad_output [B,T,H], prompts?]``,
+        where ``prompts`` is ``[n_blocks, B|1, P, H]`` when ``metadata["has_prompts"]``. The reply is
+        ``[grad_hidden]`` or ``[grad_hidden, grad_prompts]``. Stateless: no session and no KV cache."""
+        return await self._stateless(msg, backward=True)
+
+    async def rpc_backward_stream(self, msg: Message) -> Message:
+        return await self.rpc_backward(msg)
+
+    def _autograd_stage(self):
+        if getattr(self, "_ag", None) is None:
+            from .runtime.autograd_stage import AutogradStage
+
+            ex = self.executor
+            self._ag = AutogradStage(ex.cfg, ex.w, ex.device, ex.dtype)
+        return self._ag
+
+    async def _stateless(self, msg: Message, backward: bool) -> Message:
+        """Upstream ``run_rpc_forward`` / ``run_rpc_backward``. These run on the GPU worker thread,
+        so they serialise with inference batches, which are submitted first."""
+        if self.executor.is_first:
+            raise ValueError("stateless forward/backward takes hidden states; this span starts with the embedding")
+        md, ts = msg.metadata, list(msg.tensors)
+        has_prompts = bool(md.get("has_prompts", False))
+        need = (2 if backward else 1) + int(has_prompts)
+        if len(ts) != need:
+            raise ValueError(f"expected {need} tensors, got {len(ts)}")
+        hidden = ts[0] if ts[0].dim() == 3 else ts[0].unsqueeze(0)
+        prompts = ts[-1] if has_prompts else None
+
+        def run():
+            ag = self._autograd_stage()
+            if not backward:
+                with torch.no_grad():
+                    return [ag.forward(hidden, prompts).to("cpu")]
+            g = ts[1] if ts[1].dim() == 3 else ts[1].unsqueeze(0)
+            gh, gp = ag.backward(hidden, g, prompts)
+            out = [gh.to("cpu", hidden.dtype)]
+            if gp is not None:
+                out.append(gp.to("cpu", prompts.dtype))
+            return out
+
+        self.stats["backward" if backward else "forward_stateless"] = \
+            self.stats.get("backward" if backward else "forward_stateless", 0) + 1
+        outs = await asyncio.wait_for(asyncio.get_running_loop().run_in_executor(self._worker, run),
+                                      self.request_timeout * 4)
+        return Message({"session_id": md.get("session_id")}, outs)
 
     async def rpc_push(self, msg: Message) -> Message:
         """Server-to-server hop of a pushed chain (upstream ``rpc_push``); same body as rpc_forward."""

@@ -363,6 +363,94 @@ class RpcTransport:
         except Exception:
             pass
 
+    # ------------------------------------------------------------------ fine-tuning (stateless)
+    def _fresh_route(self) -> List[Hop]:
+        if self.routing == "module":
+            return self._module_route(int(self.start_block))
+        return [self._stage_hop(i) for i in range(len(self.stage_keys))]
+
+    def _prompt_slice(self, prompts: Optional[torch.Tensor], hop: Hop) -> List[torch.Tensor]:
+        if prompts is None:
+            return []
+        a, b = hop.start - int(self.start_block), hop.end - int(self.start_block)
+        return [prompts[a:b].contiguous()]
+
+    async def _call_hop(self, hop: Hop, name: str, tensors: List[torch.Tensor], md: dict) -> Message:
+        last_err = None
+        for addr in hop.maddrs:
+            try:
+                return await self.client.call(addr, "StageConnectionHandler." + name, Message(md, tensors),
+                                              self.timeout * 4)
+            except (ConnectionError, OSError) as e:
+                last_err = e
+        raise last_err if last_err else ConnectionError(f"peer {hop.peer_id[:8]} announced no addresses")
+
+    def _stateless_hop(self, route: List[Hop], k: int, name: str, tensors_of, md: dict) -> Tuple[Message, List[Hop]]:
+        """Call hop k; on failure re-route from its start block (stateless: nothing to replay)."""
+        for attempt in range(self.max_recovery_attempts + 1):
+            hop = route[k]
+            try:
+                return self._run(self._call_hop(hop, name, tensors_of(hop), md)), route
+            except RECOVERABLE as e:
+                if attempt == self.max_recovery_attempts:
+                    raise
+                logger.warning(f"[stateless] {name} failed at {hop}: {e!r}; re-routing")
+                self.failed_peers.setdefault("__stateless__", set()).add(hop.peer_id)
+                tail = self._route_tail(route, k, self.failed_peers["__stateless__"])
+                if tail[0].start != hop.start:
+                    raise
+                route = route[:k] + tail
+        raise RuntimeError("unreachable")
+
+    def forward_stateless(self, hidden: torch.Tensor, prompts: Optional[torch.Tensor] = None,
+                          route: Optional[List[Hop]] = None):
+        """Run [B, T, H] hidden states through every remote block without a session (upstream
+        ``rpc_forward`` as the training client uses it). ``prompts`` are deep prompts for the
+        remote blocks, ``[total_blocks - start_block, B|1, P, H]``; each hop receives its own
+        slice. Returns ``(output, per_hop_inputs, route)``; keep the last two for
+        :meth:`backward_stateless`."""
+        x = hidden.detach().to("cpu")
+        if x.dim() == 2:
+            x = x.unsqueeze(0)
+        p = prompts.detach().to("cpu") if prompts is not None else None
+        route = list(route or self._fresh_route())
+        md = {"stateless": True, "has_prompts": p is not None}
+        inputs = []
+        k = 0
+        while k < len(route):
+            cur = x
+            resp, route = self._stateless_hop(route, k, "rpc_forward", lambda h: [cur] + self._prompt_slice(p, h), md)
+            inputs.append(x)
+            x = resp.tensors[0]
+            k += 1
+        return x, inputs, route
+
+    def backward_stateless(self, inputs: List[torch.Tensor], route: List[Hop], grad_output: torch.Tensor,
+                           prompts: Optional[torch.Tensor] = None):
+        """Backward through the route of a :meth:`forward_stateless` call, last hop first
+        (upstream ``rpc_backward``). Returns ``(grad_hidden, grad_prompts or None)``."""
+        g = grad_output.detach().to("cpu")
+        if g.dim() == 2:
+            g = g.unsqueeze(0)
+        p = prompts.detach().to("cpu") if prompts is not None else None
+        gp = torch.zeros_like(p) if p is not None else None
+        md = {"stateless": True, "has_prompts": p is not None}
+        route = list(route)
+        for k in range(len(route) - 1, -1, -1):
+            cur_g, inp = g, inputs[k]
+            resp, route = self._stateless_hop(route, k, "rpc_backward",
+                                              lambda h: [inp, cur_g] + self._prompt_slice(p, h), md)
+            g = resp.tensors[0]
+            if gp is not None:
+                a, b = route[k].start - int(self.start_block), route[k].end - int(self.start_block)
+                gp[a:b] += resp.tensors[1]
+        return g, gp
+
+    def remote_blocks(self, hidden: torch.Tensor, prompts: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Differentiable call of the remote blocks: gradients flow to ``hidden`` and ``prompts``
+        (client-side prompt tuning, as with upstream ``RemoteSequential``)."""
+        return _RemoteBlocks.apply(hidden, prompts if prompts is not None else torch.empty(0), self)
+
     def shutdown(self):
         try:
             self._run(self.client.close())
@@ -370,3 +458,22 @@ class RpcTransport:
             pass
         if self._own_dht:
             self.dht.shutdown()
+
+
+class _RemoteBlocks(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, hidden, prompts, tx):
+        p = prompts if prompts.numel() else None
+        out, inputs, route = tx.forward_stateless(hidden, p)
+        ctx.tx, ctx.inputs, ctx.route, ctx.has_p = tx, inputs, route, p is not None
+        ctx.hshape, ctx.hdtype, ctx.hdev = hidden.shape, hidden.dtype, hidden.device
+        ctx.save_for_backward(prompts)
+        return out.to(hidden.device, hidden.dtype).reshape(hidden.shape)
+
+    @staticmethod
+    def backward(ctx, grad):
+        (prompts,) = ctx.saved_tensors
+        gh, gp = ctx.tx.backward_stateless(ctx.inputs, ctx.route, grad, prompts if ctx.has_p else None)
+        gh = gh.to(ctx.hdev, ctx.hdtype).reshape(ctx.hshape)
+        gp = gp.to(prompts.device, prompts.dtype) if gp is not None else None
+        return gh, gp, None

@@ -1,0 +1,96 @@
+"""Stateless forward/backward through a swarm with deep prompts (upstream rpc_forward/rpc_backward,
+petals/server/handler.py:352-488, block_functions.py:32-141) vs local autograd on the same weights."""
+import pytest
+import torch
+
+from src.dht_utils import get_stage_key
+from src.models.config import resolve_model
+from src.models.weights import random_stage_weights
+from src.rpc_transport import RpcTransport
+from src.runtime.autograd_stage import AutogradStage
+
+from .swarm_utils import ServerThread, server_argv, wait_for
+
+
+def test_autograd_stage_matches_reference_forward():
+    from src.models.reference_model import llama_forward
+
+    cfg = resolve_model("tiny-llama")
+    w = random_stage_weights(cfg, 0, cfg.num_hidden_layers, has_embed=True, has_head=True, device="cpu",
+                             dtype=torch.float32, seed=2)
+    ids = torch.randint(0, cfg.vocab_size, (9,), generator=torch.Generator().manual_seed(1))
+    ag = AutogradStage(cfg, w, "cpu", torch.float32)
+    out = ag.forward(w.embed[ids].unsqueeze(0))
+    torch.testing.assert_close(out[0], llama_forward([w], ids, return_hidden=True), atol=1e-5, rtol=1e-5)
+
+
+def test_prompt_gradient_is_input_gradient_slice():
+    """Upstream semantics: grad(prompt_i) == grad wrt hidden[:, :P] at block i's input."""
+    cfg = resolve_model("tiny-llama")
+    w = random_stage_weights(cfg, 0, 2, has_embed=False, has_head=False, device="cpu", dtype=torch.float32)
+    ag = AutogradStage(cfg, w, "cpu", torch.float32)
+    g = torch.Generator().manual_seed(0)
+    h = torch.randn(2, 6, cfg.hidden_size, generator=g)
+    p = 0.1 * torch.randn(2, 1, 3, cfg.hidden_size, generator=g)
+    go = torch.randn(2, 6, cfg.hidden_size, generator=g)
+    gh, gp = ag.backward(h, go, p)
+    # with a zero prompt on block 0, grad(prompt_0) is the batch-summed input grad of its first 3 tokens
+    p0 = p.clone()
+    p0[0] = 0
+    gh0, gp0 = ag.backward(h + torch.cat([p[0].expand(2, 3, -1), torch.zeros(2, 3, cfg.hidden_size)], 1), go, p0)
+    torch.testing.assert_close(gp0[0, 0], gh0[:, :3].sum(0), atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(gp[1], gp0[1], atol=1e-5, rtol=1e-5)
+
+
+@pytest.mark.gpu
+def test_autograd_stage_bf16_on_gpu_matches_fp32():
+    cfg = resolve_model("small-llama")
+    w32 = random_stage_weights(cfg, 0, 2, has_embed=False, has_head=False, device="cpu", dtype=torch.float32, seed=4)
+    wg = random_stage_weights(cfg, 0, 2, has_embed=False, has_head=False, device="cuda", dtype=torch.bfloat16, seed=4)
+    g = torch.Generator().manual_seed(0)
+    h = torch.randn(2, 40, cfg.hidden_size, generator=g)
+    p = 0.1 * torch.randn(2, 2, 4, cfg.hidden_size, generator=g)
+    go = torch.randn(2, 40, cfg.hidden_size, generator=g)
+    gh, gp = AutogradStage(cfg, wg, "cuda").backward(h.cuda(), go.cuda(), p.cuda())
+    rh, rp = AutogradStage(cfg, w32, "cpu", torch.float32).backward(h, go, p)
+    assert gh.dtype == torch.bfloat16 and gh.is_cuda
+    for a, b in ((gh, rh), (gp, rp)):
+        err = (a.float().cpu() - b).norm() / b.norm()
+        assert err < 0.03, float(err)
+
+
+@pytest.mark.timeout(180)
+@pytest.mark.parametrize("model", ["tiny-gpt2", "tiny-llama"])
+def test_remote_blocks_gradients_match_local(model):
+    cfg = resolve_model(model)
+    L, H = cfg.num_hidden_layers, cfg.hidden_size
+    s1 = ServerThread(server_argv(model, "1,2", 1)).wait()
+    s2 = ServerThread(server_argv(model, "1,2", 2, peers=s1.addr)).wait()
+    try:
+        assert wait_for(lambda: s1.dht.get(get_stage_key(2)) is not None)
+        tx = RpcTransport("cpu", 0, [s1.addr], timeout=10.0, stage_keys=[get_stage_key(1), get_stage_key(2)],
+                          model_name=model, total_blocks=L, start_block=1)
+        g = torch.Generator().manual_seed(0)
+        h = torch.randn(2, 5, H, generator=g).requires_grad_()
+        prompts = (0.1 * torch.randn(L - 1, 1, 2, H, generator=g)).requires_grad_()
+        wl = torch.randn(2, 5, H, generator=g)
+        out = tx.remote_blocks(h, prompts)
+        (out * wl).sum().backward()
+
+        w = random_stage_weights(cfg, 1, L, has_embed=False, has_head=True, device="cpu", dtype=torch.float32)
+        ag = AutogradStage(cfg, w, "cpu", torch.float32)
+        h2, p2 = h.detach().clone().requires_grad_(), prompts.detach().clone().requires_grad_()
+        out2 = ag.forward(h2, p2)
+        (out2 * wl).sum().backward()
+        torch.testing.assert_close(out, out2, atol=1e-5, rtol=1e-5)
+        torch.testing.assert_close(h.grad, h2.grad, atol=1e-5, rtol=1e-5)
+        torch.testing.assert_close(prompts.grad, p2.grad, atol=1e-5, rtol=1e-5)
+        assert s1.srv.handler.stats.get("backward") == 1 and s2.srv.handler.stats.get("backward") == 1
+        # no prompts: plain input gradient
+        h3 = h.detach().clone().requires_grad_()
+        tx.remote_blocks(h3).sum().backward()
+        assert h3.grad is not None and torch.isfinite(h3.grad).all()
+        tx.shutdown()
+    finally:
+        s1.close()
+        s2.close()

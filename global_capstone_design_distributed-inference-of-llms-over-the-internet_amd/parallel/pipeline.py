@@ -36,6 +36,7 @@ import torch.distributed as dist
 from .. import ops
 from ..runtime.executor import StageExecutor
 from ..runtime.sampler import RECENT, SamplingParams
+from ..utils.tracing import trace_range
 
 
 @dataclasses.dataclass
@@ -159,7 +160,8 @@ class PipelineEngine:
         if self.timing and self.dev.type == "cuda":
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-        out = self.ex.forward(seqs, x, reset=[reset] * len(seqs))
+        with trace_range(f"pp.stage{self.stage}.mb{mb.index}"):
+            out = self.ex.forward(seqs, x, reset=[reset] * len(seqs))
         if self.timing and self.dev.type == "cuda":
             e1.record()
             self._events.append((e0, e1))

@@ -43,6 +43,7 @@ from .comm.rpc import RemoteError, RpcClient, RpcServer
 from .comm.wire import Message
 from .runtime.kv_cache import AllocationFailed
 from .runtime.sampler import BatchSampler, SamplingParams, session_seed
+from .utils.tracing import PhaseTimer
 
 logger = logging.getLogger(__name__)
 
@@ -94,6 +95,7 @@ class StageConnectionHandler:
         self._client: Optional[RpcClient] = None  # for push forwarding (created on the server loop)
         self._steps: Dict[str, Dict[str, Message]] = {}  # session -> step_id -> reply (dedup, rpc_inference)
         self.stats = {"requests": 0, "batches": 0, "tokens": 0, "pushed": 0}
+        self.timer = PhaseTimer()  # host wall time per phase (+ roctx ranges when MPAMD_TRACE=1)
 
     # ------------------------------------------------------------------ registration
     def add_p2p_handlers(self, server: RpcServer) -> None:
@@ -265,7 +267,7 @@ class StageConnectionHandler:
         ex = self.executor
         return Message({"cache_tokens_left": ex.sessions.cache_tokens_left(), "sessions": len(ex.sessions.sessions),
                         "start_block": ex.start, "end_block": ex.end, "final_stage": self.final_stage,
-                        **self.stats})
+                        "phases": self.timer.summary(), **self.stats})
 
     async def rpc_close_session(self, msg: Message) -> Message:
         sid = msg.metadata.get("session_id")
@@ -391,7 +393,8 @@ class StageConnectionHandler:
         else:
             x = torch.cat([r.x for r in batch]).to(ex.device, ex.dtype)
         ml = max((int(r.max_length) for r in batch if r.max_length), default=None)
-        with torch.inference_mode():
+        phase = "handler.prefill" if any(r.x.shape[0] > 1 for r in batch) else "handler.decode"
+        with torch.inference_mode(), self.timer(phase):
             out = ex.forward(seqs, x, reset=[r.reset for r in batch], starts=[r.start for r in batch], max_length=ml)
             self.stats["batches"] += 1
             self.stats["tokens"] += int(x.shape[0])

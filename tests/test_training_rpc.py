@@ -44,13 +44,25 @@ def test_prompt_gradient_is_input_gradient_slice():
 
 @pytest.mark.gpu
 def test_autograd_stage_bf16_on_gpu_matches_fp32():
+    import dataclasses
+
     cfg = resolve_model("small-llama")
-    w32 = random_stage_weights(cfg, 0, 2, has_embed=False, has_head=False, device="cpu", dtype=torch.float32, seed=4)
     wg = random_stage_weights(cfg, 0, 2, has_embed=False, has_head=False, device="cuda", dtype=torch.bfloat16, seed=4)
+
+    def f32(obj):  # the same weights, fp32 on the CPU
+        return dataclasses.replace(obj, **{f.name: getattr(obj, f.name).float().cpu() for f in dataclasses.fields(obj)
+                                           if isinstance(getattr(obj, f.name), torch.Tensor)})
+
+    w32 = dataclasses.replace(wg, layers=[f32(lay) for lay in wg.layers])
     g = torch.Generator().manual_seed(0)
     h = torch.randn(2, 40, cfg.hidden_size, generator=g)
     p = 0.1 * torch.randn(2, 2, 4, cfg.hidden_size, generator=g)
     go = torch.randn(2, 40, cfg.hidden_size, generator=g)
+    with torch.no_grad():
+        fo = AutogradStage(cfg, wg, "cuda").forward(h.cuda(), p.cuda()).float().cpu()
+        ro = AutogradStage(cfg, w32, "cpu", torch.float32).forward(h, p)
+    ferr = float((fo - ro).norm() / ro.norm())
+    assert ferr < 0.02, ferr
     gh, gp = AutogradStage(cfg, wg, "cuda").backward(h.cuda(), go.cuda(), p.cuda())
     rh, rp = AutogradStage(cfg, w32, "cpu", torch.float32).backward(h, go, p)
     assert gh.dtype == torch.bfloat16 and gh.is_cuda

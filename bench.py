@@ -98,6 +98,8 @@ def main(argv=None):
     max_len = a.prompt_len + a.warmup + a.steps + 8
     max_len = 64 * math.ceil(max_len / 64)
     kv_bytes = None if device.type == "cuda" else 256 << 20
+    if os.environ.get("MPAMD_KV_GB"):  # cap the KV pool (e.g. several ranks sharing one GPU in a rehearsal)
+        kv_bytes = int(float(os.environ["MPAMD_KV_GB"]) * (1 << 30))
     ex = StageExecutor(cfg, w, device, dtype=dtype, max_sessions=M * B, max_seq_len=max(max_len, 256),
                        kv_cache_bytes=kv_bytes, use_graphs=not a.no_graphs, graph_max_batch=max(B, 1),
                        max_tokens_per_step=max(B * a.prompt_len, B))

@@ -364,8 +364,9 @@ def run_stage_server_fixed(args, device, cuts: List[int], stop: Optional[threadi
     dtype = resolve_dtype(args.dtype, device)
     full = load_stage_model(args.model, device, role, start=s, end=e, dtype=dtype, seed=args.seed,
                             use_cpu_offload=args.use_cpu_offload, **_executor_kwargs(args))
-    ex = StageExecutor(cfg, full.weights if not args.use_cpu_offload else _onto(full, device), device, dtype=dtype,
-                       **full.executor_kwargs)
+    off = bool(args.use_cpu_offload) and device.type == "cuda"
+    ex = StageExecutor(cfg, full.weights if off or not args.use_cpu_offload else _onto(full, device), device,
+                       dtype=dtype, offload=off, keep_layers_on_gpu=args.keep_layers_on_gpu, **full.executor_kwargs)
     dht = _start_dht(args)
     srv = _Server(args, dht, ex, final, k)
     stop = stop or threading.Event()

@@ -36,6 +36,12 @@ from .session import SessionManager, SessionState
 
 logger = logging.getLogger(__name__)
 
+# per-path weight tensors a layer loop reads (what CPU offload streams)
+_PACKED_FIELDS = ("input_norm", "post_norm", "qkv_p", "o_p", "gate_up_p", "down_p")
+_DENSE_FIELDS = ("input_norm", "post_norm", "qkv", "o", "gate_up", "down")
+_GPT2_FIELDS = ("ln1_w", "ln1_b", "attn_w", "attn_b", "proj_w", "proj_b", "ln2_w", "ln2_b", "fc_w", "fc_b",
+                "fc2_w", "fc2_b")
+
 
 @dataclasses.dataclass
 class Plan:
@@ -100,7 +106,8 @@ class StageExecutor:
     def __init__(self, cfg: ModelConfig, weights: StageWeights, device, *, dtype=torch.bfloat16,
                  page_size: int = 64, max_sessions: int = 256, max_seq_len: Optional[int] = None,
                  kv_cache_bytes: Optional[int] = None, kv_fraction: float = 0.9, use_graphs: Optional[bool] = None,
-                 graph_max_batch: int = 256, max_tokens_per_step: int = 8192):
+                 graph_max_batch: int = 256, max_tokens_per_step: int = 8192, offload: bool = False,
+                 keep_layers_on_gpu: int = 0):
         cfg.validate()
         self.cfg = cfg
         self.w = weights
@@ -151,6 +158,9 @@ class StageExecutor:
                     if weights.lm_head_p is not None:
                         shapes.append((16 * weights.lm_head_p.shape[0], H, 0))
                     ops.autotune_gemm(shapes, self.device)
+        self._streamer, self._n_stream = None, self.n_layers
+        if offload and self.device.type == "cuda":
+            self._setup_offload(keep_layers_on_gpu)
         logger.info(f"StageExecutor blocks [{self.start},{self.end}) embed={self.is_first} head={self.is_last} "
                     f"kv_pages={num_pages} x {page_size} tokens ({self.cache.nbytes / 2**30:.2f} GiB) "
                     f"graphs={self.use_graphs}")
@@ -375,7 +385,7 @@ class StageExecutor:
             xn = e("xn_p", (pk(T, H),))
             attn = e("attn_p", (pk(T, cfg.q_dim),))
             act = e("act_p", (pk(T, cfg.intermediate_size),))
-            for li, L in enumerate(w.layers):
+            for li, L in self._iter_layers(_PACKED_FIELDS):
                 if li == 0:
                     ops.rmsnorm(h, L.input_norm, eps, out=xn, residual=res, mode=2, packed=True)
                 else:
@@ -392,7 +402,7 @@ class StageExecutor:
             xn = e("xn", (T, H))
             attn = e("attn", (T, cfg.q_dim))
             act = e("act", (T, cfg.intermediate_size))
-            for li, L in enumerate(w.layers):
+            for li, L in self._iter_layers(_DENSE_FIELDS):
                 if li == 0:
                     ops.rmsnorm(h, L.input_norm, eps, out=xn, residual=res, mode=2)
                 else:
@@ -418,6 +428,38 @@ class StageExecutor:
             return logits[:, :V]
         fn = ops.rmsnorm(hout, w.final_norm, eps, out=e("fn", (S, H)), rows=last_rows)
         return ops.linear(fn, w.lm_head, out=e("logits", (S, V)))
+
+    def _iter_layers(self, fields):
+        """``(index, layer)`` over this stage's blocks; with CPU offload the streamed layers come
+        from the pinned-host ring (runtime/offload.py) and the resident tail follows."""
+        if self._streamer is None:
+            yield from enumerate(self.w.layers)
+            return
+        yield from self._streamer.layers(fields)
+        for j in range(self._n_stream, self.n_layers):
+            yield j, self.w.layers[j]
+
+    def _setup_offload(self, keep_layers_on_gpu: int) -> None:
+        from .offload import LayerStreamer, pin_layer
+
+        w = self.w
+        if w.fp8:
+            raise ValueError("CPU offload is not supported with fp8 weights")
+        keep = max(0, min(int(keep_layers_on_gpu), self.n_layers))
+        n_stream = self.n_layers - keep
+        host = [pin_layer(L) for L in w.layers[:n_stream]]
+        tail = [dataclasses.replace(L, **{f.name: getattr(L, f.name).to(self.device) for f in dataclasses.fields(L)
+                                          if isinstance(getattr(L, f.name), torch.Tensor)})
+                for L in w.layers[n_stream:]]
+        w.layers = host + tail
+        for name in ("embed", "pos_embed", "final_norm", "final_norm_b", "lm_head", "lm_head_p"):
+            t = getattr(w, name)
+            if t is not None:
+                setattr(w, name, t.to(self.device))
+        self._n_stream = n_stream
+        self._streamer = LayerStreamer(host, self.device) if host else None
+        self.use_graphs = False  # the slot ring is re-filled every step; graphs would pin one layer set
+        logger.info(f"CPU offload: {n_stream} layers streamed from pinned host memory, {keep} resident")
 
     def _head_packed_ok(self, M: int) -> bool:
         return self.device.type == "cuda" and ops.gemm_policy() != "hipblaslt" and 0 < M <= 64 and \
@@ -451,7 +493,7 @@ class StageExecutor:
             h = w.embed[x.long()] + w.pos_embed[plan.positions]
         else:
             h = x
-        for li, L in enumerate(w.layers):
+        for li, L in self._iter_layers(_GPT2_FIELDS):
             a = F.layer_norm(h, (H,), L.ln1_w, L.ln1_b, cfg.layer_norm_eps)
             qkv = F.linear(a, L.attn_w, L.attn_b)
             q, k, v = qkv.split(H, dim=1)

@@ -71,6 +71,7 @@ class _Req:
     fut: asyncio.Future
     t0: float
     priority: float = 2.0
+    prompts: Optional[torch.Tensor] = None  # deep prompts [n_blocks, P, H] for this step
 
 
 class StageConnectionHandler:
@@ -227,7 +228,7 @@ class StageConnectionHandler:
     async def _handle(self, msg: Message) -> Message:
         reply = await asyncio.wait_for(self._submit(msg), self.request_timeout)
         hops = msg.metadata.get("next_hops")
-        if not hops or self.final_stage:
+        if not hops or self.final_stage or msg.metadata.get("has_prompts"):  # upstream: no push with prompts
             return reply
         return await self._push(msg.metadata, reply, list(hops))
 
@@ -315,8 +316,14 @@ class StageConnectionHandler:
         params = SamplingParams(float(md.get("temperature", self._default.temperature)),
                                 float(md.get("top_p", self._default.top_p)), int(md.get("top_k", self._default.top_k)),
                                 float(md.get("repetition_penalty", self._default.repetition_penalty)))
+        prompts = None
+        if md.get("has_prompts") and len(msg.tensors) > 1:
+            # upstream layout [n_blocks, B(=1), P, H]; one session per request here
+            prompts = msg.tensors[1]
+            if prompts.dim() == 4:
+                prompts = prompts[:, 0]
         return _Req(sid, x, start, reset, params, list(md.get("generated_tokens", []) or []),
-                    md.get("max_length"), None, time.perf_counter())
+                    md.get("max_length"), None, time.perf_counter(), prompts=prompts)
 
     async def _submit(self, msg: Message) -> Message:
         req = self._parse(msg)
@@ -394,8 +401,10 @@ class StageConnectionHandler:
             x = torch.cat([r.x for r in batch]).to(ex.device, ex.dtype)
         ml = max((int(r.max_length) for r in batch if r.max_length), default=None)
         phase = "handler.prefill" if any(r.x.shape[0] > 1 for r in batch) else "handler.decode"
+        prompts = [r.prompts for r in batch] if any(r.prompts is not None for r in batch) else None
         with torch.inference_mode(), self.timer(phase):
-            out = ex.forward(seqs, x, reset=[r.reset for r in batch], starts=[r.start for r in batch], max_length=ml)
+            out = ex.forward(seqs, x, reset=[r.reset for r in batch], starts=[r.start for r in batch], max_length=ml,
+                             prompts=prompts)
             self.stats["batches"] += 1
             self.stats["tokens"] += int(x.shape[0])
             if self.final_stage:

@@ -228,12 +228,36 @@ class StageExecutor:
         boundaries, later pieces attend to the KV the earlier pieces wrote.
         """
         T = sum(int(n) for _, n in seqs)
+        prompts = plan_kw.pop("prompts", None)
+        if prompts is not None and not any(p is not None for p in prompts):
+            prompts = None
         if T > self.max_tokens:
+            if prompts is not None:
+                raise ValueError("deep prompts need the step to fit max_tokens_per_step")
             return self._forward_chunked(seqs, x, **plan_kw)
         plan = self.plan(seqs, **plan_kw)
-        out = self.run(plan, x)
+        out = self.run(plan, x, prompt=self._prompt_rows(seqs, prompts) if prompts is not None else None)
         self.commit(plan)
         return out
+
+    def _prompt_rows(self, seqs, prompts):
+        """Deep prompts (upstream iterate_rpc_inference / TransformerBackend: before every block,
+        ``hidden[:, :P] += prompt``, applied to the first P tokens of this step). ``prompts[i]`` is
+        None or ``[n_layers, P, H]`` for sequence i. Returns (rows [R], values [n_layers, R, H])."""
+        rows, vals, off = [], [], 0
+        for (sid, n), p in zip(seqs, prompts):
+            if p is not None:
+                if p.dim() != 3 or p.shape[0] != self.n_layers or p.shape[2] != self.cfg.hidden_size:
+                    raise ValueError(f"prompts must be [{self.n_layers}, P, {self.cfg.hidden_size}], "
+                                     f"got {tuple(p.shape)}")
+                k = min(int(p.shape[1]), int(n))
+                rows.extend(range(off, off + k))
+                vals.append(p[:, :k])
+            off += int(n)
+        if not rows:
+            return None
+        return (torch.tensor(rows, dtype=torch.long, device=self.device),
+                torch.cat(vals, 1).to(self.device, self.dtype))
 
     def _forward_chunked(self, seqs, x, reset: Sequence[bool] = (), starts=None, max_length=None):
         C = self.max_tokens
@@ -278,7 +302,7 @@ class StageExecutor:
             return torch.stack(logits)
         return torch.cat(hidden)
 
-    def run(self, plan: Plan, x: torch.Tensor) -> torch.Tensor:
+    def run(self, plan: Plan, x: torch.Tensor, prompt=None) -> torch.Tensor:
         if plan.T == 0:
             H = self.cfg.hidden_size
             return torch.empty(0, self.cfg.vocab_size if self.is_last else H, dtype=self.dtype, device=self.device)
@@ -289,13 +313,13 @@ class StageExecutor:
         if self.timing and self.device.type == "cuda":
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
-        if self.use_graphs and plan.is_decode and plan.T <= self.graph_max_batch:
+        if prompt is None and self.use_graphs and plan.is_decode and plan.T <= self.graph_max_batch:
             out = self._run_graph(plan, x)
         elif self.cfg.model_type == "gpt2":
-            out = self._forward_gpt2(plan, x)
+            out = self._forward_gpt2(plan, x, prompt=prompt)
         else:
             out = self._forward_llama(x, plan.positions, plan.slots, plan.q_seq, plan.q_ctx, plan.last_rows,
-                                      plan.T, plan.max_ctx, None, qblocks=plan.qblocks)
+                                      plan.T, plan.max_ctx, None, qblocks=plan.qblocks, prompt=prompt)
         if ev is not None:
             ev[1].record()
             ev[1].synchronize()
@@ -332,7 +356,7 @@ class StageExecutor:
                                    workspace=ws, part_size=ps, num_parts=np_, packed=packed)
 
     def _forward_llama(self, x, positions, slots, q_seq, q_ctx, last_rows, T, max_ctx, attn_part,
-                       bufs: Optional[dict] = None, qblocks=None):
+                       bufs: Optional[dict] = None, qblocks=None, prompt=None):
         cfg, w = self.cfg, self.w
         H, eps = cfg.hidden_size, cfg.rms_norm_eps
         dev, dt = self.device, self.dtype
@@ -352,7 +376,7 @@ class StageExecutor:
         qkv = e("qkv", (T, cfg.q_dim + 2 * cfg.kv_dim))
         o = e("o", (T, H))
         mlp = e("mlp", (T, H))
-        if self._fp8_ok(T):
+        if prompt is None and self._fp8_ok(T):
             # fp8 W8A8 decode path: packed bf16 activations are quantized per row right before
             # each GEMM (csrc/fp8.hip); weights stream at 1 byte per parameter
             pk = ops.packed_numel
@@ -379,7 +403,7 @@ class StageExecutor:
                 ops.linear_fp8(a8, asc, L.gate_up_q, L.gate_up_s, T, out=act, epilogue=1, out_packed=True)
                 ops.quant_act_fp8(act, T, F, out=a8, scale=asc)
                 ops.linear_fp8(a8, asc, L.down_q, L.down_s, T, out=mlp)
-        elif self._packed_ok(T):
+        elif prompt is None and self._packed_ok(T):
             # decode path: activations feeding a GEMM stay in the packed MFMA-fragment layout
             pk = ops.packed_numel
             xn = e("xn_p", (pk(T, H),))
@@ -403,7 +427,11 @@ class StageExecutor:
             attn = e("attn", (T, cfg.q_dim))
             act = e("act", (T, cfg.intermediate_size))
             for li, L in self._iter_layers(_DENSE_FIELDS):
-                if li == 0:
+                if prompt is not None:  # deep prompt: the block input (residual stream) += prompt[li]
+                    cur = h.clone() if li == 0 else ops.add(res, mlp)
+                    cur.index_add_(0, prompt[0], prompt[1][li])
+                    ops.rmsnorm(cur, L.input_norm, eps, out=xn, residual=res, mode=2)
+                elif li == 0:
                     ops.rmsnorm(h, L.input_norm, eps, out=xn, residual=res, mode=2)
                 else:
                     ops.rmsnorm(mlp, L.input_norm, eps, out=xn, residual=res, mode=1)
@@ -484,7 +512,7 @@ class StageExecutor:
         return self._packed_ready
 
     # ------------------------------------------------------------------ gpt2 (plumbing family)
-    def _forward_gpt2(self, plan: Plan, x):
+    def _forward_gpt2(self, plan: Plan, x, prompt=None):
         cfg, w = self.cfg, self.w
         F = torch.nn.functional
         T, H = plan.T, cfg.hidden_size
@@ -494,6 +522,8 @@ class StageExecutor:
         else:
             h = x
         for li, L in self._iter_layers(_GPT2_FIELDS):
+            if prompt is not None:
+                h = h.index_add(0, prompt[0], prompt[1][li])
             a = F.layer_norm(h, (H,), L.ln1_w, L.ln1_b, cfg.layer_norm_eps)
             qkv = F.linear(a, L.attn_w, L.attn_b)
             q, k, v = qkv.split(H, dim=1)

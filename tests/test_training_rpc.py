@@ -42,6 +42,74 @@ def test_prompt_gradient_is_input_gradient_slice():
     torch.testing.assert_close(gp[1], gp0[1], atol=1e-5, rtol=1e-5)
 
 
+@pytest.mark.parametrize("model", ["tiny-llama", "tiny-gpt2"])
+def test_inference_with_deep_prompts_matches_stateless_forward(model):
+    """Deep prompts in the KV-cached inference path (upstream iterate_rpc_inference) == stateless forward."""
+    from src.runtime.executor import StageExecutor
+
+    cfg = resolve_model(model)
+    L, H = cfg.num_hidden_layers, cfg.hidden_size
+    w = random_stage_weights(cfg, 1, L, has_embed=False, has_head=False, device="cpu", dtype=torch.float32)
+    ex = StageExecutor(cfg, w, "cpu", dtype=torch.float32, kv_cache_bytes=8 << 20, max_sessions=4, max_seq_len=128)
+    ag = AutogradStage(cfg, w, "cpu", torch.float32)
+    g = torch.Generator().manual_seed(3)
+    h = torch.randn(9, H, generator=g)
+    p = 0.5 * torch.randn(L - 1, 3, H, generator=g)
+    out = ex.forward([("a", 6), ("b", 3)], torch.cat([h[:6], h[6:]]), prompts=[p, None])
+    torch.testing.assert_close(out[:6], ag.forward(h[None, :6], p[:, None])[0], atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(out[6:], ag.forward(h[None, 6:9])[0], atol=1e-5, rtol=1e-5)
+    # next step without prompts attends to the prompted prefix
+    nxt = torch.randn(1, H, generator=g)
+    step = ex.forward([("a", 1)], nxt)
+    full = ag.forward(torch.cat([h[:6], nxt])[None], p[:, None])[0, -1]
+    torch.testing.assert_close(step[0], full, atol=1e-5, rtol=1e-5)
+
+
+@pytest.mark.timeout(120)
+def test_rpc_inference_accepts_prompts():
+    from src.comm.rpc import RpcClient, get_loop
+    from src.comm.wire import Message
+
+    model = "tiny-llama"
+    cfg = resolve_model(model)
+    s1 = ServerThread(server_argv(model, "1,2", 1)).wait()
+    try:
+        addr, cl, loop = s1.srv.maddrs[0], RpcClient(), get_loop()
+        h = torch.randn(1, 4, cfg.hidden_size)
+        p = torch.randn(1, 1, 2, cfg.hidden_size)  # [n_blocks=1, B, P, H]
+
+        def call(md, ts):
+            return loop.run(cl.call(addr, "StageConnectionHandler.rpc_inference", Message(md, ts), 10.0))
+
+        with_p = call({"session_id": "p", "has_prompts": True}, [h, p]).tensors[0]
+        without = call({"session_id": "q"}, [h]).tensors[0]
+        assert not torch.allclose(with_p[:, :2], without[:, :2])
+        w = random_stage_weights(cfg, 1, 2, has_embed=False, has_head=False, device="cpu", dtype=torch.float32)
+        ref = AutogradStage(cfg, w, "cpu", torch.float32).forward(h, p)
+        torch.testing.assert_close(with_p, ref, atol=1e-5, rtol=1e-5)
+        loop.run(cl.close())
+    finally:
+        s1.close()
+
+
+@pytest.mark.gpu
+def test_gpu_executor_deep_prompts():
+    from src.runtime.executor import StageExecutor
+
+    cfg = resolve_model("small-llama")
+    L, H = cfg.num_hidden_layers, cfg.hidden_size
+    w = random_stage_weights(cfg, 1, L, has_embed=False, has_head=False, device="cuda", seed=5)
+    ex = StageExecutor(cfg, w, "cuda", kv_cache_bytes=64 << 20, max_sessions=4, max_seq_len=256)
+    g = torch.Generator().manual_seed(0)
+    h = torch.randn(12, H, generator=g).to("cuda", torch.bfloat16)
+    p = (0.5 * torch.randn(L - 1, 4, H, generator=g)).to("cuda", torch.bfloat16)
+    out = ex.forward([("a", 12)], h, prompts=[p]).float()
+    ref = AutogradStage(cfg, w, "cuda").forward(h[None], p[:, None])[0].float()
+    assert float((out - ref).norm() / ref.norm()) < 0.02
+    plain = ex.forward([("b", 12)], h).float()
+    assert float((plain[:4] - out[:4]).norm() / out[:4].norm()) > 0.05  # the prompt changed the output
+
+
 @pytest.mark.gpu
 def test_autograd_stage_bf16_on_gpu_matches_fp32():
     import dataclasses

@@ -104,7 +104,7 @@ def main(argv=None):
                        kv_cache_bytes=kv_bytes, use_graphs=not a.no_graphs, graph_max_batch=max(B, 1),
                        max_tokens_per_step=max(B * a.prompt_len, B))
     if rank == 0 and device.type == "cuda":
-        print("gemm kernel choice (stream-K?):", {f"M{k[0]}:N{k[1]}xK{k[2]}e{k[3]}": v
+        print("gemm kernel choice:", {f"M{k[0]}:N{k[1]}xK{k[2]}e{k[3]}": v
                                                    for k, v in sorted(ops._SK_CHOICE.items())}, file=sys.stderr)
     sp = SamplingParams(a.temperature, a.top_p, a.top_k, a.repetition_penalty)
     eng = PipelineEngine(ex, rank, world, sp, n_micro=M, batch=B, seed=a.seed, stages=S, groups=groups)

@@ -89,12 +89,18 @@ def gemm_policy() -> str:
 # "off" force the stream-K kernel on / off wherever it applies.
 _GEMM_SK = os.environ.get("MPAMD_GEMM_SK", "auto")
 _GEMM_WS = {}
-_SK_CHOICE = {}  # (m_bucket, N, K, epilogue) -> bool
+_SK_CHOICE = {}  # (m_bucket, N, K, epilogue) -> kernel name (see _KERNEL_FLAGS)
+# decode-GEMM kernels (csrc/gemm.hip): one-group-per-workgroup, stream-K, and the shared-A (LDS)
+# form with (NT column tiles per wave, CH column waves sharing each k-split's A) = (2,2)/(2,4)/(4,2)
+_KERNEL_FLAGS = {"pk": 0, "sk": 4, "lds22": 16, "lds24": 16 | 32, "lds42": 16 | 96}
+_LDS_CFG = {"lds22": (2, 2), "lds24": (2, 4), "lds42": (4, 2)}
 
 
 def set_gemm_sk(mode: str) -> None:
+    """"auto" (autotuned table), "on" / "off" (stream-K wherever it applies / never), or a kernel
+    name from ``_KERNEL_FLAGS`` to force it wherever it applies."""
     global _GEMM_SK
-    assert mode in ("auto", "on", "off")
+    assert mode in ("auto", "on", "off") or mode in _KERNEL_FLAGS
     _GEMM_SK = mode
 
 
@@ -127,20 +133,41 @@ def _sk_covered(N: int, K: int) -> bool:
     return (N // 16) % 2 == 0 and nks % 8 == 0 and nks >= 32
 
 
-def _use_sk(M: int, N: int, K: int, epilogue: int) -> bool:
-    if _GEMM_SK == "off" or not _sk_covered(N, K):
-        return False
-    if _GEMM_SK == "on":
+def _lds_covered(name: str, M: int, N: int, K: int, epilogue: int) -> bool:
+    nt, ch = _LDS_CFG[name]
+    mt = (M + 15) // 16
+    return (N // 16) % (nt * ch) == 0 and K % 64 == 0 and (2 * mt) % ch == 0 and not (epilogue == 1 and nt % 2)
+
+
+def _covered(name: str, M: int, N: int, K: int, epilogue: int) -> bool:
+    if name == "pk":
         return True
-    return _SK_CHOICE.get((_m_bucket(M), N, K, int(epilogue)), False)
+    if name == "sk":
+        return _sk_covered(N, K)
+    return _lds_covered(name, M, N, K, epilogue)
+
+
+def _kernel_for(M: int, N: int, K: int, epilogue: int) -> str:
+    mode = _GEMM_SK
+    if mode == "off":
+        return "pk"
+    if mode == "on":
+        mode = "sk"
+    if mode == "auto":
+        mode = _SK_CHOICE.get((_m_bucket(M), N, K, int(epilogue)), "pk")
+    return mode if _covered(mode, M, N, K, epilogue) else "pk"
+
+
+def _use_sk(M: int, N: int, K: int, epilogue: int) -> bool:
+    return _kernel_for(M, N, K, epilogue) == "sk"
 
 
 _TUNE_POOL_BYTES = 1 << 30
 
 
 def autotune_gemm(shapes, device, ms=(16, 32, 48, 64), iters: int = 24, rounds: int = 3) -> dict:
-    """Time both decode-GEMM kernels on each (N, K, epilogue) for each M bucket and record the
-    faster one for ``linear``.  Returns the choice table.
+    """Time every applicable decode-GEMM kernel (one-group, stream-K, shared-A variants) on each
+    (N, K, epilogue) for each M bucket and record the fastest for ``linear``.  Returns the table.
 
     Conditions match the decode step: the packed weight is rotated over copies in a 1 GiB pool
     (a decode step streams gigabytes between two uses of a layer's weights, so the 256 MB
@@ -156,8 +183,6 @@ def autotune_gemm(shapes, device, ms=(16, 32, 48, 64), iters: int = 24, rounds: 
     pool = None
     try:
         for (N, K, epi) in shapes:
-            if not _sk_covered(N, K):
-                continue
             todo = [M for M in ms if (_m_bucket(M), N, K, int(epi)) not in _SK_CHOICE]
             if not todo:
                 continue
@@ -168,14 +193,18 @@ def autotune_gemm(shapes, device, ms=(16, 32, 48, 64), iters: int = 24, rounds: 
             wps = [pool[i * n:(i + 1) * n].view(N // 16, K // 32, 64, 8) for i in range(copies)]
             ncols = N // 2 if epi == 1 else N
             for M in todo:
+                cands = [k for k in _KERNEL_FLAGS if _covered(k, M, N, K, epi)]
+                if len(cands) == 1:
+                    _SK_CHOICE[(_m_bucket(M), N, K, int(epi))] = "pk"
+                    continue
                 xp = pack_act(torch.randn(M, K, device=device).to(torch.bfloat16))
                 y = torch.empty(packed_numel(M, ncols) if epi == 1 else M * ncols, dtype=torch.bfloat16,
                                 device=device)
                 res = torch.zeros(M, N, dtype=torch.bfloat16, device=device) if epi == 2 else None
                 out = y if epi == 1 else y.view(M, ncols)
-                t = {"off": float("inf"), "on": float("inf")}
+                t = {k: float("inf") for k in cands}
                 for _ in range(rounds):
-                    for mode in ("off", "on"):
+                    for mode in cands:
                         _GEMM_SK = mode
                         for i in range(2):
                             linear(xp, None, out=out, epilogue=epi, residual=res, wp=wps[i % copies], a_rows=M,
@@ -188,7 +217,9 @@ def autotune_gemm(shapes, device, ms=(16, 32, 48, 64), iters: int = 24, rounds: 
                         e1.record()
                         e1.synchronize()
                         t[mode] = min(t[mode], e0.elapsed_time(e1) / iters)
-                _SK_CHOICE[(_m_bucket(M), N, K, int(epi))] = t["on"] < 0.97 * t["off"]
+                best = min(t, key=t.get)
+                # keep the one-group kernel unless another wins by > 3 % (timing noise guard)
+                _SK_CHOICE[(_m_bucket(M), N, K, int(epi))] = best if t[best] < 0.97 * t["pk"] else "pk"
     finally:
         _GEMM_SK = saved
         del pool
@@ -430,11 +461,9 @@ def linear(x, w, out=None, epilogue=0, residual=None, policy=None, wp=None, a_ro
         if out is None:
             out = (torch.empty(packed_numel(M, ncols), dtype=x.dtype, device=x.device) if out_packed
                    else torch.empty(M, ncols, dtype=x.dtype, device=x.device))
-        flags = 1 | (2 if out_packed else 0)
-        ws = None
-        if _use_sk(M, N, K, epilogue):
-            flags |= 4
-            ws = gemm_workspace(x.device)
+        kern = _kernel_for(M, N, K, epilogue)
+        flags = 1 | (2 if out_packed else 0) | _KERNEL_FLAGS[kern]
+        ws = gemm_workspace(x.device) if kern == "sk" else None
         torch.ops.mpamd.gemm(x, wp, out, residual, int(epilogue), M, flags, ws)
         return out
     if a_rows is not None or out_packed:

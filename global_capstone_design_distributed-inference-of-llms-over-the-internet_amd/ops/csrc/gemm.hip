@@ -247,6 +247,156 @@ __device__ __forceinline__ void sk_epilogue(int qd, int g, const f32x4& v, const
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Shared-A form ("lds"): the 8 waves are KS = 8/CH k-splits x CH column groups. The CH waves
+// of a k-split need the SAME activation fragments, so each stages 1/CH of a k-group's A block
+// into LDS and all CH read it back with ds_read_b128. Global A traffic per weight byte drops by
+// CH vs the one-group kernel, and the k reduction stays inside the workgroup (no split-group
+// hand-off, which is what sank the all-column-split prototype in profiles/r1_gemm_lab.md).
+// A is double-buffered in LDS (one barrier per k-group), B in registers, as in the kernels
+// above; out-of-range k-groups of the last turn load a clamped group and skip the MFMAs so
+// every wave runs the same barrier sequence.
+template <int MT, int NT, int CH, int EPI, bool OPK>
+__global__ __launch_bounds__(512) void gemm_lds_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ wp,
+                                                       bf16_t* __restrict__ y, int64_t ys,
+                                                       const bf16_t* __restrict__ res, int64_t rs, int M, int N,
+                                                       int K) {
+  constexpr int KS = 8 / CH;
+  constexpr int GU = 2;               // k-slices (of 32) per group
+  constexpr int F = GU * MT;          // A fragments (1 KiB) per group
+  constexpr int FH = F / CH;          // fragments each wave of a k-split stages
+  constexpr int Q = MT * NT;          // accumulator quads per lane
+  constexpr int ABYTES = 2 * KS * F * 1024;
+  constexpr int RBYTES = KS * CH * Q * 64 * 16;
+  constexpr int LBYTES = ABYTES > RBYTES ? ABYTES : RBYTES;
+  static_assert(F % CH == 0, "A group must split evenly over the column waves");
+  __shared__ __attribute__((aligned(16))) unsigned char smem[LBYTES];
+  bf16_t* abuf = reinterpret_cast<bf16_t*>(smem);
+  f32x4* red = reinterpret_cast<f32x4*>(smem);
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ksp = wid % KS, ch = wid / KS;
+  const int nks = K >> 5, ngroups = nks / GU;
+  const int niter = (ngroups + KS - 1) / KS;
+  const int g0 = blockIdx.x * CH + ch;  // this wave's column group (NT tiles)
+
+  const bf16_t* wbase[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) wbase[t] = wp + ((int64_t)(g0 * NT + t) * nks) * 512 + lane * 8;
+  const bf16_t* xl = x + lane * 8;
+
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[mt][t] = (f32x4)(0.f);
+
+  u16x8 st[FH], b0[NT][GU], b1[NT][GU], a[MT][GU];
+#define MP_GRP(it) min((it) * KS + ksp, ngroups - 1)
+#define MP_LDA(it)                                                                                            \
+  _Pragma("unroll") for (int f = 0; f < FH; ++f) st[f] =                                                     \
+      *reinterpret_cast<const u16x8*>(xl + ((int64_t)MP_GRP(it) * F + ch * FH + f) * 512);
+#define MP_LDB(dst, it)                                                                                       \
+  _Pragma("unroll") for (int t = 0; t < NT; ++t) _Pragma("unroll") for (int u = 0; u < GU; ++u) dst[t][u] =    \
+      __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(wbase[t] + (int64_t)(MP_GRP(it) * GU + u) * 512));
+#define MP_STA(buf)                                                                                           \
+  _Pragma("unroll") for (int f = 0; f < FH; ++f) *reinterpret_cast<u16x8*>(                                 \
+      abuf + (((buf) * KS + ksp) * F + ch * FH + f) * 512 + lane * 8) = st[f];
+#define MP_RDA(buf)                                                                                           \
+  _Pragma("unroll") for (int mt = 0; mt < MT; ++mt) _Pragma("unroll") for (int u = 0; u < GU; ++u) a[mt][u] =  \
+      *reinterpret_cast<const u16x8*>(abuf + (((buf) * KS + ksp) * F + u * MT + mt) * 512 + lane * 8);
+#define MP_MMA(bb, it)                                                                                        \
+  if ((it) * KS + ksp < ngroups) {                                                                            \
+    _Pragma("unroll") for (int mt = 0; mt < MT; ++mt) _Pragma("unroll") for (int u = 0; u < GU; ++u)          \
+        _Pragma("unroll") for (int t = 0; t < NT; ++t) acc[mt][t] = mfma16(a[mt][u], bb[t][u], acc[mt][t]);  \
+  }
+  MP_LDA(0)
+  MP_LDB(b0, 0)
+  for (int it = 0; it < niter; it += 2) {
+    MP_STA(0)
+    if (it + 1 < niter) {
+      MP_LDA(it + 1)
+      MP_LDB(b1, it + 1)
+    }
+    lds_barrier();
+    MP_RDA(0)
+    MP_MMA(b0, it)
+    if (it + 1 >= niter) break;
+    MP_STA(1)
+    if (it + 2 < niter) {
+      MP_LDA(it + 2)
+      MP_LDB(b0, it + 2)
+    }
+    lds_barrier();
+    MP_RDA(1)
+    MP_MMA(b1, it + 1)
+  }
+#undef MP_GRP
+#undef MP_LDA
+#undef MP_LDB
+#undef MP_STA
+#undef MP_RDA
+#undef MP_MMA
+  lds_barrier();  // every wave is done reading A before the reduction buffer aliases it
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) red[((ksp * CH + ch) * Q + mt * NT + t) * 64 + lane] = acc[mt][t];
+  lds_barrier();
+  for (int i = wid; i < CH * Q; i += 8) {
+    const int chh = i / Q, qd = i % Q;
+    if (EPI == 1 && (qd % NT) & 1) continue;  // up tile: consumed with its gate tile
+    f32x4 v = (f32x4)(0.f), up = (f32x4)(0.f);
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+      v += red[((k * CH + chh) * Q + qd) * 64 + lane];
+      if (EPI == 1) up += red[((k * CH + chh) * Q + qd + 1) * 64 + lane];
+    }
+    sk_epilogue<MT, NT, EPI, OPK>(qd, blockIdx.x * CH + chh, v, up, y, ys, res, rs, M, lane);
+  }
+}
+
+template <int MT, int NT, int CH>
+static int launch_gemm_lds_cfg(const void* x, const void* w, void* y, int64_t ys, const void* res, int64_t rs, int M,
+                               int N, int K, int epi, int flags, hipStream_t stream) {
+  if constexpr ((2 * MT) % CH != 0) {
+    return 1;  // the A group does not split evenly over the column waves
+  } else {
+    const int ntiles = N / 16;
+    const bool opk = flags & 2;
+    if (ntiles % (CH * NT) || K % 64) return 1;
+    if (opk && epi != 1) return -3;
+    const dim3 grid(ntiles / (CH * NT));
+#define MP_LL(EPI_, OPK_)                                                                                      \
+  hipLaunchKernelGGL((gemm_lds_kernel<MT, NT, CH, EPI_, OPK_>), grid, dim3(512), 0, stream, (const bf16_t*)x,   \
+                     (const bf16_t*)w, (bf16_t*)y, ys, (const bf16_t*)res, rs, M, N, K)
+    if (epi == 1) {
+      if constexpr (NT % 2 == 0) {  // gate/up tile pairs must sit in one wave
+        if (opk) { MP_LL(1, true); } else { MP_LL(1, false); }
+      } else {
+        return 1;
+      }
+    } else if (epi == 2) {
+      MP_LL(2, false);
+    } else {
+      MP_LL(0, false);
+    }
+#undef MP_LL
+    return 0;
+  }
+}
+
+// flags bits 5-6 pick (NT, CH): 0 = (2, 2), 1 = (2, 4), 2 = (1, 4), 3 = (4, 2)
+template <int MT>
+static int launch_gemm_lds(const void* x, const void* w, void* y, int64_t ys, const void* res, int64_t rs, int M,
+                           int N, int K, int epi, int flags, hipStream_t stream) {
+  switch ((flags >> 5) & 3) {
+    case 1: return launch_gemm_lds_cfg<MT, 2, 4>(x, w, y, ys, res, rs, M, N, K, epi, flags, stream);
+    case 2: return launch_gemm_lds_cfg<MT, 1, 4>(x, w, y, ys, res, rs, M, N, K, epi, flags, stream);
+    case 3: return launch_gemm_lds_cfg<MT, 4, 2>(x, w, y, ys, res, rs, M, N, K, epi, flags, stream);
+    default: return launch_gemm_lds_cfg<MT, 2, 2>(x, w, y, ys, res, rs, M, N, K, epi, flags, stream);
+  }
+}
+
 template <int MT, int NT, int D, int EPI, bool OPK>
 __global__ __launch_bounds__(512) void gemm_sk_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ wp,
                                                       bf16_t* __restrict__ y, int64_t ys, const bf16_t* __restrict__ res,
@@ -510,7 +660,8 @@ extern "C" int64_t mp_gemm_workspace_bytes() {
 
 // flags: bit 0 = x is packed (Ap[K/32][ceil(M/16)][64][8]); bit 1 = SwiGLU output packed;
 //        bit 2 = use the stream-K kernel (needs ws: mp_gemm_workspace_bytes(), zero-initialised,
-//        used by one stream at a time); bit 3 = force the one-group-per-workgroup kernel.
+//        used by one stream at a time); bit 3 = force the one-group-per-workgroup kernel;
+//        bit 4 = shared-A (LDS-staged activation) kernel when the shape allows it.
 extern "C" int mp_gemm_bf16(const void* x, int64_t x_stride, const void* w, void* y, int64_t y_stride,
                             const void* res, int64_t res_stride, int M, int N, int K, int epilogue, int flags,
                             void* ws, hipStream_t stream) {
@@ -518,6 +669,14 @@ extern "C" int mp_gemm_bf16(const void* x, int64_t x_stride, const void* w, void
   if (M == 0) return 0;
   if (M > 64 || K % (32 * GU_MAX) || N % 16 || ((flags & 1) == 0 && x_stride % 8)) return -1;
   int rc;
+  if ((flags & 1) && (flags & 16) && !(flags & 8)) {  // shared-A kernel
+    if (M <= 16) rc = launch_gemm_lds<1>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, stream);
+    else if (M <= 32) rc = launch_gemm_lds<2>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, stream);
+    else if (M <= 48) rc = launch_gemm_lds<3>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, stream);
+    else rc = launch_gemm_lds<4>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, stream);
+    if (rc < 0) return rc;
+    if (rc == 0) return (int)hipGetLastError();
+  }
   if ((flags & 1) && (flags & 4) && !(flags & 8) && ws != nullptr) {
     if (M <= 16) rc = launch_gemm_sk<1>(x, y, y_stride, w, res, res_stride, M, N, K, epilogue, flags, ws, stream);
     else if (M <= 32) rc = launch_gemm_sk<2>(x, y, y_stride, w, res, res_stride, M, N, K, epilogue, flags, ws, stream);

@@ -41,6 +41,15 @@ class ModelConfig:
     bos_token_id: int = 1
     eos_token_id: int = 2
     name: str = "custom"
+    # Mixtral sparse MoE MLP (HF MixtralSparseMoeBlock): E experts, top-k softmax routing
+    num_local_experts: int = 0
+    num_experts_per_tok: int = 2
+    # Mistral / Mixtral sliding-window attention (None = full causal attention)
+    sliding_window: Optional[int] = None
+
+    @property
+    def is_moe(self) -> bool:
+        return self.num_local_experts > 0
 
     @property
     def kv_dim(self) -> int:
@@ -60,7 +69,8 @@ class ModelConfig:
         if self.model_type == "gpt2":
             n = 4 * H * H + 2 * H * F + 9 * H + F
         else:
-            n = H * (self.q_dim + 2 * self.kv_dim) + self.q_dim * H + 3 * H * F + 2 * H
+            mlp = self.num_local_experts * (3 * H * F + H) if self.is_moe else 3 * H * F
+            n = H * (self.q_dim + 2 * self.kv_dim) + self.q_dim * H + mlp + 2 * H
         return int(n * bytes_per_param)
 
     def kv_bytes_per_token_per_layer(self, bytes_per_elt: int = 2) -> int:
@@ -73,6 +83,8 @@ class ModelConfig:
             raise ValueError("num_attention_heads must be a multiple of num_key_value_heads")
         if self.head_dim % 8:
             raise ValueError("head_dim must be a multiple of 8")
+        if self.is_moe and not (1 <= self.num_experts_per_tok <= self.num_local_experts <= 64):
+            raise ValueError("MoE needs 1 <= num_experts_per_tok <= num_local_experts <= 64")
 
     def to_dict(self) -> dict:
         return dataclasses.asdict(self)
@@ -95,14 +107,21 @@ class ModelConfig:
         eos = d.get("eos_token_id", 2)
         if isinstance(eos, list):
             eos = eos[0]
+        # transformers >= 5 nests rope settings under ``rope_parameters``
+        rp = d.get("rope_parameters") or {}
+        theta = d.get("rope_theta") or rp.get("rope_theta", 10000.0)
+        scaling = d.get("rope_scaling") or (rp if rp.get("rope_type", "default") != "default" else None)
         return cls(model_type=mt, vocab_size=d["vocab_size"], hidden_size=H,
                    intermediate_size=d["intermediate_size"], num_hidden_layers=d["num_hidden_layers"],
                    num_attention_heads=nh, num_key_value_heads=d.get("num_key_value_heads", nh),
-                   head_dim=d.get("head_dim", H // nh), rms_norm_eps=d.get("rms_norm_eps", 1e-5),
-                   rope_theta=d.get("rope_theta", 10000.0), rope_scaling=d.get("rope_scaling"),
+                   head_dim=d.get("head_dim") or H // nh, rms_norm_eps=d.get("rms_norm_eps", 1e-5),
+                   rope_theta=theta, rope_scaling=scaling,
                    max_position_embeddings=d.get("max_position_embeddings", 4096),
                    tie_word_embeddings=d.get("tie_word_embeddings", False),
-                   bos_token_id=d.get("bos_token_id", 1) or 1, eos_token_id=eos, name=name)
+                   bos_token_id=d.get("bos_token_id", 1) or 1, eos_token_id=eos, name=name,
+                   num_local_experts=int(d.get("num_local_experts", 0) or 0) if mt == "mixtral" else 0,
+                   num_experts_per_tok=int(d.get("num_experts_per_tok", 2) or 2),
+                   sliding_window=d.get("sliding_window"))
 
 
 PRESETS = {
@@ -118,7 +137,16 @@ PRESETS = {
                         num_hidden_layers=12, num_attention_heads=12, num_key_value_heads=12, head_dim=64,
                         max_position_embeddings=1024, tie_word_embeddings=True, bos_token_id=50256,
                         eos_token_id=50256, name="gpt2"),
+    "mistral-7b": ModelConfig(model_type="mistral", intermediate_size=14336, num_key_value_heads=8,
+                              max_position_embeddings=32768, sliding_window=4096, name="mistral-7b"),
+    "mixtral-8x7b": ModelConfig(model_type="mixtral", intermediate_size=14336, num_key_value_heads=8,
+                                rope_theta=1e6, max_position_embeddings=32768, num_local_experts=8,
+                                num_experts_per_tok=2, name="mixtral-8x7b"),
     # small models for tests / CPU plumbing
+    "tiny-mixtral": ModelConfig(model_type="mixtral", vocab_size=512, hidden_size=256, intermediate_size=256,
+                                num_hidden_layers=4, num_attention_heads=4, num_key_value_heads=2, head_dim=64,
+                                max_position_embeddings=1024, num_local_experts=4, num_experts_per_tok=2,
+                                name="tiny-mixtral"),
     "tiny-llama": ModelConfig(vocab_size=512, hidden_size=256, intermediate_size=512, num_hidden_layers=4,
                               num_attention_heads=4, num_key_value_heads=2, head_dim=64,
                               max_position_embeddings=1024, name="tiny-llama"),
@@ -141,6 +169,8 @@ _ALIASES = {
     "llama-3-70b": "llama3-70b",
     "llama-3.1-70b": "llama3-70b",
     "llama3-70b": "llama3-70b",
+    "mixtral-8x7b": "mixtral-8x7b",
+    "mistral-7b": "mistral-7b",
 }
 
 

@@ -12,6 +12,7 @@ from typing import List, Optional
 import torch
 import torch.nn.functional as F
 
+from ..ops.moe import moe_mlp_torch
 from ..ops.reference import rope_cos_sin
 from .weights import StageWeights, split_gate_up
 
@@ -51,6 +52,10 @@ def llama_forward(weights: List[StageWeights], ids: torch.Tensor, return_hidden:
             a = torch.einsum("hqk,khd->qhd", p, v).reshape(L, nh * D)
             x = x + a @ lay.o.float().t()
             h = _rms(x, lay.post_norm.float(), cfg.rms_norm_eps)
+            if lay.router is not None:
+                x = x + moe_mlp_torch(h, lay.router.float(), lay.gate_up.float(), lay.down.float(),
+                                      cfg.num_experts_per_tok)
+                continue
             g, u = split_gate_up(lay.gate_up.float())
             x = x + (F.silu(h @ g.t()) * (h @ u.t())) @ lay.down.float().t()
     if return_hidden:

@@ -66,8 +66,16 @@ class LlamaLayer:
     gate_up_s: Optional[torch.Tensor] = None
     down_q: Optional[torch.Tensor] = None
     down_s: Optional[torch.Tensor] = None
+    # Mixtral sparse-MoE block (HF MixtralSparseMoeBlock): ``router`` [E, H]; gate_up / down
+    # (and their packed copies) are then stacked per expert: [E, 2F, H] / [E, H, F]
+    router: Optional[torch.Tensor] = None
+    router_p: Optional[torch.Tensor] = None  # router padded to 16 rows, packed (decode GEMM)
 
     PROJ = ("qkv", "o", "gate_up", "down")
+
+    @property
+    def moe(self) -> bool:
+        return self.router is not None
 
     @property
     def fp8(self) -> bool:
@@ -138,8 +146,14 @@ class StageWeights:
             if isinstance(lay, LlamaLayer) and lay.qkv_p is None and lay.qkv is not None:
                 lay.qkv_p = ops.pack_weight(lay.qkv)
                 lay.o_p = ops.pack_weight(lay.o)
-                lay.gate_up_p = ops.pack_weight(lay.gate_up)
-                lay.down_p = ops.pack_weight(lay.down)
+                if lay.moe:
+                    lay.gate_up_p = torch.stack([ops.pack_weight(w) for w in lay.gate_up])
+                    lay.down_p = torch.stack([ops.pack_weight(w) for w in lay.down])
+                    E, H = lay.router.shape
+                    lay.router_p = ops.pack_weight(torch.cat([lay.router, lay.router.new_zeros((-E) % 16, H)]))
+                else:
+                    lay.gate_up_p = ops.pack_weight(lay.gate_up)
+                    lay.down_p = ops.pack_weight(lay.down)
         if self.lm_head is not None and self.lm_head_p is None and self.cfg.model_type != "gpt2":
             V, H = self.lm_head.shape
             if H % 32 == 0:
@@ -156,6 +170,8 @@ class StageWeights:
         """
         from .. import ops
 
+        if self.cfg.is_moe:
+            raise ValueError("fp8 W8A8 weights are not supported for MoE (Mixtral) models")
         for lay in self.layers:
             if not isinstance(lay, LlamaLayer) or lay.fp8:
                 continue
@@ -202,10 +218,19 @@ def _random_llama_layer(cfg: ModelConfig, idx: int, device, dtype, seed: int) ->
     H, F = cfg.hidden_size, cfg.intermediate_size
     qkv = _randn((cfg.q_dim + 2 * cfg.kv_dim, H), g, device, dtype)
     o = _randn((H, cfg.q_dim), g, device, dtype)
+    ones = torch.ones(H, dtype=dtype, device=device)
+    if cfg.is_moe:
+        E = cfg.num_local_experts
+        router = _randn((E, H), g, device, dtype)
+        gu = torch.empty((E, 2 * F, H), dtype=dtype, device=device)
+        dn = torch.empty((E, H, F), dtype=dtype, device=device)
+        for e in range(E):
+            gu[e] = interleave_gate_up(_randn((F, H), g, device, dtype), _randn((F, H), g, device, dtype))
+            dn[e] = _randn((H, F), g, device, dtype)
+        return LlamaLayer(ones, qkv, o, ones.clone(), gu, dn, router=router)
     gate = _randn((F, H), g, device, dtype)
     up = _randn((F, H), g, device, dtype)
     down = _randn((H, F), g, device, dtype)
-    ones = torch.ones(H, dtype=dtype, device=device)
     return LlamaLayer(ones, qkv, o, ones.clone(), interleave_gate_up(gate, up), down)
 
 
@@ -320,6 +345,15 @@ def load_stage_weights(cfg: ModelConfig, path: str, start: int, end: int, *, has
         p = f"model.layers.{i}."
         qkv = torch.cat([t(p + "self_attn.q_proj.weight"), t(p + "self_attn.k_proj.weight"),
                          t(p + "self_attn.v_proj.weight")], 0).contiguous()
+        if cfg.is_moe:  # HF MixtralSparseMoeBlock: gate = router, experts.j.{w1 gate, w3 up, w2 down}
+            m = p + "block_sparse_moe."
+            E = cfg.num_local_experts
+            gu = torch.stack([interleave_gate_up(t(f"{m}experts.{j}.w1.weight"), t(f"{m}experts.{j}.w3.weight"))
+                              for j in range(E)])
+            dn = torch.stack([t(f"{m}experts.{j}.w2.weight") for j in range(E)])
+            layers.append(LlamaLayer(t(p + "input_layernorm.weight"), qkv, t(p + "self_attn.o_proj.weight"),
+                                     t(p + "post_attention_layernorm.weight"), gu, dn, router=t(m + "gate.weight")))
+            continue
         gu = interleave_gate_up(t(p + "mlp.gate_proj.weight"), t(p + "mlp.up_proj.weight")).contiguous()
         layers.append(LlamaLayer(t(p + "input_layernorm.weight"), qkv, t(p + "self_attn.o_proj.weight"),
                                  t(p + "post_attention_layernorm.weight"), gu, t(p + "mlp.down_proj.weight")))

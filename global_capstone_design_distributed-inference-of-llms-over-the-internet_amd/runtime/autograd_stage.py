@@ -28,6 +28,7 @@ import torch
 import torch.nn.functional as F
 
 from ..models.weights import split_gate_up
+from ..ops.moe import moe_mlp_torch
 from ..ops.reference import rope_cos_sin
 
 
@@ -80,6 +81,8 @@ class AutogradStage:
 
         x = x + self._attn(rot(q), rot(k), v) @ lay.o.t()
         h = _rms(x, lay.post_norm, cfg.rms_norm_eps)
+        if lay.router is not None:
+            return x + moe_mlp_torch(h, lay.router, lay.gate_up, lay.down, cfg.num_experts_per_tok)
         if i not in self._cache:
             self._cache[i] = split_gate_up(lay.gate_up)
         g, u = self._cache[i]

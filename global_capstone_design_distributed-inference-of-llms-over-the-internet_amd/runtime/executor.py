@@ -29,6 +29,7 @@ import numpy as np
 import torch
 
 from .. import native, ops
+from ..ops import moe
 from ..models.config import ModelConfig
 from ..models.weights import StageWeights
 from .kv_cache import PagedKVCache
@@ -37,8 +38,8 @@ from .session import SessionManager, SessionState
 logger = logging.getLogger(__name__)
 
 # per-path weight tensors a layer loop reads (what CPU offload streams)
-_PACKED_FIELDS = ("input_norm", "post_norm", "qkv_p", "o_p", "gate_up_p", "down_p")
-_DENSE_FIELDS = ("input_norm", "post_norm", "qkv", "o", "gate_up", "down")
+_PACKED_FIELDS = ("input_norm", "post_norm", "qkv_p", "o_p", "gate_up_p", "down_p", "router_p")
+_DENSE_FIELDS = ("input_norm", "post_norm", "qkv", "o", "gate_up", "down", "router")
 _GPT2_FIELDS = ("ln1_w", "ln1_b", "attn_w", "attn_b", "proj_w", "proj_b", "ln2_w", "ln2_b", "fc_w", "fc_b",
                 "fc2_w", "fc2_b")
 
@@ -120,6 +121,11 @@ class StageExecutor:
         self.nh, self.nkv, self.D = cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim
         self.scale = 1.0 / math.sqrt(self.D)
         self.max_seq_len = int(max_seq_len or cfg.max_position_embeddings)
+        if cfg.sliding_window and self.max_seq_len > cfg.sliding_window:
+            # Mistral / Mixtral sliding-window attention: sessions are capped at the window, inside
+            # which sliding-window and full causal attention are the same computation
+            logger.info(f"max_seq_len capped at sliding_window={cfg.sliding_window}")
+            self.max_seq_len = int(cfg.sliding_window)
         self.max_tokens = max_tokens_per_step
         if cfg.model_type != "gpt2":
             self.cos, self.sin = ops.rope_cos_sin(self.D, self.max_seq_len, cfg.rope_theta, self.device,
@@ -155,6 +161,8 @@ class StageExecutor:
                     H, F = cfg.hidden_size, cfg.intermediate_size
                     shapes = [] if (weights.fp8 or not weights.layers) else \
                         [(cfg.q_dim + 2 * cfg.kv_dim, H, 0), (H, cfg.q_dim, 0), (2 * F, H, 1), (H, F, 0)]
+                    if cfg.is_moe and shapes:
+                        shapes.append((16 * ((cfg.num_local_experts + 15) // 16), H, 0))  # router
                     if weights.lm_head_p is not None:
                         shapes.append((16 * weights.lm_head_p.shape[0], H, 0))
                     ops.autotune_gemm(shapes, self.device)
@@ -420,6 +428,9 @@ class StageExecutor:
                 self._attend(qkv, kc, vc, q_seq, q_ctx, attn, ws, ps, np_, True, qblocks, max_ctx)
                 ops.linear(attn, L.o, out=o, wp=L.o_p, a_rows=T)
                 ops.rmsnorm(o, L.post_norm, eps, out=xn, residual=res, mode=1, packed=True)
+                if L.moe:
+                    self._moe_mlp(L, xn, T, mlp, act, e, packed=True)
+                    continue
                 ops.linear(xn, L.gate_up, out=act, epilogue=1, wp=L.gate_up_p, a_rows=T, out_packed=True)
                 ops.linear(act, L.down, out=mlp, wp=L.down_p, a_rows=T)
         else:
@@ -441,6 +452,9 @@ class StageExecutor:
                 self._attend(qkv, kc, vc, q_seq, q_ctx, attn, ws, ps, np_, False, qblocks, max_ctx)
                 ops.linear(attn, L.dense("o"), out=o, wp=L.o_p)
                 ops.rmsnorm(o, L.post_norm, eps, out=xn, residual=res, mode=1)
+                if L.moe:
+                    self._moe_mlp(L, xn, T, mlp, act, e, packed=False)
+                    continue
                 ops.linear(xn, L.dense("gate_up"), out=act, epilogue=1, wp=L.gate_up_p)
                 ops.linear(act, L.dense("down"), out=mlp, wp=L.down_p)
         hout = ops.add(res, mlp, out=e("hout", (T, H)))
@@ -456,6 +470,53 @@ class StageExecutor:
             return logits[:, :V]
         fn = ops.rmsnorm(hout, w.final_norm, eps, out=e("fn", (S, H)), rows=last_rows)
         return ops.linear(fn, w.lm_head, out=e("logits", (S, V)))
+
+    def _moe_mlp(self, L, xn, T, mlp, act, e, packed: bool) -> None:
+        """Mixtral sparse-MoE MLP into ``mlp`` (ops/moe.py has the routing math and the
+        decode-vs-prefill strategy).  Decode steps run every expert on the whole batch with a
+        dense combine matrix: no host sync, so the step stays graph-capturable."""
+        cfg = self.cfg
+        E, k, H = cfg.num_local_experts, cfg.num_experts_per_tok, cfg.hidden_size
+        if packed:
+            logits = ops.linear(xn, None, out=e("moe_logits", (T, 16 * L.router_p.shape[0])), wp=L.router_p,
+                                a_rows=T)[:, :E]
+        else:
+            logits = ops.linear(xn, L.router)
+        w, idx = moe.route(logits, k)
+        acc = e("moe_acc", (T, H), torch.float32)
+        acc.zero_()
+        gp = (lambda j: L.gate_up_p[j]) if L.gate_up_p is not None else (lambda j: None)  # noqa: E731
+        dp = (lambda j: L.down_p[j]) if L.down_p is not None else (lambda j: None)  # noqa: E731
+        capturing = self.device.type == "cuda" and torch.cuda.is_current_stream_capturing()
+        if packed or T <= 64 or capturing:
+            wd = moe.dense_weights(w, idx, E, out=e("moe_w", (T, E), torch.float32))
+            y = e("moe_y", (T, H))
+            for j in range(E):
+                if packed:
+                    ops.linear(xn, L.gate_up[j], out=act, epilogue=1, wp=gp(j), a_rows=T, out_packed=True)
+                    ops.linear(act, L.down[j], out=y, wp=dp(j), a_rows=T)
+                else:
+                    ops.linear(xn, L.gate_up[j], out=act, epilogue=1, wp=gp(j))
+                    ops.linear(act, L.down[j], out=y, wp=dp(j))
+                acc.addcmul_(y, wd[:, j:j + 1])
+        else:
+            # prefill: group the T*k (token, expert) pairs by expert (one host sync per layer)
+            flat = idx.reshape(-1)
+            order = torch.argsort(flat, stable=True)
+            counts = torch.bincount(flat, minlength=E).tolist()
+            tok = order // k
+            wsel = w.reshape(-1)[order]
+            off = 0
+            for j, c in enumerate(counts):
+                if c == 0:
+                    continue
+                rows = tok[off:off + c]
+                xe = xn.index_select(0, rows)
+                a = ops.linear(xe, L.gate_up[j], epilogue=1, wp=gp(j))
+                ye = ops.linear(a, L.down[j], wp=dp(j))
+                acc.index_add_(0, rows, ye.float() * wsel[off:off + c].unsqueeze(1))
+                off += c
+        mlp.copy_(acc)
 
     def _iter_layers(self, fields):
         """``(index, layer)`` over this stage's blocks; with CPU offload the streamed layers come

@@ -60,6 +60,8 @@ def main(argv=None):
     ap.add_argument("--repetition-penalty", type=float, default=1.5)
     ap.add_argument("--gemm", default=os.environ.get("MPAMD_GEMM", "auto"), choices=["auto", "native", "hipblaslt"])
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--tp", type=int, default=1,
+                    help="tensor-parallel degree inside each stage (RCCL all-reduce after o / down)")
     ap.add_argument("--fp8", action="store_true", help="fp8 (OCP e4m3) W8A8 projections (the 70B config)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--device", default=None)
@@ -70,6 +72,7 @@ def main(argv=None):
     from src.models.weights import random_stage_weights
     from src.parallel import dist as pdist
     from src.parallel.pipeline import PipelineEngine, make_replica_groups
+    from src.parallel.tensor_parallel import make_tp_groups, shard_stage_weights
     from src.partition import even_splits, stage_ranges
     from src.runtime.executor import StageExecutor
     from src.runtime.sampler import SamplingParams
@@ -84,8 +87,12 @@ def main(argv=None):
     R = max(1, a.replicas)
     if world % R:
         raise SystemExit(f"--replicas {R} does not divide {world} GPUs")
-    S = world // R
+    TP = max(1, a.tp)
+    if world % (R * TP):
+        raise SystemExit(f"--replicas {R} x --tp {TP} does not divide {world} GPUs")
+    S = world // (R * TP)
     groups = make_replica_groups(world, S)
+    tpg = make_tp_groups(world, S, TP)
     stage = rank % S
     cuts = even_splits(cfg.num_hidden_layers, S)
     start, end = stage_ranges(cuts, cfg.num_hidden_layers)[stage]
@@ -94,20 +101,24 @@ def main(argv=None):
     dtype = torch.bfloat16
     t0 = time.time()
     w = random_stage_weights(cfg, start, end, has_embed=stage == 0, has_head=stage == S - 1, device=device,
-                             dtype=dtype, seed=a.seed, fp8=a.fp8)
+                             dtype=dtype, seed=a.seed, fp8=a.fp8 and TP == 1)
+    if TP > 1:  # shard the stage's blocks over the TP group (fp8: quantize the shard)
+        w = shard_stage_weights(w, (rank // S) % TP, TP)
+        if a.fp8:
+            w.quantize_fp8()
     max_len = a.prompt_len + a.warmup + a.steps + 8
     max_len = 64 * math.ceil(max_len / 64)
     kv_bytes = None if device.type == "cuda" else 256 << 20
     if os.environ.get("MPAMD_KV_GB"):  # cap the KV pool (e.g. several ranks sharing one GPU in a rehearsal)
         kv_bytes = int(float(os.environ["MPAMD_KV_GB"]) * (1 << 30))
-    ex = StageExecutor(cfg, w, device, dtype=dtype, max_sessions=M * B, max_seq_len=max(max_len, 256),
+    ex = StageExecutor(w.cfg, w, device, dtype=dtype, max_sessions=M * B, max_seq_len=max(max_len, 256),
                        kv_cache_bytes=kv_bytes, use_graphs=not a.no_graphs, graph_max_batch=max(B, 1),
-                       max_tokens_per_step=max(B * a.prompt_len, B))
+                       max_tokens_per_step=max(B * a.prompt_len, B), tp=tpg)
     if rank == 0 and device.type == "cuda":
         print("gemm kernel choice:", {f"M{k[0]}:N{k[1]}xK{k[2]}e{k[3]}": v
                                                    for k, v in sorted(ops._SK_CHOICE.items())}, file=sys.stderr)
     sp = SamplingParams(a.temperature, a.top_p, a.top_k, a.repetition_penalty)
-    eng = PipelineEngine(ex, rank, world, sp, n_micro=M, batch=B, seed=a.seed, stages=S, groups=groups)
+    eng = PipelineEngine(ex, rank, world, sp, n_micro=M, batch=B, seed=a.seed, stages=S, groups=groups, tp=TP)
     gen = torch.Generator().manual_seed(1234)
     prompts = [torch.randint(0, cfg.vocab_size, (B, a.prompt_len), generator=gen) for _ in range(M)]
     load_s = time.time() - t0
@@ -165,7 +176,7 @@ def main(argv=None):
                     a.model, a.model),
                 "global_batch": M * B * R,
                 "seq_len": a.prompt_len,
-                "parallelism": f"pp{S}" + (f"xdp{R}" if R > 1 else ""),
+                "parallelism": f"pp{S}" + (f"xtp{TP}" if TP > 1 else "") + (f"xdp{R}" if R > 1 else ""),
                 "micro_batches": M,
                 "sessions_per_micro_batch": B,
                 "splits": cuts,

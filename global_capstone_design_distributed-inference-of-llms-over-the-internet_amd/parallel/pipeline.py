@@ -78,7 +78,9 @@ def make_replica_groups(world: int, stages: int):
 class PipelineEngine:
     def __init__(self, executor: StageExecutor, rank: int, world: int, sampling: SamplingParams,
                  n_micro: int, batch: int, seed: int = 0, send_ring: int = 4, timing: bool = False,
-                 stages: Optional[int] = None, groups=None):
+                 stages: Optional[int] = None, groups=None, tp: int = 1):
+        """``tp`` > 1: consecutive groups of ``tp`` lanes (pipelines) are the tensor-parallel
+        shards of one replica; they sample with the same seeds so their tokens agree."""
         self.ex = executor
         self.rank, self.world = rank, world
         S = int(stages or world)
@@ -92,6 +94,7 @@ class PipelineEngine:
         self.sp = sampling
         self.B, self.M = batch, n_micro
         self.seed = seed
+        self.tp = max(1, int(tp))
         self.first = self.stage == 0
         self.last = self.stage == S - 1
         H = executor.cfg.hidden_size
@@ -148,7 +151,7 @@ class PipelineEngine:
         and the device-side history update (no host round trip, no extra device ops)."""
         B = logits.shape[0]
         seeds = (self._arange[:B] + (self.seed * 1000003 + mb.step * 7919 + mb.index * 104729
-                                     + self.replica * 15485863) * 4096)
+                                     + (self.replica // self.tp) * 15485863) * 4096)
         tok = ops.sample(logits, self._temps[:B], self._topp[:B], self._topk[:B], self._rp[:B], mb.recent,
                          mb.recent_len, seeds, update_history=True)
         mb.step += 1

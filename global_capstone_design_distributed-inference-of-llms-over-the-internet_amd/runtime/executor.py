@@ -108,8 +108,12 @@ class StageExecutor:
                  page_size: int = 64, max_sessions: int = 256, max_seq_len: Optional[int] = None,
                  kv_cache_bytes: Optional[int] = None, kv_fraction: float = 0.9, use_graphs: Optional[bool] = None,
                  graph_max_batch: int = 256, max_tokens_per_step: int = 8192, offload: bool = False,
-                 keep_layers_on_gpu: int = 0):
+                 keep_layers_on_gpu: int = 0, tp=None):
+        """``tp``: a ``parallel.tensor_parallel.TPGroup`` when ``weights`` is a tensor-parallel
+        shard (``cfg`` is then the shard config); partial sums are all-reduced after the
+        o and down projections."""
         cfg.validate()
+        self._tp = tp if (tp is not None and tp.size > 1) else None
         self.cfg = cfg
         self.w = weights
         self.device = torch.device(device)
@@ -140,6 +144,8 @@ class StageExecutor:
         self.use_graphs = (self.device.type == "cuda") if use_graphs is None else bool(use_graphs)
         self.use_graphs = self.use_graphs and self.device.type == "cuda" and cfg.model_type != "gpt2" and \
             os.environ.get("MPAMD_GRAPHS", "1") != "0"
+        if self._tp is not None and os.environ.get("MPAMD_TP_GRAPHS", "0") != "1":
+            self.use_graphs = False  # RCCL all-reduce capture is opt-in until validated on a multi-GPU node
         self.graph_max_batch = graph_max_batch
         self._graphs: Dict[Tuple[int, int, int], "_DecodeGraph"] = {}
         self._graph_pool = None
@@ -406,11 +412,13 @@ class StageExecutor:
                 self._attend(qkv, kc, vc, q_seq, q_ctx, attn, ws, ps, np_, True, qblocks, max_ctx)
                 ops.quant_act_fp8(attn, T, cfg.q_dim, out=a8, scale=asc)
                 ops.linear_fp8(a8, asc, L.o_q, L.o_s, T, out=o)
+                self._ar(o)
                 ops.rmsnorm(o, L.post_norm, eps, out=xn, residual=res, mode=1, packed=True)
                 ops.quant_act_fp8(xn, T, H, out=a8, scale=asc)
                 ops.linear_fp8(a8, asc, L.gate_up_q, L.gate_up_s, T, out=act, epilogue=1, out_packed=True)
                 ops.quant_act_fp8(act, T, F, out=a8, scale=asc)
                 ops.linear_fp8(a8, asc, L.down_q, L.down_s, T, out=mlp)
+                self._ar(mlp)
         elif prompt is None and self._packed_ok(T):
             # decode path: activations feeding a GEMM stay in the packed MFMA-fragment layout
             pk = ops.packed_numel
@@ -427,12 +435,14 @@ class StageExecutor:
                 ops.rope_kv_write(qkv, positions, self.cos, self.sin, kc, vc, slots, self.nh, self.nkv)
                 self._attend(qkv, kc, vc, q_seq, q_ctx, attn, ws, ps, np_, True, qblocks, max_ctx)
                 ops.linear(attn, L.o, out=o, wp=L.o_p, a_rows=T)
+                self._ar(o)
                 ops.rmsnorm(o, L.post_norm, eps, out=xn, residual=res, mode=1, packed=True)
                 if L.moe:
                     self._moe_mlp(L, xn, T, mlp, act, e, packed=True)
                     continue
                 ops.linear(xn, L.gate_up, out=act, epilogue=1, wp=L.gate_up_p, a_rows=T, out_packed=True)
                 ops.linear(act, L.down, out=mlp, wp=L.down_p, a_rows=T)
+                self._ar(mlp)
         else:
             xn = e("xn", (T, H))
             attn = e("attn", (T, cfg.q_dim))
@@ -451,12 +461,14 @@ class StageExecutor:
                 ops.rope_kv_write(qkv, positions, self.cos, self.sin, kc, vc, slots, self.nh, self.nkv)
                 self._attend(qkv, kc, vc, q_seq, q_ctx, attn, ws, ps, np_, False, qblocks, max_ctx)
                 ops.linear(attn, L.dense("o"), out=o, wp=L.o_p)
+                self._ar(o)
                 ops.rmsnorm(o, L.post_norm, eps, out=xn, residual=res, mode=1)
                 if L.moe:
                     self._moe_mlp(L, xn, T, mlp, act, e, packed=False)
                     continue
                 ops.linear(xn, L.dense("gate_up"), out=act, epilogue=1, wp=L.gate_up_p)
                 ops.linear(act, L.dense("down"), out=mlp, wp=L.down_p)
+                self._ar(mlp)
         hout = ops.add(res, mlp, out=e("hout", (T, H)))
         if not self.is_last:
             return hout
@@ -517,6 +529,12 @@ class StageExecutor:
                 acc.index_add_(0, rows, ye.float() * wsel[off:off + c].unsqueeze(1))
                 off += c
         mlp.copy_(acc)
+        self._ar(mlp)
+
+    def _ar(self, t: torch.Tensor) -> None:
+        """Tensor parallelism: sum the row-parallel partial results over the TP group."""
+        if self._tp is not None:
+            self._tp.all_reduce(t)
 
     def _iter_layers(self, fields):
         """``(index, layer)`` over this stage's blocks; with CPU offload the streamed layers come

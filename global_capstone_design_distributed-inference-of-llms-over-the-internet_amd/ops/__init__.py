@@ -431,7 +431,8 @@ def unpack_weight(wp: torch.Tensor) -> torch.Tensor:
     return wp.view(nt, ks, 4, 16, 8).permute(0, 3, 1, 2, 4).reshape(nt * 16, ks * 32)
 
 
-def linear(x, w, out=None, epilogue=0, residual=None, policy=None, wp=None, a_rows=None, out_packed=False):
+def linear(x, w, out=None, epilogue=0, residual=None, policy=None, wp=None, a_rows=None, out_packed=False,
+           gate=None):
     """y = epilogue(x @ w^T). epilogue 0: none; 1: SwiGLU (16-row interleaved gate/up w); 2: + residual.
 
     ``wp`` is the packed copy of ``w`` (``pack_weight``); the native decode GEMM needs it.
@@ -461,10 +462,10 @@ def linear(x, w, out=None, epilogue=0, residual=None, policy=None, wp=None, a_ro
         if out is None:
             out = (torch.empty(packed_numel(M, ncols), dtype=x.dtype, device=x.device) if out_packed
                    else torch.empty(M, ncols, dtype=x.dtype, device=x.device))
-        kern = _kernel_for(M, N, K, epilogue)
+        kern = "pk" if gate is not None else _kernel_for(M, N, K, epilogue)
         flags = 1 | (2 if out_packed else 0) | _KERNEL_FLAGS[kern]
         ws = gemm_workspace(x.device) if kern == "sk" else None
-        torch.ops.mpamd.gemm(x, wp, out, residual, int(epilogue), M, flags, ws)
+        torch.ops.mpamd.gemm(x, wp, out, residual, int(epilogue), M, flags, ws, gate)
         return out
     if a_rows is not None or out_packed:
         raise RuntimeError(f"packed activations need the native decode GEMM (M={M}, N={N}, K={K})")

@@ -38,7 +38,7 @@ int mp_quant_act_fp8(const void* ap, void* a8, float* scale, float* part, int M,
 int mp_gemm_fp8(const void* a8, const float* as, const void* wq, const float* ws, void* y, int64_t ys, const void* res,
                 int64_t rs, int M, int N, int K, int epilogue, int out_packed, hipStream_t stream);
 int mp_gemm_bf16(const void* x, int64_t x_stride, const void* w, void* y, int64_t y_stride, const void* res,
-                 int64_t res_stride, int M, int N, int K, int epilogue, int flags, void* ws,
+                 int64_t res_stride, int M, int N, int K, int epilogue, int flags, void* ws, const int* gate,
                  hipStream_t stream);
 int mp_pack_act(const void* x, int64_t xs, void* ap, int M, int K, hipStream_t stream);
 int mp_pack_weight(const void* w, void* wp, int N, int K, hipStream_t stream);
@@ -275,7 +275,8 @@ void sample(const at::Tensor& logits, const at::Tensor& temps, const at::Tensor&
 
 // flags bit 0: x is packed (holds ceil(M/16)*16*K elements, M given); bit 1: packed SwiGLU output
 void gemm(const at::Tensor& x, const at::Tensor& wp, at::Tensor& y, const c10::optional<at::Tensor>& residual,
-          int64_t epilogue, int64_t M_, int64_t flags, const c10::optional<at::Tensor>& workspace) {
+          int64_t epilogue, int64_t M_, int64_t flags, const c10::optional<at::Tensor>& workspace,
+          const c10::optional<at::Tensor>& gate) {
   check_bf16_cuda(x, "x");
   check_bf16_cuda(wp, "wp");
   check_bf16_cuda(y, "y");
@@ -317,8 +318,13 @@ void gemm(const at::Tensor& x, const at::Tensor& wp, at::Tensor& y, const c10::o
              "gemm workspace too small (ops.gemm_workspace)");
     ws = workspace->data_ptr();
   }
+  const int* gp = nullptr;
+  if (gate.has_value()) {  // MoE expert gate: one int32 on the device (0 -> the GEMM is skipped)
+    MP_CHECK(gate->is_cuda() && gate->scalar_type() == at::kInt && gate->numel() == 1, "gate must be one cuda int32");
+    gp = gate->data_ptr<int>();
+  }
   check_launch(mp_gemm_bf16(x.data_ptr(), apk ? 0 : x.stride(0), wp.data_ptr(), y.data_ptr(), opk ? 0 : y.stride(0),
-                            rp, rs, M, N, K, (int)epilogue, (int)flags, ws, cur_stream()),
+                            rp, rs, M, N, K, (int)epilogue, (int)flags, ws, gp, cur_stream()),
                "gemm");
 }
 
@@ -417,7 +423,7 @@ TORCH_LIBRARY(mpamd, m) {
       "Tensor(d!) recent_len, Tensor seeds, Tensor(a!) workspace, Tensor(b!) out, int update=0) -> ()");
   m.def(
       "gemm(Tensor x, Tensor wp, Tensor(a!) y, Tensor? residual, int epilogue, int M, int flags, "
-      "Tensor(b!)? workspace=None) -> ()");
+      "Tensor(b!)? workspace=None, Tensor? gate=None) -> ()");
   m.def("pack_act(Tensor x, Tensor(a!) ap) -> ()");
   m.def("pack_weight(Tensor w) -> Tensor");
   m.def("quant_act_fp8(Tensor ap, Tensor(a!) a8, Tensor(b!) scale, int M, int K) -> ()");

@@ -47,7 +47,12 @@ template <int MT, int NT, int EPI, bool APK, bool OPK>
 __global__ __launch_bounds__(512) void gemm_packed_kernel(const bf16_t* __restrict__ x, int64_t x_stride,
                                                           const bf16_t* __restrict__ wp, bf16_t* __restrict__ y,
                                                           int64_t y_stride, const bf16_t* __restrict__ res,
-                                                          int64_t res_stride, int M, int N, int K) {
+                                                          int64_t res_stride, int M, int N, int K,
+                                                          const int* __restrict__ gate) {
+  // MoE expert gate (ops/moe.py): a device-side count of tokens routed to this expert; 0 ->
+  // the whole grid exits before streaming any weight (output left as is, combine weight 0).
+  // One uniform scalar load per workgroup keeps hipGraph-captured decode steps shape-static.
+  if (gate != nullptr && *gate == 0) return;
   // fewer k-slices per group for the widest tiles keeps A + 2 x B + acc inside 256 VGPRs
   constexpr int GU = (MT * NT >= 6) ? 2 : 4;
   __shared__ __attribute__((aligned(16))) float red[8][MT * NT * 4][64];
@@ -164,14 +169,15 @@ __global__ __launch_bounds__(512) void gemm_packed_kernel(const bf16_t* __restri
 
 template <int MT>
 static int launch_gemm(const void* x, int64_t xs, const void* w, void* y, int64_t ys, const void* res, int64_t rs,
-                       int M, int N, int K, int epi, int flags, hipStream_t stream) {
+                       int M, int N, int K, int epi, int flags, const int* gate, hipStream_t stream) {
   const int ntiles = N / 16;
   // two column tiles per wave when there are enough workgroups to fill the 256 CUs
   const bool two = epi == 1 || (ntiles % 2 == 0 && ntiles / 2 >= 256);
   const bool apk = flags & 1, opk = flags & 2;
 #define MP_LAUNCH(NT_, EPI_, APK_, OPK_)                                                                       \
   hipLaunchKernelGGL((gemm_packed_kernel<MT, NT_, EPI_, APK_, OPK_>), dim3(ntiles / NT_), dim3(512), 0, stream, \
-                     (const bf16_t*)x, xs, (const bf16_t*)w, (bf16_t*)y, ys, (const bf16_t*)res, rs, M, N, K)
+                     (const bf16_t*)x, xs, (const bf16_t*)w, (bf16_t*)y, ys, (const bf16_t*)res, rs, M, N, K, \
+                     gate)
   // Only the packed-activation form is instantiated: row-major callers pack x first
   // (mp_pack_act).  The row-major-A variant miscompiled at MT=1/NT=1 (ROCm 7.2, wrong
   // results with several k-groups per wave) and loses to the packed form anyway.
@@ -664,11 +670,12 @@ extern "C" int64_t mp_gemm_workspace_bytes() {
 //        bit 4 = shared-A (LDS-staged activation) kernel when the shape allows it.
 extern "C" int mp_gemm_bf16(const void* x, int64_t x_stride, const void* w, void* y, int64_t y_stride,
                             const void* res, int64_t res_stride, int M, int N, int K, int epilogue, int flags,
-                            void* ws, hipStream_t stream) {
+                            void* ws, const int* gate, hipStream_t stream) {
   using namespace mp;
   if (M == 0) return 0;
   if (M > 64 || K % (32 * GU_MAX) || N % 16 || ((flags & 1) == 0 && x_stride % 8)) return -1;
   int rc;
+  if (gate != nullptr) flags &= ~(4 | 16);  // gated (MoE expert) GEMMs use the one-group kernel
   if ((flags & 1) && (flags & 16) && !(flags & 8)) {  // shared-A kernel
     if (M <= 16) rc = launch_gemm_lds<1>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, stream);
     else if (M <= 32) rc = launch_gemm_lds<2>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, stream);
@@ -686,10 +693,14 @@ extern "C" int mp_gemm_bf16(const void* x, int64_t x_stride, const void* w, void
     if (rc == 0) return (int)hipGetLastError();
     // rc == 1: shape not covered by the stream-K form -> one-group-per-workgroup kernel
   }
-  if (M <= 16) rc = launch_gemm<1>(x, x_stride, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, stream);
-  else if (M <= 32) rc = launch_gemm<2>(x, x_stride, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, stream);
-  else if (M <= 48) rc = launch_gemm<3>(x, x_stride, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, stream);
-  else rc = launch_gemm<4>(x, x_stride, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, stream);
+  if (M <= 16) rc = launch_gemm<1>(x, x_stride, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, gate,
+                                   stream);
+  else if (M <= 32) rc = launch_gemm<2>(x, x_stride, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, gate,
+                                   stream);
+  else if (M <= 48) rc = launch_gemm<3>(x, x_stride, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, gate,
+                                   stream);
+  else rc = launch_gemm<4>(x, x_stride, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, gate,
+                                   stream);
   if (rc) return rc;
   return (int)hipGetLastError();
 }

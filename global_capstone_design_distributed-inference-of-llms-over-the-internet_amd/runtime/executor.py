@@ -157,6 +157,7 @@ class StageExecutor:
         # GQA decode: the whole group of a kv head in the MFMA rows (2x the VALU kernel at nrep 8)
         self._attn_mfma_gqa = self._attn_mfma_prefill and self.nh // self.nkv >= 4
         self._decode_qb: Dict[int, torch.Tensor] = {}
+        self._moe_y: Dict[int, torch.Tensor] = {}
         self.timing = False
         if self.device.type == "cuda":
             ops.require_native()
@@ -502,11 +503,19 @@ class StageExecutor:
         capturing = self.device.type == "cuda" and torch.cuda.is_current_stream_capturing()
         if packed or T <= 64 or capturing:
             wd = moe.dense_weights(w, idx, E, out=e("moe_w", (T, E), torch.float32))
-            y = e("moe_y", (T, H))
+            # small decode batches leave experts unrouted: their GEMMs are skipped on the device
+            # (gate = routed-token count) so a 1-session step streams ~k/E of the expert bytes.
+            # y persists per T and starts zeroed: a skipped GEMM leaves finite values * weight 0.
+            gated = packed and T * k <= 2 * E
+            cnt = (wd > 0).sum(0, dtype=torch.int32) if gated else None
+            y = self._moe_y.get(T)
+            if y is None:
+                y = self._moe_y[T] = torch.zeros(T, H, dtype=self.dtype, device=self.device)
             for j in range(E):
                 if packed:
-                    ops.linear(xn, L.gate_up[j], out=act, epilogue=1, wp=gp(j), a_rows=T, out_packed=True)
-                    ops.linear(act, L.down[j], out=y, wp=dp(j), a_rows=T)
+                    g = cnt[j:j + 1] if gated else None
+                    ops.linear(xn, L.gate_up[j], out=act, epilogue=1, wp=gp(j), a_rows=T, out_packed=True, gate=g)
+                    ops.linear(act, L.down[j], out=y, wp=dp(j), a_rows=T, gate=g)
                 else:
                     ops.linear(xn, L.gate_up[j], out=act, epilogue=1, wp=gp(j))
                     ops.linear(act, L.down[j], out=y, wp=dp(j))

@@ -96,7 +96,7 @@ int main(int argc, char** argv) {
         const int flags = 1 | (kind == 0 ? 8 : kind == 1 ? 4 : 16 | ((kind - 2) << 5));
         auto run = [&](int i, unsigned short* out) {
           const unsigned short* w = pool + (size_t)(i % copies) * (wbytes / 2);
-          return mp_gemm_bf16(x, s.K, w, out, ncols, nullptr, 0, M, s.N, s.K, s.epi, flags, ws, 0);
+          return mp_gemm_bf16(x, s.K, w, out, ncols, nullptr, 0, M, s.N, s.K, s.epi, flags, ws, nullptr, 0);
         };
         int rc = run(0, kind == 0 ? yref : y);
         if (rc) {

@@ -1,0 +1,5 @@
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests -x -v --timeout 200 --timeout-method thread -m gpu > gpurun_out/pytest_gpu_s6.log 2>&1 && \
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_s6.log 2>&1 && \
+timeout -k 10 300 python -u bench.py > gpurun_out/bench_default_s6.log 2>&1

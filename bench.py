@@ -71,7 +71,7 @@ def main(argv=None):
     from src.models.config import resolve_model
     from src.models.weights import random_stage_weights
     from src.parallel import dist as pdist
-    from src.parallel.pipeline import PipelineEngine, make_replica_groups
+    from src.parallel.pipeline import PipelineEngine, make_replica_groups, make_token_groups
     from src.parallel.tensor_parallel import make_tp_groups, shard_stage_weights
     from src.partition import even_splits, stage_ranges
     from src.runtime.executor import StageExecutor
@@ -92,6 +92,7 @@ def main(argv=None):
         raise SystemExit(f"--replicas {R} x --tp {TP} does not divide {world} GPUs")
     S = world // (R * TP)
     groups = make_replica_groups(world, S)
+    tok_groups = make_token_groups(world, S)  # token return hop on its own communicator
     tpg = make_tp_groups(world, S, TP)
     stage = rank % S
     cuts = even_splits(cfg.num_hidden_layers, S)
@@ -118,7 +119,8 @@ def main(argv=None):
         print("gemm kernel choice:", {f"M{k[0]}:N{k[1]}xK{k[2]}e{k[3]}": v
                                                    for k, v in sorted(ops._SK_CHOICE.items())}, file=sys.stderr)
     sp = SamplingParams(a.temperature, a.top_p, a.top_k, a.repetition_penalty)
-    eng = PipelineEngine(ex, rank, world, sp, n_micro=M, batch=B, seed=a.seed, stages=S, groups=groups, tp=TP)
+    eng = PipelineEngine(ex, rank, world, sp, n_micro=M, batch=B, seed=a.seed, stages=S, groups=groups, tp=TP,
+                         tok_groups=tok_groups)
     gen = torch.Generator().manual_seed(1234)
     prompts = [torch.randint(0, cfg.vocab_size, (B, a.prompt_len), generator=gen) for _ in range(M)]
     load_s = time.time() - t0

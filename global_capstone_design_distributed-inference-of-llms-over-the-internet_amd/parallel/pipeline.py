@@ -23,6 +23,12 @@ direct xGMI link between neighbouring GPUs:
   replicas' hops never share a communicator.  Sessions are assigned to replicas by
   ``assign_sessions`` (throughput-proportional, the load_balancing.py rule re-expressed
   for replicas of a whole pipeline).
+* The token return hop (last stage -> stage 0) runs on its OWN communicator per replica
+  (``make_token_groups``).  RCCL serialises the P2P operations of one communicator on one
+  stream, so with 2 stages the forward hidden send (0 -> 1) and the token receive (1 -> 0)
+  would share a stream: stage 0's send of micro-batch m+1 would sit in front of the receive
+  of token m, and the pipeline would only make progress while RCCL can complete the small
+  token send eagerly.  Two communicators make the two directions independent streams.
 """
 from __future__ import annotations
 
@@ -75,10 +81,18 @@ def make_replica_groups(world: int, stages: int):
     return [dist.new_group(list(range(r * stages, (r + 1) * stages))) for r in range(world // stages)]
 
 
+def make_token_groups(world: int, stages: int):
+    """One extra communicator per replica for the last -> first token hop (see module doc).
+    Collective: every rank calls it, after ``make_replica_groups``, in the same order."""
+    if stages <= 1 or not dist.is_initialized():
+        return None
+    return [dist.new_group(list(range(r * stages, (r + 1) * stages))) for r in range(world // stages)]
+
+
 class PipelineEngine:
     def __init__(self, executor: StageExecutor, rank: int, world: int, sampling: SamplingParams,
                  n_micro: int, batch: int, seed: int = 0, send_ring: int = 4, timing: bool = False,
-                 stages: Optional[int] = None, groups=None, tp: int = 1):
+                 stages: Optional[int] = None, groups=None, tp: int = 1, tok_groups=None):
         """``tp`` > 1: consecutive groups of ``tp`` lanes (pipelines) are the tensor-parallel
         shards of one replica; they sample with the same seeds so their tokens agree."""
         self.ex = executor
@@ -90,6 +104,7 @@ class PipelineEngine:
         self.replica, self.stage = rank // S, rank % S
         self.base = self.replica * S
         self.group = groups[self.replica] if groups else None
+        self.tok_group = tok_groups[self.replica] if tok_groups else self.group
         self.dev = executor.device
         self.sp = sampling
         self.B, self.M = batch, n_micro
@@ -122,7 +137,7 @@ class PipelineEngine:
                 mb.recent_len = torch.zeros(B, dtype=torch.int32, device=dev)
 
     # ------------------------------------------------------------------ comm helpers
-    def _send(self, t: torch.Tensor, dst: int):
+    def _send(self, t: torch.Tensor, dst: int, group=None):
         k = self._ring_k
         self._ring_k = (k + 1) % len(self._ring)
         w = self._ring_work[k]
@@ -133,11 +148,11 @@ class PipelineEngine:
             buf = torch.empty_like(t)
             self._ring[k] = buf
         buf.copy_(t)
-        self._ring_work[k] = dist.isend(buf, dst, group=self.group)
+        self._ring_work[k] = dist.isend(buf, dst, group=group or self.group)
 
-    def _post_recv(self, shape, dtype, src):
+    def _post_recv(self, shape, dtype, src, group=None):
         buf = torch.empty(shape, dtype=dtype, device=self.dev)
-        return dist.irecv(buf, src, group=self.group), buf
+        return dist.irecv(buf, src, group=group or self.group), buf
 
     def _flush_sends(self):
         for i, w in enumerate(self._ring_work):
@@ -208,12 +223,13 @@ class PipelineEngine:
                     if self.record:
                         self.tokens_out[m].append(tok.clone())
                 else:
-                    self._send(tok, self.base)
+                    self._send(tok, self.base, group=self.tok_group)
             else:
                 self._send(out, self.rank + 1)
         if self.first and self.S > 1:
             # receive this round's tokens (posted after all sends of the round, in micro-batch order)
-            self._tok_recv = [self._post_recv((self.B,), torch.long, self.base + self.S - 1) for _ in range(M)]
+            self._tok_recv = [self._post_recv((self.B,), torch.long, self.base + self.S - 1, group=self.tok_group)
+                              for _ in range(M)]
 
     def prefill(self, prompts: Sequence[torch.Tensor]):
         """prompts[m]: int64 [B, L] token ids for micro-batch m (stage 0 only reads them)."""

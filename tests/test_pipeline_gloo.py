@@ -22,7 +22,7 @@ def _worker(rank, world, port, steps, out_q, stages=None):
     from src.models.config import resolve_model
     from src.models.weights import random_stage_weights
     from src.parallel import dist as pdist
-    from src.parallel.pipeline import PipelineEngine, make_replica_groups
+    from src.parallel.pipeline import PipelineEngine, make_replica_groups, make_token_groups
     from src.partition import even_splits, stage_ranges
     from src.runtime.executor import StageExecutor
     from src.runtime.sampler import SamplingParams
@@ -30,6 +30,7 @@ def _worker(rank, world, port, steps, out_q, stages=None):
     rank, world, _, dev = pdist.init_distributed("cpu")
     S = stages or world
     groups = make_replica_groups(world, S)
+    tok_groups = make_token_groups(world, S)
     cfg = resolve_model("tiny-llama")
     st = rank % S
     s, e = stage_ranges(even_splits(cfg.num_hidden_layers, S), cfg.num_hidden_layers)[st]
@@ -38,7 +39,7 @@ def _worker(rank, world, port, steps, out_q, stages=None):
     ex = StageExecutor(cfg, w, "cpu", dtype=torch.float32, kv_cache_bytes=16 << 20, max_sessions=8, max_seq_len=128)
     M, B = 2, 3
     eng = PipelineEngine(ex, rank, world, SamplingParams(0.0, 1.0, 0, 1.0), n_micro=M, batch=B, stages=S,
-                         groups=groups)
+                         groups=groups, tok_groups=tok_groups)
     eng.record = True
     g = torch.Generator().manual_seed(5)
     prompts = [torch.randint(0, cfg.vocab_size, (B, 9), generator=g) for _ in range(M)]

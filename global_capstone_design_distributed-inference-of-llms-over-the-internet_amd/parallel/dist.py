@@ -22,11 +22,8 @@ def init_distributed(device_type: Optional[str] = None, timeout_s: float = 600.0
     if device_type is None:
         device_type = "cuda" if torch.cuda.is_available() else "cpu"
     if device_type == "cuda":
-        # more ranks than visible GPUs (a one-GPU rehearsal of the N-stage path): ranks share
-        # devices round-robin; device_count() does not initialise the GPU
-        idx = local % max(1, torch.cuda.device_count())
-        torch.cuda.set_device(idx)
-        device = torch.device("cuda", idx)
+        torch.cuda.set_device(local)
+        device = torch.device("cuda", local)
     else:
         device = torch.device("cpu")
     if world > 1 and not dist.is_initialized():

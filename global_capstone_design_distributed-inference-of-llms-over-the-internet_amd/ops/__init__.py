@@ -359,6 +359,35 @@ def paged_attention(q, k_cache, v_cache, block_tables, q_seq, q_ctx, nh, nkv, sc
     return out
 
 
+def paged_attention_rope(qkv, k_cache, v_cache, block_tables, q_seq, q_ctx, positions, cos, sin, slots, nh, nkv,
+                         scale, out=None, workspace=None, part_size=None, num_parts=None, max_ctx=None,
+                         packed=False):
+    """Decode step (one query per sequence, q_ctx = position + 1): RoPE of q / new k, the new
+    token's page-slot write and paged attention in ONE kernel (csrc/attention.hip ROPE path).
+    ``qkv`` is the unrotated fused projection and is not modified."""
+    if not _native(qkv):
+        q = qkv.clone()
+        ref.rope_kv_write(q, positions, cos, sin, k_cache, v_cache, slots, nh, nkv)
+        return paged_attention(q, k_cache, v_cache, block_tables, q_seq, q_ctx, nh, nkv, scale, out=out,
+                               workspace=workspace, part_size=part_size, num_parts=num_parts, max_ctx=max_ctx,
+                               packed=packed)
+    T = qkv.shape[0]
+    D = k_cache.shape[-1]
+    if part_size is None:
+        if max_ctx is None:
+            max_ctx = int(q_ctx.max().item()) if T else 1
+        part_size, num_parts = attention_partition(T, nkv, max_ctx)
+    if out is None:
+        out = (torch.empty(packed_numel(T, nh * D), dtype=qkv.dtype, device=qkv.device) if packed
+               else torch.empty(T, nh * D, dtype=qkv.dtype, device=qkv.device))
+    if workspace is None:
+        workspace = attention_workspace(T, nh, D, num_parts, qkv.device)
+    torch.ops.mpamd.paged_attention_rope(qkv, k_cache, v_cache, block_tables, q_seq, q_ctx, positions, cos, sin,
+                                         slots, out, workspace, int(nh), int(nkv), float(scale), int(part_size),
+                                         int(num_parts), int(bool(packed)))
+    return out
+
+
 def embedding(ids, table, out=None):
     if not _native(table):
         return ref.embedding(ids, table, out=out)

@@ -21,6 +21,15 @@
 // decode (one query per sequence), chunked prefill (query i of a chunk sees
 // ctx = start + i + 1 -> causal) and replay.  ctx == 0 rows (batch padding) output 0.
 // packed_mt > 0 writes the output in the packed decode-GEMM activation layout (common.h).
+//
+// ROPE = true (decode only: one query per sequence, its own token is the last of the context):
+// `q` is the UNROTATED fused qkv projection row and the kernel does rope_kv.hip's work itself,
+// removing one launch + one qkv round trip per layer.  Every lane rotates its 8-dim chunk of
+// the query heads and of the new token's k (rotate_half: the partner chunk sits D/2 away,
+// fp32 cos/sin at pos[t], same expression order as rope_kv_kernel), keeps the rotated k and
+// the v chunk in registers and substitutes them for the cache read of token ctx - 1; the
+// first workgroup of the kv head whose context slice holds that token writes them to the
+// page slot (slots[t] < 0: padded row, nothing written) for later steps.
 #include "common.h"
 #include <stdlib.h>
 
@@ -41,13 +50,22 @@ __device__ __forceinline__ float group_sum(float v) {
   return v;
 }
 
-template <int D, int NREP>
+struct RopeFuse {
+  const int64_t* pos;   // [T] rotary positions
+  const float* cos_t;   // [max_pos, D/2]
+  const float* sin_t;
+  const int64_t* slots; // [T] cache slot of the new token (page * page_size + offset)
+  bf16_t* kw;           // the k / v caches, written only at the new token's slot
+  bf16_t* vw;
+};
+
+template <int D, int NREP, bool ROPE>
 __global__ __launch_bounds__(256) void paged_attn_kernel(
     const bf16_t* __restrict__ q, int64_t q_stride, const bf16_t* __restrict__ kc,
     const bf16_t* __restrict__ vc, const int32_t* __restrict__ block_tables, int bt_stride,
     const int32_t* __restrict__ q_seq, const int32_t* __restrict__ q_ctx, bf16_t* __restrict__ out,
     float* __restrict__ part_o, float* __restrict__ part_ml, int nkv, int nh, int page_log2, int PS, int NP,
-    float scale_log2, int packed_mt) {
+    float scale_log2, int packed_mt, RopeFuse rf) {
   constexpr int LPT = D / 8;
   constexpr int TPI = 64 / LPT;
   constexpr int U = 4;
@@ -83,11 +101,54 @@ __global__ __launch_bounds__(256) void paged_attn_kernel(
   const int64_t page_stride = (int64_t)nkv * page_size * D;
 
   float qf[NREP][8];
+  u16x8 kn = (u16x8)(0), vn = (u16x8)(0);  // ROPE: the new token's rotated k / v chunk
+  int tnew = -1;
+  if constexpr (ROPE) {
+    constexpr int HALF = D / 2;
+    const bf16_t* row = q + (int64_t)t * q_stride;
+    const int c0 = (sl * 8) & (HALF - 1);
+    const bool lo = sl * 8 < HALF;
+    const int po = lo ? HALF : -HALF;
+    const int64_t ps_ = rf.pos[t];
+    const f32x4 ca = *reinterpret_cast<const f32x4*>(rf.cos_t + ps_ * HALF + c0);
+    const f32x4 cb = *reinterpret_cast<const f32x4*>(rf.cos_t + ps_ * HALF + c0 + 4);
+    const f32x4 sa = *reinterpret_cast<const f32x4*>(rf.sin_t + ps_ * HALF + c0);
+    const f32x4 sb = *reinterpret_cast<const f32x4*>(rf.sin_t + ps_ * HALF + c0 + 4);
+    auto rot = [&](const bf16_t* hp) {
+      const u16x8 me = *reinterpret_cast<const u16x8*>(hp + sl * 8);
+      const u16x8 ot = *reinterpret_cast<const u16x8*>(hp + sl * 8 + po);
+      u16x8 r;
 #pragma unroll
-  for (int r = 0; r < NREP; ++r) {
-    const u16x8 v = *reinterpret_cast<const u16x8*>(q + (int64_t)t * q_stride + (hbase + r) * D + sl * 8);
+      for (int j = 0; j < 8; ++j) {
+        const float c = j < 4 ? ca[j] : cb[j - 4], s = j < 4 ? sa[j] : sb[j - 4];
+        const float x = bf2f(me[j]), y = bf2f(ot[j]);
+        r[j] = lo ? f2bf(x * c - y * s) : f2bf(x * c + y * s);
+      }
+      return r;
+    };
 #pragma unroll
-    for (int j = 0; j < 8; ++j) qf[r][j] = bf2f(v[j]) * scale_log2;
+    for (int r = 0; r < NREP; ++r) {
+      const u16x8 v = rot(row + (hbase + r) * D);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qf[r][j] = bf2f(v[j]) * scale_log2;
+    }
+    kn = rot(row + (nh + g) * D);
+    vn = *reinterpret_cast<const u16x8*>(row + (nh + nkv + g) * D + sl * 8);
+    tnew = ctx - 1;
+    const int64_t slot = rf.slots[t];
+    if (tnew >= start && tnew < end && slot >= 0 && tid < LPT && hbase % (nh / nkv) == 0) {
+      const int64_t pg = slot >> page_log2, off = slot & (page_size - 1);
+      const int64_t dst = pg * page_stride + head_off + off * D;
+      *reinterpret_cast<u16x8*>(rf.kw + dst) = kn;
+      *reinterpret_cast<u16x8*>(rf.vw + dst) = vn;
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < NREP; ++r) {
+      const u16x8 v = *reinterpret_cast<const u16x8*>(q + (int64_t)t * q_stride + (hbase + r) * D + sl * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qf[r][j] = bf2f(v[j]) * scale_log2;
+    }
   }
 
   // ---- pass 1: scores (log2 domain) into LDS, running max per head ----
@@ -99,12 +160,23 @@ __global__ __launch_bounds__(256) void paged_attn_kernel(
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int tok = base + u * TPI + tg;
-      if (tok < end) {
-        const int64_t pg = bt[tok >> page_log2];
-        kv[u] = *reinterpret_cast<const u16x8*>(kc + pg * page_stride + head_off +
-                                                 (int64_t)(tok & (page_size - 1)) * D);
-      } else {
-        kv[u] = (u16x8)(0);
+      // unconditional load of a clamped token (no exec-masked branch between the U loads),
+      // then select: the ROPE path's new token comes from registers, past the end is 0
+      const int tc = min(tok, end - 1);
+      const int64_t pg = bt[tc >> page_log2];
+      const u16x8 ld = *reinterpret_cast<const u16x8*>(kc + pg * page_stride + head_off +
+                                                        (int64_t)(tc & (page_size - 1)) * D);
+      kv[u] = ROPE ? ld : (tok < end ? ld : (u16x8)(0));
+    }
+    if constexpr (ROPE) {
+      // pin the U loads as unconditional (otherwise the compiler sinks each into a
+      // tok != tnew branch with a full vmcnt(0) wait), then substitute the new token
+#pragma unroll
+      for (int u = 0; u < U; ++u) asm volatile("" : "+v"(kv[u]));
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int tok = base + u * TPI + tg;
+        kv[u] = tok == tnew ? kn : (tok < end ? kv[u] : (u16x8)(0));
       }
     }
 #pragma unroll
@@ -160,12 +232,23 @@ __global__ __launch_bounds__(256) void paged_attn_kernel(
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int tok = base + u * TPI + tg;
-      if (tok < end) {
-        const int64_t pg = bt[tok >> page_log2];
-        vv[u] = *reinterpret_cast<const u16x8*>(vc + pg * page_stride + head_off +
-                                                 (int64_t)(tok & (page_size - 1)) * D);
-      } else {
-        vv[u] = (u16x8)(0);
+      // unconditional load of a clamped token (no exec-masked branch between the U loads),
+      // then select: the ROPE path's new token comes from registers, past the end is 0
+      const int tc = min(tok, end - 1);
+      const int64_t pg = bt[tc >> page_log2];
+      const u16x8 ld = *reinterpret_cast<const u16x8*>(vc + pg * page_stride + head_off +
+                                                        (int64_t)(tc & (page_size - 1)) * D);
+      vv[u] = ROPE ? ld : (tok < end ? ld : (u16x8)(0));
+    }
+    if constexpr (ROPE) {
+      // pin the U loads as unconditional (otherwise the compiler sinks each into a
+      // tok != tnew branch with a full vmcnt(0) wait), then substitute the new token
+#pragma unroll
+      for (int u = 0; u < U; ++u) asm volatile("" : "+v"(vv[u]));
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int tok = base + u * TPI + tg;
+        vv[u] = tok == tnew ? vn : (tok < end ? vv[u] : (u16x8)(0));
       }
     }
 #pragma unroll
@@ -254,11 +337,15 @@ template <int D, int NREP>
 static void launch_attn(const void* q, int64_t q_stride, const void* kc, const void* vc, const int32_t* bt,
                         int bt_stride, const int32_t* q_seq, const int32_t* q_ctx, void* out, float* ws_o,
                         float* ws_ml, int T, int nkv, int nh, int page_log2, int PS, int NP, float scale_log2,
-                        int packed_mt, hipStream_t stream) {
+                        int packed_mt, const RopeFuse& rf, hipStream_t stream) {
   const size_t lds = (size_t)(NREP * PS + 8 * NREP + 4 * NREP * D) * sizeof(float);
-  hipLaunchKernelGGL((paged_attn_kernel<D, NREP>), dim3(NP, nh / NREP, T), dim3(256), lds, stream, (const bf16_t*)q,
-                     q_stride, (const bf16_t*)kc, (const bf16_t*)vc, bt, bt_stride, q_seq, q_ctx, (bf16_t*)out,
-                     ws_o, ws_ml, nkv, nh, page_log2, PS, NP, scale_log2, packed_mt);
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(NP, nh / NREP, T), dim3(256), lds, stream, (const bf16_t*)q, q_stride,
+                       (const bf16_t*)kc, (const bf16_t*)vc, bt, bt_stride, q_seq, q_ctx, (bf16_t*)out, ws_o, ws_ml,
+                       nkv, nh, page_log2, PS, NP, scale_log2, packed_mt, rf);
+  };
+  if (rf.pos) go(paged_attn_kernel<D, NREP, true>);
+  else go(paged_attn_kernel<D, NREP, false>);
 }
 
 }  // namespace mp
@@ -266,8 +353,10 @@ static void launch_attn(const void* q, int64_t q_stride, const void* kc, const v
 extern "C" int mp_paged_attention(const void* q, int64_t q_stride, const void* kc, const void* vc,
                                   const int32_t* bt, int bt_stride, const int32_t* q_seq, const int32_t* q_ctx,
                                   void* out, float* workspace, int T, int nh, int nkv, int D, int page_size,
-                                  int PS, int NP, float scale, int packed_mt, hipStream_t stream) {
+                                  int PS, int NP, float scale, int packed_mt, const int64_t* rope_pos,
+                                  const float* cos_t, const float* sin_t, const int64_t* slots, hipStream_t stream) {
   using namespace mp;
+  const RopeFuse rf{rope_pos, cos_t, sin_t, slots, (bf16_t*)const_cast<void*>(kc), (bf16_t*)const_cast<void*>(vc)};
   if (T == 0) return 0;
   if (nh % nkv != 0 || PS % 64 != 0 || PS > 2048 || NP < 1) return -1;
   int page_log2 = 0;
@@ -287,7 +376,7 @@ extern "C" int mp_paged_attention(const void* q, int64_t q_stride, const void* k
 #define MP_ATTN_CASE(DD, RR)                                                                                  \
   if (D == DD && hpb == RR) {                                                                                 \
     launch_attn<DD, RR>(q, q_stride, kc, vc, bt, bt_stride, q_seq, q_ctx, out, ws_o, ws_ml, T, nkv, nh,       \
-                        page_log2, PS, NP, scale_log2, packed_mt, stream);                                    \
+                        page_log2, PS, NP, scale_log2, packed_mt, rf, stream);                                \
     goto launched;                                                                                            \
   }
   MP_ATTN_CASE(128, 1)

@@ -21,6 +21,7 @@ int mp_kv_write(const void* k, int64_t k_stride, const void* v, int64_t v_stride
 int mp_paged_attention(const void* q, int64_t q_stride, const void* kc, const void* vc, const int32_t* bt,
                        int bt_stride, const int32_t* q_seq, const int32_t* q_ctx, void* out, float* workspace, int T,
                        int nh, int nkv, int D, int page_size, int PS, int NP, float scale, int packed_mt,
+                       const int64_t* rope_pos, const float* cos_t, const float* sin_t, const int64_t* slots,
                        hipStream_t stream);
 int mp_embedding(const int64_t* ids, const void* table, void* out, int T, int H, int64_t vocab, hipStream_t stream);
 int mp_swiglu(const void* gu, void* out, int64_t T, int F, hipStream_t stream);
@@ -145,10 +146,11 @@ void kv_write(const at::Tensor& k, const at::Tensor& v, at::Tensor& k_cache, at:
                "kv_write");
 }
 
-void paged_attention(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
-                     const at::Tensor& block_tables, const at::Tensor& q_seq, const at::Tensor& q_ctx,
-                     at::Tensor& out, at::Tensor& workspace, int64_t nh, int64_t nkv, double scale, int64_t part_size,
-                     int64_t num_parts, int64_t packed) {
+static void paged_attention_impl(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
+                                 const at::Tensor& block_tables, const at::Tensor& q_seq, const at::Tensor& q_ctx,
+                                 at::Tensor& out, at::Tensor& workspace, int64_t nh, int64_t nkv, double scale,
+                                 int64_t part_size, int64_t num_parts, int64_t packed, const int64_t* rope_pos,
+                                 const float* cos_t, const float* sin_t, const int64_t* slots) {
   check_bf16_cuda(q, "q");
   check_rows(q, "q");
   check_bf16_cuda(out, "out");
@@ -172,8 +174,39 @@ void paged_attention(const at::Tensor& q, const at::Tensor& k_cache, const at::T
                                   block_tables.data_ptr<int32_t>(), block_tables.stride(0), q_seq.data_ptr<int32_t>(),
                                   q_ctx.data_ptr<int32_t>(), out.data_ptr(), workspace.data_ptr<float>(), T, nh, nkv,
                                   D, k_cache.size(2), part_size, num_parts, (float)scale,
-                                  packed ? (int)((T + 15) / 16) : 0, cur_stream()),
+                                  packed ? (int)((T + 15) / 16) : 0, rope_pos, cos_t, sin_t, slots, cur_stream()),
                "paged_attention");
+}
+
+void paged_attention(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
+                     const at::Tensor& block_tables, const at::Tensor& q_seq, const at::Tensor& q_ctx,
+                     at::Tensor& out, at::Tensor& workspace, int64_t nh, int64_t nkv, double scale, int64_t part_size,
+                     int64_t num_parts, int64_t packed) {
+  paged_attention_impl(q, k_cache, v_cache, block_tables, q_seq, q_ctx, out, workspace, nh, nkv, scale, part_size,
+                       num_parts, packed, nullptr, nullptr, nullptr, nullptr);
+}
+
+// Decode attention with RoPE + KV write fused in (attention.hip ROPE path): q is the unrotated
+// fused qkv row; k_cache / v_cache receive the new token at slots[t].
+void paged_attention_rope(const at::Tensor& qkv, at::Tensor& k_cache, at::Tensor& v_cache,
+                          const at::Tensor& block_tables, const at::Tensor& q_seq, const at::Tensor& q_ctx,
+                          const at::Tensor& positions, const at::Tensor& cos, const at::Tensor& sin,
+                          const at::Tensor& slots, at::Tensor& out, at::Tensor& workspace, int64_t nh, int64_t nkv,
+                          double scale, int64_t part_size, int64_t num_parts, int64_t packed) {
+  check_bf16_cuda(k_cache, "k_cache");
+  check_bf16_cuda(v_cache, "v_cache");
+  MP_CHECK(k_cache.dim() == 4 && k_cache.sizes() == v_cache.sizes(), "cache [pages, nkv, page, D]");
+  const int D = k_cache.size(3), T = qkv.size(0);
+  MP_CHECK(qkv.size(1) == (nh + 2 * nkv) * D, "qkv width");
+  MP_CHECK(positions.scalar_type() == at::kLong && positions.numel() == T && positions.is_contiguous(), "positions");
+  MP_CHECK(slots.scalar_type() == at::kLong && slots.numel() == T && slots.is_contiguous(), "slots");
+  MP_CHECK(cos.scalar_type() == at::kFloat && sin.scalar_type() == at::kFloat && cos.is_contiguous() &&
+               sin.is_contiguous() && cos.size(1) == D / 2 && sin.sizes() == cos.sizes(),
+           "cos/sin tables fp32 [max_pos, D/2]");
+  MP_CHECK(D % 16 == 0, "head dim");
+  paged_attention_impl(qkv, k_cache, v_cache, block_tables, q_seq, q_ctx, out, workspace, nh, nkv, scale, part_size,
+                       num_parts, packed, positions.data_ptr<int64_t>(), cos.data_ptr<float>(), sin.data_ptr<float>(),
+                       slots.data_ptr<int64_t>());
 }
 
 void attention_mfma(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
@@ -411,6 +444,10 @@ TORCH_LIBRARY(mpamd, m) {
       "Tensor(a!) out, Tensor(b!) workspace, int nh, int nkv, float scale, int part_size, int num_parts, "
       "int packed) -> ()");
   m.def(
+      "paged_attention_rope(Tensor qkv, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor block_tables, Tensor q_seq, "
+      "Tensor q_ctx, Tensor positions, Tensor cos, Tensor sin, Tensor slots, Tensor(c!) out, Tensor(d!) workspace, "
+      "int nh, int nkv, float scale, int part_size, int num_parts, int packed) -> ()");
+  m.def(
       "attention_mfma(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor q_seq, Tensor q_ctx, "
       "Tensor qblocks, Tensor(a!) out, Tensor(b!) workspace, int nh, int nkv, float scale, int part_size, "
       "int num_parts, int packed) -> ()");
@@ -437,6 +474,7 @@ TORCH_LIBRARY_IMPL(mpamd, CUDA, m) {
   m.impl("rope_kv_write", &rope_kv_write);
   m.impl("kv_write", &kv_write);
   m.impl("paged_attention", &paged_attention);
+  m.impl("paged_attention_rope", &paged_attention_rope);
   m.impl("attention_mfma", &attention_mfma);
   m.impl("embedding", &embedding);
   m.impl("swiglu", &swiglu);

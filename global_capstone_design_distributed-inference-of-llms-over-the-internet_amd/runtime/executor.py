@@ -156,6 +156,8 @@ class StageExecutor:
             cfg.model_type != "gpt2" and cfg.head_dim in (64, 128)
         # GQA decode: the whole group of a kv head in the MFMA rows (2x the VALU kernel at nrep 8)
         self._attn_mfma_gqa = self._attn_mfma_prefill and self.nh // self.nkv >= 4
+        # decode steps on the flash-decoding kernel fold RoPE + the KV page write into it
+        self._fuse_rope = os.environ.get("MPAMD_FUSE_ROPE", "1") != "0"
         self._decode_qb: Dict[int, torch.Tensor] = {}
         self._moe_y: Dict[int, torch.Tensor] = {}
         self.timing = False
@@ -334,7 +336,8 @@ class StageExecutor:
             out = self._forward_gpt2(plan, x, prompt=prompt)
         else:
             out = self._forward_llama(x, plan.positions, plan.slots, plan.q_seq, plan.q_ctx, plan.last_rows,
-                                      plan.T, plan.max_ctx, None, qblocks=plan.qblocks, prompt=prompt)
+                                      plan.T, plan.max_ctx, None, qblocks=plan.qblocks, prompt=prompt,
+                                      decode=plan.is_decode)
         if ev is not None:
             ev[1].record()
             ev[1].synchronize()
@@ -370,8 +373,20 @@ class StageExecutor:
         return ops.paged_attention(qkv, kc, vc, table, q_seq, q_ctx, self.nh, self.nkv, self.scale, out=out,
                                    workspace=ws, part_size=ps, num_parts=np_, packed=packed)
 
+    def _rope_attend(self, qkv, positions, slots, kc, vc, q_seq, q_ctx, out, ws, ps, np_, packed, qblocks, max_ctx,
+                     decode):
+        """RoPE + KV write + attention.  Decode steps that run on the flash-decoding kernel do all
+        three in one launch (ops.paged_attention_rope); everything else keeps rope_kv_write."""
+        if decode and qblocks is None and self._fuse_rope and not (
+                self._attn_mfma_gqa and self.device.type == "cuda"):
+            return ops.paged_attention_rope(qkv, kc, vc, self.sessions.table_dev, q_seq, q_ctx, positions, self.cos,
+                                            self.sin, slots, self.nh, self.nkv, self.scale, out=out, workspace=ws,
+                                            part_size=ps, num_parts=np_, packed=packed)
+        ops.rope_kv_write(qkv, positions, self.cos, self.sin, kc, vc, slots, self.nh, self.nkv)
+        return self._attend(qkv, kc, vc, q_seq, q_ctx, out, ws, ps, np_, packed, qblocks, max_ctx)
+
     def _forward_llama(self, x, positions, slots, q_seq, q_ctx, last_rows, T, max_ctx, attn_part,
-                       bufs: Optional[dict] = None, qblocks=None, prompt=None):
+                       bufs: Optional[dict] = None, qblocks=None, prompt=None, decode=False):
         cfg, w = self.cfg, self.w
         H, eps = cfg.hidden_size, cfg.rms_norm_eps
         dev, dt = self.device, self.dtype
@@ -409,8 +424,8 @@ class StageExecutor:
                 ops.quant_act_fp8(xn, T, H, out=a8, scale=asc)
                 ops.linear_fp8(a8, asc, L.qkv_q, L.qkv_s, T, out=qkv)
                 kc, vc = self.cache.layer(li)
-                ops.rope_kv_write(qkv, positions, self.cos, self.sin, kc, vc, slots, self.nh, self.nkv)
-                self._attend(qkv, kc, vc, q_seq, q_ctx, attn, ws, ps, np_, True, qblocks, max_ctx)
+                self._rope_attend(qkv, positions, slots, kc, vc, q_seq, q_ctx, attn, ws, ps, np_, True, qblocks,
+                                  max_ctx, decode)
                 ops.quant_act_fp8(attn, T, cfg.q_dim, out=a8, scale=asc)
                 ops.linear_fp8(a8, asc, L.o_q, L.o_s, T, out=o)
                 self._ar(o)
@@ -433,8 +448,8 @@ class StageExecutor:
                     ops.rmsnorm(mlp, L.input_norm, eps, out=xn, residual=res, mode=1, packed=True)
                 ops.linear(xn, L.qkv, out=qkv, wp=L.qkv_p, a_rows=T)
                 kc, vc = self.cache.layer(li)
-                ops.rope_kv_write(qkv, positions, self.cos, self.sin, kc, vc, slots, self.nh, self.nkv)
-                self._attend(qkv, kc, vc, q_seq, q_ctx, attn, ws, ps, np_, True, qblocks, max_ctx)
+                self._rope_attend(qkv, positions, slots, kc, vc, q_seq, q_ctx, attn, ws, ps, np_, True, qblocks,
+                                  max_ctx, decode)
                 ops.linear(attn, L.o, out=o, wp=L.o_p, a_rows=T)
                 self._ar(o)
                 ops.rmsnorm(o, L.post_norm, eps, out=xn, residual=res, mode=1, packed=True)
@@ -459,8 +474,8 @@ class StageExecutor:
                     ops.rmsnorm(mlp, L.input_norm, eps, out=xn, residual=res, mode=1)
                 ops.linear(xn, L.dense("qkv"), out=qkv, wp=L.qkv_p)
                 kc, vc = self.cache.layer(li)
-                ops.rope_kv_write(qkv, positions, self.cos, self.sin, kc, vc, slots, self.nh, self.nkv)
-                self._attend(qkv, kc, vc, q_seq, q_ctx, attn, ws, ps, np_, False, qblocks, max_ctx)
+                self._rope_attend(qkv, positions, slots, kc, vc, q_seq, q_ctx, attn, ws, ps, np_, False, qblocks,
+                                  max_ctx, decode)
                 ops.linear(attn, L.dense("o"), out=o, wp=L.o_p)
                 self._ar(o)
                 ops.rmsnorm(o, L.post_norm, eps, out=xn, residual=res, mode=1)
@@ -681,11 +696,11 @@ class _DecodeGraph:
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for _ in range(2):  # warm up (allocator, hipBLASLt heuristics) outside capture
-                ex._forward_llama(*args)
+                ex._forward_llama(*args, decode=True)
         torch.cuda.current_stream().wait_stream(s)
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph, pool=pool):
-            self.out = ex._forward_llama(*args)
+            self.out = ex._forward_llama(*args, decode=True)
 
     def replay(self, plan: Plan, x: torch.Tensor) -> torch.Tensor:
         b, B = plan.T, self.B

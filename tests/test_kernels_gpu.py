@@ -501,3 +501,39 @@ def test_query_blocks():
     assert qb.tolist() == [[0, 5, 6, 22], [5, 1, 16, 1]]
     qb = ops.query_blocks([5, 1], 8)  # 2 tokens x 8 heads per block
     assert qb.tolist() == [[0, 2, 4, 5], [2, 2, 1, 1]]
+
+
+@pytest.mark.parametrize("nh,nkv,D", [(32, 32, 128), (32, 8, 128), (12, 12, 64)])
+@pytest.mark.parametrize("parts", [None, (64, 8)])
+@pytest.mark.parametrize("packed", [False, True])
+def test_paged_attention_rope_fused_matches_two_kernels(nh, nkv, D, parts, packed):
+    """Decode attention with RoPE + KV write folded in == rope_kv_write then paged_attention
+    (and the fp32 reference); the cache receives the same rotated k / copied v; a padded row
+    (ctx 0, slot -1) writes nothing and outputs 0."""
+    ctxs = [1, 5, 64, 200, 0]
+    ps = 64
+    q, kc, vc, bt, q_seq, q_ctx = _attn_case(nh, nkv, D, [max(c, 1) for c in ctxs], ps=ps)
+    q_ctx[-1] = 0
+    pos = (q_ctx.long() - 1).clamp(min=0)
+    slots = torch.stack([bt[i, int(p) // ps].long() * ps + int(p) % ps for i, p in enumerate(pos.tolist())])
+    slots[-1] = -1
+    cos, sin = ops.rope_cos_sin(D, 2048, 10000.0, DEV)
+    scale = 1 / math.sqrt(D)
+    kw = dict(part_size=parts[0], num_parts=parts[1]) if parts else dict(max_ctx=max(ctxs))
+    k2, v2, q2 = kc.clone(), vc.clone(), q.clone()
+    ops.rope_kv_write(q2, pos, cos, sin, k2, v2, slots, nh, nkv)
+    o2 = ops.paged_attention(q2, k2, v2, bt, q_seq, q_ctx, nh, nkv, scale, packed=packed, **kw)
+    q_in = q.clone()
+    o1 = ops.paged_attention_rope(q, kc, vc, bt, q_seq, q_ctx, pos, cos, sin, slots, nh, nkv, scale,
+                                  packed=packed, **kw)
+    assert torch.equal(q, q_in), "fused op must not modify qkv"
+    torch.testing.assert_close(kc.float(), k2.float(), atol=1e-2, rtol=1e-2)
+    assert torch.equal(vc, v2)
+    T = q.shape[0]
+    if packed:
+        o1, o2 = ref.unpack_act(o1, T, nh * D), ref.unpack_act(o2, T, nh * D)
+    torch.testing.assert_close(o1.float(), o2.float(), atol=2e-2, rtol=2e-2)
+    if not packed:
+        o_ref = ref.paged_attention(q2.float(), k2.float(), v2.float(), bt, q_seq, q_ctx, nh, nkv, scale)
+        torch.testing.assert_close(o1.float(), o_ref.float(), atol=2e-2, rtol=2e-2)
+        assert torch.count_nonzero(o1[-1]) == 0

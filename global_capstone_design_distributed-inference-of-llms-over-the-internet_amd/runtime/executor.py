@@ -158,6 +158,8 @@ class StageExecutor:
         self._attn_mfma_gqa = self._attn_mfma_prefill and self.nh // self.nkv >= 4
         # decode steps on the flash-decoding kernel fold RoPE + the KV page write into it
         self._fuse_rope = os.environ.get("MPAMD_FUSE_ROPE", "1") != "0"
+        # shortest split-K context slice (ops.attention_partition): longer on the MFMA GQA kernel
+        self._attn_min_part = 256 if self._attn_mfma_gqa else 64
         self._decode_qb: Dict[int, torch.Tensor] = {}
         self._moe_y: Dict[int, torch.Tensor] = {}
         self.timing = False
@@ -399,7 +401,7 @@ class StageExecutor:
         else:
             h = x
         if attn_part is None:
-            attn_part = ops.attention_partition(T, self.nkv, max_ctx)
+            attn_part = ops.attention_partition(T, self.nkv, max_ctx, min_part=self._attn_min_part)
         ps, np_ = attn_part
         ws = e("attn_ws", (max(1, T * self.nh * np_ * (self.D + 2)),), torch.float32)
         res = e("res", (T, H))
@@ -658,7 +660,7 @@ class StageExecutor:
     def _run_graph(self, plan: Plan, x: torch.Tensor) -> torch.Tensor:
         B = self._bucket(plan.T)
         ctxb = min(self._ctx_bucket(plan.max_ctx), self._ctx_bucket(self.max_seq_len))
-        part = ops.attention_partition(B, self.nkv, ctxb)
+        part = ops.attention_partition(B, self.nkv, ctxb, min_part=self._attn_min_part)
         key = (B, part[0], part[1])
         g = self._graphs.get(key)
         if g is None:

@@ -189,8 +189,14 @@ def autotune_gemm(shapes, device, ms=(16, 32, 48, 64), iters: int = 24, rounds: 
             if pool is None:
                 pool = (torch.randn(_TUNE_POOL_BYTES // 2, device=device) * 0.02).to(torch.bfloat16)
             n = N * K
-            copies = max(1, min(16, pool.numel() // n))
-            wps = [pool[i * n:(i + 1) * n].view(N // 16, K // 32, 64, 8) for i in range(copies)]
+            if n > pool.numel():  # one weight larger than the pool (e.g. a 128K-vocab lm_head): it is
+                # MALL-cold by itself, so a single dedicated copy gives the same conditions
+                wps = [torch.empty(n, dtype=torch.bfloat16, device=device).normal_(0, 0.02)
+                       .view(N // 16, K // 32, 64, 8)]
+            else:
+                wps = [pool[i * n:(i + 1) * n].view(N // 16, K // 32, 64, 8)
+                       for i in range(min(16, pool.numel() // n))]
+            copies = len(wps)
             ncols = N // 2 if epi == 1 else N
             for M in todo:
                 cands = [k for k in _KERNEL_FLAGS if _covered(k, M, N, K, epi)]

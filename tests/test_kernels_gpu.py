@@ -537,3 +537,15 @@ def test_paged_attention_rope_fused_matches_two_kernels(nh, nkv, D, parts, packe
         o_ref = ref.paged_attention(q2.float(), k2.float(), v2.float(), bt, q_seq, q_ctx, nh, nkv, scale)
         torch.testing.assert_close(o1.float(), o_ref.float(), atol=2e-2, rtol=2e-2)
         assert torch.count_nonzero(o1[-1]) == 0
+
+
+def test_autotune_weight_larger_than_pool(monkeypatch):
+    """A weight bigger than the rotation pool (Llama-3-70B's 128K-vocab lm_head vs the 1 GiB
+    pool) is timed on one dedicated copy instead of failing to view the pool."""
+    monkeypatch.setattr(ops, "_TUNE_POOL_BYTES", 1 << 20)
+    N, K = 4096 + 16 * 7, 4096
+    key = (64, N, K, 0)
+    ops._SK_CHOICE.pop(key, None)
+    table = ops.autotune_gemm([(N, K, 0)], DEV, ms=(64,), iters=2, rounds=1)
+    assert ops._SK_CHOICE.get(key) in (set(ops._KERNEL_FLAGS) | {"pk"}), table
+    ops._SK_CHOICE.pop(key, None)

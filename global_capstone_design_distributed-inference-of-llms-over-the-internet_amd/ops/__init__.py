@@ -349,6 +349,35 @@ def attention_mfma(q, k_cache, v_cache, block_tables, q_seq, q_ctx, qblocks, nh,
     return out
 
 
+def attention_mfma_rope(qkv, k_cache, v_cache, block_tables, q_seq, q_ctx, qblocks, positions, cos, sin, slots, nh,
+                        nkv, scale, out=None, workspace=None, part_size=None, num_parts=None, max_ctx=None,
+                        packed=False):
+    """GQA decode step on the MFMA kernel with RoPE of q / new k and the new token's page-slot
+    write folded in (csrc/attention_mfma.hip ROPE path).  ``qblocks`` holds one token per block
+    (``decode_qblocks``); ``qkv`` is the unrotated fused projection and is not modified."""
+    if not _native(qkv):
+        q = qkv.clone()
+        ref.rope_kv_write(q, positions, cos, sin, k_cache, v_cache, slots, nh, nkv)
+        return paged_attention(q, k_cache, v_cache, block_tables, q_seq, q_ctx, nh, nkv, scale, out=out,
+                               packed=packed)
+    T = qkv.shape[0]
+    D = k_cache.shape[-1]
+    if part_size is None:
+        if max_ctx is None:
+            max_ctx = int(q_ctx.max().item()) if T else 1
+        part_size = 128 * math.ceil(max(max_ctx, 1) / 128)
+        num_parts = 1
+    if out is None:
+        out = (torch.empty(packed_numel(T, nh * D), dtype=qkv.dtype, device=qkv.device) if packed
+               else torch.empty(T, nh * D, dtype=qkv.dtype, device=qkv.device))
+    if workspace is None or (num_parts > 1 and workspace.numel() < T * nh * num_parts * (D + 2)):
+        workspace = attention_workspace(T, nh, D, num_parts, qkv.device)
+    torch.ops.mpamd.attention_mfma_rope(qkv, k_cache, v_cache, block_tables, q_seq, q_ctx, qblocks, positions, cos,
+                                        sin, slots, out, workspace, nh, nkv, float(scale), int(part_size),
+                                        int(num_parts), int(bool(packed)))
+    return out
+
+
 def attention_workspace(num_queries: int, nh: int, head_dim: int, num_parts: int, device) -> torch.Tensor:
     return torch.empty(max(1, num_queries * nh * num_parts * (head_dim + 2)), dtype=torch.float32, device=device)
 

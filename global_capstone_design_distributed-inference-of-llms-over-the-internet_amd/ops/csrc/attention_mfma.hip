@@ -22,9 +22,27 @@
 //       -> two ds_read_b64 per fragment, in the same permuted k order.
 // The 4 waves' (m, l, O) are merged through LDS; with num_parts > 1 the merged partials go
 // to the split-K workspace reduced by paged_attn_reduce_kernel (attention.hip).
+//
+// ROPE = true (GQA decode: every block is ONE token of one sequence, the last of its context):
+// `q` is the unrotated fused qkv row and the kernel also does rope_kv.hip's work.  The partner
+// of a lane's q chunk kd (rotate_half, D/2 away) is its own chunk kd ^ KD/2, so q rotates in
+// registers; the new token's k is rotated the same way, its score q.k_new is summed over the
+// 4 lanes of the row with two xor shuffles and replaces the (stale) cache score of token
+// ctx - 1, and its v chunk overwrites that token's column of the wave's LDS V tile.  The cache
+// loads stay exactly as without ROPE.  Wave 0 of the first block of the kv head whose slice
+// holds the token writes k / v to the page slot (slots[t] < 0: nothing written).
 #include "common.h"
 
 namespace mp {
+
+struct RopeFuseM {
+  const int64_t* pos;
+  const float* cos_t;
+  const float* sin_t;
+  const int64_t* slots;
+  bf16_t* kw;
+  bf16_t* vw;
+};
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_mf;
 
@@ -35,13 +53,13 @@ __device__ __forceinline__ f32x4 mfma_bf16(const u16x8& a, const u16x8& b, const
 
 constexpr int VT_PITCH = 36;  // bf16 per LDS row of the transposed V tile (32 tokens + pad; 8-B aligned rows)
 
-template <int D, int HB>
+template <int D, int HB, bool ROPE>
 __global__ __launch_bounds__(256) void attn_mfma_kernel(
     const bf16_t* __restrict__ q, int64_t q_stride, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
     const int32_t* __restrict__ block_tables, int bt_stride, const int32_t* __restrict__ q_seq,
     const int32_t* __restrict__ q_ctx, const int32_t* __restrict__ qb_tok0, const int32_t* __restrict__ qb_ntok,
     bf16_t* __restrict__ out, float* __restrict__ part_o, float* __restrict__ part_ml, int nkv, int nh,
-    int page_log2, int PS, int NP, float scale_log2, int packed_mt) {
+    int page_log2, int PS, int NP, float scale_log2, int packed_mt, RopeFuseM rf) {
   constexpr int TB = 16 / HB;
   constexpr int KD = D / 32;  // k-chunks of the QK^T product
   constexpr int DT = D / 16;  // 16-column tiles of O
@@ -77,6 +95,63 @@ __global__ __launch_bounds__(256) void attn_mfma_kernel(
     else qf[kd] = (u16x8)(0);
   }
 
+  int tnew = -1;
+  float qk_new = 0.f;
+  u16x8 vn = (u16x8)(0);
+  if constexpr (ROPE) {
+    constexpr int HK = KD / 2, HALF = D / 2;
+    const int64_t ps_ = rf.pos[tok0];
+    const bf16_t* row = q + (int64_t)tok0 * q_stride;
+    u16x8 kr[KD];
+#pragma unroll
+    for (int kd = 0; kd < KD; ++kd) kr[kd] = *reinterpret_cast<const u16x8*>(row + (nh + g) * D + kd * 32 + qd * 8);
+    vn = *reinterpret_cast<const u16x8*>(row + (nh + nkv + g) * D + ((lane * 8) % D));
+    f32x4 cs[HK][2], sn[HK][2];
+#pragma unroll
+    for (int h = 0; h < HK; ++h) {
+      const int64_t ci = ps_ * HALF + h * 32 + qd * 8;
+      cs[h][0] = *reinterpret_cast<const f32x4*>(rf.cos_t + ci);
+      cs[h][1] = *reinterpret_cast<const f32x4*>(rf.cos_t + ci + 4);
+      sn[h][0] = *reinterpret_cast<const f32x4*>(rf.sin_t + ci);
+      sn[h][1] = *reinterpret_cast<const f32x4*>(rf.sin_t + ci + 4);
+    }
+    auto rot = [&](const u16x8 (&a)[KD], u16x8 (&r)[KD]) {
+#pragma unroll
+      for (int kd = 0; kd < KD; ++kd) {
+        const int h = kd % HK;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float c_ = cs[h][j >> 2][j & 3], s_ = sn[h][j >> 2][j & 3];
+          const float x = bf2f(a[kd][j]), y = bf2f(a[kd ^ HK][j]);
+          r[kd][j] = kd < HK ? f2bf(x * c_ - y * s_) : f2bf(x * c_ + y * s_);
+        }
+      }
+    };
+    u16x8 qr[KD], kn[KD];
+    rot(qf, qr);
+    rot(kr, kn);
+#pragma unroll
+    for (int kd = 0; kd < KD; ++kd) qf[kd] = row_ok ? qr[kd] : (u16x8)(0);
+    float part = 0.f;
+#pragma unroll
+    for (int kd = 0; kd < KD; ++kd)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) part += bf2f(qf[kd][j]) * bf2f(kn[kd][j]);
+    part += __shfl_xor(part, 16, 64);
+    part += __shfl_xor(part, 32, 64);
+    qk_new = part;
+    tnew = blk_ctx - 1;
+    const int64_t slot = rf.slots[tok0];
+    if (w == 0 && tnew >= start && tnew < end && slot >= 0 && hbase % (nh / nkv) == 0) {
+      const int64_t dst = (slot >> page_log2) * page_stride + head_off + (slot & (page_size - 1)) * D;
+      if (c == 0) {
+#pragma unroll
+        for (int kd = 0; kd < KD; ++kd) *reinterpret_cast<u16x8*>(rf.kw + dst + kd * 32 + qd * 8) = kn[kd];
+      }
+      if (lane * 8 < D) *reinterpret_cast<u16x8*>(rf.vw + dst + lane * 8) = vn;
+    }
+  }
+
   f32x4 o[DT];
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt) o[dt] = (f32x4)(0.f);
@@ -107,6 +182,23 @@ __global__ __launch_bounds__(256) void attn_mfma_kernel(
       if (b0 + tk >= end) vv = (u16x8)(0);
 #pragma unroll
       for (int e = 0; e < 8; ++e) vt[(d0 + e) * VT_PITCH + tk] = vv[e];
+    }
+    if constexpr (ROPE) {  // the new token: its score and its V column come from registers
+      const int rel = tnew - b0;
+      if (rel >= 0 && rel < 32) {
+        if (lane * 8 < D) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) vt[(lane * 8 + e) * VT_PITCH + rel] = vn[e];
+        }
+        if (qd == ((rel & 15) >> 2)) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (r == (rel & 3)) {
+              if (rel < 16) st[0][r] = qk_new;
+              else st[1][r] = qk_new;
+            }
+        }
+      }
     }
     // ---- online softmax for row c over this lane's 8 tokens {4qd + r, 16 + 4qd + r} ----
     float s8[8];
@@ -200,10 +292,15 @@ template <int D, int HB>
 static void launch_attn_mfma(const void* q, int64_t q_stride, const void* kc, const void* vc, const int32_t* bt,
                              int bt_stride, const int32_t* q_seq, const int32_t* q_ctx, const int32_t* qb_tok0,
                              const int32_t* qb_ntok, int NB, void* out, float* ws_o, float* ws_ml, int nkv, int nh,
-                             int page_log2, int PS, int NP, float scale_log2, int packed_mt, hipStream_t stream) {
-  hipLaunchKernelGGL((attn_mfma_kernel<D, HB>), dim3(NB, nh / HB, NP), dim3(256), 0, stream, (const bf16_t*)q,
-                     q_stride, (const bf16_t*)kc, (const bf16_t*)vc, bt, bt_stride, q_seq, q_ctx, qb_tok0, qb_ntok,
-                     (bf16_t*)out, ws_o, ws_ml, nkv, nh, page_log2, PS, NP, scale_log2, packed_mt);
+                             int page_log2, int PS, int NP, float scale_log2, int packed_mt, const RopeFuseM& rf,
+                             hipStream_t stream) {
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(NB, nh / HB, NP), dim3(256), 0, stream, (const bf16_t*)q, q_stride,
+                       (const bf16_t*)kc, (const bf16_t*)vc, bt, bt_stride, q_seq, q_ctx, qb_tok0, qb_ntok,
+                       (bf16_t*)out, ws_o, ws_ml, nkv, nh, page_log2, PS, NP, scale_log2, packed_mt, rf);
+  };
+  if (rf.pos) go(attn_mfma_kernel<D, HB, true>);
+  else go(attn_mfma_kernel<D, HB, false>);
 }
 
 __global__ void paged_attn_reduce_kernel(const float* __restrict__ part_o, const float* __restrict__ part_ml,
@@ -216,8 +313,11 @@ __global__ void paged_attn_reduce_kernel(const float* __restrict__ part_o, const
 extern "C" int mp_attention_mfma(const void* q, int64_t q_stride, const void* kc, const void* vc, const int32_t* bt,
                                  int bt_stride, const int32_t* q_seq, const int32_t* q_ctx, const int32_t* qb_tok0,
                                  const int32_t* qb_ntok, int NB, void* out, float* workspace, int T, int nh, int nkv,
-                                 int D, int page_size, int PS, int NP, float scale, int packed_mt, hipStream_t stream) {
+                                 int D, int page_size, int PS, int NP, float scale, int packed_mt,
+                                 const int64_t* rope_pos, const float* cos_t, const float* sin_t,
+                                 const int64_t* slots, hipStream_t stream) {
   using namespace mp;
+  const RopeFuseM rf{rope_pos, cos_t, sin_t, slots, (bf16_t*)const_cast<void*>(kc), (bf16_t*)const_cast<void*>(vc)};
   if (NB == 0 || T == 0) return 0;
   if (nh % nkv != 0 || PS % 128 != 0 || NP < 1 || page_size % 32 != 0) return -1;
   int page_log2 = 0;
@@ -232,7 +332,7 @@ extern "C" int mp_attention_mfma(const void* q, int64_t q_stride, const void* kc
 #define MP_AM_CASE(DD, HH)                                                                                      \
   if (D == DD && hb == HH) {                                                                                    \
     launch_attn_mfma<DD, HH>(q, q_stride, kc, vc, bt, bt_stride, q_seq, q_ctx, qb_tok0, qb_ntok, NB, out, ws_o,  \
-                             ws_ml, nkv, nh, page_log2, PS, NP, scale_log2, packed_mt, stream);                 \
+                             ws_ml, nkv, nh, page_log2, PS, NP, scale_log2, packed_mt, rf, stream);             \
     goto launched;                                                                                              \
   }
   MP_AM_CASE(128, 1)

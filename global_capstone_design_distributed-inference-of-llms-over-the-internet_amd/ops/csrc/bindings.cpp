@@ -34,7 +34,8 @@ int64_t mp_gemm_workspace_bytes();
 int mp_attention_mfma(const void* q, int64_t q_stride, const void* kc, const void* vc, const int32_t* bt, int bt_stride,
                       const int32_t* q_seq, const int32_t* q_ctx, const int32_t* qb_tok0, const int32_t* qb_ntok, int NB,
                       void* out, float* workspace, int T, int nh, int nkv, int D, int page_size, int PS, int NP,
-                      float scale, int packed_mt, hipStream_t stream);
+                      float scale, int packed_mt, const int64_t* rope_pos, const float* cos_t, const float* sin_t,
+                      const int64_t* slots, hipStream_t stream);
 int mp_quant_act_fp8(const void* ap, void* a8, float* scale, float* part, int M, int K, hipStream_t stream);
 int mp_gemm_fp8(const void* a8, const float* as, const void* wq, const float* ws, void* y, int64_t ys, const void* res,
                 int64_t rs, int M, int N, int K, int epilogue, int out_packed, hipStream_t stream);
@@ -209,10 +210,12 @@ void paged_attention_rope(const at::Tensor& qkv, at::Tensor& k_cache, at::Tensor
                        slots.data_ptr<int64_t>());
 }
 
-void attention_mfma(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
-                     const at::Tensor& block_tables, const at::Tensor& q_seq, const at::Tensor& q_ctx,
-                     const at::Tensor& qblocks, at::Tensor& out, at::Tensor& workspace, int64_t nh, int64_t nkv, double scale, int64_t part_size,
-                     int64_t num_parts, int64_t packed) {
+static void attention_mfma_impl(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
+                                const at::Tensor& block_tables, const at::Tensor& q_seq, const at::Tensor& q_ctx,
+                                const at::Tensor& qblocks, at::Tensor& out, at::Tensor& workspace, int64_t nh,
+                                int64_t nkv, double scale, int64_t part_size, int64_t num_parts, int64_t packed,
+                                const int64_t* rope_pos, const float* cos_t, const float* sin_t,
+                                const int64_t* slots) {
   check_bf16_cuda(q, "q");
   check_rows(q, "q");
   check_bf16_cuda(out, "out");
@@ -240,8 +243,38 @@ void attention_mfma(const at::Tensor& q, const at::Tensor& k_cache, const at::Te
                                  q_ctx.data_ptr<int32_t>(), qblocks.data_ptr<int32_t>(),
                                  qblocks.data_ptr<int32_t>() + NB, NB, out.data_ptr(), workspace.data_ptr<float>(), T,
                                  nh, nkv, D, k_cache.size(2), part_size, num_parts, (float)scale,
-                                 packed ? (int)((T + 15) / 16) : 0, cur_stream()),
+                                 packed ? (int)((T + 15) / 16) : 0, rope_pos, cos_t, sin_t, slots, cur_stream()),
                "attention_mfma");
+}
+
+void attention_mfma(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
+                    const at::Tensor& block_tables, const at::Tensor& q_seq, const at::Tensor& q_ctx,
+                    const at::Tensor& qblocks, at::Tensor& out, at::Tensor& workspace, int64_t nh, int64_t nkv,
+                    double scale, int64_t part_size, int64_t num_parts, int64_t packed) {
+  attention_mfma_impl(q, k_cache, v_cache, block_tables, q_seq, q_ctx, qblocks, out, workspace, nh, nkv, scale,
+                      part_size, num_parts, packed, nullptr, nullptr, nullptr, nullptr);
+}
+
+// GQA decode with RoPE + KV write fused (attention_mfma.hip ROPE path): one token per query block.
+void attention_mfma_rope(const at::Tensor& qkv, at::Tensor& k_cache, at::Tensor& v_cache,
+                         const at::Tensor& block_tables, const at::Tensor& q_seq, const at::Tensor& q_ctx,
+                         const at::Tensor& qblocks, const at::Tensor& positions, const at::Tensor& cos,
+                         const at::Tensor& sin, const at::Tensor& slots, at::Tensor& out, at::Tensor& workspace,
+                         int64_t nh, int64_t nkv, double scale, int64_t part_size, int64_t num_parts, int64_t packed) {
+  check_bf16_cuda(k_cache, "k_cache");
+  check_bf16_cuda(v_cache, "v_cache");
+  MP_CHECK(k_cache.dim() == 4 && k_cache.sizes() == v_cache.sizes(), "cache [pages, nkv, page, D]");
+  const int D = k_cache.size(3), T = qkv.size(0);
+  MP_CHECK(qkv.size(1) == (nh + 2 * nkv) * D, "qkv width");
+  MP_CHECK(positions.scalar_type() == at::kLong && positions.numel() == T && positions.is_contiguous(), "positions");
+  MP_CHECK(slots.scalar_type() == at::kLong && slots.numel() == T && slots.is_contiguous(), "slots");
+  MP_CHECK(cos.scalar_type() == at::kFloat && sin.scalar_type() == at::kFloat && cos.is_contiguous() &&
+               sin.is_contiguous() && cos.size(1) == D / 2 && sin.sizes() == cos.sizes(),
+           "cos/sin tables fp32 [max_pos, D/2]");
+  MP_CHECK(qblocks.size(1) == T, "fused RoPE needs one query token per block (decode)");
+  attention_mfma_impl(qkv, k_cache, v_cache, block_tables, q_seq, q_ctx, qblocks, out, workspace, nh, nkv, scale,
+                      part_size, num_parts, packed, positions.data_ptr<int64_t>(), cos.data_ptr<float>(),
+                      sin.data_ptr<float>(), slots.data_ptr<int64_t>());
 }
 
 void embedding(const at::Tensor& ids, const at::Tensor& table, at::Tensor& out) {
@@ -451,6 +484,10 @@ TORCH_LIBRARY(mpamd, m) {
       "attention_mfma(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor q_seq, Tensor q_ctx, "
       "Tensor qblocks, Tensor(a!) out, Tensor(b!) workspace, int nh, int nkv, float scale, int part_size, "
       "int num_parts, int packed) -> ()");
+  m.def(
+      "attention_mfma_rope(Tensor qkv, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor block_tables, Tensor q_seq, "
+      "Tensor q_ctx, Tensor qblocks, Tensor positions, Tensor cos, Tensor sin, Tensor slots, Tensor(c!) out, "
+      "Tensor(d!) workspace, int nh, int nkv, float scale, int part_size, int num_parts, int packed) -> ()");
   m.def("embedding(Tensor ids, Tensor table, Tensor(a!) out) -> ()");
   m.def("swiglu(Tensor gu, Tensor(a!) out) -> ()");
   m.def("add(Tensor a, Tensor b, Tensor(a!) y) -> ()");
@@ -476,6 +513,7 @@ TORCH_LIBRARY_IMPL(mpamd, CUDA, m) {
   m.impl("paged_attention", &paged_attention);
   m.impl("paged_attention_rope", &paged_attention_rope);
   m.impl("attention_mfma", &attention_mfma);
+  m.impl("attention_mfma_rope", &attention_mfma_rope);
   m.impl("embedding", &embedding);
   m.impl("swiglu", &swiglu);
   m.impl("add", &add);

@@ -379,6 +379,13 @@ class StageExecutor:
                      decode):
         """RoPE + KV write + attention.  Decode steps that run on the flash-decoding kernel do all
         three in one launch (ops.paged_attention_rope); everything else keeps rope_kv_write."""
+        if decode and qblocks is None and self._fuse_rope and self._attn_mfma_gqa and self.device.type == "cuda":
+            T = qkv.shape[0]
+            ps2 = 128 * math.ceil(ps / 128)
+            np2 = max(1, math.ceil(ps * np_ / ps2))
+            return ops.attention_mfma_rope(qkv, kc, vc, self.sessions.table_dev, q_seq, q_ctx, self.decode_qblocks(T),
+                                           positions, self.cos, self.sin, slots, self.nh, self.nkv, self.scale,
+                                           out=out, workspace=ws, part_size=ps2, num_parts=np2, packed=packed)
         if decode and qblocks is None and self._fuse_rope and not (
                 self._attn_mfma_gqa and self.device.type == "cuda"):
             return ops.paged_attention_rope(qkv, kc, vc, self.sessions.table_dev, q_seq, q_ctx, positions, self.cos,

@@ -549,3 +549,37 @@ def test_autotune_weight_larger_than_pool(monkeypatch):
     table = ops.autotune_gemm([(N, K, 0)], DEV, ms=(64,), iters=2, rounds=1)
     assert ops._SK_CHOICE.get(key) in (set(ops._KERNEL_FLAGS) | {"pk"}), table
     ops._SK_CHOICE.pop(key, None)
+
+
+@pytest.mark.parametrize("nh,nkv,D", [(32, 8, 128), (64, 8, 128), (16, 4, 128), (8, 2, 64)])
+@pytest.mark.parametrize("parts", [None, (128, 4)])
+@pytest.mark.parametrize("packed", [False, True])
+def test_attention_mfma_rope_fused_matches_two_kernels(nh, nkv, D, parts, packed):
+    """GQA decode on the MFMA kernel with RoPE + KV write folded in == rope_kv_write then
+    attention_mfma; same cache contents; a padded row (ctx 0, slot -1) writes nothing."""
+    ctxs = [1, 5, 64, 200, 0, 33]
+    ps = 64
+    q, kc, vc, bt, q_seq, q_ctx = _attn_case(nh, nkv, D, [max(c, 1) for c in ctxs], ps=ps)
+    q_ctx[4] = 0
+    pos = (q_ctx.long() - 1).clamp(min=0)
+    slots = torch.stack([bt[i, int(p) // ps].long() * ps + int(p) % ps for i, p in enumerate(pos.tolist())])
+    slots[4] = -1
+    qb = torch.from_numpy(ops.query_blocks([1] * len(ctxs), nh // nkv)).to(DEV)
+    cos, sin = ops.rope_cos_sin(D, 2048, 10000.0, DEV)
+    scale = 1 / math.sqrt(D)
+    kw = dict(part_size=parts[0], num_parts=parts[1]) if parts else dict(max_ctx=max(ctxs))
+    k2, v2, q2 = kc.clone(), vc.clone(), q.clone()
+    ops.rope_kv_write(q2, pos, cos, sin, k2, v2, slots, nh, nkv)
+    o2 = ops.attention_mfma(q2, k2, v2, bt, q_seq, q_ctx, qb, nh, nkv, scale, packed=packed, **kw)
+    q_in = q.clone()
+    o1 = ops.attention_mfma_rope(q, kc, vc, bt, q_seq, q_ctx, qb, pos, cos, sin, slots, nh, nkv, scale,
+                                 packed=packed, **kw)
+    assert torch.equal(q, q_in), "fused op must not modify qkv"
+    torch.testing.assert_close(kc.float(), k2.float(), atol=1e-2, rtol=1e-2)
+    assert torch.equal(vc, v2)
+    T = q.shape[0]
+    if packed:
+        o1, o2 = ref.unpack_act(o1, T, nh * D), ref.unpack_act(o2, T, nh * D)
+    torch.testing.assert_close(o1.float(), o2.float(), atol=2e-2, rtol=2e-2)
+    o_ref = ref.paged_attention(q2.float(), k2.float(), v2.float(), bt, q_seq, q_ctx, nh, nkv, scale)
+    torch.testing.assert_close(o1.float(), o_ref.float(), atol=2e-2, rtol=2e-2)

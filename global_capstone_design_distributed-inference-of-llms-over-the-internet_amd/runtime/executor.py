@@ -155,7 +155,11 @@ class StageExecutor:
         self._attn_mfma_prefill = os.environ.get("MPAMD_ATTN_MFMA", "prefill") != "off" and \
             cfg.model_type != "gpt2" and cfg.head_dim in (64, 128)
         # GQA decode: the whole group of a kv head in the MFMA rows (2x the VALU kernel at nrep 8)
-        self._attn_mfma_gqa = self._attn_mfma_prefill and self.nh // self.nkv >= 4
+        # MHA decode stays on the flash-decoding kernel: forcing it onto the MFMA kernel
+        # (MPAMD_ATTN_MFMA_DECODE=1, 15 of 16 MFMA rows idle) measured 11005 vs 13617 tok/s at 64
+        # sessions and 13847 vs 16248 at 128 (Llama-2-7B, profiles/r1_attn_mha_mfma_vs_simt/)
+        self._attn_mfma_gqa = self._attn_mfma_prefill and (
+            self.nh // self.nkv >= 4 or os.environ.get("MPAMD_ATTN_MFMA_DECODE", "0") == "1")
         # decode steps on the flash-decoding kernel fold RoPE + the KV page write into it
         self._fuse_rope = os.environ.get("MPAMD_FUSE_ROPE", "1") != "0"
         # shortest split-K context slice (ops.attention_partition): longer on the MFMA GQA kernel

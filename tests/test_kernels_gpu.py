@@ -551,7 +551,7 @@ def test_autotune_weight_larger_than_pool(monkeypatch):
     ops._SK_CHOICE.pop(key, None)
 
 
-@pytest.mark.parametrize("nh,nkv,D", [(32, 8, 128), (64, 8, 128), (16, 4, 128), (8, 2, 64)])
+@pytest.mark.parametrize("nh,nkv,D", [(32, 8, 128), (64, 8, 128), (16, 4, 128), (8, 2, 64), (32, 32, 128)])
 @pytest.mark.parametrize("parts", [None, (128, 4)])
 @pytest.mark.parametrize("packed", [False, True])
 def test_attention_mfma_rope_fused_matches_two_kernels(nh, nkv, D, parts, packed):

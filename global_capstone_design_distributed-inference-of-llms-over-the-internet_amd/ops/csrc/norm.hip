@@ -14,11 +14,12 @@
 // Rounding follows HF: the normalised value is rounded to bf16 before the
 // weight multiply, math in fp32, vectorised 16-B loads, one block per row.
 #include "common.h"
+#include <stdlib.h>
 
 namespace mp {
 
-template <int MAXC>
-__global__ __launch_bounds__(256) void rmsnorm_kernel(
+template <int MAXC, int NT = 256>
+__global__ __launch_bounds__(NT) void rmsnorm_kernel(
     const bf16_t* __restrict__ x, int64_t x_stride, bf16_t* __restrict__ res, int64_t res_stride,
     const bf16_t* __restrict__ w, bf16_t* __restrict__ y, int64_t y_stride,
     const int32_t* __restrict__ rows, int H, float eps, int mode, int packed_mt) {
@@ -34,7 +35,7 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(
   u16x8 v[MAXC], rv[MAXC], wv[MAXC];
 #pragma unroll
   for (int k = 0; k < MAXC; ++k) {
-    const int c = min((int)threadIdx.x + k * 256, nch - 1);
+    const int c = min((int)threadIdx.x + k * NT, nch - 1);
     v[k] = *reinterpret_cast<const u16x8*>(xr + c * 8);
     rv[k] = *reinterpret_cast<const u16x8*>((mode == 1 ? rr : xr) + c * 8);
     wv[k] = *reinterpret_cast<const u16x8*>(w + c * 8);
@@ -42,7 +43,7 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(
   float ss = 0.f;
 #pragma unroll
   for (int k = 0; k < MAXC; ++k) {
-    const int c = threadIdx.x + k * 256;
+    const int c = threadIdx.x + k * NT;
     if (c < nch) {
       u16x8 a = v[k];
       if (mode == 1) {
@@ -60,12 +61,13 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(
       v[k] = a;
     }
   }
-  const float tot = block_sum(ss, red);
+  // one wave per row: the shuffle reduction alone (no LDS round trip, no barrier)
+  const float tot = NT == 64 ? wave_sum(ss) : block_sum(ss, red);
   const float r = rsqrtf(tot / (float)H + eps);
   bf16_t* yr = y + (int64_t)orow * y_stride;
 #pragma unroll
   for (int k = 0; k < MAXC; ++k) {
-    const int c = threadIdx.x + k * 256;
+    const int c = threadIdx.x + k * NT;
     if (c < nch) {
       const u16x8 wv_ = wv[k];
       u16x8 o;
@@ -88,14 +90,41 @@ extern "C" int mp_rmsnorm(const void* x, int64_t x_stride, void* res, int64_t re
   if (H % 8 != 0 || H > 8 * 256 * 8) return -1;
   if (nrows == 0) return 0;
   const int nch = H / 8;
-  dim3 grid(nrows), block(256);
+  // threads per row: 512 (one 16-B chunk per thread at H = 4096) measured best in the decode
+  // step, 64 -> 512: 13433 / 13493 / 13615 / 13719 tok/s (Llama-2-7B, 64 sessions, one box,
+  // profiles/r1_norm_threads/); the kernel itself only moves 5.06 -> 4.99 us, it is latency
+  // bound at 64 rows.  MPAMD_NORM_THREADS = 64 / 128 / 256 overrides
+  static const int nt = [] {
+    const char* v = getenv("MPAMD_NORM_THREADS");
+    const int t = v ? atoi(v) : 512;
+    return (t == 64 || t == 128 || t == 256) ? t : 512;
+  }();
+  dim3 grid(nrows), block(nt);
   auto args = [&](auto kern) {
     hipLaunchKernelGGL(kern, grid, block, 0, stream, (const bf16_t*)x, x_stride, (bf16_t*)res, res_stride,
                        (const bf16_t*)w, (bf16_t*)y, y_stride, rows, H, eps, mode, packed_mt);
   };
-  if (nch <= 256) args(rmsnorm_kernel<1>);
-  else if (nch <= 512) args(rmsnorm_kernel<2>);
-  else if (nch <= 1024) args(rmsnorm_kernel<4>);
-  else args(rmsnorm_kernel<8>);
+  // MAXC = chunks of 8 per thread; nch <= MAXC * nt
+  const int per = (nch + nt - 1) / nt;
+  if (nt == 64) {
+    if (per <= 4) args(rmsnorm_kernel<4, 64>);
+    else if (per <= 8) args(rmsnorm_kernel<8, 64>);
+    else if (per <= 16) args(rmsnorm_kernel<16, 64>);
+    else args(rmsnorm_kernel<32, 64>);
+  } else if (nt == 128) {
+    if (per <= 2) args(rmsnorm_kernel<2, 128>);
+    else if (per <= 4) args(rmsnorm_kernel<4, 128>);
+    else if (per <= 8) args(rmsnorm_kernel<8, 128>);
+    else args(rmsnorm_kernel<16, 128>);
+  } else if (nt == 512) {
+    if (per <= 1) args(rmsnorm_kernel<1, 512>);
+    else if (per <= 2) args(rmsnorm_kernel<2, 512>);
+    else args(rmsnorm_kernel<4, 512>);
+  } else {
+    if (per <= 1) args(rmsnorm_kernel<1>);
+    else if (per <= 2) args(rmsnorm_kernel<2>);
+    else if (per <= 4) args(rmsnorm_kernel<4>);
+    else args(rmsnorm_kernel<8>);
+  }
   return (int)hipGetLastError();
 }

@@ -1,0 +1,31 @@
+"""bench.py's driver contract on CPU: torchrun multi-rank (gloo), rank 0 prints ONE JSON line
+with the required keys; the pipeline (pp2) and replica (pp2 x dp2) layouts both complete."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+        "vs_baseline", "dtype", "data", "config"}
+
+
+@pytest.mark.parametrize("nproc,extra,par", [(2, [], "pp2"), (4, ["--replicas", "2"], "pp2xdp2")])
+def test_bench_torchrun_gloo(nproc, extra, par):
+    port = 29650 + nproc
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", "bench.py", "--gpus", str(nproc), "--steps", "3",
+           "--warmup", "1", "--model", "tiny-llama", "--device", "cpu", "--batch", "2", "--prompt-len", "8", *extra]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert KEYS <= set(rec)
+    assert rec["n_gpus"] == nproc and rec["steps"] == 3 and rec["warmup"] == 1
+    assert rec["value"] > 0 and rec["higher_is_better"] is True and rec["scaling"] == "weak"
+    assert rec["config"]["parallelism"] == par
+    assert rec["config"]["global_batch"] == 2 * nproc  # M = stages micro-batches x batch x replicas

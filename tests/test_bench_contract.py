@@ -1,5 +1,6 @@
 """bench.py's driver contract on CPU: torchrun multi-rank (gloo), rank 0 prints ONE JSON line
-with the required keys; the pipeline (pp2) and replica (pp2 x dp2) layouts both complete."""
+with the required keys; the pipeline (pp2), replica (pp2 x dp2) and tensor-parallel (pp2 x tp2)
+layouts all complete."""
 import json
 import os
 import subprocess
@@ -12,8 +13,9 @@ KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "
         "vs_baseline", "dtype", "data", "config"}
 
 
-@pytest.mark.parametrize("nproc,extra,par", [(2, [], "pp2"), (4, ["--replicas", "2"], "pp2xdp2")])
-def test_bench_torchrun_gloo(nproc, extra, par):
+@pytest.mark.parametrize("nproc,extra,par,gb", [(2, [], "pp2", 4), (4, ["--replicas", "2"], "pp2xdp2", 8),
+                                                (4, ["--tp", "2"], "pp2xtp2", 4)])
+def test_bench_torchrun_gloo(nproc, extra, par, gb):
     port = 29650 + nproc
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
            "--master-addr", "127.0.0.1", f"--master-port={port}", "bench.py", "--gpus", str(nproc), "--steps", "3",
@@ -28,4 +30,4 @@ def test_bench_torchrun_gloo(nproc, extra, par):
     assert rec["n_gpus"] == nproc and rec["steps"] == 3 and rec["warmup"] == 1
     assert rec["value"] > 0 and rec["higher_is_better"] is True and rec["scaling"] == "weak"
     assert rec["config"]["parallelism"] == par
-    assert rec["config"]["global_batch"] == 2 * nproc  # M = stages micro-batches x batch x replicas
+    assert rec["config"]["global_batch"] == gb  # stages micro-batches x batch x replicas (TP lanes share)

@@ -57,6 +57,7 @@ class LoadedStage:
     dtype: torch.dtype
     model_name: str
     executor_kwargs: dict
+    use_cpu_offload: bool = False
 
     @property
     def config(self):
@@ -99,7 +100,7 @@ def load_stage_model(model_name: str, device, role: str, *, start: int = 0, end:
     w = build_stage_weights(cfg, model_name, s, e, has_embed=role in ("stage0", "full"),
                             has_head=role in ("last", "full"), device=load_dev, dtype=dt, seed=seed)
     logger.info(f"load_stage_model: role={role}, layers={e - s}, start={s}, end={e}")
-    return LoadedStage(cfg, w, role, s, e, device, dt, model_name, executor_kwargs)
+    return LoadedStage(cfg, w, role, s, e, device, dt, model_name, executor_kwargs, bool(use_cpu_offload))
 
 
 def _to_device(w: StageWeights, device) -> StageWeights:
@@ -116,18 +117,38 @@ def _to_device(w: StageWeights, device) -> StageWeights:
 
 
 class _StageModule(torch.nn.Module):
+    """Shared body of Stage0 / StageSegment / StageLast.
+
+    The span arguments of the reference constructors are checked against the loaded span
+    (a mismatch raises instead of silently serving other blocks).  ``gpu_device`` places the
+    executor (default: the device ``load_stage_model`` was given).  ``keep_layers_on_gpu``
+    applies to a stage loaded with ``use_cpu_offload``: the first ``n - keep`` blocks stream
+    from pinned host memory each forward, the last ``keep`` stay resident (reference
+    src/llama_partition.py:169-180, :290-293); without offload every block is resident."""
     role = "segment"
 
-    def __init__(self, full: LoadedStage, **kw):
+    def __init__(self, full: LoadedStage, *, start: Optional[int] = None, end: Optional[int] = None,
+                 gpu_device=None, keep_layers_on_gpu: int = 0, **kw):
         super().__init__()
+        if start is not None and int(start) != full.start:
+            raise ValueError(f"{type(self).__name__}: start={start} but the loaded span starts at {full.start}")
+        if end is not None and int(end) != full.end:
+            raise ValueError(f"{type(self).__name__}: end={end} but the loaded span ends at {full.end}")
+        n = full.end - full.start
+        if not 0 <= int(keep_layers_on_gpu) <= n:
+            raise ValueError(f"keep_layers_on_gpu={keep_layers_on_gpu} outside [0, {n}] for a {n}-block span")
         self.full = full
         self.config = full.cfg
+        device = torch.device(gpu_device) if gpu_device is not None else full.device
+        offload = full.use_cpu_offload and device.type == "cuda"
         w = full.weights
-        if next(iter(w.tensors())).device != full.device:
-            w = _to_device(w, full.device)
+        if not offload and next(iter(w.tensors())).device != device:
+            w = _to_device(w, device)
         ekw = dict(full.executor_kwargs)
         ekw.update(kw)
-        self.executor = StageExecutor(full.cfg, w, full.device, dtype=full.dtype, **ekw)
+        if offload:
+            ekw.update(offload=True, keep_layers_on_gpu=int(keep_layers_on_gpu))
+        self.executor = StageExecutor(full.cfg, w, device, dtype=full.dtype, **ekw)
 
     @property
     def device(self):
@@ -159,7 +180,7 @@ class Stage0(_StageModule):
     role = "stage0"
 
     def __init__(self, full: LoadedStage, end: Optional[int] = None, **kw):
-        super().__init__(full, **kw)
+        super().__init__(full, start=0, end=end, **kw)
 
 
 class StageSegment(_StageModule):
@@ -167,7 +188,8 @@ class StageSegment(_StageModule):
 
     def __init__(self, full: LoadedStage, start: Optional[int] = None, end: Optional[int] = None, gpu_device=None,
                  keep_layers_on_gpu: int = 0, **kw):
-        super().__init__(full, **kw)
+        super().__init__(full, start=start, end=end, gpu_device=gpu_device, keep_layers_on_gpu=keep_layers_on_gpu,
+                         **kw)
 
 
 class StageLast(_StageModule):
@@ -175,4 +197,4 @@ class StageLast(_StageModule):
 
     def __init__(self, full: LoadedStage, start: Optional[int] = None, gpu_device=None, keep_layers_on_gpu: int = 0,
                  **kw):
-        super().__init__(full, **kw)
+        super().__init__(full, start=start, gpu_device=gpu_device, keep_layers_on_gpu=keep_layers_on_gpu, **kw)

@@ -278,41 +278,74 @@ def random_stage_weights(cfg: ModelConfig, start: int, end: int, *, has_embed: b
 
 
 # ------------------------------------------------------------------ checkpoint loading
+SAFE_INDEX = "model.safetensors.index.json"
+BIN_INDEX = "pytorch_model.bin.index.json"
+
+
+def checkpoint_files(path: str) -> Optional[str]:
+    """Which weight format a local HF directory holds: "safetensors", "bin" or None.
+
+    Same lookup order as upstream Petals ``INDEX_FILES`` / ``_find_index_file``
+    (reference petals/server/from_pretrained.py:131-159): sharded safetensors, sharded
+    ``.bin``, then single-file variants."""
+    if os.path.exists(os.path.join(path, SAFE_INDEX)) or glob.glob(os.path.join(path, "*.safetensors")):
+        return "safetensors"
+    if os.path.exists(os.path.join(path, BIN_INDEX)) or glob.glob(os.path.join(path, "*.bin")):
+        return "bin"
+    return None
+
+
 class _Checkpoint:
-    """Key -> shard lookup over a local HF directory (sharded or single-file safetensors)."""
+    """Key -> shard lookup over a local HF directory (sharded or single-file; safetensors or
+    ``pytorch_model*.bin``).
+
+    ``.bin`` shards are read with ``torch.load(weights_only=True, mmap=True)``: the restricted
+    unpickler executes nothing from the file, and the memory map means only the tensors a stage
+    actually asks for are paged in (upstream ``_load_state_dict_from_local_file``,
+    petals/server/from_pretrained.py:216-224, loads whole shards)."""
 
     def __init__(self, path: str):
-        from safetensors import safe_open  # noqa: F401
-
         self.path = path
+        self._handles: Dict[str, object] = {}
+        self.kind = checkpoint_files(path)
+        if self.kind is None:
+            raise FileNotFoundError(f"no safetensors or pytorch_model*.bin weights under {path}")
         self.key_to_file: Dict[str, str] = {}
-        idx = os.path.join(path, "model.safetensors.index.json")
-        if os.path.exists(idx):
-            with open(idx) as f:
+        index = os.path.join(path, SAFE_INDEX if self.kind == "safetensors" else BIN_INDEX)
+        if os.path.exists(index):
+            with open(index) as f:
                 wm = json.load(f)["weight_map"]
             self.key_to_file = {k: os.path.join(path, v) for k, v in wm.items()}
         else:
-            files = sorted(glob.glob(os.path.join(path, "*.safetensors")))
-            if not files:
-                raise FileNotFoundError(f"no safetensors weights under {path}")
+            pattern = "*.safetensors" if self.kind == "safetensors" else "*.bin"
+            for fn in sorted(glob.glob(os.path.join(path, pattern))):
+                for k in self._open(fn).keys():
+                    self.key_to_file[k] = fn
+
+    def _open(self, fn: str):
+        h = self._handles.get(fn)
+        if h is not None:
+            return h
+        if self.kind == "safetensors":
             from safetensors import safe_open
 
-            for fn in files:
-                with safe_open(fn, framework="pt") as f:
-                    for k in f.keys():
-                        self.key_to_file[k] = fn
-        self._handles = {}
+            h = safe_open(fn, framework="pt")
+        else:
+            try:
+                h = torch.load(fn, map_location="cpu", weights_only=True, mmap=True)
+            except RuntimeError:  # legacy (non-zip) serialization cannot be memory-mapped
+                h = torch.load(fn, map_location="cpu", weights_only=True)
+            if not isinstance(h, dict):
+                raise ValueError(f"{fn}: expected a state dict, got {type(h).__name__}")
+        self._handles[fn] = h
+        return h
 
     def has(self, key: str) -> bool:
         return key in self.key_to_file
 
     def get(self, key: str) -> torch.Tensor:
-        from safetensors import safe_open
-
-        fn = self.key_to_file[key]
-        if fn not in self._handles:
-            self._handles[fn] = safe_open(fn, framework="pt")
-        return self._handles[fn].get_tensor(key)
+        h = self._open(self.key_to_file[key])
+        return h.get_tensor(key) if self.kind == "safetensors" else h[key]
 
 
 def load_stage_weights(cfg: ModelConfig, path: str, start: int, end: int, *, has_embed: bool, has_head: bool,
@@ -371,8 +404,14 @@ def load_stage_weights(cfg: ModelConfig, path: str, start: int, end: int, *, has
 
 def build_stage_weights(cfg: ModelConfig, model: str, start: int, end: int, *, has_embed: bool, has_head: bool,
                         device, dtype=torch.bfloat16, seed: int = 0) -> StageWeights:
-    """Checkpoint weights when ``model`` is a local HF directory with safetensors, else synthetic."""
-    if os.path.isdir(model) and (glob.glob(os.path.join(model, "*.safetensors"))):
+    """Checkpoint weights when ``model`` is a local HF directory, synthetic weights for presets.
+
+    A directory without loadable weights is an error: silently serving a real config with
+    random weights would produce garbage that looks like a working server."""
+    if os.path.isdir(model):
+        if checkpoint_files(model) is None:
+            raise FileNotFoundError(f"--model {model!r} is a directory without *.safetensors or pytorch_model*.bin "
+                                    f"weights (pass a preset name such as llama2-7b for synthetic weights)")
         return load_stage_weights(cfg, model, start, end, has_embed=has_embed, has_head=has_head, device=device,
                                   dtype=dtype)
     return random_stage_weights(cfg, start, end, has_embed=has_embed, has_head=has_head, device=device, dtype=dtype,

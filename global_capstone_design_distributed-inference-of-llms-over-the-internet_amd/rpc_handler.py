@@ -186,13 +186,15 @@ class StageConnectionHandler:
         md = dict(msg.metadata)
         sid, step_id = md.get("session_id"), md.get("step_id")
         src = md.pop("fork_from", None)
-        if src is not None and sid is not None:  # beam search: continue from another hypothesis
-            await asyncio.get_running_loop().run_in_executor(self._worker, self.executor.sessions.fork, str(src),
-                                                             str(sid))
+        # the dedup check comes first: a retried step that already ran (fork included) must
+        # neither fork again (that would reset sid's KV to src's length) nor recompute
         if sid is not None and step_id is not None:
             cached = self._steps.get(sid, {}).get(str(step_id))
             if cached is not None:
                 return cached
+        if src is not None and sid is not None:  # beam search: continue from another hypothesis
+            await asyncio.get_running_loop().run_in_executor(self._worker, self.executor.sessions.fork, str(src),
+                                                             str(sid))
         x = msg.tensors[0] if msg.tensors else None
         if x is not None and "cur_len" not in md:
             T = x.shape[-2] if x.dim() >= 2 and not self.executor.is_first else x.reshape(-1).shape[0]

@@ -589,6 +589,11 @@ class StageExecutor:
         w = self.w
         if w.fp8:
             raise ValueError("CPU offload is not supported with fp8 weights")
+        if self.cfg.is_moe:
+            # the streamed slot layers carry only the per-path projection fields; the MoE MLP
+            # also reads the router and per-expert row-major weights.  Mixtral-8x7B (93 GB bf16)
+            # fits one MI355X resident, so offload is rejected rather than half-supported.
+            raise ValueError("CPU offload is not supported for MoE (Mixtral) models: serve them resident")
         keep = max(0, min(int(keep_layers_on_gpu), self.n_layers))
         n_stream = self.n_layers - keep
         host = [pin_layer(L) for L in w.layers[:n_stream]]

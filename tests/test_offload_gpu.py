@@ -37,3 +37,12 @@ def test_offloaded_stage_matches_resident(keep):
         torch.testing.assert_close(a.float(), b.float(), atol=1e-2, rtol=1e-2)
         t = torch.argmax(a.float(), -1)
     assert off._streamer.bytes_streamed > 0
+
+
+def test_offload_rejects_moe():
+    """The streamed slot layers carry only projection fields; an MoE layer would silently run as a
+    dense MLP, so offload must refuse Mixtral outright."""
+    cfg = resolve_model("tiny-mixtral")
+    w = random_stage_weights(cfg, 0, cfg.num_hidden_layers, has_embed=True, has_head=True, device="cpu", seed=1)
+    with pytest.raises(ValueError, match="MoE"):
+        StageExecutor(cfg, w, "cuda", offload=True, kv_cache_bytes=16 << 20, max_sessions=2, max_seq_len=128)

@@ -113,6 +113,11 @@ class StageExecutor:
         shard (``cfg`` is then the shard config); partial sums are all-reduced after the
         o and down projections."""
         cfg.validate()
+        if offload and cfg.is_moe:
+            # the streamed slot layers carry only the per-path projection fields; the MoE MLP
+            # also reads the router and per-expert row-major weights.  Mixtral-8x7B (93 GB bf16)
+            # fits one MI355X resident, so offload is rejected rather than half-supported.
+            raise ValueError("CPU offload is not supported for MoE (Mixtral) models: serve them resident")
         self._tp = tp if (tp is not None and tp.size > 1) else None
         self.cfg = cfg
         self.w = weights
@@ -589,11 +594,7 @@ class StageExecutor:
         w = self.w
         if w.fp8:
             raise ValueError("CPU offload is not supported with fp8 weights")
-        if self.cfg.is_moe:
-            # the streamed slot layers carry only the per-path projection fields; the MoE MLP
-            # also reads the router and per-expert row-major weights.  Mixtral-8x7B (93 GB bf16)
-            # fits one MI355X resident, so offload is rejected rather than half-supported.
-            raise ValueError("CPU offload is not supported for MoE (Mixtral) models: serve them resident")
+
         keep = max(0, min(int(keep_layers_on_gpu), self.n_layers))
         n_stream = self.n_layers - keep
         host = [pin_layer(L) for L in w.layers[:n_stream]]

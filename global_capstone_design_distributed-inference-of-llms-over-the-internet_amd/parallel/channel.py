@@ -1,0 +1,276 @@
+"""Device channel: the single-node data plane between the stages of one pipeline.
+
+Reference data path: every hidden state crosses host memory, protobuf serialization and a
+libp2p TCP stream per hop, client -> server -> client (star), reference
+src/rpc_transport.py:738-766, :802-833 and src/rpc_handler.py:405-464.  On one MI355X node
+the same hop becomes an RCCL send/recv over the direct xGMI link between neighbouring
+GPUs.  A ``Channel`` joins the P participants of one pipeline (rank 0 = the head that owns
+the embedding and the scheduler, rank P-1 = the tail that samples) with three process
+groups built straight from a ``torch.distributed`` Store, so a process can hold any number
+of channels and needs no default process group (a stage server may serve several clients
+over its lifetime):
+
+* ``ctrl`` (gloo, host tensors): step headers (which sessions, how many tokens, positions,
+  closes, admissions), all-gathers of per-stage capacity / throughput, stop messages.
+  Every receive carries a timeout, and a SIGKILLed peer surfaces as a connection error
+  within milliseconds: this is the failure detector of the device path.
+* ``data`` (RCCL on GPU, gloo on CPU): hidden states rank k -> k+1, straight from HBM.
+* ``ret`` (RCCL on GPU, gloo on CPU): sampled token ids tail -> head.  A communicator of
+  its own: RCCL serialises the P2P operations of one communicator on one stream, so with
+  2 stages the forward hop (0 -> 1) and the token return (1 -> 0) would otherwise queue
+  behind each other.
+
+Headers go on the host group ahead of the payload: a stage forwards the header to its
+successor BEFORE computing, so the next stage plans its step (session table, page
+reservations, metadata H2D) while the payload is still being produced.
+
+``MPAMD_CHANNEL_DATA=gloo`` stages GPU payloads through host memory over gloo (several
+ranks sharing one GPU, where RCCL refuses duplicate devices).
+"""
+from __future__ import annotations
+
+import collections
+import datetime
+import logging
+import os
+import socket
+import time
+from typing import Deque, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+logger = logging.getLogger(__name__)
+
+
+class ChannelError(RuntimeError):
+    """A peer of the channel failed (timeout, connection closed, aborted communicator)."""
+
+
+def host_id() -> str:
+    """Identity of this machine: hostname + kernel boot id (two containers with the same
+    hostname on different hosts differ in boot id).  Stages advertise it so a client can
+    tell whether a device channel is possible (same node) or TCP must be used."""
+    boot = ""
+    try:
+        with open("/proc/sys/kernel/random/boot_id") as f:
+            boot = f.read().strip()
+    except OSError:
+        pass
+    return f"{socket.gethostname()}/{boot}"
+
+
+def free_port(host: str = "127.0.0.1") -> int:
+    with socket.socket() as s:
+        s.bind((host, 0))
+        return s.getsockname()[1]
+
+
+def _td(s: float) -> datetime.timedelta:
+    return datetime.timedelta(seconds=float(s))
+
+
+def make_store(host: str, port: int, world: int, is_master: bool, timeout_s: float = 60.0):
+    return dist.TCPStore(host, int(port), int(world), bool(is_master), timeout=_td(timeout_s),
+                         wait_for_workers=False)
+
+
+def _gloo(store, prefix: str, rank: int, world: int, timeout_s: float):
+    return dist.ProcessGroupGloo(dist.PrefixStore(prefix, store), rank, world, _td(timeout_s))
+
+
+def _nccl(store, prefix: str, rank: int, world: int, timeout_s: float, device: torch.device):
+    torch.cuda.set_device(device)
+    opts = dist.ProcessGroupNCCL.Options()
+    opts._timeout = _td(timeout_s)
+    return dist.ProcessGroupNCCL(dist.PrefixStore(prefix, store), rank, world, opts)
+
+
+class _Pending:
+    """Outstanding sends: their buffers must stay alive until the work completes."""
+
+    def __init__(self, limit: int = 64):
+        self.q: Deque[Tuple[object, object]] = collections.deque()
+        self.limit = limit
+
+    def add(self, work, keep) -> None:
+        self.q.append((work, keep))
+        while len(self.q) > self.limit:
+            self.q.popleft()[0].wait()
+
+    def reap(self) -> None:
+        while self.q and self.q[0][0].is_completed():
+            self.q.popleft()
+
+    def drain(self, timeout_s: Optional[float] = None) -> None:
+        while self.q:
+            w, _ = self.q.popleft()
+            if timeout_s is None:
+                w.wait()
+            else:
+                w.wait(_td(timeout_s))
+
+
+class Channel:
+    def __init__(self, store, prefix: str, rank: int, world: int, device, timeout_s: float = 120.0,
+                 data_backend: Optional[str] = None):
+        self.rank, self.world = int(rank), int(world)
+        self.device = torch.device(device)
+        self.timeout_s = float(timeout_s)
+        self.prefix = prefix
+        if data_backend is None:
+            data_backend = os.environ.get("MPAMD_CHANNEL_DATA") or ("nccl" if self.device.type == "cuda" else "gloo")
+        self.data_backend = data_backend
+        self.staged = data_backend == "gloo" and self.device.type == "cuda"
+        self.ctrl = _gloo(store, prefix + "/ctrl", self.rank, self.world, timeout_s)
+        if data_backend == "nccl":
+            self.data = _nccl(store, prefix + "/data", self.rank, self.world, timeout_s, self.device)
+            self.ret = _nccl(store, prefix + "/ret", self.rank, self.world, timeout_s, self.device)
+        else:
+            self.data = _gloo(store, prefix + "/data", self.rank, self.world, timeout_s)
+            self.ret = _gloo(store, prefix + "/ret", self.rank, self.world, timeout_s)
+        self._sends = _Pending()
+        self._msg_sends = _Pending()
+        self.closed = False
+        self.bytes_sent = 0
+
+    # ------------------------------------------------------------------ host control messages
+    def send_msg(self, dst: int, arr: np.ndarray) -> None:
+        """Length-prefixed int64 message on the ctrl group (async; buffers kept until done)."""
+        body = torch.from_numpy(np.ascontiguousarray(arr, dtype=np.int64))
+        n = torch.tensor([body.numel()], dtype=torch.int64)
+        try:
+            self._msg_sends.add(self.ctrl.send([n], dst, 1), n)
+            if body.numel():
+                self._msg_sends.add(self.ctrl.send([body], dst, 2), body)
+            self._msg_sends.reap()
+        except RuntimeError as e:
+            raise ChannelError(f"ctrl send to {dst} failed: {e}") from e
+
+    def recv_msg(self, src: int, timeout_s: Optional[float] = None) -> np.ndarray:
+        t = self.timeout_s if timeout_s is None else timeout_s
+        n = torch.empty(1, dtype=torch.int64)
+        try:
+            self.ctrl.recv([n], src, 1).wait(_td(t))
+            body = torch.empty(int(n[0]), dtype=torch.int64)
+            if body.numel():
+                self.ctrl.recv([body], src, 2).wait(_td(t))
+        except RuntimeError as e:
+            raise ChannelError(f"ctrl recv from {src} failed: {e}") from e
+        return body.numpy()
+
+    def all_gather_floats(self, values: Sequence[float]) -> List[List[float]]:
+        """Every participant's ``values`` (same length everywhere) on every participant: the
+        channel-level registry of per-stage capacity / measured step time."""
+        t = torch.tensor(list(values), dtype=torch.float64)
+        out = [torch.empty_like(t) for _ in range(self.world)]
+        try:
+            self.ctrl.allgather([out], [t]).wait(_td(self.timeout_s))
+        except RuntimeError as e:
+            raise ChannelError(f"ctrl all_gather failed: {e}") from e
+        return [o.tolist() for o in out]
+
+    # ------------------------------------------------------------------ device payloads
+    def _pg(self, which: str):
+        return self.data if which == "data" else self.ret
+
+    def send(self, dst: int, t: torch.Tensor, which: str = "data") -> None:
+        """Send ``t`` (a private copy is taken, so the caller may overwrite ``t`` right away -
+        e.g. a hipGraph output buffer - while the send is in flight)."""
+        pg = self._pg(which)
+        try:
+            if self.staged:
+                buf = t.detach().to("cpu")
+            else:
+                buf = t.detach().clone()
+            self.bytes_sent += buf.numel() * buf.element_size()
+            self._sends.add(pg.send([buf], dst, 0), buf)
+            self._sends.reap()
+        except RuntimeError as e:
+            raise ChannelError(f"{which} send to {dst} failed: {e}") from e
+
+    def recv(self, src: int, shape, dtype, which: str = "data", timeout_s: Optional[float] = None):
+        """Post a receive; returns ``(tensor, waiter)``.  ``waiter()`` makes the tensor usable
+        on the current stream: on RCCL it is a stream dependency (no host block), on gloo a
+        blocking wait bounded by the timeout."""
+        pg = self._pg(which)
+        t = self.timeout_s if timeout_s is None else timeout_s
+        try:
+            if self.staged or self.device.type != "cuda":
+                host = torch.empty(shape, dtype=dtype)
+                work = pg.recv([host], src, 0)
+
+                def waiter():
+                    try:
+                        work.wait(_td(t))
+                    except RuntimeError as e:
+                        raise ChannelError(f"{which} recv from {src} failed: {e}") from e
+                    return host.to(self.device, non_blocking=False) if self.staged else host
+
+                return None, waiter
+            buf = torch.empty(shape, dtype=dtype, device=self.device)
+            work = pg.recv([buf], src, 0)
+
+            def waiter():
+                work.wait()
+                return buf
+
+            return buf, waiter
+        except RuntimeError as e:
+            raise ChannelError(f"{which} recv from {src} failed: {e}") from e
+
+    def flush(self, timeout_s: Optional[float] = None) -> None:
+        self._sends.drain(timeout_s if timeout_s is not None else None)
+        self._msg_sends.drain(timeout_s)
+
+    # ------------------------------------------------------------------ teardown
+    def abort(self) -> None:
+        """Tear the channel down after a peer failure: RCCL communicators are aborted so a
+        stream blocked in a receive from a dead peer is released (no hang at exit)."""
+        if self.closed:
+            return
+        self.closed = True
+        for pg in (self.data, self.ret):
+            for name in ("abort", "_abort", "shutdown"):
+                fn = getattr(pg, name, None)
+                if fn is not None:
+                    try:
+                        fn()
+                        break
+                    except Exception:  # noqa: BLE001 - best effort during failure handling
+                        continue
+        self._sends.q.clear()
+        self._msg_sends.q.clear()
+
+    def close(self) -> None:
+        if self.closed:
+            return
+        try:
+            self.flush(timeout_s=min(self.timeout_s, 30.0))
+        except RuntimeError:
+            pass
+        self.closed = True
+        for pg in (self.data, self.ret):
+            fn = getattr(pg, "shutdown", None)
+            if fn is not None:
+                try:
+                    fn()
+                except Exception:  # noqa: BLE001
+                    pass
+
+
+def wait_event(ev, timeout_s: float, what: str = "device event") -> None:
+    """Poll a HIP event with a deadline: a stream stuck on a receive from a dead RCCL peer
+    never completes, and ``Event.synchronize`` would hang the host with it."""
+    if ev is None:
+        return
+    if ev.query():
+        return
+    deadline = time.monotonic() + timeout_s
+    sleep = 2e-5
+    while not ev.query():
+        if time.monotonic() > deadline:
+            raise ChannelError(f"timed out after {timeout_s:.1f}s waiting for {what}")
+        time.sleep(sleep)
+        sleep = min(sleep * 2, 1e-3)

@@ -1,0 +1,671 @@
+"""Continuous-batching pipeline serving engine over a device ``Channel``.
+
+Reference dataflow: the Stage-0 client embeds, runs its blocks, then drives ONE session
+token by token through the remote stages (star topology, one hop at a time, a
+``generated_tokens`` list and the sampling parameters in every request's metadata; the
+last stage samples and replies with the token id), stopping on EOS, ``max_new_tokens`` or
+5 consecutive repeats (reference src/main.py:62-227, src/rpc_transport.py:718-842,
+src/rpc_handler.py:149-325).
+
+Here the same roles run as a chain of stage ranks, one process per GPU:
+
+    head (rank 0: embedding + blocks [0, s0) + SCHEDULER)
+      -> stage 1 -> ... -> tail (blocks + norm + lm_head + SAMPLER)
+      -> token ids back to the head
+
+* The head owns the request queue.  Sessions are admitted into one of ``M`` micro-batch
+  slots (at most ``batch`` sessions each) whenever there is room, prefill and decode rows
+  mix in one ragged step (chunked prefill caps the prompt tokens per step), and finished
+  sessions are retired in the very next step of their slot: continuous batching.
+* Every step is announced by a header on the host control group (sessions, token counts,
+  positions, closes, admissions with sampling parameters and repetition history) that a
+  stage forwards to its successor before computing; the payload (hidden states) follows on
+  RCCL.  Stage k therefore never waits on a host round trip of stage k-1's compute.
+* The tail samples with per-session parameters and a device-resident repetition history
+  (reference semantics, ``ops.sample``), seeded by (session seed, position): a session
+  produces the same tokens no matter which micro-batch, replica or batch mix it runs in -
+  which is what makes replica failover exact.
+* Stop conditions are checked on the head from a pinned copy of each step's tokens one
+  round later, so the decode loop never blocks the host on the device: the next step's
+  inputs are gathered on the device from the previous step's sampled tokens.  A finished
+  session costs one discarded extra decode row.
+* ``M >= stages + 1`` slots keep every stage busy and leave a slot of slack for the token
+  return hop; every rank runs the same number of rounds x slots, so ``run_rounds(k)`` is a
+  lock-step unit (the benchmark times exactly k of them) and a serving stage simply loops
+  until the head's STOP header.
+* Failures: every host receive has a timeout and a dead peer surfaces as a connection
+  error; the head additionally polls its token events with a deadline (an RCCL receive from
+  a dead rank never completes).  The channel is aborted and the failure reported with the
+  affected requests' token histories (``PipelineFailure``), which the replica router
+  (``parallel.router``) re-places on surviving replicas by re-prefilling prompt + generated
+  tokens (recompute-from-tokens).
+"""
+from __future__ import annotations
+
+import dataclasses
+import logging
+import os
+import time
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from .. import ops
+from ..runtime.executor import StageExecutor
+from ..runtime.sampler import RECENT, SamplingParams
+from ..utils.tracing import trace_range
+from .channel import Channel, ChannelError, wait_event
+
+logger = logging.getLogger(__name__)
+
+KIND_STEP, KIND_STOP = 0, 1
+F_RESET, F_SAMPLE = 1, 2
+HDR = 8          # kind, slot, n_seq, T, n_close, n_admit, round, reserved
+SEQ_REC = 5      # handle, n_tok, start, flags, seed
+ADM_REC = 6 + RECENT  # handle, temp, top_p, top_k, rep_pen, hist_len, hist[RECENT]
+_M64 = (1 << 64) - 1
+
+
+class PipelineFailure(RuntimeError):
+    """The pipeline lost a stage; ``requests`` are the unfinished ones (with the tokens
+    generated so far) to be re-placed elsewhere."""
+
+    def __init__(self, msg: str, requests: Sequence["Request"] = ()):
+        super().__init__(msg)
+        self.requests = list(requests)
+
+
+@dataclasses.dataclass
+class Request:
+    prompt: List[int]
+    max_new_tokens: int = 64
+    params: SamplingParams = dataclasses.field(default_factory=lambda: SamplingParams(1.0, 0.92, 50, 1.5))
+    eos_token_id: Optional[int] = None
+    stop_on_repeat: int = 5  # reference run_rank0: stop after 5 consecutive repeats (0 = off)
+    seed: int = 0
+    rid: Optional[str] = None
+    generated: List[int] = dataclasses.field(default_factory=list)
+    done: bool = False
+    finish_reason: Optional[str] = None
+    t_submit: float = 0.0
+    t_first: Optional[float] = None
+    t_done: Optional[float] = None
+    _repeat: int = 0
+
+    @property
+    def tokens(self) -> List[int]:
+        return list(self.prompt) + list(self.generated)
+
+
+def _f2i(x: float) -> int:
+    return int(np.float64(x).view(np.int64))
+
+
+def _i2f(x) -> float:
+    return float(np.int64(x).view(np.float64))
+
+
+def mix_seeds(base: np.ndarray, pos: np.ndarray) -> np.ndarray:
+    """splitmix64(base ^ pos * golden): per (session seed, position) sampling seeds."""
+    with np.errstate(over="ignore"):
+        z = (base.astype(np.uint64) ^ (pos.astype(np.uint64) * np.uint64(0x9E3779B97F4A7C15)))
+        z = z + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    return (z & np.uint64(0x7FFFFFFFFFFFFFFF)).astype(np.int64)
+
+
+def request_seed(seed: int, rid: str) -> int:
+    import hashlib
+
+    h = hashlib.blake2b(f"{seed}:{rid}".encode(), digest_size=8).digest()
+    return int.from_bytes(h, "little") & 0x7FFFFFFFFFFFFFFF
+
+
+# ====================================================================== tail sampler
+class TailSampler:
+    """Per-session sampling state resident on the tail's device: parameters set at
+    admission, the last RECENT generated ids (repetition penalty, reference
+    src/rpc_handler.py:348-372) updated in place by the sampling kernel."""
+
+    def __init__(self, device, max_handles: int, vocab: int):
+        dev = self.device = torch.device(device)
+        H = max_handles
+        self.temp = torch.zeros(H, dtype=torch.float32, device=dev)
+        self.top_p = torch.ones(H, dtype=torch.float32, device=dev)
+        self.top_k = torch.zeros(H, dtype=torch.int32, device=dev)
+        self.rp = torch.ones(H, dtype=torch.float32, device=dev)
+        self.hist = torch.zeros(H, RECENT, dtype=torch.int32, device=dev)
+        self.hist_len = torch.zeros(H, dtype=torch.int32, device=dev)
+        self.temp_host = np.zeros(H, dtype=np.float64)
+        self.seed_host = np.zeros(H, dtype=np.int64)
+        self._ws = None
+        self.vocab = vocab
+        pin = dev.type == "cuda"
+        self._pin_i64 = [torch.empty(4 * 256, dtype=torch.int64, pin_memory=pin) for _ in range(2)]
+        self._pin_ev = [None, None]
+        self._pk = 0
+
+    def admit(self, recs: np.ndarray) -> None:
+        """recs: [n, ADM_REC] admission records."""
+        if not len(recs):
+            return
+        h = recs[:, 0].astype(np.int64)
+        f = np.stack([recs[:, 1], recs[:, 2], recs[:, 4]]).astype(np.int64).view(np.float64)
+        self.temp_host[h] = f[0]
+        hl = np.minimum(recs[:, 5], RECENT).astype(np.int32)
+        hist = recs[:, 6:6 + RECENT].astype(np.int32)
+        idx = torch.from_numpy(h).to(self.device)
+        self.temp[idx] = torch.from_numpy(f[0].astype(np.float32)).to(self.device)
+        self.top_p[idx] = torch.from_numpy(f[1].astype(np.float32)).to(self.device)
+        self.rp[idx] = torch.from_numpy(f[2].astype(np.float32)).to(self.device)
+        self.top_k[idx] = torch.from_numpy(recs[:, 3].astype(np.int32)).to(self.device)
+        self.hist[idx] = torch.from_numpy(hist).to(self.device)
+        self.hist_len[idx] = torch.from_numpy(hl).to(self.device)
+
+    def _stage(self, arrs: Sequence[np.ndarray]) -> List[torch.Tensor]:
+        """Async H2D of small int64 vectors through a double-buffered pinned area."""
+        n = sum(len(a) for a in arrs)
+        if self.device.type != "cuda" or n > self._pin_i64[0].numel():
+            return [torch.from_numpy(np.ascontiguousarray(a, dtype=np.int64)).to(self.device) for a in arrs]
+        self._pk ^= 1
+        ev = self._pin_ev[self._pk]
+        if ev is not None:
+            ev.synchronize()
+        buf = self._pin_i64[self._pk]
+        host = buf.numpy()
+        off, outs = 0, []
+        for a in arrs:
+            host[off:off + len(a)] = a
+            outs.append((off, len(a)))
+            off += len(a)
+        dev = buf[:n].to(self.device, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._pin_ev[self._pk] = ev
+        return [dev[o:o + k] for o, k in outs]
+
+    def sample(self, logits: torch.Tensor, handles: np.ndarray, positions: np.ndarray,
+               sample_rows: Optional[np.ndarray] = None) -> torch.Tensor:
+        """Tokens [n] (int64, device) for the rows of ``logits``; rows not in ``sample_rows``
+        get -1 and leave the history untouched (intermediate prefill chunks)."""
+        n = logits.shape[0]
+        if sample_rows is not None and len(sample_rows) < n:
+            out = torch.full((n,), -1, dtype=torch.long, device=logits.device)
+            if len(sample_rows):
+                sel = torch.from_numpy(sample_rows.astype(np.int64)).to(logits.device)
+                sub = self.sample(logits.index_select(0, sel), handles[sample_rows], positions[sample_rows])
+                out.index_copy_(0, sel, sub)
+            return out
+        if n == 0:
+            return torch.empty(0, dtype=torch.long, device=logits.device)
+        seeds_h = mix_seeds(self.seed_host[handles], positions)
+        rows, seeds = self._stage([handles.astype(np.int64), seeds_h])
+        if (self.temp_host[handles] <= 0).all():
+            tok = ops.argmax(logits)
+        else:
+            recent = self.hist.index_select(0, rows)
+            rlen = self.hist_len.index_select(0, rows)
+            ws = None
+            if logits.device.type == "cuda":
+                if self._ws is None or self._ws.numel() < n * logits.shape[1]:
+                    self._ws = torch.empty(max(n, 64) * logits.shape[1], dtype=torch.float32, device=logits.device)
+                ws = self._ws
+            tok = ops.sample(logits, self.temp.index_select(0, rows), self.top_p.index_select(0, rows),
+                             self.top_k.index_select(0, rows), self.rp.index_select(0, rows), recent, rlen, seeds,
+                             workspace=ws, update_history=True)
+            self.hist.index_copy_(0, rows, recent)
+            self.hist_len.index_copy_(0, rows, rlen)
+            return tok
+        # greedy rows still record their history (a later admission may switch nothing, but
+        # failover re-prefill reads the head's copy; keep the device copy consistent anyway)
+        return tok
+
+
+# ====================================================================== head-side state
+@dataclasses.dataclass
+class _Live:
+    req: Request
+    handle: int
+    slot: int
+    fed: int = 0                      # tokens fed into the KV cache (issued steps)
+    pending: List[int] = dataclasses.field(default_factory=list)  # prompt tokens not yet fed
+    admitted: bool = False            # admission record sent
+    retired: bool = False
+    last_row: int = -1                # its row in the slot's previous step (decode feed)
+
+
+@dataclasses.dataclass
+class _Step:
+    slot: int
+    rows: List[Tuple[_Live, int, bool]]  # (session, n_tokens, samples)
+    tok_dev: Optional[torch.Tensor] = None
+    waiter: Optional[Callable] = None
+    tok_host: Optional[torch.Tensor] = None
+    event: Optional[object] = None
+    consumed: bool = False
+    booked: bool = False
+    t_issue: float = 0.0
+
+
+class PipelineServingEngine:
+    """One stage rank of a serving pipeline.  Rank 0 (the head) also schedules."""
+
+    def __init__(self, executor: StageExecutor, channel: Optional[Channel], *, n_slots: Optional[int] = None,
+                 batch: int = 64, max_step_tokens: Optional[int] = None, prefill_chunk: Optional[int] = None,
+                 timeout_s: float = 120.0, max_handles: Optional[int] = None, timing: bool = False,
+                 name: str = "pipe"):
+        self.ex = executor
+        self.ch = channel
+        self.rank = channel.rank if channel is not None else 0
+        self.S = channel.world if channel is not None else 1
+        self.is_head = self.rank == 0
+        self.is_tail = self.rank == self.S - 1
+        self.dev = executor.device
+        self.H = executor.cfg.hidden_size
+        self.M = int(n_slots or (self.S + 1 if self.S > 1 else 1))
+        self.B = int(batch)
+        self.timeout_s = float(timeout_s)
+        self.max_step_tokens = int(max_step_tokens or executor.max_tokens)
+        self.prefill_chunk = int(prefill_chunk or self.max_step_tokens)
+        self.name = name
+        self.max_handles = int(max_handles or executor.sessions.max_sessions)
+        self.timing = timing
+        self._events: List = []
+        self.stopped = False
+        self.failed: Optional[str] = None
+        self.rounds = 0
+        self.steps_run = 0
+        if self.is_tail:
+            self.sampler = TailSampler(self.dev, self.max_handles, executor.cfg.vocab_size)
+        if self.is_head:
+            self.queue: List[Request] = []
+            self.slots: List[List[_Live]] = [[] for _ in range(self.M)]
+            self.inflight: List[Optional[_Step]] = [None] * self.M
+            self.booking: List[Optional[_Step]] = [None] * self.M
+            self.closes: List[List[int]] = [[] for _ in range(self.M)]
+            self.free_handles = list(range(self.max_handles - 1, -1, -1))
+            self.live: Dict[str, _Live] = {}
+            self.finished: List[Request] = []
+            self.on_token: Optional[Callable[[Request, int], None]] = None
+            self.on_finish: Optional[Callable[[Request], None]] = None
+            self._rid = 0
+            self._pin = [torch.empty(max(self.B, 1) * 4, dtype=torch.int64, pin_memory=self.dev.type == "cuda")
+                         for _ in range(2 * self.M + 2)]
+            self._pin_k = 0
+            self.capacity_tokens: Optional[int] = None
+            self.reserved_tokens = 0
+            self.tokens_generated = 0
+        self._exchange_capacity()
+
+    # ------------------------------------------------------------------ setup
+    def _exchange_capacity(self) -> None:
+        """All-gather (free KV tokens, max sessions, page size) over the channel: the head
+        admits only what EVERY stage can hold (stages with more blocks hold fewer tokens)."""
+        ex = self.ex
+        mine = [float(ex.sessions.cache_tokens_left()), float(ex.sessions.max_sessions), float(ex.cache.page_size),
+                float(ex.max_seq_len)]
+        allv = self.ch.all_gather_floats(mine) if self.ch is not None else [mine]
+        self.stage_capacity = allv
+        cap = int(min(v[0] for v in allv))
+        self.max_handles = min(self.max_handles, int(min(v[1] for v in allv)))
+        self.page = int(max(v[2] for v in allv))
+        self.max_len = int(min(v[3] for v in allv))
+        if self.is_head:
+            self.capacity_tokens = cap
+            self.free_handles = list(range(self.max_handles - 1, -1, -1))
+
+    # ------------------------------------------------------------------ head API
+    def submit(self, req: Request) -> Request:
+        if not self.is_head:
+            raise RuntimeError("submit() is a head (rank 0) operation")
+        if req.rid is None:
+            req.rid = f"{self.name}-{self._rid}"
+            self._rid += 1
+        if not req.prompt:
+            raise ValueError("empty prompt")
+        need = len(req.prompt) + len(req.generated) + req.max_new_tokens + 2
+        if need > self.max_len:
+            raise ValueError(f"request needs {need} tokens > max_seq_len {self.max_len}")
+        req.t_submit = req.t_submit or time.perf_counter()
+        self.queue.append(req)
+        return req
+
+    @property
+    def idle(self) -> bool:
+        return self.is_head and not self.queue and not self.live
+
+    def _key(self, h: int) -> str:
+        return f"{self.name}:{h}"
+
+    def _reserve(self, req: Request) -> int:
+        n = len(req.prompt) + len(req.generated) + req.max_new_tokens + 2
+        return self.page * ((n + self.page - 1) // self.page)
+
+    def _admit(self, m: int, budget: int) -> List[Tuple[_Live, int]]:
+        """Move queued requests into slot m while there is room (sessions, handles, KV
+        tokens on every stage, this step's prefill token budget).  Returns (session, first
+        chunk length) pairs; the first admission of a step always gets at least one chunk."""
+        out: List[Tuple[_Live, int]] = []
+        while self.queue and len(self.slots[m]) < self.B and self.free_handles:
+            req = self.queue[0]
+            res = self._reserve(req)
+            if self.reserved_tokens + res > self.capacity_tokens and self.live:
+                break  # wait for retirements
+            feed = list(req.prompt) + list(req.generated)  # failover re-prefill: prompt + generated
+            take = min(len(feed), self.prefill_chunk, max(budget, 0))
+            if take <= 0:
+                if out:
+                    break
+                take = min(len(feed), self.prefill_chunk)
+            self.queue.pop(0)
+            lv = _Live(req, self.free_handles.pop(), m, pending=feed)
+            self.reserved_tokens += res
+            self.slots[m].append(lv)
+            self.live[req.rid] = lv
+            out.append((lv, take))
+            budget -= take
+        return out
+
+    def _retire(self, lv: _Live, reason: str) -> None:
+        if lv.retired:
+            return
+        lv.retired = True
+        req = lv.req
+        req.done = True
+        req.finish_reason = req.finish_reason or reason
+        req.t_done = time.perf_counter()
+        self.slots[lv.slot].remove(lv)
+        self.closes[lv.slot].append(lv.handle)
+        self.free_handles.append(lv.handle)
+        self.live.pop(req.rid, None)
+        self.reserved_tokens -= self._reserve(req)
+        self.ex.sessions.close(self._key(lv.handle))
+        self.finished.append(req)
+        if self.on_finish is not None:
+            self.on_finish(req)
+
+    def _accept(self, lv: _Live, tok: int) -> None:
+        """Reference client stop rules (src/main.py:190-205): EOS is not emitted, a token
+        repeated ``stop_on_repeat`` times in a row ends generation, max_new_tokens."""
+        req = lv.req
+        if req.done:
+            return
+        if req.t_first is None:
+            req.t_first = time.perf_counter()
+        if req.eos_token_id is not None and tok == req.eos_token_id:
+            self._retire(lv, "eos")
+            return
+        if req.stop_on_repeat and req.generated and tok == req.generated[-1] and len(req.generated) > 1:
+            req._repeat += 1
+            if req._repeat >= req.stop_on_repeat:
+                self._retire(lv, "repeat")
+                return
+        else:
+            req._repeat = 0
+        req.generated.append(int(tok))
+        self.tokens_generated += 1
+        if self.on_token is not None:
+            self.on_token(req, int(tok))
+        if len(req.generated) >= req.max_new_tokens:
+            self._retire(lv, "length")
+
+    def _book(self, step: Optional[_Step]) -> None:
+        """Host bookkeeping of a step's tokens (pinned copy issued a round ago)."""
+        if step is None or step.booked:
+            return
+        step.booked = True
+        if not step.consumed:
+            self._consume(step)
+        wait_event(step.event, self.timeout_s, "token copy")
+        toks = step.tok_host[: len(step.rows)].tolist() if step.tok_host is not None else []
+        for (lv, n, samples), t in zip(step.rows, toks):
+            if samples and not lv.retired and t >= 0:
+                self._accept(lv, int(t))
+
+    def _consume(self, step: _Step) -> None:
+        """Make the step's tokens usable on the device and start their async host copy."""
+        if step.consumed:
+            return
+        step.consumed = True
+        if step.waiter is not None:
+            step.tok_dev = step.waiter()
+        n = len(step.rows)
+        if n == 0 or step.tok_dev is None:
+            return
+        self._pin_k = (self._pin_k + 1) % len(self._pin)
+        host = self._pin[self._pin_k]
+        if host.numel() < n:
+            host = self._pin[self._pin_k] = torch.empty(2 * n, dtype=torch.int64,
+                                                        pin_memory=self.dev.type == "cuda")
+        host[:n].copy_(step.tok_dev[:n], non_blocking=True)
+        step.tok_host = host
+        if self.dev.type == "cuda":
+            ev = torch.cuda.Event()
+            ev.record()
+            step.event = ev
+
+    # ------------------------------------------------------------------ one head step
+    def _head_step(self, m: int) -> None:
+        prev2, prev = self.booking[m], self.inflight[m]
+        self._book(prev2)                       # tokens of two steps ago: stop checks
+        if prev is not None:
+            self._consume(prev)                 # tokens of the last step: device feed
+        # (a session retired just now still had a row in ``prev``: that token is ignored)
+        budget = self.max_step_tokens
+        dec: List[_Live] = [lv for lv in self.slots[m] if not lv.pending]
+        budget -= len(dec)
+        chunks: List[Tuple[_Live, int]] = []
+        for lv in self.slots[m]:
+            if lv.pending and lv.admitted and budget > 0:
+                take = min(len(lv.pending), self.prefill_chunk, budget)
+                chunks.append((lv, take))
+                budget -= take
+        admitted = self._admit(m, budget)
+        chunks.extend(admitted)
+        rows: List[Tuple[_Live, int, bool]] = [(lv, 1, True) for lv in dec]
+        recs = [(lv.handle, 1, lv.fed, F_SAMPLE, lv.req.seed) for lv in dec]
+        ids_host: List[int] = []
+        for lv, take in chunks:
+            last = take == len(lv.pending)
+            flags = (F_RESET if lv.fed == 0 else 0) | (F_SAMPLE if last else 0)
+            recs.append((lv.handle, take, lv.fed, flags, lv.req.seed))
+            rows.append((lv, take, last))
+            ids_host.extend(lv.pending[:take])
+        closes = self.closes[m]
+        self.closes[m] = []
+        hdr = self._header(m, recs, closes, [lv for lv, _ in admitted])
+        for lv, _ in admitted:
+            lv.admitted = True
+        step = _Step(m, rows, t_issue=time.perf_counter())
+        if self.S > 1:
+            self.ch.send_msg(1, hdr)
+        if rows:
+            # inputs: decode tokens gathered on the device from the last step + prompt chunk ids
+            parts = []
+            if dec:
+                idx = torch.tensor([lv.last_row for lv in dec], dtype=torch.long)
+                parts.append(prev.tok_dev.index_select(0, idx.to(self.dev, non_blocking=True)))
+            if ids_host:
+                parts.append(torch.tensor(ids_host, dtype=torch.long).to(self.dev, non_blocking=True))
+            x = parts[0] if len(parts) == 1 else torch.cat(parts)
+            out = self._compute(recs, x, m)
+            for r, (lv, n, _) in enumerate(rows):
+                lv.fed += n
+                lv.last_row = r
+                if lv.pending:
+                    del lv.pending[:n]
+            if self.S == 1:
+                step.tok_dev = self._sample_tail(hdr, out)
+            else:
+                self.ch.send(1, out)
+                _, step.waiter = self.ch.recv(self.S - 1, (len(rows),), torch.long, which="ret")
+        self.booking[m] = prev
+        self.inflight[m] = step
+        self.steps_run += 1
+
+    def _header(self, m: int, recs, closes: List[int], admitted: List[_Live]) -> np.ndarray:
+        hdr = np.zeros(HDR + SEQ_REC * len(recs) + len(closes) + ADM_REC * len(admitted), dtype=np.int64)
+        T = sum(int(r[1]) for r in recs)
+        hdr[:HDR] = (KIND_STEP, m, len(recs), T, len(closes), len(admitted), self.rounds, 0)
+        off = HDR
+        if recs:
+            hdr[off:off + SEQ_REC * len(recs)] = np.asarray(recs, dtype=np.int64).reshape(-1)
+            off += SEQ_REC * len(recs)
+        if closes:
+            hdr[off:off + len(closes)] = closes
+            off += len(closes)
+        for lv in admitted:
+            p = lv.req.params
+            hist = list(lv.req.generated)[-RECENT:]
+            hdr[off:off + 6] = (lv.handle, _f2i(p.temperature), _f2i(p.top_p), int(p.top_k),
+                                _f2i(p.repetition_penalty), len(hist))
+            hdr[off + 6:off + 6 + len(hist)] = hist
+            off += ADM_REC
+        return hdr
+
+    # ------------------------------------------------------------------ shared compute
+    def _compute(self, seq_recs, x, m: int):
+        ex = self.ex
+        seqs = [(self._key(int(h)), int(n)) for h, n, _, _, _ in seq_recs]
+        reset = [bool(int(f) & F_RESET) for _, _, _, f, _ in seq_recs]
+        starts = [int(s) for _, _, s, _, _ in seq_recs]
+        e0 = e1 = None
+        if self.timing and self.dev.type == "cuda":
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        with trace_range(f"pp.rank{self.rank}.slot{m}"):
+            out = ex.forward(seqs, x, reset=reset, starts=starts, max_length=self.max_len)
+        if e1 is not None:
+            e1.record()
+            self._events.append((e0, e1))
+        return out
+
+    def _sample_tail(self, hdr: np.ndarray, logits: torch.Tensor) -> torch.Tensor:
+        n_seq, n_close, n_adm = int(hdr[2]), int(hdr[4]), int(hdr[5])
+        recs = hdr[HDR:HDR + SEQ_REC * n_seq].reshape(n_seq, SEQ_REC)
+        off = HDR + SEQ_REC * n_seq + n_close
+        adm = hdr[off:off + ADM_REC * n_adm].reshape(n_adm, ADM_REC)
+        if n_adm:
+            self.sampler.admit(adm)
+        handles = recs[:, 0]
+        self.sampler.seed_host[handles] = recs[:, 4]
+        positions = recs[:, 2] + recs[:, 1]  # index of the token being sampled
+        samples = (recs[:, 3] & F_SAMPLE) != 0
+        rows = None if samples.all() else np.nonzero(samples)[0]
+        return self.sampler.sample(logits, handles, positions, rows)
+
+    # ------------------------------------------------------------------ non-head stage
+    def _stage_step(self) -> bool:
+        """Receive one header (+ payload), compute, forward.  False on STOP."""
+        hdr = self.ch.recv_msg(self.rank - 1, timeout_s=self.idle_timeout_s)
+        kind = int(hdr[0])
+        if kind == KIND_STOP:
+            if not self.is_tail:
+                self.ch.send_msg(self.rank + 1, hdr)
+            return False
+        m, n_seq, T, n_close = int(hdr[1]), int(hdr[2]), int(hdr[3]), int(hdr[4])
+        if not self.is_tail:
+            self.ch.send_msg(self.rank + 1, hdr)  # the successor plans while we compute
+        recs = hdr[HDR:HDR + SEQ_REC * n_seq].reshape(n_seq, SEQ_REC)
+        closes = hdr[HDR + SEQ_REC * n_seq:HDR + SEQ_REC * n_seq + n_close]
+        for c in closes:  # before the compute: a closed handle may be re-admitted in this very step
+            self.ex.sessions.close(self._key(int(c)))
+        if n_seq:
+            _, waiter = self.ch.recv(self.rank - 1, (T, self.H), self.ex.dtype)
+            x = waiter()
+            out = self._compute(recs.tolist(), x, m)
+            if self.is_tail:
+                tok = self._sample_tail(hdr, out)
+                self.ch.send(0, tok, which="ret")
+            else:
+                self.ch.send(self.rank + 1, out)
+        self.steps_run += 1
+        return True
+
+    idle_timeout_s: Optional[float] = None  # None: the channel timeout
+
+    # ------------------------------------------------------------------ driving
+    def run_rounds(self, n: int) -> None:
+        """n rounds x M slot-steps on every rank (lock-step unit of the benchmark)."""
+        try:
+            for _ in range(n):
+                for m in range(self.M):
+                    if self.is_head:
+                        self._head_step(m)
+                    elif not self._stage_step():
+                        self.stopped = True
+                        return
+                self.rounds += 1
+        except ChannelError as e:
+            self._fail(str(e))
+
+    def serve(self) -> None:
+        """Non-head ranks: process steps until the head's STOP."""
+        try:
+            while self._stage_step():
+                pass
+            self.stopped = True
+        except ChannelError as e:
+            self._fail(str(e))
+
+    def run_until_idle(self, max_rounds: Optional[int] = None) -> List[Request]:
+        """Head: run rounds until every submitted request has finished."""
+        k = 0
+        while not self.idle:
+            self.run_rounds(1)
+            k += 1
+            if max_rounds is not None and k >= max_rounds:
+                break
+        self.drain()
+        return self.finished
+
+    def drain(self) -> None:
+        """Head: book every outstanding step (end of a run)."""
+        if not self.is_head:
+            return
+        try:
+            for m in range(self.M):
+                self._book(self.booking[m])
+                self.booking[m] = None
+            for m in range(self.M):
+                self._book(self.inflight[m])
+                self.inflight[m] = None
+            for m in range(self.M):  # rows decided finished at this point: nothing in flight anymore
+                for lv in list(self.slots[m]):
+                    if lv.req.done:
+                        self._retire(lv, lv.req.finish_reason or "done")
+        except ChannelError as e:
+            self._fail(str(e))
+
+    def stop(self) -> None:
+        """Head: close every session downstream and stop the serving ranks."""
+        if not self.is_head or self.ch is None or self.failed:
+            return
+        try:
+            hdr = np.zeros(HDR, dtype=np.int64)
+            hdr[0] = KIND_STOP
+            self.ch.send_msg(1, hdr)
+            self.ch.flush(timeout_s=self.timeout_s)
+        except (ChannelError, RuntimeError) as e:
+            logger.warning(f"stop: {e}")
+
+    def _fail(self, why: str) -> None:
+        self.failed = why
+        logger.error(f"[{self.name} rank {self.rank}] pipeline failure: {why}")
+        if self.ch is not None:
+            self.ch.abort()
+        if self.is_head:
+            pend = [lv.req for m in range(self.M) for lv in self.slots[m] if not lv.req.done] + list(self.queue)
+            raise PipelineFailure(why, pend)
+        raise PipelineFailure(why)
+
+    def stage_ms(self) -> Optional[float]:
+        if not self._events:
+            return None
+        torch.cuda.synchronize()
+        ms = [a.elapsed_time(b) for a, b in self._events]
+        self._events.clear()
+        return sum(ms) / len(ms)

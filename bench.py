@@ -8,8 +8,9 @@ states hop stage->stage over RCCL (xGMI), the last stage samples server-side wit
 reference CLI's defaults (temperature 1.0, top_p 0.92, top_k 50, repetition penalty 1.5) and
 returns token ids to rank 0.
 
-Work per GPU is fixed as N grows ("weak" scaling): N micro-batches x --batch sessions are in
-flight, so every GPU processes N micro-batch ticks of its 32/N blocks per step.  A step
+Work per GPU is fixed as N grows ("weak" scaling): N+1 micro-batches x --batch sessions are in
+flight (one slot of slack for the token hop), so every GPU processes N+1 micro-batch ticks of
+its 32/N blocks per step (continuous-batching engine, parallel/engine.py).  A step
 advances every session by one token; value = generated tokens/s over the whole node.
 
     python bench.py                       # N=1 (defaults finish in ~1-2 minutes)
@@ -50,7 +51,7 @@ def main(argv=None):
     ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--model", default="llama2-7b")
     ap.add_argument("--batch", type=int, default=64, help="sessions per micro-batch")
-    ap.add_argument("--micro", type=int, default=None, help="micro-batches in flight (default: N stages)")
+    ap.add_argument("--micro", type=int, default=None, help="micro-batches in flight (default: stages + 1, or 1 on one GPU)")
     ap.add_argument("--replicas", type=int, default=1,
                     help="independent pipelines (data parallel): N GPUs = replicas x stages, e.g. 8 = 2 x 4")
     ap.add_argument("--prompt-len", type=int, default=128)
@@ -71,7 +72,8 @@ def main(argv=None):
     from src.models.config import resolve_model
     from src.models.weights import random_stage_weights
     from src.parallel import dist as pdist
-    from src.parallel.pipeline import PipelineEngine, make_replica_groups, make_token_groups
+    from src.parallel.channel import Channel
+    from src.parallel.engine import PipelineServingEngine, Request
     from src.parallel.tensor_parallel import make_tp_groups, shard_stage_weights
     from src.partition import even_splits, stage_ranges
     from src.runtime.executor import StageExecutor
@@ -91,71 +93,90 @@ def main(argv=None):
     if world % (R * TP):
         raise SystemExit(f"--replicas {R} x --tp {TP} does not divide {world} GPUs")
     S = world // (R * TP)
-    groups = make_replica_groups(world, S)
-    tok_groups = make_token_groups(world, S)  # token return hop on its own communicator
     tpg = make_tp_groups(world, S, TP)
     stage = rank % S
+    lane = rank // S                      # pipeline index: replica * TP + tensor-parallel shard
     cuts = even_splits(cfg.num_hidden_layers, S)
     start, end = stage_ranges(cuts, cfg.num_hidden_layers)[stage]
-    M = a.micro or S
+    M = a.micro or (S + 1 if S > 1 else 1)  # one slot of slack for the token-return hop
     B = a.batch
     dtype = torch.bfloat16
     t0 = time.time()
     w = random_stage_weights(cfg, start, end, has_embed=stage == 0, has_head=stage == S - 1, device=device,
                              dtype=dtype, seed=a.seed, fp8=a.fp8 and TP == 1)
     if TP > 1:  # shard the stage's blocks over the TP group (fp8: quantize the shard)
-        w = shard_stage_weights(w, (rank // S) % TP, TP)
+        w = shard_stage_weights(w, lane % TP, TP)
         if a.fp8:
             w.quantize_fp8()
-    max_len = a.prompt_len + a.warmup + a.steps + 8
+    rounds = 2 + a.warmup + a.steps
+    max_len = a.prompt_len + rounds + 8
     max_len = 64 * math.ceil(max_len / 64)
     kv_bytes = None if device.type == "cuda" else 256 << 20
     if os.environ.get("MPAMD_KV_GB"):  # cap the KV pool (e.g. several ranks sharing one GPU in a rehearsal)
         kv_bytes = int(float(os.environ["MPAMD_KV_GB"]) * (1 << 30))
-    ex = StageExecutor(w.cfg, w, device, dtype=dtype, max_sessions=M * B, max_seq_len=max(max_len, 256),
+    ex = StageExecutor(w.cfg, w, device, dtype=dtype, max_sessions=M * B + 8, max_seq_len=max(max_len, 256),
                        kv_cache_bytes=kv_bytes, use_graphs=not a.no_graphs, graph_max_batch=max(B, 1),
                        max_tokens_per_step=max(B * a.prompt_len, B), tp=tpg)
     if rank == 0 and device.type == "cuda":
         print("gemm kernel choice:", {f"M{k[0]}:N{k[1]}xK{k[2]}e{k[3]}": v
                                                    for k, v in sorted(ops._SK_CHOICE.items())}, file=sys.stderr)
-    sp = SamplingParams(a.temperature, a.top_p, a.top_k, a.repetition_penalty)
-    eng = PipelineEngine(ex, rank, world, sp, n_micro=M, batch=B, seed=a.seed, stages=S, groups=groups, tp=TP,
-                         tok_groups=tok_groups)
-    gen = torch.Generator().manual_seed(1234)
-    prompts = [torch.randint(0, cfg.vocab_size, (B, a.prompt_len), generator=gen) for _ in range(M)]
+    ch = None
+    if S > 1:  # this pipeline's device channel: ranks [lane*S, (lane+1)*S) over RCCL / xGMI
+        from torch.distributed import distributed_c10d as c10d
+
+        ch = Channel(c10d._get_default_store(), f"bench/pipe{lane}", stage, S, device, timeout_s=600.0)
+    eng = PipelineServingEngine(ex, ch, n_slots=M, batch=B, max_step_tokens=B * a.prompt_len, name=f"p{lane}")
+    if stage == 0:
+        # synthetic requests: every pipeline of a TP group submits the same ones (same seeds),
+        # so its shards take identical scheduling decisions and sample identical tokens
+        sp = SamplingParams(a.temperature, a.top_p, a.top_k, a.repetition_penalty)
+        gen = torch.Generator().manual_seed(1234 + (lane // TP))
+        for i in range(M * B):
+            prompt = torch.randint(0, cfg.vocab_size, (a.prompt_len,), generator=gen).tolist()
+            eng.submit(Request(prompt, max_new_tokens=rounds + 8, params=sp, stop_on_repeat=0,
+                               seed=a.seed * 1000003 + (lane // TP) * 7919 + i, rid=f"s{i}"))
     load_s = time.time() - t0
 
     def sync():
         if device.type == "cuda":
             torch.cuda.synchronize()
 
-    # prefill (TTFT of the whole batch through the pipeline)
+    # prefill (TTFT of the whole batch through the pipeline) + first decode round (graph capture)
     pdist.barrier(device)
     sync()
     tp0 = time.perf_counter()
-    eng.prefill(prompts)
-    eng.decode(1)  # first decode round also captures the decode hipGraphs
+    eng.run_rounds(2)
     sync()
     pdist.barrier(device)
     prefill_s = time.perf_counter() - tp0
 
-    eng.decode(a.warmup)
+    eng.run_rounds(a.warmup)
     sync()
     pdist.barrier(device)
     sync()
     t1 = time.perf_counter()
     eng.timing = True
-    eng.decode(a.steps)
+    eng.run_rounds(a.steps)
     sync()
     pdist.barrier(device)
     sync()
     dt_local = time.perf_counter() - t1
     eng.timing = False
     stage_ms = eng.stage_ms() or 0.0
-    eng.finish()
+    n_tokens = 0
+    if stage == 0:
+        eng.drain()
+        n_tokens = eng.tokens_generated
+        if any(r.done for r in eng.finished):
+            raise SystemExit("a benchmark session finished early: the timed rounds would be short of work")
+        eng.stop()
+    else:
+        eng.serve()  # until the head's STOP
+    if ch is not None:
+        ch.close()
     dt = pdist.all_max(dt_local, device)
     per_stage = pdist.all_gather_floats([stage_ms, float(end - start)], device)
-    tokens = a.steps * M * B * R
+    tokens = a.steps * M * B * R  # every session advances one token per round
     value = tokens / dt
     base = baseline_value() if a.model == "llama2-7b" else None  # the baseline is a Llama-2-7B number
     if rank == 0:
@@ -180,6 +201,7 @@ def main(argv=None):
                 "seq_len": a.prompt_len,
                 "parallelism": f"pp{S}" + (f"xtp{TP}" if TP > 1 else "") + (f"xdp{R}" if R > 1 else ""),
                 "micro_batches": M,
+                "engine": "PipelineServingEngine (continuous batching, device channel)",
                 "sessions_per_micro_batch": B,
                 "splits": cuts,
                 "sampling": {"temperature": a.temperature, "top_p": a.top_p, "top_k": a.top_k,

@@ -147,11 +147,23 @@ class TailSampler:
         self._pin_i64 = [torch.empty(4 * 256, dtype=torch.int64, pin_memory=pin) for _ in range(2)]
         self._pin_ev = [None, None]
         self._pk = 0
+        # working set of the last sampled batch: in steady decode the same handles come back
+        # in the same order every step, so their parameters / history stay gathered
+        self._cur_key: Optional[bytes] = None
+        self._cur: Optional[dict] = None
+
+    def _writeback(self) -> None:
+        if self._cur is not None:
+            c = self._cur
+            self.hist.index_copy_(0, c["rows"], c["recent"])
+            self.hist_len.index_copy_(0, c["rows"], c["rlen"])
+        self._cur, self._cur_key = None, None
 
     def admit(self, recs: np.ndarray) -> None:
         """recs: [n, ADM_REC] admission records."""
         if not len(recs):
             return
+        self._writeback()
         h = recs[:, 0].astype(np.int64)
         f = np.stack([recs[:, 1], recs[:, 2], recs[:, 4]]).astype(np.int64).view(np.float64)
         self.temp_host[h] = f[0]
@@ -201,27 +213,29 @@ class TailSampler:
             return out
         if n == 0:
             return torch.empty(0, dtype=torch.long, device=logits.device)
-        seeds_h = mix_seeds(self.seed_host[handles], positions)
-        rows, seeds = self._stage([handles.astype(np.int64), seeds_h])
         if (self.temp_host[handles] <= 0).all():
-            tok = ops.argmax(logits)
+            return ops.argmax(logits)  # greedy: no penalty, no history (reference temp <= 0 branch)
+        handles = np.ascontiguousarray(handles, dtype=np.int64)
+        seeds_h = mix_seeds(self.seed_host[handles], positions)
+        key = handles.tobytes()
+        if key != self._cur_key:
+            self._writeback()
+            rows, seeds = self._stage([handles, seeds_h])
+            self._cur = dict(rows=rows, recent=self.hist.index_select(0, rows),
+                             rlen=self.hist_len.index_select(0, rows), temp=self.temp.index_select(0, rows),
+                             top_p=self.top_p.index_select(0, rows), top_k=self.top_k.index_select(0, rows),
+                             rp=self.rp.index_select(0, rows))
+            self._cur_key = key
         else:
-            recent = self.hist.index_select(0, rows)
-            rlen = self.hist_len.index_select(0, rows)
-            ws = None
-            if logits.device.type == "cuda":
-                if self._ws is None or self._ws.numel() < n * logits.shape[1]:
-                    self._ws = torch.empty(max(n, 64) * logits.shape[1], dtype=torch.float32, device=logits.device)
-                ws = self._ws
-            tok = ops.sample(logits, self.temp.index_select(0, rows), self.top_p.index_select(0, rows),
-                             self.top_k.index_select(0, rows), self.rp.index_select(0, rows), recent, rlen, seeds,
-                             workspace=ws, update_history=True)
-            self.hist.index_copy_(0, rows, recent)
-            self.hist_len.index_copy_(0, rows, rlen)
-            return tok
-        # greedy rows still record their history (a later admission may switch nothing, but
-        # failover re-prefill reads the head's copy; keep the device copy consistent anyway)
-        return tok
+            (seeds,) = self._stage([seeds_h])
+        c = self._cur
+        ws = None
+        if logits.device.type == "cuda":
+            if self._ws is None or self._ws.numel() < n * logits.shape[1]:
+                self._ws = torch.empty(max(n, 64) * logits.shape[1], dtype=torch.float32, device=logits.device)
+            ws = self._ws
+        return ops.sample(logits, c["temp"], c["top_p"], c["top_k"], c["rp"], c["recent"], c["rlen"], seeds,
+                          workspace=ws, update_history=True)
 
 
 # ====================================================================== head-side state
@@ -486,8 +500,12 @@ class PipelineServingEngine:
             # inputs: decode tokens gathered on the device from the last step + prompt chunk ids
             parts = []
             if dec:
-                idx = torch.tensor([lv.last_row for lv in dec], dtype=torch.long)
-                parts.append(prev.tok_dev.index_select(0, idx.to(self.dev, non_blocking=True)))
+                src_rows = [lv.last_row for lv in dec]
+                if src_rows == list(range(prev.tok_dev.shape[0])):
+                    parts.append(prev.tok_dev)  # steady decode: same sessions, same order
+                else:
+                    idx = torch.tensor(src_rows, dtype=torch.long)
+                    parts.append(prev.tok_dev.index_select(0, idx.to(self.dev, non_blocking=True)))
             if ids_host:
                 parts.append(torch.tensor(ids_host, dtype=torch.long).to(self.dev, non_blocking=True))
             x = parts[0] if len(parts) == 1 else torch.cat(parts)

@@ -13,8 +13,8 @@ KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "
         "vs_baseline", "dtype", "data", "config"}
 
 
-@pytest.mark.parametrize("nproc,extra,par,gb", [(2, [], "pp2", 4), (4, ["--replicas", "2"], "pp2xdp2", 8),
-                                                (4, ["--tp", "2"], "pp2xtp2", 4)])
+@pytest.mark.parametrize("nproc,extra,par,gb", [(2, [], "pp2", 6), (4, ["--replicas", "2"], "pp2xdp2", 12),
+                                                (4, ["--tp", "2"], "pp2xtp2", 6)])
 def test_bench_torchrun_gloo(nproc, extra, par, gb):
     port = 29650 + nproc
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
@@ -30,4 +30,4 @@ def test_bench_torchrun_gloo(nproc, extra, par, gb):
     assert rec["n_gpus"] == nproc and rec["steps"] == 3 and rec["warmup"] == 1
     assert rec["value"] > 0 and rec["higher_is_better"] is True and rec["scaling"] == "weak"
     assert rec["config"]["parallelism"] == par
-    assert rec["config"]["global_batch"] == gb  # stages micro-batches x batch x replicas (TP lanes share)
+    assert rec["config"]["global_batch"] == gb  # (stages + 1) slots x batch x replicas (TP lanes share)

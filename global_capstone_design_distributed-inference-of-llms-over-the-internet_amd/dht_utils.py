@@ -69,7 +69,9 @@ def register_blocks_on_dht(dht: DHT, peer_id, block_indices: List[int], model_na
                            p2p_maddrs: Optional[List[str]] = None, start_block: Optional[int] = None,
                            end_block: Optional[int] = None, throughput: Optional[float] = None,
                            final_stage: bool = False, state: ServerState = ServerState.ONLINE,
-                           expiration_time: Optional[float] = None) -> bool:
+                           expiration_time: Optional[float] = None, extra: Optional[dict] = None) -> bool:
+    """``extra``: additional record fields (e.g. ``channel_host`` / ``device`` of a server that
+    accepts same-node device channels)."""
     exp = expiration_time if expiration_time is not None else get_dht_time() + 90
     try:
         for b in block_indices:
@@ -78,6 +80,8 @@ def register_blocks_on_dht(dht: DHT, peer_id, block_indices: List[int], model_na
                    "end_block": None if end_block is None else int(end_block),
                    "throughput": None if throughput is None else float(throughput), "state": state.value,
                    "p2p_maddrs": list(p2p_maddrs or []), "final_stage": bool(final_stage)}
+            if extra:
+                rec.update(extra)
             dht.store(get_module_key(b, model_name), rec, exp, subkey=str(peer_id))
         return True
     except Exception as e:  # pragma: no cover

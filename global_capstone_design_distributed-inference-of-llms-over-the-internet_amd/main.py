@@ -15,7 +15,12 @@
 
 The reference hard-wires 4 stages (3 cut points); here the stage count follows the number
 of cut points (``--splits 6`` for gpt2 = 2 stages, ``8,16,24`` = 4 stages, ...).
-Single-node multi-GPU serving over RCCL is ``bench.py`` / ``src.parallel.pipeline``.
+Same-node fast path (``--device_channel auto``, default): servers announce their machine and
+device; when every hop of the client's route is on the client's machine, the client opens a
+device channel through them (one ``rpc_channel_open`` handshake per hop over TCP) and the
+generation runs on the continuous-batching pipeline engine with hidden states moving
+GPU -> GPU over RCCL and token ids returning on the channel (``parallel/channel.py``,
+``parallel/engine.py``).  Off-node routes use the TCP path below.
 """
 from __future__ import annotations
 
@@ -104,6 +109,11 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--inference_max_length", type=int, default=None,
                    help="server: longest session (tokens) a client may open; alias of --max_seq_len")
     p.add_argument("--public_name", type=str, default=None, help="server: human-readable name in announcements")
+    p.add_argument("--device_channel", choices=["auto", "on", "off"], default="auto",
+                   help="same-node fast path: hidden states GPU->GPU over RCCL (xGMI) instead of TCP. Servers "
+                        "announce it; the client uses it when every hop runs on its machine (auto) or always (on)")
+    p.add_argument("--num_sessions", type=int, default=1,
+                   help="client: generate this many sessions concurrently (prompt repeated, distinct seeds)")
     return p
 
 
@@ -182,6 +192,11 @@ def run_rank0(args, device, cuts: List[int]):
     Lp = int(ids.numel())
     sid = str(uuid.uuid4())
     max_length = Lp + args.max_new_tokens
+    if args.device_channel != "off":
+        route = tx._get_route(sid)
+        if args.device_channel == "on" or tx.device_channel_possible(route, device):
+            return _run_rank0_channel(args, device, ex, tok, tx, route, ids)
+        logger.info("device channel not possible (a hop is on another machine or did not announce one): TCP path")
     t0 = time.perf_counter()
     hidden = ex.forward([(sid, Lp)], ids.to(device), reset=[True], max_length=max_length)
     tx.send_prefill(Lp, hidden, session_id=sid, max_length=max_length)
@@ -229,6 +244,47 @@ def run_rank0(args, device, cuts: List[int]):
     return generated
 
 
+def _run_rank0_channel(args, device, ex, tok, tx, route, ids):
+    """Same-node fast path of run_rank0: this process is the head of a device channel
+    (parallel/channel.py) through the route's servers, and generation runs on the
+    continuous-batching engine (parallel/engine.py); the TCP RPC only did discovery and the
+    channel handshake."""
+    from .parallel.engine import PipelineServingEngine, Request, request_seed
+    from .runtime.sampler import SamplingParams
+
+    n = max(1, int(args.num_sessions))
+    S = len(route) + 1
+    M = max(1, min(S + 1, n))
+    B = (n + M - 1) // M
+    ch = tx.open_device_channel(route, device, n_slots=M, batch=B, timeout=max(30.0, args.request_timeout * 2))
+    eng = PipelineServingEngine(ex, ch, n_slots=M, batch=B, name="client")
+    eos = getattr(tok, "eos_token_id", None)
+    rp = args.repetition_penalty if args.repetition_penalty is not None else 1.5
+    sp = SamplingParams(args.temperature, args.top_p, args.top_k, rp)
+    t0 = time.perf_counter()
+    reqs = [eng.submit(Request(ids.tolist(), max_new_tokens=args.max_new_tokens, params=sp, eos_token_id=eos,
+                               seed=request_seed(args.seed, f"s{i}"), rid=f"s{i}")) for i in range(n)]
+    try:
+        with torch.inference_mode():
+            eng.run_until_idle()
+    finally:
+        eng.stop()
+        ch.close()
+    t2 = time.perf_counter()
+    gen = reqs[0].generated
+    text = tok.decode(gen, skip_special_tokens=True)
+    print(f"\n{'=' * 80}\nPROMPT: {args.prompt}\nGENERATED: {text}\n{'=' * 80}\n", flush=True)
+    ttft = (reqs[0].t_first or t2) - t0
+    total = sum(len(r.generated) for r in reqs)
+    logger.info(f"device channel: {S} stages, {n} session(s), {M} slot(s) x {B}")
+    logger.info(f"Decode completed in {t2 - t0 - ttft:.3f}s ({total / max(t2 - t0, 1e-9):.2f} tokens/s over "
+                f"{n} session(s))")
+    logger.info(f"Total time: {t2 - t0:.3f}s")
+    logger.info(f"TTFT (Time to First Token): {ttft:.3f}s")
+    tx.shutdown()
+    return gen
+
+
 # ================================================================================ servers
 class _Server:
     """RPC server + handler + heartbeat for one loaded span."""
@@ -268,6 +324,12 @@ class _Server:
             extra.update(blocks=[ex.start, ex.end], throughput=self.throughput)
         if getattr(a, "public_name", None):
             extra["public_name"] = a.public_name
+        chan = {}
+        if getattr(a, "device_channel", "auto") != "off":
+            from .parallel.channel import host_id
+
+            chan = dict(channel_host=host_id(), device=str(ex.device))
+            extra.update(chan)
         if state == ServerState.ONLINE:
             register_stage_on_dht(self.dht, self.stage_idx, self.peer_id, self.maddrs, ttl=a.ttl, **extra)
         register_model_on_dht(self.dht, a.model, getattr(a, "total_blocks", None) or ex.cfg.num_hidden_layers,
@@ -277,7 +339,7 @@ class _Server:
                                    a.model, p2p_maddrs=self.maddrs, final_stage=self.final, state=state,
                                    expiration_time=exp)
             register_blocks_on_dht(self.dht, self.peer_id, list(range(ex.start, ex.end)), a.model, self.maddrs,
-                                   ex.start, ex.end, self.throughput, self.final, state, exp)
+                                   ex.start, ex.end, self.throughput, self.final, state, exp, extra=chan)
 
     def measure_next_pings(self, max_peers: int = 5, timeout: float = 2.0) -> dict:
         """RTT (s) to servers hosting the block right after this span (upstream Petals

@@ -589,17 +589,18 @@ class PipelineServingEngine:
             self.ch.send_msg(self.rank + 1, hdr)  # the successor plans while we compute
         recs = hdr[HDR:HDR + SEQ_REC * n_seq].reshape(n_seq, SEQ_REC)
         closes = hdr[HDR + SEQ_REC * n_seq:HDR + SEQ_REC * n_seq + n_close]
-        for c in closes:  # before the compute: a closed handle may be re-admitted in this very step
-            self.ex.sessions.close(self._key(int(c)))
-        if n_seq:
-            _, waiter = self.ch.recv(self.rank - 1, (T, self.H), self.ex.dtype)
-            x = waiter()
-            out = self._compute(recs.tolist(), x, m)
-            if self.is_tail:
-                tok = self._sample_tail(hdr, out)
-                self.ch.send(0, tok, which="ret")
-            else:
-                self.ch.send(self.rank + 1, out)
+        with self.ex.exec_lock:
+            for c in closes:  # before the compute: a closed handle may be re-admitted in this very step
+                self.ex.sessions.close(self._key(int(c)))
+            if n_seq:
+                _, waiter = self.ch.recv(self.rank - 1, (T, self.H), self.ex.dtype)
+                x = waiter()
+                out = self._compute(recs.tolist(), x, m)
+                if self.is_tail:
+                    tok = self._sample_tail(hdr, out)
+                    self.ch.send(0, tok, which="ret")
+                else:
+                    self.ch.send(self.rank + 1, out)
         self.steps_run += 1
         return True
 

@@ -110,6 +110,7 @@ class StageConnectionHandler:
         server.add_handler(HANDLER_PREFIX + "rpc_check_reachability", self.rpc_check_reachability)
         server.add_handler(HANDLER_PREFIX + "rpc_backward", self.rpc_backward)
         server.add_handler(HANDLER_PREFIX + "rpc_backward_stream", self.rpc_backward_stream)
+        server.add_handler(HANDLER_PREFIX + "rpc_channel_open", self.rpc_channel_open)
 
     # ------------------------------------------------------------------ handlers
     async def rpc_forward(self, msg: Message) -> Message:
@@ -169,6 +170,56 @@ class StageConnectionHandler:
         outs = await asyncio.wait_for(asyncio.get_running_loop().run_in_executor(self._worker, run),
                                       self.request_timeout * 4)
         return Message({"session_id": md.get("session_id")}, outs)
+
+    async def rpc_channel_open(self, msg: Message) -> Message:
+        """Join a same-node device channel (``parallel.channel``): the client found every hop
+        of its route on its own machine and asks this server to take rank ``rank`` of a
+        pipeline whose rank 0 is the client.  Hidden states then hop GPU -> GPU over RCCL
+        (xGMI) and token ids come back on the channel; this TCP RPC only carries the
+        rendezvous.  The serving loop runs on its own thread (``PipelineServingEngine.serve``)
+        until the client's STOP or a peer failure; TCP requests keep being served meanwhile."""
+        md = msg.metadata
+        import threading
+
+        from .parallel.channel import host_id
+
+        if md.get("host_id") not in (None, host_id()):
+            return Message({"ok": False, "error": "not on the same host"})
+        rank, world = int(md["rank"]), int(md["world"])
+        if (rank == world - 1) != bool(self.final_stage):
+            return Message({"ok": False, "error": f"rank {rank}/{world} does not match final_stage={self.final_stage}"})
+        t = threading.Thread(target=self._channel_serve, args=(dict(md),), daemon=True,
+                             name=f"channel-{md.get('prefix')}")
+        t.start()
+        self.stats["channels"] = self.stats.get("channels", 0) + 1
+        return Message({"ok": True, "start_block": self.executor.start, "end_block": self.executor.end})
+
+    def _channel_serve(self, md: dict) -> None:
+        from .parallel.channel import Channel, make_store
+        from .parallel.engine import PipelineFailure, PipelineServingEngine
+
+        ex = self.executor
+        ch = None
+        name = str(md.get("prefix", "chan"))
+        try:
+            store = make_store(md["store_host"], int(md["store_port"]), int(md["world"]), False,
+                               timeout_s=float(md.get("timeout", 60.0)))
+            ch = Channel(store, name, int(md["rank"]), int(md["world"]), ex.device,
+                         timeout_s=float(md.get("timeout", 60.0)), data_backend=md.get("data_backend"))
+            eng = PipelineServingEngine(ex, ch, n_slots=int(md.get("n_slots", 1)), batch=int(md.get("batch", 64)),
+                                        name=name)
+            eng.idle_timeout_s = float(md.get("idle_timeout", 3600.0))
+            with torch.inference_mode():
+                eng.serve()
+            logger.info(f"device channel {name}: stopped after {eng.steps_run} steps")
+        except (PipelineFailure, RuntimeError) as e:
+            logger.warning(f"device channel {name} failed: {e}")
+        finally:
+            with ex.exec_lock:
+                for sid in [k for k in ex.sessions.sessions if k.startswith(name + ":")]:
+                    ex.sessions.close(sid)
+            if ch is not None:
+                ch.close()
 
     async def rpc_push(self, msg: Message) -> Message:
         """Server-to-server hop of a pushed chain (upstream ``rpc_push``); same body as rpc_forward."""
@@ -404,7 +455,7 @@ class StageConnectionHandler:
         ml = max((int(r.max_length) for r in batch if r.max_length), default=None)
         phase = "handler.prefill" if any(r.x.shape[0] > 1 for r in batch) else "handler.decode"
         prompts = [r.prompts for r in batch] if any(r.prompts is not None for r in batch) else None
-        with torch.inference_mode(), self.timer(phase):
+        with torch.inference_mode(), self.timer(phase), ex.exec_lock:
             out = ex.forward(seqs, x, reset=[r.reset for r in batch], starts=[r.start for r in batch], max_length=ml,
                              prompts=prompts)
             self.stats["batches"] += 1
@@ -415,12 +466,13 @@ class StageConnectionHandler:
                 return [Message({"token_id": int(t), "session_id": r.sid}, [torch.tensor([[int(t)]], dtype=torch.long)])
                         for r, t in zip(batch, toks)]
             out_cpu = out.to("cpu", non_blocking=False)
+            amaxes = out_cpu.float().abs().amax(-1) if out_cpu.numel() else out_cpu
         res, off = [], 0
         for r in batch:
             n = r.x.shape[0]
             h = out_cpu[off:off + n]
+            amax = float(amaxes[off:off + n].max()) if n else 0.0
             off += n
-            amax = float(h.float().abs().max()) if h.numel() else 0.0
             if amax > 100:
                 logger.warning(f"[{r.sid[:8]}] large activation values detected (|x|max={amax:.2f})")
             res.append(Message({"session_id": r.sid}, [h.unsqueeze(0)]))

@@ -53,9 +53,11 @@ RECOVERABLE = (asyncio.TimeoutError, ConnectionError, OSError, RemoteError)
 class Hop:
     """One hop of a route: a peer serving blocks [start, end) (``key`` names the record it came from)."""
 
-    def __init__(self, key: str, peer_id: str, maddrs: List[str], start: int, end: int, final: bool):
+    def __init__(self, key: str, peer_id: str, maddrs: List[str], start: int, end: int, final: bool,
+                 info: Optional[dict] = None):
         self.key, self.peer_id, self.maddrs = key, peer_id, list(maddrs)
         self.start, self.end, self.final = start, end, final
+        self.info = dict(info or {})  # the registry record (channel_host / device for device channels)
 
     @property
     def expect_hidden(self) -> bool:
@@ -146,7 +148,7 @@ class RpcTransport:
         e = self._discover_peer(key, exclude, max_retries=retries, retry_delay=delay)
         final = i == len(self.stage_keys) - 1
         return Hop(key, str(e["peer_id"]), e.get("p2p_maddrs") or [], int(e.get("start_block", i)),
-                   int(e.get("end_block", i + 1)), final)
+                   int(e.get("end_block", i + 1)), final, e)
 
     def _module_route(self, cur: int, exclude: Set[str] = frozenset()) -> List[Hop]:
         if self.total_blocks is None:
@@ -163,7 +165,7 @@ class RpcTransport:
             if final and not bool(e.get("final_stage", False)):
                 raise RuntimeError("[module routing] last hop server is not a final stage (needs lm_head)")
             hops.append(Hop(f"petals:module:{self.model_name}:block_{cur}", str(e["peer_id"]),
-                            e.get("p2p_maddrs") or [], cur, end, final))
+                            e.get("p2p_maddrs") or [], cur, end, final, e))
             cur = end
             if len(hops) > self.total_blocks + 5:
                 raise RuntimeError("[module routing] route did not converge")
@@ -362,6 +364,51 @@ class RpcTransport:
             self._run(_close())
         except Exception:
             pass
+
+    # ------------------------------------------------------------------ same-node device channel
+    def device_channel_possible(self, route: List[Hop], device) -> bool:
+        """GPU client and every hop announced a device channel on THIS machine.  (CPU swarms stay
+        on the TCP RPC path: BASELINE config 1 is "rpc_transport over localhost"; ``--device_channel
+        on`` forces the channel anyway, over gloo.)"""
+        from .parallel.channel import host_id
+
+        me = host_id()
+        return torch.device(device).type == "cuda" and bool(route) and route[-1].final and \
+            all(h.info.get("channel_host") == me for h in route)
+
+    def open_device_channel(self, route: List[Hop], device, *, n_slots: int = 1, batch: int = 64,
+                            timeout: float = 60.0, idle_timeout: float = 3600.0):
+        """Rendezvous a ``parallel.channel.Channel`` with every hop of ``route``: this client
+        is rank 0 (head), hop i is rank i + 1, the final hop the tail.  The TCP RPC carries
+        only this handshake; afterwards hidden states move GPU -> GPU (RCCL over xGMI) and the
+        tail returns token ids on the channel.  Payloads are staged through gloo when two
+        participants share a GPU (RCCL refuses duplicate devices) or on CPU."""
+        import uuid
+
+        from .parallel.channel import Channel, free_port, host_id, make_store
+
+        world = len(route) + 1
+        devs = [str(torch.device(device))] + [str(h.info.get("device", "")) for h in route]
+        gpu = torch.device(device).type == "cuda"
+        data = "nccl" if gpu and len(set(devs)) == len(devs) else "gloo"
+        port = free_port("127.0.0.1")
+        store = make_store("127.0.0.1", port, world, True, timeout_s=timeout)
+        prefix = f"chan-{uuid.uuid4().hex[:12]}"
+
+        async def _open():
+            for i, hop in enumerate(route):
+                md = {"store_host": "127.0.0.1", "store_port": port, "prefix": prefix, "rank": i + 1, "world": world,
+                      "timeout": timeout, "idle_timeout": idle_timeout, "data_backend": data, "n_slots": n_slots,
+                      "batch": batch, "host_id": host_id()}
+                r = await self._call_hop(hop, "rpc_channel_open", [], md)
+                if not r.metadata.get("ok"):
+                    raise ConnectionError(f"{hop}: device channel refused: {r.metadata.get('error')}")
+
+        self._run(_open())
+        ch = Channel(store, prefix, 0, world, device, timeout_s=timeout, data_backend=data)
+        ch._store = store  # the client hosts the rendezvous store: keep it alive with the channel
+        logger.info(f"device channel {prefix}: {world} ranks, data over {data}")
+        return ch
 
     # ------------------------------------------------------------------ fine-tuning (stateless)
     def _fresh_route(self) -> List[Hop]:

@@ -23,6 +23,7 @@ import dataclasses
 import logging
 import math
 import os
+import threading
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -172,6 +173,9 @@ class StageExecutor:
         self._decode_qb: Dict[int, torch.Tensor] = {}
         self._moe_y: Dict[int, torch.Tensor] = {}
         self.timing = False
+        # one executor may be driven by the TCP handler's GPU worker AND a device-channel
+        # engine thread: every device step (incl. hipGraph capture) runs under this lock
+        self.exec_lock = threading.RLock()
         if self.device.type == "cuda":
             ops.require_native()
             if cfg.model_type != "gpt2" and ops.gemm_policy() != "hipblaslt":

@@ -250,3 +250,32 @@ def test_next_pings_announced():
     finally:
         s1.close()
         s2.close()
+
+
+@pytest.mark.timeout(240)
+def test_cli_client_over_device_channel_matches_reference(capsys):
+    """``python -m src.main`` servers + the stage-0 client with ``--device_channel on``: the
+    client rendezvouses a channel through both servers (rpc_channel_open over TCP), then the
+    hidden states and token ids move on the channel (gloo here, RCCL on GPUs).  Greedy output
+    equals the single-process reference; the servers keep serving TCP afterwards."""
+    from src import main as M
+
+    s1 = ServerThread(server_argv(MODEL, "1,2", 1)).wait()
+    s2 = ServerThread(server_argv(MODEL, "1,2", 2, peers=s1.addr)).wait()
+    try:
+        assert wait_for(lambda: s1.dht.get(get_stage_key(2)) is not None)
+        rec = s1.dht.get(get_stage_key(1)).value
+        assert all("channel_host" in (v.value if hasattr(v, "value") else v) for v in rec.values())
+        args = client_args(MODEL, "1,2", s1.addr, "--device_channel on --temperature 0 --max_new_tokens 6 "
+                                                  "--num_sessions 3")
+        gen = M.run_rank0(args, M.pick_device(args), [1, 2])
+        assert gen == _reference(6)
+        assert s1.srv.handler.stats.get("channels") == 1 and s2.srv.handler.stats.get("channels") == 1
+        assert wait_for(lambda: not s1.srv.ex.sessions.sessions and not s2.srv.ex.sessions.sessions)
+        # the TCP path still works on the same servers
+        cfg, ex, tx = _client(s1.addr, [1, 2])
+        assert _generate(ex, tx, 4) == _reference(4)
+        tx.shutdown()
+    finally:
+        s1.close()
+        s2.close()

@@ -126,12 +126,31 @@ def main(argv=None):
 
         ch = Channel(c10d._get_default_store(), f"bench/pipe{lane}", stage, S, device, timeout_s=600.0)
     eng = PipelineServingEngine(ex, ch, n_slots=M, batch=B, max_step_tokens=B * a.prompt_len, name=f"p{lane}")
+    n_sessions = M * B
+    if R > 1:
+        # replica placement from measured throughput: every rank times its stage's decode step,
+        # the node all-gathers them (host control group) and the sessions are split in
+        # proportion to each replica's slowest stage (parallel/router.py, parallel/pipeline.py)
+        from torch.distributed import distributed_c10d as c10d
+
+        from src.parallel.channel import HostLink
+        from src.parallel.pipeline import assign_sessions
+        from src.parallel.router import gather_replica_throughput
+
+        link = HostLink(c10d._get_default_store(), "bench/all", rank, world, timeout_s=600.0)
+        thr = gather_replica_throughput(link, ex, lane // TP, stage, R, batch=min(B, 16))
+        counts = [assign_sessions(M * B * R, thr).count(r) for r in range(R)]
+        n_sessions = min(M * B, counts[lane // TP])  # a slot holds B sessions: never over-admit
+        link.close()
+        if rank == 0:
+            print(f"replica throughput (tok/s, probe batch {min(B, 16)}): {[round(t, 1) for t in thr]} -> "
+                  f"sessions {counts}", file=sys.stderr)
     if stage == 0:
         # synthetic requests: every pipeline of a TP group submits the same ones (same seeds),
         # so its shards take identical scheduling decisions and sample identical tokens
         sp = SamplingParams(a.temperature, a.top_p, a.top_k, a.repetition_penalty)
         gen = torch.Generator().manual_seed(1234 + (lane // TP))
-        for i in range(M * B):
+        for i in range(n_sessions):
             prompt = torch.randint(0, cfg.vocab_size, (a.prompt_len,), generator=gen).tolist()
             eng.submit(Request(prompt, max_new_tokens=rounds + 8, params=sp, stop_on_repeat=0,
                                seed=a.seed * 1000003 + (lane // TP) * 7919 + i, rid=f"s{i}"))
@@ -175,8 +194,10 @@ def main(argv=None):
     if ch is not None:
         ch.close()
     dt = pdist.all_max(dt_local, device)
-    per_stage = pdist.all_gather_floats([stage_ms, float(end - start)], device)
-    tokens = a.steps * M * B * R  # every session advances one token per round
+    counted = float(n_sessions) if (stage == 0 and lane % TP == 0) else 0.0  # TP lanes mirror one replica
+    per_stage = pdist.all_gather_floats([stage_ms, float(end - start), counted], device)
+    global_batch = int(sum(p[2] for p in per_stage))
+    tokens = a.steps * global_batch  # every session advances one token per round
     value = tokens / dt
     base = baseline_value() if a.model == "llama2-7b" else None  # the baseline is a Llama-2-7B number
     if rank == 0:
@@ -197,7 +218,7 @@ def main(argv=None):
             "config": {
                 "model": {"llama2-7b": "Llama-2-7B", "llama3-70b": "Llama-3-70B", "llama3-8b": "Llama-3-8B"}.get(
                     a.model, a.model),
-                "global_batch": M * B * R,
+                "global_batch": global_batch,
                 "seq_len": a.prompt_len,
                 "parallelism": f"pp{S}" + (f"xtp{TP}" if TP > 1 else "") + (f"xdp{R}" if R > 1 else ""),
                 "micro_batches": M,

@@ -260,6 +260,33 @@ class Channel:
                     pass
 
 
+class HostLink:
+    """A host-only (gloo) group: the replica router's link to a remote replica head, or the
+    node-wide control group that all-gathers measured stage throughput."""
+
+    def __init__(self, store, prefix: str, rank: int, world: int, timeout_s: float = 120.0):
+        self.rank, self.world, self.timeout_s = int(rank), int(world), float(timeout_s)
+        self.ctrl = _gloo(store, prefix, self.rank, self.world, timeout_s)
+        self._msg_sends = _Pending()
+        self.closed = False
+
+    send_msg = Channel.send_msg
+    recv_msg = Channel.recv_msg
+    all_gather_floats = Channel.all_gather_floats
+
+    def close(self) -> None:
+        if not self.closed:
+            self.closed = True
+            try:
+                self._msg_sends.drain(timeout_s=min(self.timeout_s, 10.0))
+            except RuntimeError:
+                pass
+
+    def abort(self) -> None:
+        self.closed = True
+        self._msg_sends.q.clear()
+
+
 def wait_event(ev, timeout_s: float, what: str = "device event") -> None:
     """Poll a HIP event with a deadline: a stream stuck on a receive from a dead RCCL peer
     never completes, and ``Event.synchronize`` would hang the host with it."""

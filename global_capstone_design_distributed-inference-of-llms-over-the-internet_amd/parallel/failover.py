@@ -63,6 +63,20 @@ class ReplicaRouter:
             out[sid] = live[k]
         return out
 
+    def place_one(self, session_id: str, prompt: Sequence[int]) -> int:
+        """Online placement of ONE new session: the live replica with the lowest
+        throughput-normalised load after adding it (ties to the lower index)."""
+        live = self.live()
+        if not live:
+            raise RuntimeError("no live replica")
+        load: Dict[int, int] = {}
+        for r in self.placement.values():
+            load[r] = load.get(r, 0) + 1
+        best = min(live, key=lambda k: ((load.get(k, 0) + 1) / max(float(self.throughput[k]), 1e-9), k))
+        self.placement[session_id] = best
+        self.history[session_id] = [int(t) for t in prompt]
+        return best
+
     def record(self, session_id: str, token: int) -> None:
         self.history[session_id].append(int(token))
 

@@ -1,0 +1,282 @@
+"""Replica router and failover for single-node pipelines (BASELINE configs "4 stages x 2
+replicas, load_balancing.py routing over RCCL subgroups" and "... + fault-tolerance replica
+failover").
+
+Reference: servers hosting the same blocks register under the same keys; the client routes
+each session greedily over the live spans (src/rpc_transport.py:393-501), and when a hop
+fails it excludes the peer, re-discovers a replacement and replays the session's cached
+inputs to rebuild its KV (src/rpc_transport.py:587-712).
+
+On one node a replica is a whole pipeline (its own device channel), so routing and
+recovery work one level up, in a front end on global rank 0 (which is also replica 0's
+head):
+
+* **Throughput registry.** Every rank measures its stage's decode rate and the node
+  all-gathers them on a host control group (``gather_replica_throughput``); a replica's
+  rate is its slowest stage's.  Running replica heads keep reporting their measured
+  tokens/s, and the router's placement weights follow (EMA).
+* **Placement.** New sessions go to live replicas in proportion to throughput
+  (``ReplicaRouter`` / ``assign_sessions``); a per-replica host link (gloo) carries
+  admissions (prompt, generated-so-far, sampling parameters, seed) to remote heads and
+  token / finish reports back, one exchange per head round, each on its own router thread
+  so replicas never wait on each other.
+* **Failure detection.** A head whose pipeline loses a stage reports it (its channel
+  aborted, see ``engine.PipelineFailure``); a head that dies shows up as a link error or
+  timeout.  Either way the replica is marked dead and its unfinished sessions are
+  re-placed on the survivors by **re-prefilling prompt + generated tokens** (token history
+  is all a pipeline needs to rebuild KV).  Sampling is seeded by (session seed, position),
+  so the survivors produce exactly the tokens the failed replica would have.
+"""
+from __future__ import annotations
+
+import logging
+import threading
+import time
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from ..runtime.sampler import SamplingParams
+from .channel import ChannelError, HostLink
+from .engine import PipelineFailure, PipelineServingEngine, Request, _f2i, _i2f
+from .failover import ReplicaRouter
+
+logger = logging.getLogger(__name__)
+
+REPORT, CMD = 1, 2
+REASONS = {"eos": 1, "length": 2, "repeat": 3, "max_length": 4, "done": 5}
+REASON_OF = {v: k for k, v in REASONS.items()}
+
+
+def gather_replica_throughput(link: HostLink, executor, replica: int, stage: int, n_replicas: int,
+                              batch: int = 16) -> List[float]:
+    """All-gather every rank's measured decode rate; replica tokens/s = batch x its slowest
+    stage's steps/s (the C3 "throughput registry over an all-gather")."""
+    from ..throughput_measurement import measure_compute_throughput
+
+    sps = measure_compute_throughput(executor, n_warmup=1, n_steps=3, batch=batch)
+    rows = link.all_gather_floats([float(replica), float(stage), float(sps)])
+    per = [float("inf")] * n_replicas
+    for r, _, v in rows:
+        per[int(r)] = min(per[int(r)], v)
+    return [batch * v for v in per]
+
+
+# ------------------------------------------------------------------ wire format (int64)
+def encode_cmd(reqs: Sequence[Tuple[int, Request]], stop: bool) -> np.ndarray:
+    out = [CMD, int(stop), len(reqs)]
+    for rid, r in reqs:
+        p = r.params
+        out += [rid, r.max_new_tokens, r.seed, -1 if r.eos_token_id is None else int(r.eos_token_id),
+                r.stop_on_repeat, _f2i(p.temperature), _f2i(p.top_p), int(p.top_k), _f2i(p.repetition_penalty),
+                len(r.prompt), len(r.generated)]
+        out += list(r.prompt) + list(r.generated)
+    return np.asarray(out, dtype=np.int64)
+
+
+def decode_cmd(a: np.ndarray) -> Tuple[bool, List[Request]]:
+    assert int(a[0]) == CMD
+    stop, n = bool(a[1]), int(a[2])
+    off, reqs = 3, []
+    for _ in range(n):
+        rid, mx, seed, eos, rep, t, tp, tk, rp, lp, lg = (int(v) for v in a[off:off + 11])
+        off += 11
+        prompt = a[off:off + lp].tolist()
+        gen = a[off + lp:off + lp + lg].tolist()
+        off += lp + lg
+        reqs.append(Request(prompt, max_new_tokens=mx, params=SamplingParams(_i2f(t), _i2f(tp), tk, _i2f(rp)),
+                            eos_token_id=None if eos < 0 else eos, stop_on_repeat=rep, seed=seed, rid=str(rid),
+                            generated=gen))
+    return stop, reqs
+
+
+def encode_report(tokens: Sequence[Tuple[int, int]], finished: Sequence[Tuple[int, int]], failed: bool,
+                  tok_per_s: float) -> np.ndarray:
+    out = [REPORT, int(failed), len(tokens), len(finished), int(tok_per_s * 1000)]
+    for a, b in tokens:
+        out += [a, b]
+    for a, b in finished:
+        out += [a, b]
+    return np.asarray(out, dtype=np.int64)
+
+
+def decode_report(a: np.ndarray):
+    assert int(a[0]) == REPORT
+    failed, nt, nf, thr = bool(a[1]), int(a[2]), int(a[3]), int(a[4]) / 1000.0
+    toks = a[5:5 + 2 * nt].reshape(nt, 2).tolist()
+    fin = a[5 + 2 * nt:5 + 2 * nt + 2 * nf].reshape(nf, 2).tolist()
+    return failed, toks, fin, thr
+
+
+# ------------------------------------------------------------------ remote replica head
+def serve_replica_head(engine: PipelineServingEngine, link: HostLink, timeout_s: float = 120.0) -> str:
+    """Loop of a replica head (global rank r*S, r >= 1): report tokens, take admissions,
+    run one round.  Returns "stopped" or "failed"."""
+    toks: List[Tuple[int, int]] = []
+    fin: List[Tuple[int, int]] = []
+    engine.on_token = lambda req, t: toks.append((int(req.rid), int(t)))
+    engine.on_finish = lambda req: fin.append((int(req.rid), REASONS.get(req.finish_reason, 5)))
+    failed = False
+    t_last, n_last = time.perf_counter(), 0
+    while True:
+        now = time.perf_counter()
+        rate = (engine.tokens_generated - n_last) / max(now - t_last, 1e-6) if engine.is_head else 0.0
+        t_last, n_last = now, engine.tokens_generated
+        link.send_msg(0, encode_report(toks, fin, failed, rate))
+        toks.clear()
+        fin.clear()
+        if failed:
+            link.close()
+            return "failed"
+        stop, adm = decode_cmd(link.recv_msg(0, timeout_s))
+        for r in adm:
+            engine.submit(r)
+        if stop:
+            engine.drain()
+            engine.stop()
+            link.close()
+            return "stopped"
+        try:
+            if engine.idle:
+                time.sleep(0.002)
+            else:
+                engine.run_rounds(1)
+        except PipelineFailure as e:
+            logger.error(f"replica head: pipeline failed ({e}); reporting to the router")
+            failed = True
+
+
+# ------------------------------------------------------------------ front end (global rank 0)
+class ReplicaFrontend:
+    def __init__(self, n_replicas: int, local: Optional[PipelineServingEngine], links: Dict[int, HostLink],
+                 throughputs: Optional[Sequence[float]] = None, timeout_s: float = 120.0):
+        self.n = int(n_replicas)
+        self.router = ReplicaRouter(self.n, throughputs, timeout_s)
+        self.local = local
+        self.links = links
+        self.timeout_s = timeout_s
+        self.lock = threading.RLock()
+        self.requests: Dict[int, Request] = {}
+        self.pending: Dict[int, List[int]] = {r: [] for r in range(self.n)}
+        self.failures: List[Tuple[int, str]] = []
+        self._next = 0
+        self._local_map: Dict[str, int] = {}
+        self._threads: List[threading.Thread] = []
+        self.replica_tokens = [0] * self.n
+        if local is not None:
+            local.on_token = self._local_token
+            local.on_finish = self._local_finish
+
+    # ---------------------------------------------------------------- API
+    def submit(self, req: Request) -> Request:
+        with self.lock:
+            rid = self._next
+            self._next += 1
+            req.rid = req.rid or f"q{rid}"
+            self.requests[rid] = req
+            rep = self.router.place_one(str(rid), req.prompt)
+            self.pending[rep].append(rid)
+        return req
+
+    def all_done(self) -> bool:
+        with self.lock:
+            return all(r.done for r in self.requests.values())
+
+    def run(self, poll_s: float = 0.002) -> List[Request]:
+        for r, link in self.links.items():
+            t = threading.Thread(target=self._remote_loop, args=(r, link), daemon=True, name=f"router-{r}")
+            t.start()
+            self._threads.append(t)
+        while not self.all_done():
+            if self.local is not None and self.router.alive[0]:
+                self._feed_local()
+                try:
+                    if self.local.idle:
+                        time.sleep(poll_s)
+                    else:
+                        self.local.run_rounds(1)
+                except PipelineFailure as e:
+                    self._fail(0, f"local pipeline: {e}")
+            else:
+                if not any(self.router.alive):
+                    raise RuntimeError("every replica failed")
+                time.sleep(poll_s)
+        if self.local is not None and self.router.alive[0]:
+            self.local.drain()
+            self.local.stop()
+        for t in self._threads:
+            t.join(self.timeout_s)
+        return [self.requests[k] for k in sorted(self.requests)]
+
+    # ---------------------------------------------------------------- bookkeeping
+    def _token(self, r: int, rid: int, tok: int) -> None:
+        with self.lock:
+            req = self.requests.get(rid)
+            if req is None or req.done or self.router.placement.get(str(rid)) != r:
+                return
+            if req.t_first is None:
+                req.t_first = time.perf_counter()
+            req.generated.append(int(tok))
+            self.router.record(str(rid), int(tok))
+            self.replica_tokens[r] += 1
+
+    def _finish(self, r: int, rid: int, reason: str) -> None:
+        with self.lock:
+            req = self.requests.get(rid)
+            if req is None or req.done or self.router.placement.get(str(rid)) != r:
+                return
+            req.done, req.finish_reason, req.t_done = True, reason, time.perf_counter()
+            self.router.close(str(rid))  # finished sessions no longer count as replica load
+
+    def _local_token(self, req: Request, tok: int) -> None:
+        self._token(0, int(req.rid), tok)
+
+    def _local_finish(self, req: Request) -> None:
+        self._finish(0, int(req.rid), req.finish_reason or "done")
+
+    def _take(self, r: int) -> List[Tuple[int, Request]]:
+        with self.lock:
+            rids, self.pending[r] = self.pending[r], []
+            return [(rid, self.requests[rid]) for rid in rids if not self.requests[rid].done]
+
+    def _feed_local(self) -> None:
+        for rid, m in self._take(0):
+            self.local.submit(Request(list(m.prompt), max_new_tokens=m.max_new_tokens, params=m.params,
+                                      eos_token_id=m.eos_token_id, stop_on_repeat=m.stop_on_repeat, seed=m.seed,
+                                      rid=str(rid), generated=list(m.generated)))
+
+    def _fail(self, r: int, why: str) -> None:
+        with self.lock:
+            if not self.router.alive[r]:
+                return
+            logger.error(f"replica {r} failed: {why}; re-placing its sessions")
+            self.failures.append((r, why))
+            # every unfinished session placed on r (delivered or still pending) moves to a
+            # survivor, which re-prefills prompt + generated tokens (the master copies)
+            plans = self.router.fail(r)
+            self.pending[r] = []
+            for plan in plans:
+                self.pending[plan.replica].append(int(plan.session_id))
+
+    def _remote_loop(self, r: int, link: HostLink) -> None:
+        try:
+            while True:
+                failed, toks, fin, thr = decode_report(link.recv_msg(1, self.timeout_s))
+                for rid, t in toks:
+                    self._token(r, rid, t)
+                for rid, code in fin:
+                    self._finish(r, rid, REASON_OF.get(code, "done"))
+                if failed:
+                    self._fail(r, "head reported a pipeline failure")
+                    return
+                if thr > 0:
+                    with self.lock:
+                        self.router.throughput[r] = 0.8 * self.router.throughput[r] + 0.2 * thr
+                        self.router.heartbeat(r)
+                stop = self.all_done()
+                link.send_msg(1, encode_cmd(self._take(r), stop))
+                if stop:
+                    link.close()
+                    return
+        except ChannelError as e:
+            self._fail(r, f"link: {e}")

@@ -70,6 +70,7 @@ class LlamaLayer:
     # (and their packed copies) are then stacked per expert: [E, 2F, H] / [E, H, F]
     router: Optional[torch.Tensor] = None
     router_p: Optional[torch.Tensor] = None  # router padded to 16 rows, packed (decode GEMM)
+    folded: bool = False  # qkv_p / gate_up_p carry the input / post-attention norm weights
 
     PROJ = ("qkv", "o", "gate_up", "down")
 
@@ -134,16 +135,29 @@ class StageWeights:
             n += t.numel() * t.element_size()
         return n
 
-    def pack_for_decode(self) -> None:
+    def pack_for_decode(self, fold_norms: bool = False) -> None:
         """Add fragment-native copies of every projection (MI355X decode GEMM layout).
 
         The row-major weights stay for the hipBLASLt prefill path: 2x weight bytes, which
         288 GB of HBM affords (13.5 GB -> 27 GB for Llama-2-7B on one GPU).
+
+        ``fold_norms``: the packed qkv / gate_up copies carry the RMSNorm weight folded into
+        their K columns (W' = W diag(g)) for the fused-norm decode path, whose GEMMs take the raw
+        residual stream and apply rsqrt(mean x^2) per row in the epilogue (ops/csrc/gemm.hip).
         """
         from .. import ops
 
         for lay in self.layers:
             if isinstance(lay, LlamaLayer) and lay.qkv_p is None and lay.qkv is not None:
+                if fold_norms and not lay.moe:
+                    lay.qkv_p = ops.pack_weight((lay.qkv.float() * lay.input_norm.float()[None, :])
+                                                .to(lay.qkv.dtype).contiguous())
+                    lay.o_p = ops.pack_weight(lay.o)
+                    lay.gate_up_p = ops.pack_weight((lay.gate_up.float() * lay.post_norm.float()[None, :])
+                                                    .to(lay.gate_up.dtype).contiguous())
+                    lay.down_p = ops.pack_weight(lay.down)
+                    lay.folded = True
+                    continue
                 lay.qkv_p = ops.pack_weight(lay.qkv)
                 lay.o_p = ops.pack_weight(lay.o)
                 if lay.moe:

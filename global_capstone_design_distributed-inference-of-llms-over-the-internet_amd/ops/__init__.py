@@ -206,20 +206,24 @@ def autotune_gemm(shapes, device, ms=(16, 32, 48, 64), iters: int = 24, rounds: 
                 xp = pack_act(torch.randn(M, K, device=device).to(torch.bfloat16))
                 y = torch.empty(packed_numel(M, ncols) if epi == 1 else M * ncols, dtype=torch.bfloat16,
                                 device=device)
-                res = torch.zeros(M, N, dtype=torch.bfloat16, device=device) if epi == 2 else None
-                out = y if epi == 1 else y.view(M, ncols)
+                res = torch.zeros(M, N, dtype=torch.bfloat16, device=device) if epi in (2, 3) else None
+                extra = {}
+                if epi == 3:  # fused-norm producer: packed copy + per-row sum of squares
+                    extra = dict(ap_out=torch.zeros(packed_numel(M, N), dtype=torch.bfloat16, device=device),
+                                 ss_out=norm_stats_buffer(device)[0], ss_zero=norm_stats_buffer(device)[0])
+                out = y if epi == 1 else (res if epi == 3 else y.view(M, ncols))
                 t = {k: float("inf") for k in cands}
                 for _ in range(rounds):
                     for mode in cands:
                         _GEMM_SK = mode
                         for i in range(2):
                             linear(xp, None, out=out, epilogue=epi, residual=res, wp=wps[i % copies], a_rows=M,
-                                   out_packed=epi == 1)
+                                   out_packed=epi == 1, **extra)
                         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                         e0.record()
                         for i in range(iters):
                             linear(xp, None, out=out, epilogue=epi, residual=res, wp=wps[i % copies], a_rows=M,
-                                   out_packed=epi == 1)
+                                   out_packed=epi == 1, **extra)
                         e1.record()
                         e1.synchronize()
                         t[mode] = min(t[mode], e0.elapsed_time(e1) / iters)
@@ -254,19 +258,27 @@ def unpack_act(ap, M, K):
     return ref.unpack_act(ap, M, K)
 
 
-def rmsnorm(x, w, eps, out=None, residual=None, mode=0, rows=None, packed=False):
-    """mode 0: y = norm(x)*w; 1: residual += x, y = norm(residual)*w; 2: residual = x, y = norm(x)*w.
+def norm_stats_buffer(device, n: int = 1) -> torch.Tensor:
+    """Zeroed fixed-point row statistics for the fused-norm decode path: int64 [n, 32, 64]
+    (32 atomic shards x 64 rows of exact sums of round(x^2 * 2^20), csrc/gemm.hip EpiArgs)."""
+    return torch.zeros(n, ref.SS_SHARDS, 64, dtype=torch.int64, device=device)
+
+
+def rmsnorm(x, w, eps, out=None, residual=None, mode=0, rows=None, packed=False, ss=None):
+    """mode 0: y = norm(x)*w; 1: residual += x, y = norm(residual)*w; 2: residual = x, y = norm(x)*w;
+    3: residual = x, y = x, ``ss`` = fixed-point row sums of squares (``norm_stats_buffer``; entry of
+    the fused-norm decode path).
 
     ``packed``: write y in the packed decode-GEMM activation layout (``out`` flat)."""
     if not _native(x):
-        y = ref.rmsnorm(x, w, eps, out=None if packed else out, residual=residual, mode=mode, rows=rows)
+        y = ref.rmsnorm(x, w, eps, out=None if packed else out, residual=residual, mode=mode, rows=rows, ss=ss)
         return ref.pack_act(y, out=out) if packed else y
     n = rows.numel() if rows is not None else x.shape[0]
     if out is None:
         out = (torch.empty(packed_numel(n, x.shape[1]), dtype=x.dtype, device=x.device) if packed
                else torch.empty(n, x.shape[1], dtype=x.dtype, device=x.device))
     torch.ops.mpamd.rmsnorm(x, residual if residual is not None else x, w, out, float(eps), int(mode), rows,
-                            int(bool(packed)))
+                            int(bool(packed)), ss)
     return out
 
 
@@ -506,19 +518,24 @@ def unpack_weight(wp: torch.Tensor) -> torch.Tensor:
 
 
 def linear(x, w, out=None, epilogue=0, residual=None, policy=None, wp=None, a_rows=None, out_packed=False,
-           gate=None):
-    """y = epilogue(x @ w^T). epilogue 0: none; 1: SwiGLU (16-row interleaved gate/up w); 2: + residual.
+           gate=None, ss_in=None, eps=0.0, ap_out=None, ss_out=None, ss_zero=None):
+    """y = epilogue(x @ w^T). epilogue 0: none; 1: SwiGLU (16-row interleaved gate/up w); 2: + residual;
+    3: fused-norm producer (``residual`` updated in place to bf16(y + residual), also written packed to
+    ``ap_out``, per-row sum of squares added to ``ss_out``; ``ss_zero`` is cleared).
 
     ``wp`` is the packed copy of ``w`` (``pack_weight``); the native decode GEMM needs it.
     ``a_rows`` (int) says ``x`` is a PACKED activation holding that many rows (decode path);
     ``out_packed`` (SwiGLU only) writes the output packed for the next GEMM.
+    ``ss_in`` (fused-norm consumer): ``x`` is the raw residual stream, ``w`` has the RMSNorm weight
+    folded into its columns, and row r of the product is scaled by rsqrt(ss_in[r] / K + eps).
     """
     if not _native(x):
+        K = 32 * wp.shape[1] if wp is not None else w.shape[1]
         if a_rows is not None:
-            K = 32 * wp.shape[1] if wp is not None else w.shape[1]
             x = ref.unpack_act(x, a_rows, K)
-        y = ref.linear(x, w if w is not None else unpack_weight(wp), out=None if out_packed else out,
-                       epilogue=epilogue, residual=residual)
+        y = ref.linear(x, w if w is not None else unpack_weight(wp), out=None if out_packed or epilogue == 3 else out,
+                       epilogue=epilogue, residual=residual, ss_in=ss_in, inv_k=1.0 / K, eps=eps, ap_out=ap_out,
+                       ss_out=ss_out, ss_zero=ss_zero)
         return ref.pack_act(y, out=out) if out_packed else y
     if a_rows is not None:
         M = int(a_rows)
@@ -539,8 +556,11 @@ def linear(x, w, out=None, epilogue=0, residual=None, policy=None, wp=None, a_ro
         kern = "pk" if gate is not None else _kernel_for(M, N, K, epilogue)
         flags = 1 | (2 if out_packed else 0) | _KERNEL_FLAGS[kern]
         ws = gemm_workspace(x.device) if kern == "sk" else None
-        torch.ops.mpamd.gemm(x, wp, out, residual, int(epilogue), M, flags, ws, gate)
+        torch.ops.mpamd.gemm(x, wp, out, residual, int(epilogue), M, flags, ws, gate, ap_out, ss_out, ss_zero, ss_in,
+                             1.0 / K, float(eps))
         return out
+    if epilogue == 3 or ss_in is not None:
+        raise RuntimeError(f"the fused-norm epilogues need the native decode GEMM (M={M}, N={N}, K={K})")
     if a_rows is not None or out_packed:
         raise RuntimeError(f"packed activations need the native decode GEMM (M={M}, N={N}, K={K})")
     if w is None:

@@ -12,7 +12,7 @@
 extern "C" {
 int mp_rmsnorm(const void* x, int64_t x_stride, void* res, int64_t res_stride, const void* w, void* y,
                int64_t y_stride, const int32_t* rows, int nrows, int H, float eps, int mode, int packed_mt,
-               hipStream_t stream);
+               void* ss_out, hipStream_t stream);
 int mp_rope_kv_write(void* qkv, int64_t qkv_stride, const int64_t* pos, const float* cos_t, const float* sin_t,
                      void* kc, void* vc, const int64_t* slots, int T, int nh, int nkv, int D, int page_size,
                      hipStream_t stream);
@@ -41,7 +41,9 @@ int mp_gemm_fp8(const void* a8, const float* as, const void* wq, const float* ws
                 int64_t rs, int M, int N, int K, int epilogue, int out_packed, hipStream_t stream);
 int mp_gemm_bf16(const void* x, int64_t x_stride, const void* w, void* y, int64_t y_stride, const void* res,
                  int64_t res_stride, int M, int N, int K, int epilogue, int flags, void* ws, const int* gate,
+                 void* ap, void* ss_out, void* ss_zero, const void* ss_in, float inv_k, float eps,
                  hipStream_t stream);
+int mp_gemm_ss_elems();
 int mp_pack_act(const void* x, int64_t xs, void* ap, int M, int K, hipStream_t stream);
 int mp_pack_weight(const void* w, void* wp, int N, int K, hipStream_t stream);
 }
@@ -70,8 +72,16 @@ inline void check_rows(const at::Tensor& t, const char* name) {
 
 inline int64_t packed_numel(int64_t M, int64_t K) { return ((M + 15) / 16) * 16 * K; }
 
+// fused-norm row statistics: int64 [32 shards][64 rows] fixed-point sums (gemm.hip EpiArgs)
+inline void* opt_ss(const c10::optional<at::Tensor>& t, const char* name) {
+  if (!t.has_value()) return nullptr;
+  MP_CHECK(t->is_cuda() && t->scalar_type() == at::kLong && t->is_contiguous() && t->numel() >= mp_gemm_ss_elems(),
+           std::string(name) + ": int64 cuda contiguous [32, 64] (ops.norm_stats_buffer)");
+  return t->data_ptr();
+}
+
 void rmsnorm(const at::Tensor& x, at::Tensor& residual, const at::Tensor& w, at::Tensor& y, double eps, int64_t mode,
-             const c10::optional<at::Tensor>& rows, int64_t packed) {
+             const c10::optional<at::Tensor>& rows, int64_t packed, const c10::optional<at::Tensor>& ss) {
   check_bf16_cuda(x, "x");
   check_bf16_cuda(w, "w");
   check_bf16_cuda(y, "y");
@@ -82,7 +92,9 @@ void rmsnorm(const at::Tensor& x, at::Tensor& residual, const at::Tensor& w, at:
     check_rows(y, "y");
     MP_CHECK(y.size(1) == H, "y cols");
   }
-  MP_CHECK(mode >= 0 && mode <= 2, "mode");
+  MP_CHECK(mode >= 0 && mode <= 3, "mode");
+  void* ssp = opt_ss(ss, "ss");
+  MP_CHECK(mode != 3 || (ssp != nullptr && x.size(0) <= 64), "mode 3 needs ss and <= 64 rows");
   if (mode != 0) {
     check_bf16_cuda(residual, "residual");
     check_rows(residual, "residual");
@@ -105,7 +117,7 @@ void rmsnorm(const at::Tensor& x, at::Tensor& residual, const at::Tensor& w, at:
   }
   check_launch(mp_rmsnorm(x.data_ptr(), x.stride(0), mode ? residual.data_ptr() : nullptr,
                           mode ? residual.stride(0) : 0, w.data_ptr(), y.data_ptr(), packed ? 0 : y.stride(0), rp,
-                          nrows, H, (float)eps, (int)mode, pmt, cur_stream()),
+                          nrows, H, (float)eps, (int)mode, pmt, ssp, cur_stream()),
                "rmsnorm");
 }
 
@@ -342,7 +354,9 @@ void sample(const at::Tensor& logits, const at::Tensor& temps, const at::Tensor&
 // flags bit 0: x is packed (holds ceil(M/16)*16*K elements, M given); bit 1: packed SwiGLU output
 void gemm(const at::Tensor& x, const at::Tensor& wp, at::Tensor& y, const c10::optional<at::Tensor>& residual,
           int64_t epilogue, int64_t M_, int64_t flags, const c10::optional<at::Tensor>& workspace,
-          const c10::optional<at::Tensor>& gate) {
+          const c10::optional<at::Tensor>& gate, const c10::optional<at::Tensor>& ap,
+          const c10::optional<at::Tensor>& ss_out, const c10::optional<at::Tensor>& ss_zero,
+          const c10::optional<at::Tensor>& ss_in, double inv_k, double eps) {
   check_bf16_cuda(x, "x");
   check_bf16_cuda(wp, "wp");
   check_bf16_cuda(y, "y");
@@ -375,8 +389,18 @@ void gemm(const at::Tensor& x, const at::Tensor& wp, at::Tensor& y, const c10::o
     rp = residual->data_ptr();
     rs = residual->stride(0);
   }
-  MP_CHECK(epilogue != 2 || rp != nullptr, "residual epilogue needs residual");
-  MP_CHECK(epilogue >= 0 && epilogue <= 2, "epilogue");
+  MP_CHECK(epilogue < 2 || rp != nullptr, "residual epilogue needs residual");
+  MP_CHECK(epilogue >= 0 && epilogue <= 3, "epilogue");
+  void* app = nullptr;
+  if (ap.has_value()) {
+    check_bf16_cuda(*ap, "ap");
+    MP_CHECK(ap->is_contiguous() && ap->numel() >= packed_numel(M, N), "ap: packed [ceil(M/16)*16*N]");
+    app = ap->data_ptr();
+  }
+  void* sso = opt_ss(ss_out, "ss_out");
+  void* ssz = opt_ss(ss_zero, "ss_zero");
+  const void* ssi = opt_ss(ss_in, "ss_in");
+  MP_CHECK(epilogue != 3 || (app != nullptr && sso != nullptr && !opk), "epilogue 3 needs ap and ss_out");
   void* ws = nullptr;
   if (workspace.has_value()) {
     MP_CHECK(workspace->is_cuda() && workspace->is_contiguous() &&
@@ -390,7 +414,8 @@ void gemm(const at::Tensor& x, const at::Tensor& wp, at::Tensor& y, const c10::o
     gp = gate->data_ptr<int>();
   }
   check_launch(mp_gemm_bf16(x.data_ptr(), apk ? 0 : x.stride(0), wp.data_ptr(), y.data_ptr(), opk ? 0 : y.stride(0),
-                            rp, rs, M, N, K, (int)epilogue, (int)flags, ws, gp, cur_stream()),
+                            rp, rs, M, N, K, (int)epilogue, (int)flags, ws, gp, app, sso, ssz, ssi, (float)inv_k,
+                            (float)eps, cur_stream()),
                "gemm");
 }
 
@@ -467,7 +492,7 @@ TORCH_LIBRARY(mpamd, m) {
   m.def("gemm_workspace_bytes() -> int", &gemm_workspace_bytes);
   m.def(
       "rmsnorm(Tensor x, Tensor(a!) residual, Tensor w, Tensor(b!) y, float eps, int mode, Tensor? rows, "
-      "int packed) -> ()");
+      "int packed, Tensor(c!)? ss=None) -> ()");
   m.def(
       "rope_kv_write(Tensor(a!) qkv, Tensor positions, Tensor cos, Tensor sin, Tensor(b!) k_cache, "
       "Tensor(c!) v_cache, Tensor slots, int nh, int nkv) -> ()");
@@ -497,7 +522,8 @@ TORCH_LIBRARY(mpamd, m) {
       "Tensor(d!) recent_len, Tensor seeds, Tensor(a!) workspace, Tensor(b!) out, int update=0) -> ()");
   m.def(
       "gemm(Tensor x, Tensor wp, Tensor(a!) y, Tensor? residual, int epilogue, int M, int flags, "
-      "Tensor(b!)? workspace=None, Tensor? gate=None) -> ()");
+      "Tensor(b!)? workspace=None, Tensor? gate=None, Tensor(c!)? ap=None, Tensor(d!)? ss_out=None, "
+      "Tensor(e!)? ss_zero=None, Tensor? ss_in=None, float inv_k=0., float eps=0.) -> ()");
   m.def("pack_act(Tensor x, Tensor(a!) ap) -> ()");
   m.def("pack_weight(Tensor w) -> Tensor");
   m.def("quant_act_fp8(Tensor ap, Tensor(a!) a8, Tensor(b!) scale, int M, int K) -> ()");

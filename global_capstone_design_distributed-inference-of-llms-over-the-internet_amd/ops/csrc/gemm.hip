@@ -22,7 +22,15 @@
 //     (no atomics, no second pass); B is double-buffered in registers across groups.
 //   * fused epilogues: 0 = store bf16; 1 = SwiGLU for a gate/up weight whose rows are
 //     interleaved in 16-row blocks [g16 u16 g16 u16 ...] (tile 2t = gate, 2t+1 = up;
-//     output N/2 columns); 2 = y = bf16(bf16(acc) + residual).
+//     output N/2 columns); 2 = y = bf16(bf16(acc) + residual); 3 = the residual-stream
+//     producer of the fused-norm decode path: r = bf16(bf16(acc) + residual) stored in place
+//     (row-major) AND packed (the next GEMM's A operand), and sum(r^2) per row accumulated
+//     into an fp32 vector with atomics (16 lanes reduce a row first).
+//   * RMSNorm folded away (EpiArgs::ss_in): the consumer GEMMs (qkv, gate/up) read the RAW
+//     residual stream with the norm weight folded into their packed weight columns
+//     (W' = W diag(g)), and scale accumulator row r by rsqrt(ss[r] / H + eps) in the
+//     epilogue - RMSNorm(x) W^T = rs * (x (gW)^T).  No normalisation kernel runs on the
+//     decode path (2 launches per layer fewer).
 #include "common.h"
 #include <stdlib.h>
 
@@ -36,6 +44,92 @@ typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
 #define MP_LOAD_A_FRAG(p) (*reinterpret_cast<const u16x8*>(p))
 #endif
 
+// Epilogue side inputs/outputs of the fused-norm decode path (see the header).
+//
+// Row statistics travel as FIXED-POINT sums of squares: every element contributes
+// round(x^2 * 2^20) as a 64-bit integer, so the sum is exact and independent of the order in
+// which the 16-lane groups / workgroups / atomics add up (bitwise reproducible, and equal to
+// what the stage-entry kernel computes for the same rows: a model split over stages gives
+// the same bits as one stage).  Producers add into NSH shards [NSH][64] (shard = block % NSH:
+// same-address atomics serialise at the memory side, 256 adders on one row cost ~20 us);
+// consumers sum the shards of every row once per workgroup into LDS.
+constexpr int SS_NSH = 32;
+constexpr float SS_FX = 1048576.f;  // 2^20
+typedef unsigned long long u64;
+
+struct EpiArgs {
+  bf16_t* ap;          // EPI 3: packed copy of the output rows (mt_out row tiles)
+  u64* ss_out;         // EPI 3: [SS_NSH][64] fixed-point sums of squares (atomics)
+  u64* ss_zero;        // cleared by block 0 at kernel start: the other norm buffer
+  const u64* ss_in;    // non-null: scale accumulator row r by rsqrt(sum_r / K + eps)
+  float inv_k;
+  float eps;
+  int mt_out;
+};
+
+__device__ __forceinline__ u64 fx_sq(float f) { return (u64)__float2ull_rn(f * f * SS_FX); }
+
+__device__ __forceinline__ void clear_other(const EpiArgs& ep) {
+  if (ep.ss_zero != nullptr && blockIdx.x == 0) {
+    for (int i = threadIdx.x; i < SS_NSH * 64; i += blockDim.x) ep.ss_zero[i] = 0ull;
+  }
+}
+
+// Consumer side, in two halves around the main loop (512-thread workgroups): the shard loads
+// are issued at kernel start (unconditional, from a valid address: no vmcnt(0) trap) and
+// reduced through LDS only in the epilogue, after the main loop's last barrier.
+struct RowScale {
+  u64 v[SS_NSH / 8];
+  __device__ __forceinline__ void load(const EpiArgs& ep, const void* any_valid) {
+    const u64* src = ep.ss_in != nullptr ? ep.ss_in : reinterpret_cast<const u64*>(any_valid);
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int j = 0; j < SS_NSH / 8; ++j) v[j] = src[ep.ss_in != nullptr ? ((tid >> 6) + 8 * j) * 64 + (tid & 63) : 0];
+  }
+  // every thread of the workgroup calls this (two barriers inside when ss_in is set)
+  __device__ __forceinline__ void finish(const EpiArgs& ep, u64 (*part)[64], float* rs) {
+    if (ep.ss_in == nullptr) return;
+    const int tid = threadIdx.x;
+    u64 t = 0;
+#pragma unroll
+    for (int j = 0; j < SS_NSH / 8; ++j) t += v[j];
+    part[tid >> 6][tid & 63] = t;
+    __syncthreads();
+    if (tid < 64) {
+      u64 s = 0;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) s += part[w][tid];
+      rs[tid] = rsqrtf((float)s * (1.f / SS_FX) * ep.inv_k + ep.eps);
+    }
+    __syncthreads();
+  }
+};
+
+__device__ __forceinline__ float row_scale(const EpiArgs& ep, const float* rs, int row) {
+  return ep.ss_in != nullptr ? rs[row] : 1.f;
+}
+
+// sum over the 16 lanes that share lane >> 4 (one accumulator row of a 16x16 MFMA tile)
+__device__ __forceinline__ u64 sum16(u64 v) {
+  v += __shfl_xor(v, 1, 64);
+  v += __shfl_xor(v, 2, 64);
+  v += __shfl_xor(v, 4, 64);
+  v += __shfl_xor(v, 8, 64);
+  return v;
+}
+
+// EPI 3 store of one element (called by all 16 lanes of a row group together: sum16 inside).
+// ``rv`` is the old residual value, PREFETCHED by the caller before its main loop: loaded here
+// it would add one exposed memory round trip (~1.5 us) to every producer GEMM's tail.
+__device__ __forceinline__ void epi3_store(const EpiArgs& ep, bf16_t* __restrict__ y, int64_t ys, int row, int col,
+                                           float v, int c, bf16_t rv) {
+  const bf16_t o = f2bf(round_bf(v) + bf2f(rv));
+  y[(int64_t)row * ys + col] = o;
+  ep.ap[apk_off(row, col, ep.mt_out)] = o;
+  const u64 t = sum16(fx_sq(bf2f(o)));
+  if (c == 0) atomicAdd(ep.ss_out + (blockIdx.x % SS_NSH) * 64 + row, t);
+}
+
 __device__ __forceinline__ f32x4 mfma16(const u16x8& a, const u16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b), c,
                                                   0, 0, 0);
@@ -48,7 +142,12 @@ __global__ __launch_bounds__(512) void gemm_packed_kernel(const bf16_t* __restri
                                                           const bf16_t* __restrict__ wp, bf16_t* __restrict__ y,
                                                           int64_t y_stride, const bf16_t* __restrict__ res,
                                                           int64_t res_stride, int M, int N, int K,
-                                                          const int* __restrict__ gate) {
+                                                          const int* __restrict__ gate, const EpiArgs ep) {
+  clear_other(ep);
+  __shared__ u64 rs_part[8][64];
+  __shared__ float rs_lds[64];
+  RowScale rsc;
+  rsc.load(ep, wp);
   // MoE expert gate (ops/moe.py): a device-side count of tokens routed to this expert; 0 ->
   // the whole grid exits before streaming any weight (output left as is, combine weight 0).
   // One uniform scalar load per workgroup keeps hipGraph-captured decode steps shape-static.
@@ -67,6 +166,18 @@ __global__ __launch_bounds__(512) void gemm_packed_kernel(const bf16_t* __restri
   const bf16_t* wbase[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) wbase[t] = wp + ((int64_t)(nt0 + t) * nks) * 512 + lane * 8;
+
+  // EPI 3: this wave's residual elements (slots i = wid + 8 j), in flight during the main loop
+  constexpr int NSLOT = (MT * NT * 4 + 7) / 8;
+  bf16_t rpre[NSLOT];
+  if constexpr (EPI == 3) {
+#pragma unroll
+    for (int j = 0; j < NSLOT; ++j) {
+      const int i = min(wid + 8 * j, MT * NT * 4 - 1);
+      const int row = min((i / (NT * 4)) * 16 + q * 4 + (i & 3), M - 1);
+      rpre[j] = res[(int64_t)row * res_stride + (nt0 + (i / 4) % NT) * 16 + c];
+    }
+  }
 
   // A rows >= M are clamped to a valid row (their accumulator rows are never stored): no
   // per-load branches, so hipcc can count vmcnt through the loop (guide §5 trap (c)).
@@ -130,6 +241,7 @@ __global__ __launch_bounds__(512) void gemm_packed_kernel(const bf16_t* __restri
 #undef MP_MMA
 
   // ---- combine the 8 waves' partial tiles through LDS ----
+  rsc.finish(ep, rs_part, rs_lds);
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -138,7 +250,10 @@ __global__ __launch_bounds__(512) void gemm_packed_kernel(const bf16_t* __restri
       for (int r = 0; r < 4; ++r) red[wid][(mt * NT + t) * 4 + r][lane] = acc[mt][t][r];
   __syncthreads();
   // wave w finalises element slots i = w, w + 8, ... of the MT*NT*4 per-lane slots
-  for (int i = wid; i < MT * NT * 4; i += 8) {
+#pragma unroll
+  for (int j = 0; j < NSLOT; ++j) {
+    const int i = wid + 8 * j;
+    if (i >= MT * NT * 4) break;
     const int mt = i / (NT * 4), t = (i / 4) % NT, r = i & 3;
     const int row = mt * 16 + q * 4 + r;
     float s = 0.f;
@@ -151,17 +266,22 @@ __global__ __launch_bounds__(512) void gemm_packed_kernel(const bf16_t* __restri
       for (int w = 0; w < 8; ++w) up += red[w][i + 4][lane];
       if (row < M) {
         const int ncol = ((nt0 + t) >> 1) * 16 + c;
-        const float gg = round_bf(s);
+        const float sc = row_scale(ep, rs_lds, row);
+        const float gg = round_bf(s * sc);
         const float a = round_bf(gg / (1.f + __expf(-gg)));
         const int64_t yo = OPK ? apk_off(row, ncol, MT) : (int64_t)row * y_stride + ncol;
-        y[yo] = f2bf(a * round_bf(up));
+        y[yo] = f2bf(a * round_bf(up * sc));
       }
     } else {
-      if (row < M) {
+      if (row < M) {  // uniform over the 16 lanes of a row: sum16 in epi3_store is safe
         const int col = (nt0 + t) * 16 + c;
-        float v = s;
-        if constexpr (EPI == 2) v = round_bf(v) + bf2f(res[(int64_t)row * res_stride + col]);
-        y[(int64_t)row * y_stride + col] = f2bf(v);
+        float v = s * row_scale(ep, rs_lds, row);
+        if constexpr (EPI == 3) {
+          epi3_store(ep, y, y_stride, row, col, v, c, rpre[j]);
+        } else {
+          if constexpr (EPI == 2) v = round_bf(v) + bf2f(res[(int64_t)row * res_stride + col]);
+          y[(int64_t)row * y_stride + col] = f2bf(v);
+        }
       }
     }
   }
@@ -169,7 +289,8 @@ __global__ __launch_bounds__(512) void gemm_packed_kernel(const bf16_t* __restri
 
 template <int MT>
 static int launch_gemm(const void* x, int64_t xs, const void* w, void* y, int64_t ys, const void* res, int64_t rs,
-                       int M, int N, int K, int epi, int flags, const int* gate, hipStream_t stream) {
+                       int M, int N, int K, int epi, int flags, const int* gate, const EpiArgs& ep,
+                       hipStream_t stream) {
   const int ntiles = N / 16;
   // two column tiles per wave when there are enough workgroups to fill the 256 CUs
   const bool two = epi == 1 || (ntiles % 2 == 0 && ntiles / 2 >= 256);
@@ -177,7 +298,7 @@ static int launch_gemm(const void* x, int64_t xs, const void* w, void* y, int64_
 #define MP_LAUNCH(NT_, EPI_, APK_, OPK_)                                                                       \
   hipLaunchKernelGGL((gemm_packed_kernel<MT, NT_, EPI_, APK_, OPK_>), dim3(ntiles / NT_), dim3(512), 0, stream, \
                      (const bf16_t*)x, xs, (const bf16_t*)w, (bf16_t*)y, ys, (const bf16_t*)res, rs, M, N, K, \
-                     gate)
+                     gate, ep)
   // Only the packed-activation form is instantiated: row-major callers pack x first
   // (mp_pack_act).  The row-major-A variant miscompiled at MT=1/NT=1 (ROCm 7.2, wrong
   // results with several k-groups per wave) and loses to the packed form anyway.
@@ -190,6 +311,8 @@ static int launch_gemm(const void* x, int64_t xs, const void* w, void* y, int64_
     return -3;  // packed output only for the SwiGLU epilogue (it feeds the down projection)
   } else if (epi == 2) {
     if (two) { MP_APK(2, 2, false) } else { MP_APK(1, 2, false) }
+  } else if (epi == 3) {
+    if (two) { MP_APK(2, 3, false) } else { MP_APK(1, 3, false) }
   } else {
     if (two) { MP_APK(2, 0, false) } else { MP_APK(1, 0, false) }
   }
@@ -229,24 +352,40 @@ constexpr int SK_ZERO_BYTES = 4 * 1024;  // zero A fragments (MT <= 4) for maske
 
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// EPI 3 residual prefetch of one accumulator quad (4 rows x this lane's column)
+template <int NT>
+__device__ __forceinline__ u16x4 res_quad(const bf16_t* __restrict__ res, int64_t rs, int qd, int g, int M, int lane) {
+  const int mt = qd / NT, t = qd % NT, c = lane & 15, q = lane >> 4;
+  const int col = (g * NT + t) * 16 + c;
+  u16x4 o;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) o[r] = res[(int64_t)min(mt * 16 + q * 4 + r, M - 1) * rs + col];
+  return o;
+}
+
 template <int MT, int NT, int EPI, bool OPK>
 __device__ __forceinline__ void sk_epilogue(int qd, int g, const f32x4& v, const f32x4& up, bf16_t* __restrict__ y,
-                                            int64_t ys, const bf16_t* __restrict__ res, int64_t rs, int M, int lane) {
+                                            int64_t ys, const bf16_t* __restrict__ res, int64_t rs, int M, int lane,
+                                            const EpiArgs& ep, const float* rsl, const u16x4* rpv = nullptr) {
   const int mt = qd / NT, t = qd % NT, c = lane & 15, q = lane >> 4;
   const int tile = g * NT + t;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int row = mt * 16 + q * 4 + r;
-    if (row >= M) continue;
+    if (row >= M) continue;  // uniform over the 16 lanes of a row (sum16 in epi3_store)
+    const float sc = row_scale(ep, rsl, row);
     if constexpr (EPI == 1) {
       const int ncol = (tile >> 1) * 16 + c;
-      const float gg = round_bf(v[r]);
+      const float gg = round_bf(v[r] * sc);
       const float a = round_bf(gg / (1.f + __expf(-gg)));
       const int64_t yo = OPK ? apk_off(row, ncol, MT) : (int64_t)row * ys + ncol;
-      y[yo] = f2bf(a * round_bf(up[r]));
+      y[yo] = f2bf(a * round_bf(up[r] * sc));
+    } else if constexpr (EPI == 3) {
+      const bf16_t rv = rpv != nullptr ? (*rpv)[r] : res[(int64_t)row * rs + tile * 16 + c];
+      epi3_store(ep, y, ys, row, tile * 16 + c, v[r] * sc, c, rv);
     } else {
       const int col = tile * 16 + c;
-      float o = v[r];
+      float o = v[r] * sc;
       if constexpr (EPI == 2) o = round_bf(o) + bf2f(res[(int64_t)row * rs + col]);
       y[(int64_t)row * ys + col] = f2bf(o);
     }
@@ -266,8 +405,15 @@ template <int MT, int NT, int CH, int EPI, bool OPK>
 __global__ __launch_bounds__(512) void gemm_lds_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ wp,
                                                        bf16_t* __restrict__ y, int64_t ys,
                                                        const bf16_t* __restrict__ res, int64_t rs, int M, int N,
-                                                       int K) {
+                                                       int K, const EpiArgs ep) {
+  clear_other(ep);
+  __shared__ u64 rs_part[8][64];
+  __shared__ float rs_lds[64];
+  RowScale rsc;
+  rsc.load(ep, wp);
   constexpr int KS = 8 / CH;
+  constexpr int NSL = (CH * MT * NT + 7) / 8;  // epilogue quads per wave
+  u16x4 rpre[NSL];
   constexpr int GU = 2;               // k-slices (of 32) per group
   constexpr int F = GU * MT;          // A fragments (1 KiB) per group
   constexpr int FH = F / CH;          // fragments each wave of a k-split stages
@@ -289,6 +435,13 @@ __global__ __launch_bounds__(512) void gemm_lds_kernel(const bf16_t* __restrict_
 #pragma unroll
   for (int t = 0; t < NT; ++t) wbase[t] = wp + ((int64_t)(g0 * NT + t) * nks) * 512 + lane * 8;
   const bf16_t* xl = x + lane * 8;
+  if constexpr (EPI == 3) {
+#pragma unroll
+    for (int j = 0; j < NSL; ++j) {
+      const int i = min(wid + 8 * j, CH * Q - 1);
+      rpre[j] = res_quad<NT>(res, rs, i % Q, blockIdx.x * CH + i / Q, M, lane);
+    }
+  }
 
   f32x4 acc[MT][NT];
 #pragma unroll
@@ -343,12 +496,16 @@ __global__ __launch_bounds__(512) void gemm_lds_kernel(const bf16_t* __restrict_
 #undef MP_RDA
 #undef MP_MMA
   lds_barrier();  // every wave is done reading A before the reduction buffer aliases it
+  rsc.finish(ep, rs_part, rs_lds);
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
     for (int t = 0; t < NT; ++t) red[((ksp * CH + ch) * Q + mt * NT + t) * 64 + lane] = acc[mt][t];
   lds_barrier();
-  for (int i = wid; i < CH * Q; i += 8) {
+#pragma unroll
+  for (int j = 0; j < NSL; ++j) {
+    const int i = wid + 8 * j;
+    if (i >= CH * Q) break;
     const int chh = i / Q, qd = i % Q;
     if (EPI == 1 && (qd % NT) & 1) continue;  // up tile: consumed with its gate tile
     f32x4 v = (f32x4)(0.f), up = (f32x4)(0.f);
@@ -357,13 +514,14 @@ __global__ __launch_bounds__(512) void gemm_lds_kernel(const bf16_t* __restrict_
       v += red[((k * CH + chh) * Q + qd) * 64 + lane];
       if (EPI == 1) up += red[((k * CH + chh) * Q + qd + 1) * 64 + lane];
     }
-    sk_epilogue<MT, NT, EPI, OPK>(qd, blockIdx.x * CH + chh, v, up, y, ys, res, rs, M, lane);
+    sk_epilogue<MT, NT, EPI, OPK>(qd, blockIdx.x * CH + chh, v, up, y, ys, res, rs, M, lane, ep, rs_lds,
+                                  EPI == 3 ? &rpre[j] : nullptr);
   }
 }
 
 template <int MT, int NT, int CH>
 static int launch_gemm_lds_cfg(const void* x, const void* w, void* y, int64_t ys, const void* res, int64_t rs, int M,
-                               int N, int K, int epi, int flags, hipStream_t stream) {
+                               int N, int K, int epi, int flags, const EpiArgs& ep, hipStream_t stream) {
   if constexpr ((2 * MT) % CH != 0) {
     return 1;  // the A group does not split evenly over the column waves
   } else {
@@ -374,7 +532,7 @@ static int launch_gemm_lds_cfg(const void* x, const void* w, void* y, int64_t ys
     const dim3 grid(ntiles / (CH * NT));
 #define MP_LL(EPI_, OPK_)                                                                                      \
   hipLaunchKernelGGL((gemm_lds_kernel<MT, NT, CH, EPI_, OPK_>), grid, dim3(512), 0, stream, (const bf16_t*)x,   \
-                     (const bf16_t*)w, (bf16_t*)y, ys, (const bf16_t*)res, rs, M, N, K)
+                     (const bf16_t*)w, (bf16_t*)y, ys, (const bf16_t*)res, rs, M, N, K, ep)
     if (epi == 1) {
       if constexpr (NT % 2 == 0) {  // gate/up tile pairs must sit in one wave
         if (opk) { MP_LL(1, true); } else { MP_LL(1, false); }
@@ -383,6 +541,8 @@ static int launch_gemm_lds_cfg(const void* x, const void* w, void* y, int64_t ys
       }
     } else if (epi == 2) {
       MP_LL(2, false);
+    } else if (epi == 3) {
+      MP_LL(3, false);
     } else {
       MP_LL(0, false);
     }
@@ -394,12 +554,12 @@ static int launch_gemm_lds_cfg(const void* x, const void* w, void* y, int64_t ys
 // flags bits 5-6 pick (NT, CH): 0 = (2, 2), 1 = (2, 4), 2 = (1, 4), 3 = (4, 2)
 template <int MT>
 static int launch_gemm_lds(const void* x, const void* w, void* y, int64_t ys, const void* res, int64_t rs, int M,
-                           int N, int K, int epi, int flags, hipStream_t stream) {
+                           int N, int K, int epi, int flags, const EpiArgs& ep, hipStream_t stream) {
   switch ((flags >> 5) & 3) {
-    case 1: return launch_gemm_lds_cfg<MT, 2, 4>(x, w, y, ys, res, rs, M, N, K, epi, flags, stream);
-    case 2: return launch_gemm_lds_cfg<MT, 1, 4>(x, w, y, ys, res, rs, M, N, K, epi, flags, stream);
-    case 3: return launch_gemm_lds_cfg<MT, 4, 2>(x, w, y, ys, res, rs, M, N, K, epi, flags, stream);
-    default: return launch_gemm_lds_cfg<MT, 2, 2>(x, w, y, ys, res, rs, M, N, K, epi, flags, stream);
+    case 1: return launch_gemm_lds_cfg<MT, 2, 4>(x, w, y, ys, res, rs, M, N, K, epi, flags, ep, stream);
+    case 2: return launch_gemm_lds_cfg<MT, 1, 4>(x, w, y, ys, res, rs, M, N, K, epi, flags, ep, stream);
+    case 3: return launch_gemm_lds_cfg<MT, 4, 2>(x, w, y, ys, res, rs, M, N, K, epi, flags, ep, stream);
+    default: return launch_gemm_lds_cfg<MT, 2, 2>(x, w, y, ys, res, rs, M, N, K, epi, flags, ep, stream);
   }
 }
 
@@ -407,7 +567,12 @@ template <int MT, int NT, int D, int EPI, bool OPK>
 __global__ __launch_bounds__(512) void gemm_sk_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ wp,
                                                       bf16_t* __restrict__ y, int64_t ys, const bf16_t* __restrict__ res,
                                                       int64_t rs, int M, int N, int K, int* __restrict__ cnt,
-                                                      f32x4* __restrict__ slab, int remap) {
+                                                      f32x4* __restrict__ slab, int remap, const EpiArgs ep) {
+  clear_other(ep);
+  __shared__ u64 rs_part[8][64];
+  __shared__ float rs_lds[64];
+  RowScale rsc;
+  rsc.load(ep, wp);
   constexpr int Q = MT * NT;  // accumulator quads (f32x4) per lane
   __shared__ __attribute__((aligned(16))) f32x4 red[8 * Q * 64 + 16];
   int* s_flag = reinterpret_cast<int*>(red + 8 * Q * 64);
@@ -453,6 +618,15 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(const bf16_t* __restrict__
     for (int w = 1; w < 8; ++w) s += red[(w * Q + qd) * 64 + lane];
     return s;
   };
+  // EPI 3: residual quads of the group being staged (finalised by reduce() one ring turn later)
+  constexpr int NSQ = (Q + 7) / 8;
+  u16x4 rpre[NSQ];
+  auto prefetch_res = [&](int g) {
+    if constexpr (EPI == 3) {
+#pragma unroll
+      for (int j = 0; j < NSQ; ++j) rpre[j] = res_quad<NT>(res, rs, min(wid + 8 * j, Q - 1), g, M, lane);
+    }
+  };
   auto stage = [&]() {
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
@@ -470,14 +644,22 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(const bf16_t* __restrict__
   const __amdgpu_buffer_rsrc_t slab_rsrc =
       __builtin_amdgcn_make_buffer_rsrc(slab, (short)0, (int)(SK_MAX_BLOCKS * 2 * Q * 64 * 16), 0x00020000);
   int split_g0 = -1, split_g1 = -1;  // split head / tail group of this range (uniform)
+  bool rs_ready = false;             // row scales reduced (at the first group boundary; uniform)
   auto reduce = [&](int g) {
     lds_barrier();
+    if (!rs_ready) {
+      rsc.finish(ep, rs_part, rs_lds);
+      rs_ready = true;
+    }
     const bool whole = g * nks >= u0 && (g + 1) * nks <= u1;
     if (whole) {
-      for (int qd = wid; qd < Q; qd += 8) {
+#pragma unroll
+      for (int j = 0; j < NSQ; ++j) {
+        const int qd = wid + 8 * j;
+        if (qd >= Q) break;
         if (EPI == 1 && (qd % NT) & 1) continue;  // up tile: consumed with its gate tile
         sk_epilogue<MT, NT, EPI, OPK>(qd, g, red_sum(qd), EPI == 1 ? red_sum(qd + 1) : (f32x4)(0.f), y, ys, res, rs,
-                                      M, lane);
+                                      M, lane, ep, rs_lds, EPI == 3 ? &rpre[j] : nullptr);
       }
     } else {
       const int side = (u0 / nks == g) ? 0 : 1;
@@ -525,7 +707,7 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(const bf16_t* __restrict__
             up += __builtin_bit_cast(
                 f32x4, __builtin_amdgcn_raw_buffer_load_b128(slab_rsrc, ((base + (qd + 1) * 64) + lane) * 16, 0, 16));
         }
-        sk_epilogue<MT, NT, EPI, OPK>(qd, g, v, up, y, ys, res, rs, M, lane);
+        sk_epilogue<MT, NT, EPI, OPK>(qd, g, v, up, y, ys, res, rs, M, lane, ep, rs_lds);
       }
     }
   };
@@ -551,6 +733,7 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(const bf16_t* __restrict__
       const int g = chunk_group(cc);
       if (g != cur_g) {  // at most one group boundary per ring turn (nks >= 8 D)
         stage();
+        prefetch_res(cur_g);
         pending = true;
         pend_g = cur_g;
         cur_g = g;
@@ -565,6 +748,7 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(const bf16_t* __restrict__
 #undef SK_LOAD
   if (pending) reduce(pend_g);
   stage();
+  prefetch_res(cur_g);
   reduce(cur_g);
   finish_splits();
 }
@@ -583,7 +767,8 @@ static int sk_num_cus() {
 
 template <int MT, int NT, int D>
 static int launch_gemm_sk_cfg(const void* x, void* y, int64_t ys, const void* w, const void* res, int64_t rs, int M,
-                              int N, int K, int epi, int flags, void* ws, int G, hipStream_t stream) {
+                              int N, int K, int epi, int flags, void* ws, int G, const EpiArgs& ep,
+                              hipStream_t stream) {
   const int nks = K / 32;
   const int ngrp = (N / 16) / NT;
   if ((N / 16) % NT || nks % 8 || nks < 8 * D || ngrp > SK_MAX_GROUPS) return 1;  // caller falls back
@@ -595,7 +780,7 @@ static int launch_gemm_sk_cfg(const void* x, void* y, int64_t ys, const void* w,
   const bool opk = flags & 2;
 #define MP_SK(EPI_, OPK_)                                                                                         \
   hipLaunchKernelGGL((gemm_sk_kernel<MT, NT, D, EPI_, OPK_>), dim3(G), dim3(512), 0, stream, (const bf16_t*)x,     \
-                     (const bf16_t*)w, (bf16_t*)y, ys, (const bf16_t*)res, rs, M, N, K, cnt, slab, 1)
+                     (const bf16_t*)w, (bf16_t*)y, ys, (const bf16_t*)res, rs, M, N, K, cnt, slab, 1, ep)
   if (epi == 1) {
     if constexpr (NT % 2 == 0) {
       if (opk) { MP_SK(1, true); } else { MP_SK(1, false); }
@@ -606,6 +791,8 @@ static int launch_gemm_sk_cfg(const void* x, void* y, int64_t ys, const void* w,
     return -3;
   } else if (epi == 2) {
     MP_SK(2, false);
+  } else if (epi == 3) {
+    MP_SK(3, false);
   } else {
     MP_SK(0, false);
   }
@@ -626,18 +813,18 @@ static int sk_whole_grid(int ngrp, int C) {
 // split groups (deferred sc1 hand-off).
 template <int MT>
 static int launch_gemm_sk(const void* x, void* y, int64_t ys, const void* w, const void* res, int64_t rs, int M, int N,
-                          int K, int epi, int flags, void* ws, hipStream_t stream) {
+                          int K, int epi, int flags, void* ws, const EpiArgs& ep, hipStream_t stream) {
   // ring depth 4 (3 when MT x NT >= 16: the 256-VGPR cap)
   constexpr int DW = (MT * 4 >= 16) ? 3 : 4, D3 = (MT * 3 >= 16) ? 3 : 4;
   const int C = sk_num_cus(), nt = N / 16;
   int G;
   if (nt % 4 == 0 && (G = sk_whole_grid(nt / 4, C)))
-    return launch_gemm_sk_cfg<MT, 4, DW>(x, y, ys, w, res, rs, M, N, K, epi, flags, ws, G, stream);
+    return launch_gemm_sk_cfg<MT, 4, DW>(x, y, ys, w, res, rs, M, N, K, epi, flags, ws, G, ep, stream);
   if (epi != 1 && nt % 3 == 0 && (G = sk_whole_grid(nt / 3, C)))
-    return launch_gemm_sk_cfg<MT, 3, D3>(x, y, ys, w, res, rs, M, N, K, epi, flags, ws, G, stream);
+    return launch_gemm_sk_cfg<MT, 3, D3>(x, y, ys, w, res, rs, M, N, K, epi, flags, ws, G, ep, stream);
   if (nt % 2 == 0 && (G = sk_whole_grid(nt / 2, C)))
-    return launch_gemm_sk_cfg<MT, 2, 4>(x, y, ys, w, res, rs, M, N, K, epi, flags, ws, G, stream);
-  return launch_gemm_sk_cfg<MT, 4, DW>(x, y, ys, w, res, rs, M, N, K, epi, flags, ws, C, stream);
+    return launch_gemm_sk_cfg<MT, 2, 4>(x, y, ys, w, res, rs, M, N, K, epi, flags, ws, G, ep, stream);
+  return launch_gemm_sk_cfg<MT, 4, DW>(x, y, ys, w, res, rs, M, N, K, epi, flags, ws, C, ep, stream);
 }
 
 // Pack W[N, K] (row-major) into the fragment-native layout Wp[N/16][K/32][64][8].
@@ -658,6 +845,8 @@ __global__ __launch_bounds__(256) void pack_weight_kernel(const bf16_t* __restri
 
 }  // namespace mp
 
+extern "C" int mp_gemm_ss_elems() { return mp::SS_NSH * 64; }
+
 extern "C" int64_t mp_gemm_workspace_bytes() {
   using namespace mp;
   return (int64_t)SK_MAX_GROUPS * sizeof(int) + SK_ZERO_BYTES +
@@ -668,39 +857,45 @@ extern "C" int64_t mp_gemm_workspace_bytes() {
 //        bit 2 = use the stream-K kernel (needs ws: mp_gemm_workspace_bytes(), zero-initialised,
 //        used by one stream at a time); bit 3 = force the one-group-per-workgroup kernel;
 //        bit 4 = shared-A (LDS-staged activation) kernel when the shape allows it.
+//        epilogue 3 / ss_in: the fused-norm decode path (EpiArgs above; ap / ss_out / ss_zero /
+//        ss_in may be null when unused).
 extern "C" int mp_gemm_bf16(const void* x, int64_t x_stride, const void* w, void* y, int64_t y_stride,
                             const void* res, int64_t res_stride, int M, int N, int K, int epilogue, int flags,
-                            void* ws, const int* gate, hipStream_t stream) {
+                            void* ws, const int* gate, void* ap, void* ss_out, void* ss_zero, const void* ss_in,
+                            float inv_k, float eps, hipStream_t stream) {
   using namespace mp;
   if (M == 0) return 0;
+  if (epilogue == 3 && (ap == nullptr || ss_out == nullptr || res == nullptr)) return -5;
+  const EpiArgs ep{(bf16_t*)ap, (u64*)ss_out, (u64*)ss_zero, (const u64*)ss_in, inv_k, eps, (M + 15) / 16};
   if (M > 64 || K % (32 * GU_MAX) || N % 16 || ((flags & 1) == 0 && x_stride % 8)) return -1;
   int rc;
   if (gate != nullptr) flags &= ~(4 | 16);  // gated (MoE expert) GEMMs use the one-group kernel
   if ((flags & 1) && (flags & 16) && !(flags & 8)) {  // shared-A kernel
-    if (M <= 16) rc = launch_gemm_lds<1>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, stream);
-    else if (M <= 32) rc = launch_gemm_lds<2>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, stream);
-    else if (M <= 48) rc = launch_gemm_lds<3>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, stream);
-    else rc = launch_gemm_lds<4>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, stream);
+    if (M <= 16) rc = launch_gemm_lds<1>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, ep, stream);
+    else if (M <= 32) rc = launch_gemm_lds<2>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, ep, stream);
+    else if (M <= 48) rc = launch_gemm_lds<3>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, ep, stream);
+    else rc = launch_gemm_lds<4>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, ep, stream);
     if (rc < 0) return rc;
     if (rc == 0) return (int)hipGetLastError();
   }
   if ((flags & 1) && (flags & 4) && !(flags & 8) && ws != nullptr) {
-    if (M <= 16) rc = launch_gemm_sk<1>(x, y, y_stride, w, res, res_stride, M, N, K, epilogue, flags, ws, stream);
-    else if (M <= 32) rc = launch_gemm_sk<2>(x, y, y_stride, w, res, res_stride, M, N, K, epilogue, flags, ws, stream);
-    else if (M <= 48) rc = launch_gemm_sk<3>(x, y, y_stride, w, res, res_stride, M, N, K, epilogue, flags, ws, stream);
-    else rc = launch_gemm_sk<4>(x, y, y_stride, w, res, res_stride, M, N, K, epilogue, flags, ws, stream);
+    if (M <= 16) rc = launch_gemm_sk<1>(x, y, y_stride, w, res, res_stride, M, N, K, epilogue, flags, ws, ep, stream);
+    else if (M <= 32)
+      rc = launch_gemm_sk<2>(x, y, y_stride, w, res, res_stride, M, N, K, epilogue, flags, ws, ep, stream);
+    else if (M <= 48)
+      rc = launch_gemm_sk<3>(x, y, y_stride, w, res, res_stride, M, N, K, epilogue, flags, ws, ep, stream);
+    else rc = launch_gemm_sk<4>(x, y, y_stride, w, res, res_stride, M, N, K, epilogue, flags, ws, ep, stream);
     if (rc < 0) return rc;
     if (rc == 0) return (int)hipGetLastError();
     // rc == 1: shape not covered by the stream-K form -> one-group-per-workgroup kernel
   }
-  if (M <= 16) rc = launch_gemm<1>(x, x_stride, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, gate,
+  if (M <= 16) rc = launch_gemm<1>(x, x_stride, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, gate, ep,
                                    stream);
   else if (M <= 32) rc = launch_gemm<2>(x, x_stride, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, gate,
-                                   stream);
+                                        ep, stream);
   else if (M <= 48) rc = launch_gemm<3>(x, x_stride, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, gate,
-                                   stream);
-  else rc = launch_gemm<4>(x, x_stride, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, gate,
-                                   stream);
+                                        ep, stream);
+  else rc = launch_gemm<4>(x, x_stride, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, gate, ep, stream);
   if (rc) return rc;
   return (int)hipGetLastError();
 }

@@ -7,6 +7,9 @@
 //   mode 0:  y = rmsnorm(x) * w
 //   mode 1:  residual = bf16(residual + x);  y = rmsnorm(residual) * w   (fused add)
 //   mode 2:  residual = x;                   y = rmsnorm(x) * w          (stage entry)
+//   mode 3:  residual = x;  y = x (raw);  ss[0][row] = sum(round(x^2 * 2^20)) as an exact u64,
+//            ss[1..31][row] = 0   (stage entry of the fused-norm decode path: the GEMMs apply
+//            the norm themselves and keep these fixed-point statistics, see gemm.hip EpiArgs)
 // packed_mt > 0 writes y in the packed decode-GEMM activation layout (common.h apk_off).
 //
 // `rows` (optional) gathers input rows (e.g. the last token of each prompt for
@@ -22,8 +25,10 @@ template <int MAXC, int NT = 256>
 __global__ __launch_bounds__(NT) void rmsnorm_kernel(
     const bf16_t* __restrict__ x, int64_t x_stride, bf16_t* __restrict__ res, int64_t res_stride,
     const bf16_t* __restrict__ w, bf16_t* __restrict__ y, int64_t y_stride,
-    const int32_t* __restrict__ rows, int H, float eps, int mode, int packed_mt) {
+    const int32_t* __restrict__ rows, int H, float eps, int mode, int packed_mt,
+    unsigned long long* __restrict__ ss_out) {
   __shared__ float red[16];
+  __shared__ unsigned long long redq[16];
   const int orow = blockIdx.x;
   const int irow = rows ? rows[orow] : orow;
   const int nch = H >> 3;
@@ -41,6 +46,7 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(
     wv[k] = *reinterpret_cast<const u16x8*>(w + c * 8);
   }
   float ss = 0.f;
+  unsigned long long ssq = 0;
 #pragma unroll
   for (int k = 0; k < MAXC; ++k) {
     const int c = threadIdx.x + k * NT;
@@ -50,13 +56,14 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(
 #pragma unroll
         for (int j = 0; j < 8; ++j) a[j] = f2bf(bf2f(a[j]) + bf2f(rv[k][j]));
         *reinterpret_cast<u16x8*>(rr + c * 8) = a;
-      } else if (mode == 2) {
+      } else if (mode >= 2) {
         *reinterpret_cast<u16x8*>(rr + c * 8) = a;
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float f = bf2f(a[j]);
         ss += f * f;
+        if (mode == 3) ssq += (unsigned long long)__float2ull_rn(f * f * 1048576.f);
       }
       v[k] = a;
     }
@@ -64,6 +71,18 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(
   // one wave per row: the shuffle reduction alone (no LDS round trip, no barrier)
   const float tot = NT == 64 ? wave_sum(ss) : block_sum(ss, red);
   const float r = rsqrtf(tot / (float)H + eps);
+  if (mode == 3) {  // exact integer block sum (order-independent), then the 32 shards of this row
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) ssq += __shfl_xor(ssq, o, WAVE);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (NT > 64) {
+      if (lane == 0) redq[wid] = ssq;
+      __syncthreads();
+      ssq = 0;
+      for (int i = 0; i < NT / 64; ++i) ssq += redq[i];
+    }
+    if (threadIdx.x < 32) ss_out[threadIdx.x * 64 + orow] = threadIdx.x == 0 ? ssq : 0ull;
+  }
   bf16_t* yr = y + (int64_t)orow * y_stride;
 #pragma unroll
   for (int k = 0; k < MAXC; ++k) {
@@ -72,7 +91,7 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(
       const u16x8 wv_ = wv[k];
       u16x8 o;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = f2bf(round_bf(bf2f(v[k][j]) * r) * bf2f(wv_[j]));
+      for (int j = 0; j < 8; ++j) o[j] = mode == 3 ? v[k][j] : f2bf(round_bf(bf2f(v[k][j]) * r) * bf2f(wv_[j]));
       if (packed_mt > 0)
         *reinterpret_cast<u16x8*>(y + apk_off(orow, c * 8, packed_mt)) = o;
       else
@@ -85,9 +104,10 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(
 
 extern "C" int mp_rmsnorm(const void* x, int64_t x_stride, void* res, int64_t res_stride, const void* w,
                           void* y, int64_t y_stride, const int32_t* rows, int nrows, int H, float eps,
-                          int mode, int packed_mt, hipStream_t stream) {
+                          int mode, int packed_mt, void* ss_out, hipStream_t stream) {
   using namespace mp;
   if (H % 8 != 0 || H > 8 * 256 * 8) return -1;
+  if (mode == 3 && (ss_out == nullptr || nrows > 64)) return -2;
   if (nrows == 0) return 0;
   const int nch = H / 8;
   // threads per row: 512 (one 16-B chunk per thread at H = 4096) measured best in the decode
@@ -102,7 +122,8 @@ extern "C" int mp_rmsnorm(const void* x, int64_t x_stride, void* res, int64_t re
   dim3 grid(nrows), block(nt);
   auto args = [&](auto kern) {
     hipLaunchKernelGGL(kern, grid, block, 0, stream, (const bf16_t*)x, x_stride, (bf16_t*)res, res_stride,
-                       (const bf16_t*)w, (bf16_t*)y, y_stride, rows, H, eps, mode, packed_mt);
+                       (const bf16_t*)w, (bf16_t*)y, y_stride, rows, H, eps, mode, packed_mt,
+                       (unsigned long long*)ss_out);
   };
   // MAXC = chunks of 8 per thread; nch <= MAXC * nt
   const int per = (nch + nt - 1) / nt;

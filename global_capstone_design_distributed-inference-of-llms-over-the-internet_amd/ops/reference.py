@@ -37,8 +37,24 @@ def unpack_act(ap, M, K):
     return x[:M]
 
 
-def rmsnorm(x, w, eps, out=None, residual=None, mode=0, rows=None):
+SS_SHARDS, SS_FX = 32, float(1 << 20)
+
+
+def fx_sumsq(x):
+    """Per-row sum of round(x^2 * 2^20) as exact int64 (gemm.hip fused-norm row statistics)."""
+    return torch.round(x.float().pow(2).double() * SS_FX).to(torch.int64).sum(-1)
+
+
+def rmsnorm(x, w, eps, out=None, residual=None, mode=0, rows=None, ss=None):
     dt = x.dtype
+    if mode == 3:  # fused-norm stage entry: residual = x, y = raw x, ss = fixed-point sum(x^2) per row
+        residual.copy_(x)
+        ss.view(SS_SHARDS, 64).zero_()
+        ss.view(SS_SHARDS, 64)[0, : x.shape[0]] = fx_sumsq(x)
+        if out is not None:
+            out[: x.shape[0]].copy_(x)
+            return out
+        return x.clone()
     if mode == 1:
         residual.copy_((residual.float() + x.float()).to(dt))
         src = residual
@@ -179,9 +195,24 @@ def argmax(logits, out=None):
     return y
 
 
-def linear(x, w, out=None, epilogue=0, residual=None):
+def linear(x, w, out=None, epilogue=0, residual=None, ss_in=None, inv_k=0.0, eps=0.0, ap_out=None, ss_out=None,
+           ss_zero=None):
+    """``ss_in``: scale row r of x @ w^T by rsqrt(ss_in[r] * inv_k + eps) (fused-norm consumer);
+    epilogue 3: r = bf16(bf16(y) + residual) -> residual (in place) and ``ap_out`` (packed),
+    ``ss_out[r] += sum(r^2)`` (fused-norm producer)."""
+    if ss_zero is not None:
+        ss_zero.zero_()
     y = torch.nn.functional.linear(x, w) if x.dtype == w.dtype else torch.nn.functional.linear(x.to(w.dtype), w)
+    if ss_in is not None:
+        tot = ss_in.view(SS_SHARDS, 64).sum(0)[: y.shape[0]].double() / SS_FX
+        y = y.float() * torch.rsqrt(tot.float() * inv_k + eps)[:, None]
     y = y.to(x.dtype)
+    if epilogue == 3:
+        o = add(y, residual)
+        residual.copy_(o)
+        pack_act(o, out=ap_out)
+        ss_out.view(SS_SHARDS, 64)[0, : o.shape[0]] += fx_sumsq(o)
+        return residual
     if epilogue == 1:
         y = swiglu(y)
     elif epilogue == 2:

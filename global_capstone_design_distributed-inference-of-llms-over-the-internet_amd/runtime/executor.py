@@ -176,15 +176,26 @@ class StageExecutor:
         # one executor may be driven by the TCP handler's GPU worker AND a device-channel
         # engine thread: every device step (incl. hipGraph capture) runs under this lock
         self.exec_lock = threading.RLock()
+        # fused-norm decode path (ops/csrc/gemm.hip EpiArgs): no RMSNorm kernels between the
+        # layers' GEMMs - dense bf16 Llama stages without TP (MoE / fp8 / TP keep the norm kernels)
+        self._fused = (self.device.type == "cuda" and cfg.model_type != "gpt2" and not cfg.is_moe and
+                       self._tp is None and not weights.fp8 and ops.gemm_policy() != "hipblaslt" and
+                       os.environ.get("MPAMD_FUSED_NORM", "1") != "0" and
+                       all(d % 128 == 0 for d in (cfg.hidden_size, cfg.q_dim, cfg.intermediate_size)))
+        self._ss = ops.norm_stats_buffer(self.device, 2) if self._fused else None
         if self.device.type == "cuda":
             ops.require_native()
             if cfg.model_type != "gpt2" and ops.gemm_policy() != "hipblaslt":
-                weights.pack_for_decode()
+                weights.pack_for_decode(fold_norms=self._fused)
+                if self._fused and not all(getattr(L, "folded", False) for L in weights.layers):
+                    self._fused = False  # packed before (e.g. a shared weights object): norm kernels
                 ops.gemm_workspace(self.device)  # allocated before any hipGraph capture
                 if os.environ.get("MPAMD_GEMM_AUTOTUNE", "1") != "0":
                     H, F = cfg.hidden_size, cfg.intermediate_size
                     shapes = [] if (weights.fp8 or not weights.layers) else \
                         [(cfg.q_dim + 2 * cfg.kv_dim, H, 0), (H, cfg.q_dim, 0), (2 * F, H, 1), (H, F, 0)]
+                    if self._fused and shapes:
+                        shapes += [(H, cfg.q_dim, 3), (H, F, 3)]
                     if cfg.is_moe and shapes:
                         shapes.append((16 * ((cfg.num_local_experts + 15) // 16), H, 0))  # router
                     if weights.lm_head_p is not None:
@@ -457,6 +468,32 @@ class StageExecutor:
                 ops.quant_act_fp8(act, T, F, out=a8, scale=asc)
                 ops.linear_fp8(a8, asc, L.down_q, L.down_s, T, out=mlp)
                 self._ar(mlp)
+        elif prompt is None and self._fused and self._packed_ok(T):
+            # fused-norm decode path: 5 launches per layer (qkv, attention, o, gate/up, down).
+            # The residual stream r lives row-major in ``res`` and packed in ``xr``; o / down add
+            # their product into it in their epilogue and accumulate sum(r^2) per row, and qkv /
+            # gate_up (norm weights folded into their packed weights) scale their rows by
+            # rsqrt(mean r^2 + eps).  ss[0] / ss[1]: input- / post-attention-norm statistics;
+            # each producer clears the other buffer, whose consumer has already run.
+            pk = ops.packed_numel
+            xr = e("xr_p", (pk(T, H),))
+            attn = e("attn_p", (pk(T, cfg.q_dim),))
+            act = e("act_p", (pk(T, cfg.intermediate_size),))
+            ss_in, ss_post = self._ss[0], self._ss[1]
+            for li, L in self._iter_layers(_PACKED_FIELDS):
+                if li == 0:
+                    ops.rmsnorm(h, L.input_norm, eps, out=xr, residual=res, mode=3, packed=True, ss=ss_in)
+                ops.linear(xr, None, out=qkv, wp=L.qkv_p, a_rows=T, ss_in=ss_in, eps=eps)
+                kc, vc = self.cache.layer(li)
+                self._rope_attend(qkv, positions, slots, kc, vc, q_seq, q_ctx, attn, ws, ps, np_, True, qblocks,
+                                  max_ctx, decode)
+                ops.linear(attn, None, out=res, epilogue=3, residual=res, wp=L.o_p, a_rows=T, ap_out=xr,
+                           ss_out=ss_post, ss_zero=ss_in)
+                ops.linear(xr, None, out=act, epilogue=1, wp=L.gate_up_p, a_rows=T, out_packed=True, ss_in=ss_post,
+                           eps=eps)
+                ops.linear(act, None, out=res, epilogue=3, residual=res, wp=L.down_p, a_rows=T, ap_out=xr,
+                           ss_out=ss_in, ss_zero=ss_post)
+            mlp = None
         elif prompt is None and self._packed_ok(T):
             # decode path: activations feeding a GEMM stay in the packed MFMA-fragment layout
             pk = ops.packed_numel
@@ -507,7 +544,7 @@ class StageExecutor:
                 ops.linear(xn, L.dense("gate_up"), out=act, epilogue=1, wp=L.gate_up_p)
                 ops.linear(act, L.dense("down"), out=mlp, wp=L.down_p)
                 self._ar(mlp)
-        hout = ops.add(res, mlp, out=e("hout", (T, H)))
+        hout = res if mlp is None else ops.add(res, mlp, out=e("hout", (T, H)))
         if not self.is_last:
             return hout
         S = last_rows.numel()

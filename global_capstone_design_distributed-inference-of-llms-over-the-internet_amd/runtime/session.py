@@ -44,6 +44,14 @@ class SessionManager:
         self.table = np.full((max_sessions, self.max_pages), -1, dtype=np.int32)
         self.table_dev = torch.from_numpy(self.table.copy()).to(cache.device)
         self._dirty = False
+        # double-buffered pinned staging: the H2D copy of a changed table is asynchronous and
+        # stream-ordered before the step's kernels (a pageable copy_ would block the host until
+        # the GPU drained every queued step); buffer k is reused only after its copy's event
+        self._pinned = None
+        if self.table_dev.is_cuda:
+            self._pinned = [torch.empty(self.table.shape, dtype=torch.int32, pin_memory=True) for _ in range(2)]
+            self._pin_ev = [None, None]
+            self._pin_k = 0
         self._free_rows = list(range(max_sessions - 1, -1, -1))
         self.sessions: Dict[str, SessionState] = {}
         self.lock = threading.RLock()
@@ -149,7 +157,18 @@ class SessionManager:
     def sync_table(self, stream=None) -> torch.Tensor:
         if self._dirty:
             with self.lock:
-                self.table_dev.copy_(torch.from_numpy(self.table), non_blocking=False)
+                if self._pinned is None:
+                    self.table_dev.copy_(torch.from_numpy(self.table), non_blocking=False)
+                else:
+                    self._pin_k ^= 1
+                    k = self._pin_k
+                    if self._pin_ev[k] is not None:
+                        self._pin_ev[k].synchronize()  # the copy issued two syncs ago
+                    self._pinned[k].numpy()[...] = self.table
+                    self.table_dev.copy_(self._pinned[k], non_blocking=True)
+                    ev = torch.cuda.Event()
+                    ev.record()
+                    self._pin_ev[k] = ev
                 self._dirty = False
         return self.table_dev
 

@@ -1,0 +1,157 @@
+"""Fused-norm decode path (ops/csrc/gemm.hip EpiArgs, norm.hip mode 3, executor fused branch).
+
+RMSNorm(x) W^T == rsqrt(mean x^2 + eps) * (x (g W)^T): the consumer GEMMs take the raw
+residual stream with the norm weight folded into the packed weight and scale rows in the
+epilogue; the producer GEMMs (o, down) add into the residual in place, write the packed copy
+and accumulate per-row sums of squares with atomics.  Every kernel family (pk, stream-K,
+shared-A) is checked against an fp32 PyTorch reference of the unfused math, and a whole
+decode step of the fused executor against the unfused packed path and the fp32 oracle.
+"""
+import pytest
+import torch
+
+from src import ops
+from src.ops import reference as ref
+
+EPS = 1e-5
+
+
+def _rms_ref(x, g):
+    xf = x.float()
+    n = (xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + EPS)).to(x.dtype)
+    return (n.float() * g.float()).to(x.dtype)
+
+
+def test_reference_fold_identity_cpu():
+    """The CPU reference ops implement the same identity the kernels use."""
+    g = torch.Generator().manual_seed(0)
+    M, K, N = 5, 64, 48
+    x = torch.randn(M, K, generator=g)
+    gw = torch.rand(K, generator=g) + 0.5
+    w = torch.randn(N, K, generator=g) * 0.05
+    ss = ops.norm_stats_buffer("cpu")[0]
+    res = torch.zeros(M, K)
+    xr = ops.rmsnorm(x, gw, EPS, residual=res, mode=3, ss=ss)
+    torch.testing.assert_close(ss.sum(0)[:M].double() / 2 ** 20, x.double().pow(2).sum(-1), atol=1e-3, rtol=1e-6)
+    torch.testing.assert_close(res, x)
+    y = ops.linear(xr, w * gw[None, :], ss_in=ss, eps=EPS)
+    torch.testing.assert_close(y, _rms_ref(x, gw) @ w.t(), atol=1e-4, rtol=1e-4)
+    # producer: residual in place + packed copy + sum of squares
+    a = torch.randn(M, N, generator=g)
+    wo = torch.randn(K, N, generator=g) * 0.05
+    res0 = res.clone()
+    ap = torch.zeros(ops.packed_numel(M, K))
+    sso, ssz = ops.norm_stats_buffer("cpu")[0], ops.norm_stats_buffer("cpu")[0] + 5
+    ops.linear(a, wo, out=res, epilogue=3, residual=res, ap_out=ap, ss_out=sso, ss_zero=ssz)
+    o = res0 + a @ wo.t()
+    torch.testing.assert_close(res, o, atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(ref.unpack_act(ap, M, K), o, atol=1e-5, rtol=1e-5)
+    assert torch.equal(sso.sum(0)[:M], ref.fx_sumsq(res))
+    assert int(ssz.abs().sum()) == 0
+
+
+KERNELS = ["pk", "sk", "lds22", "lds24", "lds42"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kern", KERNELS)
+@pytest.mark.parametrize("M", [1, 17, 64])
+def test_consumer_row_scale_matches_rmsnorm_then_gemm(kern, M):
+    dev = "cuda"
+    g = torch.Generator(device=dev).manual_seed(M)
+    K, N = 1024, 2048
+    x = (torch.randn(M, K, device=dev, generator=g) * 0.7).to(torch.bfloat16)
+    gw = (torch.rand(K, device=dev, generator=g) + 0.5).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=dev, generator=g) * 0.03).to(torch.bfloat16)
+    ss = ops.norm_stats_buffer(dev)[0] + 3  # stale shards: mode 3 must overwrite all of a row's
+    res = torch.empty_like(x)
+    xp = torch.zeros(ops.packed_numel(M, K), dtype=torch.bfloat16, device=dev)
+    ops.rmsnorm(x, gw, EPS, out=xp, residual=res, mode=3, packed=True, ss=ss)
+    assert torch.equal(ss.sum(0)[:M].cpu(), ref.fx_sumsq(x.cpu()))  # exact fixed-point sums
+    assert torch.equal(res, x)
+    wp = ops.pack_weight((w.float() * gw.float()[None, :]).to(torch.bfloat16).contiguous())
+    ops.set_gemm_sk(kern)
+    try:
+        y = ops.linear(xp, None, wp=wp, a_rows=M, ss_in=ss, eps=EPS)
+        # SwiGLU consumer (gate/up interleaved weight), packed output
+        wgu = (torch.randn(2 * N, K, device=dev, generator=g) * 0.03).to(torch.bfloat16)
+        wgup = ops.pack_weight((wgu.float() * gw.float()[None, :]).to(torch.bfloat16).contiguous())
+        act = torch.zeros(ops.packed_numel(M, N), dtype=torch.bfloat16, device=dev)
+        ops.linear(xp, None, out=act, epilogue=1, wp=wgup, a_rows=M, out_packed=True, ss_in=ss, eps=EPS)
+    finally:
+        ops.set_gemm_sk("auto")
+    xn = _rms_ref(x, gw).float()
+    torch.testing.assert_close(y.float(), xn @ w.float().t(), atol=3e-2, rtol=3e-2)
+    gu = xn @ wgu.float().t()
+    exp = ref.swiglu(gu.to(torch.bfloat16)).float()
+    torch.testing.assert_close(ref.unpack_act(act, M, N).float(), exp, atol=3e-2, rtol=3e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kern", KERNELS)
+@pytest.mark.parametrize("M", [1, 33, 64])
+def test_producer_epilogue_residual_pack_and_sumsq(kern, M):
+    dev = "cuda"
+    g = torch.Generator(device=dev).manual_seed(100 + M)
+    K, N = 2048, 1024
+    a = (torch.randn(M, K, device=dev, generator=g) * 0.5).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=dev, generator=g) * 0.03).to(torch.bfloat16)
+    res = (torch.randn(M, N, device=dev, generator=g)).to(torch.bfloat16)
+    res0 = res.clone()
+    ap = torch.zeros(ops.packed_numel(M, N), dtype=torch.bfloat16, device=dev)
+    sso = ops.norm_stats_buffer(dev)[0]
+    ssz = ops.norm_stats_buffer(dev)[0] + 7
+    ops.set_gemm_sk(kern)
+    try:
+        ops.linear(ops.pack_act(a), None, out=res, epilogue=3, residual=res, wp=ops.pack_weight(w), a_rows=M,
+                   ap_out=ap, ss_out=sso, ss_zero=ssz)
+    finally:
+        ops.set_gemm_sk("auto")
+    exp = (res0.float() + (a.float() @ w.float().t()).to(torch.bfloat16).float()).to(torch.bfloat16)
+    torch.testing.assert_close(res.float(), exp.float(), atol=2e-2, rtol=2e-2)
+    assert torch.equal(ref.unpack_act(ap, M, N), res)
+    assert torch.equal(sso.sum(0)[:M].cpu(), ref.fx_sumsq(res.cpu()))  # exact, order-independent
+    assert int(ssz.abs().sum()) == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("graphs", [False, True])
+def test_fused_executor_matches_unfused_and_oracle(graphs, monkeypatch):
+    from src.models.config import resolve_model
+    from src.models.reference_model import reference_forward
+    from src.models.weights import random_stage_weights
+    from src.runtime.executor import StageExecutor
+
+    cfg = resolve_model("small-llama")
+    L = cfg.num_hidden_layers
+
+    def build(fused):
+        monkeypatch.setenv("MPAMD_FUSED_NORM", "1" if fused else "0")
+        w = random_stage_weights(cfg, 0, L, has_embed=True, has_head=True, device="cuda", seed=21)
+        for i, lay in enumerate(w.layers):  # non-trivial norm weights: folding must matter
+            gen = torch.Generator(device="cuda").manual_seed(1000 + i)
+            lay.input_norm = (torch.rand(cfg.hidden_size, device="cuda", generator=gen) + 0.5).to(torch.bfloat16)
+            lay.post_norm = (torch.rand(cfg.hidden_size, device="cuda", generator=gen) + 0.5).to(torch.bfloat16)
+        ex = StageExecutor(cfg, w, "cuda", kv_cache_bytes=128 << 20, max_sessions=8, max_seq_len=256,
+                           use_graphs=graphs)
+        assert ex._fused == fused
+        return w, ex
+
+    w, fx = build(True)
+    _, ux = build(False)
+    gen = torch.Generator().manual_seed(3)
+    prompts = [torch.randint(0, cfg.vocab_size, (n,), generator=gen) for n in (23, 70, 5)]
+    seqs = [("a", 23), ("b", 70), ("c", 5)]
+    ids = torch.cat(prompts).cuda()
+    lf = fx.forward(seqs, ids, reset=[True] * 3)
+    lu = ux.forward(seqs, ids, reset=[True] * 3)
+    cur = [p.clone() for p in prompts]
+    for step in range(4):
+        tok = torch.argmax(lu.float(), -1)
+        cur = [torch.cat([c, tok[i:i + 1].cpu()]) for i, c in enumerate(cur)]
+        lf = fx.forward([(s, 1) for s, _ in seqs], tok)
+        lu = ux.forward([(s, 1) for s, _ in seqs], tok)
+        torch.testing.assert_close(lf.float(), lu.float(), atol=0.08, rtol=0.05)
+        for i in range(3):
+            r = reference_forward([w], cur[i].cuda())[-1]
+            torch.testing.assert_close(lf[i].float(), r, atol=0.08, rtol=0.05)

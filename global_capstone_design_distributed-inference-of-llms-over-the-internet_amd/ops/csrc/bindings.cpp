@@ -400,7 +400,7 @@ void gemm(const at::Tensor& x, const at::Tensor& wp, at::Tensor& y, const c10::o
   void* sso = opt_ss(ss_out, "ss_out");
   void* ssz = opt_ss(ss_zero, "ss_zero");
   const void* ssi = opt_ss(ss_in, "ss_in");
-  MP_CHECK(epilogue != 3 || (app != nullptr && sso != nullptr && !opk), "epilogue 3 needs ap and ss_out");
+  MP_CHECK(epilogue != 3 || (app != nullptr && !opk), "epilogue 3 needs ap (and ss_out outside ablations)");
   void* ws = nullptr;
   if (workspace.has_value()) {
     MP_CHECK(workspace->is_cuda() && workspace->is_contiguous() &&

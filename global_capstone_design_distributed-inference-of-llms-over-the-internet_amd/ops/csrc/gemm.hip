@@ -33,6 +33,7 @@
 //     decode path (2 launches per layer fewer).
 #include "common.h"
 #include <stdlib.h>
+#include <type_traits>
 
 namespace mp {
 
@@ -75,37 +76,46 @@ __device__ __forceinline__ void clear_other(const EpiArgs& ep) {
   }
 }
 
-// Consumer side, in two halves around the main loop (512-thread workgroups): the shard loads
-// are issued at kernel start (unconditional, from a valid address: no vmcnt(0) trap) and
-// reduced through LDS only in the epilogue, after the main loop's last barrier.
+// Consumer side (EPI 0 / 1 only; compiled out of the producer epilogues), in two halves around
+// the main loop (512-thread workgroups): each thread loads SS_NSH/8 shard words right AFTER the
+// kernel's first weight loads and folds them into one 64-bit partial (in-order vmcnt: waiting
+// for them costs nothing beyond the first weight chunk the loop waits for anyway, and only 2
+// VGPRs stay live through the loop); the partials are reduced through LDS in the epilogue,
+// after the main loop's last barrier.
+template <bool ON>
 struct RowScale {
-  u64 v[SS_NSH / 8];
+  u64 v = 0;
   __device__ __forceinline__ void load(const EpiArgs& ep, const void* any_valid) {
-    const u64* src = ep.ss_in != nullptr ? ep.ss_in : reinterpret_cast<const u64*>(any_valid);
-    const int tid = threadIdx.x;
+    if constexpr (ON) {
+      const u64* src = ep.ss_in != nullptr ? ep.ss_in : reinterpret_cast<const u64*>(any_valid);
+      const int tid = threadIdx.x;
+      u64 t = 0;
 #pragma unroll
-    for (int j = 0; j < SS_NSH / 8; ++j) v[j] = src[ep.ss_in != nullptr ? ((tid >> 6) + 8 * j) * 64 + (tid & 63) : 0];
+      for (int j = 0; j < SS_NSH / 8; ++j) t += src[ep.ss_in != nullptr ? ((tid >> 6) + 8 * j) * 64 + (tid & 63) : 0];
+      v = t;
+    }
   }
   // every thread of the workgroup calls this (two barriers inside when ss_in is set)
   __device__ __forceinline__ void finish(const EpiArgs& ep, u64 (*part)[64], float* rs) {
-    if (ep.ss_in == nullptr) return;
-    const int tid = threadIdx.x;
-    u64 t = 0;
+    if constexpr (ON) {
+      if (ep.ss_in == nullptr) return;
+      const int tid = threadIdx.x;
+      part[tid >> 6][tid & 63] = v;
+      __syncthreads();
+      if (tid < 64) {
+        u64 s = 0;
 #pragma unroll
-    for (int j = 0; j < SS_NSH / 8; ++j) t += v[j];
-    part[tid >> 6][tid & 63] = t;
-    __syncthreads();
-    if (tid < 64) {
-      u64 s = 0;
-#pragma unroll
-      for (int w = 0; w < 8; ++w) s += part[w][tid];
-      rs[tid] = rsqrtf((float)s * (1.f / SS_FX) * ep.inv_k + ep.eps);
+        for (int w = 0; w < 8; ++w) s += part[w][tid];
+        rs[tid] = rsqrtf((float)s * (1.f / SS_FX) * ep.inv_k + ep.eps);
+      }
+      __syncthreads();
     }
-    __syncthreads();
   }
 };
 
+template <int EPI>
 __device__ __forceinline__ float row_scale(const EpiArgs& ep, const float* rs, int row) {
+  if constexpr (EPI >= 2) return 1.f;
   return ep.ss_in != nullptr ? rs[row] : 1.f;
 }
 
@@ -126,6 +136,7 @@ __device__ __forceinline__ void epi3_store(const EpiArgs& ep, bf16_t* __restrict
   const bf16_t o = f2bf(round_bf(v) + bf2f(rv));
   y[(int64_t)row * ys + col] = o;
   ep.ap[apk_off(row, col, ep.mt_out)] = o;
+  if (ep.ss_out == nullptr) return;  // (benchmark ablation only: the executor always passes ss_out)
   const u64 t = sum16(fx_sq(bf2f(o)));
   if (c == 0) atomicAdd(ep.ss_out + (blockIdx.x % SS_NSH) * 64 + row, t);
 }
@@ -146,8 +157,7 @@ __global__ __launch_bounds__(512) void gemm_packed_kernel(const bf16_t* __restri
   clear_other(ep);
   __shared__ u64 rs_part[8][64];
   __shared__ float rs_lds[64];
-  RowScale rsc;
-  rsc.load(ep, wp);
+  RowScale<EPI < 2> rsc;
   // MoE expert gate (ops/moe.py): a device-side count of tokens routed to this expert; 0 ->
   // the whole grid exits before streaming any weight (output left as is, combine weight 0).
   // One uniform scalar load per workgroup keeps hipGraph-captured decode steps shape-static.
@@ -216,6 +226,7 @@ __global__ __launch_bounds__(512) void gemm_packed_kernel(const bf16_t* __restri
   if (g < ngroups) {
     MP_LOAD_B(b0, g)
   }
+  rsc.load(ep, wp);
   while (g < ngroups) {
     MP_LOAD_A(g)
     if (g + 8 < ngroups) {
@@ -266,7 +277,7 @@ __global__ __launch_bounds__(512) void gemm_packed_kernel(const bf16_t* __restri
       for (int w = 0; w < 8; ++w) up += red[w][i + 4][lane];
       if (row < M) {
         const int ncol = ((nt0 + t) >> 1) * 16 + c;
-        const float sc = row_scale(ep, rs_lds, row);
+        const float sc = row_scale<EPI>(ep, rs_lds, row);
         const float gg = round_bf(s * sc);
         const float a = round_bf(gg / (1.f + __expf(-gg)));
         const int64_t yo = OPK ? apk_off(row, ncol, MT) : (int64_t)row * y_stride + ncol;
@@ -275,7 +286,7 @@ __global__ __launch_bounds__(512) void gemm_packed_kernel(const bf16_t* __restri
     } else {
       if (row < M) {  // uniform over the 16 lanes of a row: sum16 in epi3_store is safe
         const int col = (nt0 + t) * 16 + c;
-        float v = s * row_scale(ep, rs_lds, row);
+        float v = s * row_scale<EPI>(ep, rs_lds, row);
         if constexpr (EPI == 3) {
           epi3_store(ep, y, y_stride, row, col, v, c, rpre[j]);
         } else {
@@ -373,7 +384,7 @@ __device__ __forceinline__ void sk_epilogue(int qd, int g, const f32x4& v, const
   for (int r = 0; r < 4; ++r) {
     const int row = mt * 16 + q * 4 + r;
     if (row >= M) continue;  // uniform over the 16 lanes of a row (sum16 in epi3_store)
-    const float sc = row_scale(ep, rsl, row);
+    const float sc = row_scale<EPI>(ep, rsl, row);
     if constexpr (EPI == 1) {
       const int ncol = (tile >> 1) * 16 + c;
       const float gg = round_bf(v[r] * sc);
@@ -409,8 +420,7 @@ __global__ __launch_bounds__(512) void gemm_lds_kernel(const bf16_t* __restrict_
   clear_other(ep);
   __shared__ u64 rs_part[8][64];
   __shared__ float rs_lds[64];
-  RowScale rsc;
-  rsc.load(ep, wp);
+  RowScale<EPI < 2> rsc;
   constexpr int KS = 8 / CH;
   constexpr int NSL = (CH * MT * NT + 7) / 8;  // epilogue quads per wave
   u16x4 rpre[NSL];
@@ -470,6 +480,7 @@ __global__ __launch_bounds__(512) void gemm_lds_kernel(const bf16_t* __restrict_
   }
   MP_LDA(0)
   MP_LDB(b0, 0)
+  rsc.load(ep, wp);
   for (int it = 0; it < niter; it += 2) {
     MP_STA(0)
     if (it + 1 < niter) {
@@ -571,8 +582,7 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(const bf16_t* __restrict__
   clear_other(ep);
   __shared__ u64 rs_part[8][64];
   __shared__ float rs_lds[64];
-  RowScale rsc;
-  rsc.load(ep, wp);
+  RowScale<EPI < 2> rsc;
   constexpr int Q = MT * NT;  // accumulator quads (f32x4) per lane
   __shared__ __attribute__((aligned(16))) f32x4 red[8 * Q * 64 + 16];
   int* s_flag = reinterpret_cast<int*>(red + 8 * Q * 64);
@@ -618,14 +628,27 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(const bf16_t* __restrict__
     for (int w = 1; w < 8; ++w) s += red[(w * Q + qd) * 64 + lane];
     return s;
   };
-  // EPI 3: residual quads of the group being staged (finalised by reduce() one ring turn later)
+  // EPI 3 (decode shapes; the launcher only picks this form when a range is at most one group
+  // long, so every range spans <= 2 groups and any group finalised INSIDE the ring loop is a
+  // split one): the in-loop reduce only writes slabs, keeping the epilogue's registers out of
+  // the loop (it spilled otherwise), and the residual quads of the range's first / last group
+  // - the only groups this workgroup can finalise - are loaded right after the loop, in flight
+  // behind the ticket / slab hand-off.
   constexpr int NSQ = (Q + 7) / 8;
-  u16x4 rpre[NSQ];
-  auto prefetch_res = [&](int g) {
+  u16x4 rp_first[NSQ], rp_last[NSQ];
+  const int g_first = u0 / nks, g_last = (u1 - 1) / nks;
+  auto load_rp = [&]() {
     if constexpr (EPI == 3) {
 #pragma unroll
-      for (int j = 0; j < NSQ; ++j) rpre[j] = res_quad<NT>(res, rs, min(wid + 8 * j, Q - 1), g, M, lane);
+      for (int j = 0; j < NSQ; ++j) {
+        rp_first[j] = res_quad<NT>(res, rs, min(wid + 8 * j, Q - 1), g_first, M, lane);
+        rp_last[j] = res_quad<NT>(res, rs, min(wid + 8 * j, Q - 1), g_last, M, lane);
+      }
     }
+  };
+  auto rp_of = [&](int g, int j) -> const u16x4* {
+    if constexpr (EPI == 3) return g == g_first ? &rp_first[j] : (g == g_last ? &rp_last[j] : nullptr);
+    return nullptr;
   };
   auto stage = [&]() {
 #pragma unroll
@@ -645,23 +668,29 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(const bf16_t* __restrict__
       __builtin_amdgcn_make_buffer_rsrc(slab, (short)0, (int)(SK_MAX_BLOCKS * 2 * Q * 64 * 16), 0x00020000);
   int split_g0 = -1, split_g1 = -1;  // split head / tail group of this range (uniform)
   bool rs_ready = false;             // row scales reduced (at the first group boundary; uniform)
-  auto reduce = [&](int g) {
+  auto reduce = [&](int g, auto in_loop) {
     lds_barrier();
     if (!rs_ready) {
       rsc.finish(ep, rs_part, rs_lds);
       rs_ready = true;
     }
+    constexpr bool no_epi = decltype(in_loop)::value && EPI == 3;
     const bool whole = g * nks >= u0 && (g + 1) * nks <= u1;
-    if (whole) {
+    bool done = false;
+    if constexpr (!no_epi) {
+      if (whole) {
 #pragma unroll
-      for (int j = 0; j < NSQ; ++j) {
-        const int qd = wid + 8 * j;
-        if (qd >= Q) break;
-        if (EPI == 1 && (qd % NT) & 1) continue;  // up tile: consumed with its gate tile
-        sk_epilogue<MT, NT, EPI, OPK>(qd, g, red_sum(qd), EPI == 1 ? red_sum(qd + 1) : (f32x4)(0.f), y, ys, res, rs,
-                                      M, lane, ep, rs_lds, EPI == 3 ? &rpre[j] : nullptr);
+        for (int j = 0; j < NSQ; ++j) {
+          const int qd = wid + 8 * j;
+          if (qd >= Q) break;
+          if (EPI == 1 && (qd % NT) & 1) continue;  // up tile: consumed with its gate tile
+          sk_epilogue<MT, NT, EPI, OPK>(qd, g, red_sum(qd), EPI == 1 ? red_sum(qd + 1) : (f32x4)(0.f), y, ys, res,
+                                        rs, M, lane, ep, rs_lds, rp_of(g, j));
+        }
+        done = true;
       }
-    } else {
+    }
+    if (!done) {
       const int side = (u0 / nks == g) ? 0 : 1;
       if (side == 0) split_g0 = g; else split_g1 = g;
       for (int qd = wid; qd < Q; qd += 8)
@@ -695,7 +724,10 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(const bf16_t* __restrict__
       const int g = side ? split_g1 : split_g0;
       const int bf = block_of(g * nks), bl = block_of((g + 1) * nks - 1);
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keep the slab loads below the ticket
-      for (int qd = wid; qd < Q; qd += 8) {
+#pragma unroll
+      for (int j = 0; j < NSQ; ++j) {
+        const int qd = wid + 8 * j;
+        if (qd >= Q) break;
         if (EPI == 1 && (qd % NT) & 1) continue;
         f32x4 v = (f32x4)(0.f), up = (f32x4)(0.f);
         for (int b = bf; b <= bl; ++b) {  // fixed order: deterministic sums
@@ -707,7 +739,7 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(const bf16_t* __restrict__
             up += __builtin_bit_cast(
                 f32x4, __builtin_amdgcn_raw_buffer_load_b128(slab_rsrc, ((base + (qd + 1) * 64) + lane) * 16, 0, 16));
         }
-        sk_epilogue<MT, NT, EPI, OPK>(qd, g, v, up, y, ys, res, rs, M, lane, ep, rs_lds);
+        sk_epilogue<MT, NT, EPI, OPK>(qd, g, v, up, y, ys, res, rs, M, lane, ep, rs_lds, rp_of(g, j));
       }
     }
   };
@@ -716,6 +748,7 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(const bf16_t* __restrict__
   const int nch_pad = ((nch + D - 1) / D) * D;
 #pragma unroll
   for (int s = 0; s < D; ++s) SK_LOAD(s, c_first + s)
+  rsc.load(ep, wp);
 
   // group of a chunk (chunks never straddle groups; padding chunks clamp to the last one)
   auto chunk_group = [&](int cc) { return min(max(cc * 8, u0), u1 - 1) / nks; };
@@ -724,7 +757,7 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(const bf16_t* __restrict__
   int pend_g = 0;
   for (int j0 = 0; j0 < nch_pad; j0 += D) {
     if (pending) {
-      reduce(pend_g);
+      reduce(pend_g, std::true_type{});
       pending = false;
     }
 #pragma unroll
@@ -733,7 +766,6 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(const bf16_t* __restrict__
       const int g = chunk_group(cc);
       if (g != cur_g) {  // at most one group boundary per ring turn (nks >= 8 D)
         stage();
-        prefetch_res(cur_g);
         pending = true;
         pend_g = cur_g;
         cur_g = g;
@@ -746,10 +778,10 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(const bf16_t* __restrict__
     }
   }
 #undef SK_LOAD
-  if (pending) reduce(pend_g);
+  load_rp();
+  if (pending) reduce(pend_g, std::true_type{});
   stage();
-  prefetch_res(cur_g);
-  reduce(cur_g);
+  reduce(cur_g, std::false_type{});
   finish_splits();
 }
 
@@ -775,6 +807,8 @@ static int launch_gemm_sk_cfg(const void* x, void* y, int64_t ys, const void* w,
   const int U = ngrp * nks;
   if (G > SK_MAX_BLOCKS) G = SK_MAX_BLOCKS;
   if (G > U) G = U;
+  // EPI 3 keeps its epilogue out of the ring loop, which needs every range <= one group
+  if (epi == 3 && (U + G - 1) / G > nks) return 1;
   int* cnt = (int*)ws;  // [SK_MAX_GROUPS] counters, [SK_ZERO_BYTES] zeros, slabs
   f32x4* slab = (f32x4*)((char*)ws + SK_MAX_GROUPS * sizeof(int) + SK_ZERO_BYTES);
   const bool opk = flags & 2;
@@ -865,7 +899,7 @@ extern "C" int mp_gemm_bf16(const void* x, int64_t x_stride, const void* w, void
                             float inv_k, float eps, hipStream_t stream) {
   using namespace mp;
   if (M == 0) return 0;
-  if (epilogue == 3 && (ap == nullptr || ss_out == nullptr || res == nullptr)) return -5;
+  if (epilogue == 3 && (ap == nullptr || res == nullptr)) return -5;
   const EpiArgs ep{(bf16_t*)ap, (u64*)ss_out, (u64*)ss_zero, (const u64*)ss_in, inv_k, eps, (M + 15) / 16};
   if (M > 64 || K % (32 * GU_MAX) || N % 16 || ((flags & 1) == 0 && x_stride % 8)) return -1;
   int rc;

@@ -47,16 +47,36 @@ _GPT2_FIELDS = ("ln1_w", "ln1_b", "attn_w", "attn_b", "proj_w", "proj_b", "ln2_w
 
 @dataclasses.dataclass
 class Plan:
-    """Host-side description of one ragged step."""
+    """Host-side description of one ragged step.
+
+    ``h64`` / ``h32`` are the step's metadata in pinned host memory; the device copies
+    (``meta_i64`` / ``meta_i32``) are made on first use.  A graph-replayed decode step never
+    touches them: it stages the padded metadata of its batch bucket in ONE host-to-device
+    copy of its own (``_DecodeGraph.replay``)."""
     sessions: List[SessionState]
     ntoks: np.ndarray
     starts: np.ndarray
     T: int
     max_ctx: int
     is_decode: bool
-    meta_i64: torch.Tensor  # [2, T] positions, slots (device)
-    meta_i32: torch.Tensor  # [2*T + S] q_seq, q_ctx, last_rows (device)
+    h64: np.ndarray                     # [2, T] positions, slots (pinned host view)
+    h32: np.ndarray                     # [2*T + S] q_seq, q_ctx, last_rows (pinned host view)
     qblocks: Optional[torch.Tensor] = None  # [2, NB] MFMA-attention query blocks (prefill steps)
+    _dev: Optional[Tuple[torch.Tensor, torch.Tensor]] = None
+    _upload: Optional[object] = None    # callable making the device copies
+
+    def _device(self):
+        if self._dev is None:
+            self._dev = self._upload()
+        return self._dev
+
+    @property
+    def meta_i64(self) -> torch.Tensor:
+        return self._device()[0]
+
+    @property
+    def meta_i32(self) -> torch.Tensor:
+        return self._device()[1]
 
     @property
     def positions(self):
@@ -240,21 +260,25 @@ class StageExecutor:
         n32 = h32[: 2 * T + S].numpy()
         native.build_meta(rows, st, ntoks, self.sessions.table, self.cache.page_size, n64[0], n64[1], n32[:T],
                           n32[T:2 * T], n32[2 * T:])
-        table = self.sessions.sync_table()
-        del table
-        if self.device.type == "cuda":
-            meta64 = h64[: 2 * T].view(2, T).to(self.device, non_blocking=True)
-            meta32 = h32[: 2 * T + S].to(self.device, non_blocking=True)
-        else:
-            meta64 = h64[: 2 * T].view(2, T).clone()
-            meta32 = h32[: 2 * T + S].clone()
-        self._pinned.mark()
+        self.sessions.sync_table()
         max_ctx = int((st + ntoks).max()) if S else 0
         is_decode = bool(S and (ntoks == 1).all())
+        pinned = self._pinned
+
+        def upload():
+            if self.device.type == "cuda":
+                d64 = h64[: 2 * T].view(2, T).to(self.device, non_blocking=True)
+                d32 = h32[: 2 * T + S].to(self.device, non_blocking=True)
+                pinned.mark()  # the pinned buffers are reused two plans later: after this copy
+            else:
+                d64 = h64[: 2 * T].view(2, T).clone()
+                d32 = h32[: 2 * T + S].clone()
+            return d64, d32
+
         qb = None
         if self.device.type == "cuda" and not is_decode and self._attn_mfma_prefill:
             qb = torch.from_numpy(ops.query_blocks(ntoks, self.nh // self.nkv)).to(self.device, non_blocking=True)
-        return Plan(sess, ntoks, st, T, max_ctx, is_decode, meta64, meta32, qb)
+        return Plan(sess, ntoks, st, T, max_ctx, is_decode, n64, n32, qb, _upload=upload)
 
     def commit(self, plan: Plan) -> None:
         for s, n in zip(plan.sessions, plan.ntoks):
@@ -733,7 +757,12 @@ class StageExecutor:
 
 
 class _DecodeGraph:
-    """A captured decode step for a fixed (batch bucket, attention partition)."""
+    """A captured decode step for a fixed (batch bucket, attention partition).
+
+    Its metadata lives in ONE device blob (positions, slots | q_seq, q_ctx, last_rows) that a
+    replay refills with a single host-to-device copy from a double-buffered pinned staging
+    blob, padded for the bucket (padding rows: slot -1, context 0): round 1 issued six small
+    copies / fills per step (profiles/r2_decode_step_*.txt)."""
 
     def __init__(self, ex: StageExecutor, B: int, part: Tuple[int, int], pool):
         self.ex, self.B, self.part = ex, B, part
@@ -742,13 +771,24 @@ class _DecodeGraph:
             self.x = torch.zeros(B, dtype=torch.long, device=dev)
         else:
             self.x = torch.zeros(B, H, dtype=dt, device=dev)
-        self.meta64 = torch.zeros(2, B, dtype=torch.int64, device=dev)
-        self.meta32 = torch.zeros(3 * B, dtype=torch.int32, device=dev)
-        self.meta64[1].fill_(-1)
+        nbytes = 16 * B + 12 * B  # int64 [2, B] + int32 [3 B]
+        self.blob = torch.zeros(nbytes, dtype=torch.uint8, device=dev)
+        self.meta64 = self.blob[: 16 * B].view(torch.int64).view(2, B)
+        self.meta32 = self.blob[16 * B:].view(torch.int32)
+        self._stage = [torch.zeros(nbytes, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
+        self._stage_ev = [None, None]
+        self._k = 0
+        host = self._stage[0].numpy()
+        h64 = host[: 16 * B].view(np.int64).reshape(2, B)
+        h32 = host[16 * B:].view(np.int32)
+        h64[0] = 0
+        h64[1] = -1
+        h32[:] = 0
+        h32[2 * B:] = np.arange(B, dtype=np.int32)
+        self.blob.copy_(self._stage[0])
+        self._stage[1].copy_(self._stage[0])
         if ex._attn_mfma_gqa:
             ex.decode_qblocks(B)  # allocated outside the capture
-        self.meta32[B: 2 * B].fill_(0)
-        self.meta32[2 * B:] = torch.arange(B, dtype=torch.int32, device=dev)
         self.bufs: dict = {}
         args = (self.x, self.meta64[0], self.meta64[1], self.meta32[:B], self.meta32[B:2 * B], self.meta32[2 * B:], B,
                 0, part)
@@ -764,13 +804,24 @@ class _DecodeGraph:
 
     def replay(self, plan: Plan, x: torch.Tensor) -> torch.Tensor:
         b, B = plan.T, self.B
-        if b < B:
-            self.meta64[1, b:].fill_(-1)
-            self.meta32[B + b: 2 * B].fill_(0)
-            self.meta32[b:B].fill_(0)
-        self.meta64[:, :b].copy_(plan.meta_i64)
-        self.meta32[:b].copy_(plan.q_seq)
-        self.meta32[B: B + b].copy_(plan.q_ctx)
+        self._k ^= 1
+        k = self._k
+        if self._stage_ev[k] is not None:
+            self._stage_ev[k].synchronize()  # the copy issued two replays ago
+        host = self._stage[k].numpy()
+        h64 = host[: 16 * B].view(np.int64).reshape(2, B)
+        h32 = host[16 * B:].view(np.int32)
+        h64[:, :b] = plan.h64
+        h64[0, b:] = 0
+        h64[1, b:] = -1
+        h32[:b] = plan.h32[:b]
+        h32[b:B] = 0
+        h32[B:B + b] = plan.h32[b:2 * b]
+        h32[B + b:2 * B] = 0
+        self.blob.copy_(self._stage[k], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._stage_ev[k] = ev
         if self.ex.is_first:
             self.x[:b].copy_(x.view(-1))
         else:

@@ -32,7 +32,8 @@ def main():
     shapes = [("qkv", 12288, 4096, 0, False), ("qkv+rs", 12288, 4096, 0, True), ("o", 4096, 4096, 0, False),
               ("o+res3", 4096, 4096, 3, False), ("gate_up", 22016, 4096, 1, False),
               ("gate_up+rs", 22016, 4096, 1, True), ("down", 4096, 11008, 0, False),
-              ("down+res3", 4096, 11008, 3, False)]
+              ("down+res3", 4096, 11008, 3, False), ("o+res3-noatomic", 4096, 4096, 3, None),
+              ("down+res3-noatomic", 4096, 11008, 3, None)]
     for M in a.m:
         ss = ops.norm_stats_buffer(dev, 3)
         for name, N, K, epi, rs in shapes:
@@ -46,7 +47,7 @@ def main():
                    else (res if epi == 3 else torch.empty(M, ncols, dtype=torch.bfloat16, device=dev)))
             kw = dict(out=out, epilogue=epi, a_rows=M, out_packed=epi == 1)
             if epi == 3:
-                kw.update(residual=res, ap_out=apo, ss_out=ss[0], ss_zero=ss[1])
+                kw.update(residual=res, ap_out=apo, ss_out=ss[0] if rs is not None else None, ss_zero=ss[1])
             if rs:
                 kw.update(ss_in=ss[2], eps=1e-5)
             for kern in ops._KERNEL_FLAGS:

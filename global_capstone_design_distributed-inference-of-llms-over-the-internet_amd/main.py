@@ -112,6 +112,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--device_channel", choices=["auto", "on", "off"], default="auto",
                    help="same-node fast path: hidden states GPU->GPU over RCCL (xGMI) instead of TCP. Servers "
                         "announce it; the client uses it when every hop runs on its machine (auto) or always (on)")
+    p.add_argument("--throughput_batch", type=int, default=16,
+                   help="LB server: concurrent one-token steps of the compute-throughput probe (tokens/s)")
     p.add_argument("--num_sessions", type=int, default=1,
                    help="client: generate this many sessions concurrently (prompt repeated, distinct seeds)")
     return p
@@ -290,9 +292,10 @@ class _Server:
     """RPC server + handler + heartbeat for one loaded span."""
 
     def __init__(self, args, dht: DHT, executor: StageExecutor, final: bool, stage_idx: int,
-                 throughput: Optional[float] = None, lb: bool = False):
+                 throughput: Optional[float] = None, lb: bool = False, announce: bool = True):
         self.args, self.dht, self.ex, self.final, self.stage_idx = args, dht, executor, final, stage_idx
         self.throughput, self.lb = throughput, lb
+        self.link_mbps: Optional[float] = getattr(args, "network_bandwidth_mbps", None)
         self.loop = get_loop()
         self.server = RpcServer(args.host, args.rpc_port, announce_host=args.public_ip or None,
                                 announce_port=args.public_rpc_port)
@@ -307,7 +310,8 @@ class _Server:
         self.peer_id = self.server.peer_id
         self.next_pings: dict = {}
         self._stop = threading.Event()
-        self.store_once()
+        if announce:
+            self.store_once()
         logger.info(f"StageConnectionHandler handlers registered (stage {stage_idx}, blocks "
                     f"[{executor.start},{executor.end}), final={final}, peer {self.peer_id}, maddrs {self.maddrs})")
         self._hb = threading.Thread(target=self._heartbeat, daemon=True)
@@ -494,8 +498,15 @@ def run_stage_server_with_load_balancing(args, device, cuts: List[int], stop: Op
         full = load_stage_model(args.model, device, "last" if final else "segment", start=s, end=e, dtype=dtype,
                                 seed=args.seed, **_executor_kwargs(args))
         ex = StageExecutor(cfg, full.weights, device, dtype=dtype, **full.executor_kwargs)
-        thr = get_server_throughput(ex, args.network_bandwidth_mbps, cache=tcache)
-        srv = _Server(args, dht, ex, final, args.stage, throughput=thr, lb=True)
+        tb = max(1, int(getattr(args, "throughput_batch", 16)))
+        srv = _Server(args, dht, ex, final, args.stage, throughput=FALLBACK_THROUGHPUT, lb=True, announce=False)
+        mbps = args.network_bandwidth_mbps
+        if mbps is None:  # measure the link instead of assuming 100 Mbit/s
+            mbps = _measure_network(args, dht, srv, ex, total)
+        thr = get_server_throughput(ex, mbps, cache=tcache, batch=tb)
+        srv.throughput = thr
+        srv.link_mbps = mbps
+        srv.store_once()
         if on_ready is not None:
             on_ready(dht, srv)
         rebalance = False
@@ -505,7 +516,7 @@ def run_stage_server_with_load_balancing(args, device, cuts: List[int], stop: Op
             if stop.wait(random.uniform(0, 2 * args.mean_balance_check_period)):
                 break
             try:
-                srv.throughput = get_server_throughput(ex, args.network_bandwidth_mbps, n_steps=3)
+                srv.throughput = get_server_throughput(ex, srv.link_mbps, n_steps=3, batch=tb)
                 infos = get_remote_module_infos(dht, args.model, total)
                 if should_choose_other_blocks(srv.peer_id, infos, args.balance_quality, total, min_block):
                     logger.info("Rebalancing: choosing other blocks")
@@ -520,6 +531,32 @@ def run_stage_server_with_load_balancing(args, device, cuts: List[int], stop: Op
         if not rebalance:
             break
     dht.shutdown()
+
+
+def _measure_network(args, dht, srv, ex, total) -> Optional[float]:
+    """Measured Mbit/s for the network term: echo round trips to another server of the swarm
+    (the span after ours first, else any), or to our own RPC endpoint when we are alone (the
+    local stack's ceiling).  None (-> the reference's 100 Mbit/s) if nothing answers."""
+    from .throughput_measurement import measure_peer_bandwidth
+
+    addrs = []
+    try:
+        for e in get_module_entries(dht, min(ex.end, total - 1), args.model).values():
+            if str(e.get("peer_id")) != srv.peer_id:
+                addrs.extend(e.get("p2p_maddrs") or [])
+        if not addrs:
+            for b in range(total):
+                for e in get_module_entries(dht, b, args.model).values():
+                    if str(e.get("peer_id")) != srv.peer_id:
+                        addrs.extend(e.get("p2p_maddrs") or [])
+                if addrs:
+                    break
+    except Exception as e:  # pragma: no cover
+        logger.warning(f"peer lookup for the bandwidth probe failed: {e}")
+    mbps = measure_peer_bandwidth((addrs or list(srv.maddrs))[:3], ex.cfg.hidden_size, ex.dtype)
+    logger.info(f"measured link bandwidth: {mbps if mbps is None else round(mbps, 1)} Mbit/s "
+                f"({'peer' if addrs else 'loopback'})")
+    return mbps
 
 
 def run_stage_server(args, device, cuts, stop=None, on_ready=None):

@@ -148,15 +148,23 @@ def estimate_network_throughput(hidden_size: int, dtype_bytes: int = 2,
 
 def get_server_throughput(executor, network_bandwidth_mbps: Optional[float] = None,
                           relay_penalty: float = RELAY_PENALTY, n_warmup: int = 2, n_steps: int = 10,
-                          cache: Optional[ThroughputCache] = None, force_eval: bool = False) -> float:
-    key = ThroughputCache.key(executor) if cache is not None else None
+                          cache: Optional[ThroughputCache] = None, force_eval: bool = False, batch: int = 1) -> float:
+    """min(compute, network x (1 - relay penalty)) in tokens/s.
+
+    ``batch``: the compute term is measured as ``batch`` concurrent one-token decode steps
+    (tokens/s = batch x steps/s): a stage serves many sessions at once, and batch 1 (the
+    reference's probe) under-reports an MI355X span by an order of magnitude.  The network term
+    is per token too, so the two stay comparable.  ``network_bandwidth_mbps`` is the MEASURED
+    link rate when the caller has one (``measure_link_bandwidth``), else the 100 Mbit/s
+    assumption of the reference."""
+    key = ThroughputCache.key(executor) + f"|b{batch}" if cache is not None else None
     cached = cache.get(key) if (cache is not None and not force_eval) else None
     if cached and "compute_rps" in cached:
         compute = float(cached["compute_rps"])
         logger.info(f"Server throughput: cached compute={compute:.2f} rps ({key})")
     else:
         try:
-            compute = measure_compute_throughput(executor, n_warmup, n_steps)
+            compute = batch * measure_compute_throughput(executor, n_warmup, n_steps, batch=batch)
         except Exception as e:
             logger.warning(f"compute throughput probe failed ({e!r}); using fallback {FALLBACK_THROUGHPUT}")
             return FALLBACK_THROUGHPUT
@@ -170,10 +178,40 @@ def get_server_throughput(executor, network_bandwidth_mbps: Optional[float] = No
 
 
 def measure_link_bandwidth(rpc_call, payload_bytes: int, rounds: int = 5) -> float:
-    """Mbit/s measured with ``rpc_call(bytes)`` round trips (echo handler on the peer)."""
+    """Mbit/s measured with ``rpc_call(bytes)`` round trips (echo handler on the peer): the
+    measured replacement of the reference's speedtest / 100 Mbit/s constant
+    (src/throughput_measurement.py:157-190, petals/server/throughput.py:147-187)."""
     rpc_call(payload_bytes)
     t0 = time.perf_counter()
     for _ in range(rounds):
         rpc_call(payload_bytes)
     dt = (time.perf_counter() - t0) / rounds
     return 2 * payload_bytes * 8 / dt / 1e6
+
+
+def measure_peer_bandwidth(maddrs, hidden_size: int, dtype=torch.bfloat16, tokens: int = 256, rounds: int = 4,
+                           timeout: float = 10.0) -> Optional[float]:
+    """Measured Mbit/s to the first reachable address in ``maddrs``: ``rpc_echo`` round trips of
+    a [1, tokens, H] activation (a prefill-sized message, so the number is bandwidth rather than
+    RPC latency).  None if no address answers."""
+    from .comm.rpc import RpcClient, get_loop
+    from .comm.wire import Message
+
+    loop = get_loop()
+    client = RpcClient()
+    x = torch.zeros(1, tokens, hidden_size, dtype=dtype)
+    try:
+        for addr in maddrs:
+            def call(nbytes, addr=addr):
+                loop.run(client.call(addr, "StageConnectionHandler.rpc_echo", Message({"bw": True}, [x]), timeout),
+                         timeout=timeout + 1)
+            try:
+                return measure_link_bandwidth(call, x.numel() * x.element_size(), rounds)
+            except Exception as e:  # noqa: BLE001 - try the next address
+                logger.info(f"bandwidth probe to {addr} failed: {e!r}")
+        return None
+    finally:
+        try:
+            loop.run(client.close(), timeout=2)
+        except Exception:  # noqa: BLE001
+            pass

@@ -279,3 +279,26 @@ def test_cli_client_over_device_channel_matches_reference(capsys):
     finally:
         s1.close()
         s2.close()
+
+
+@pytest.mark.timeout(240)
+def test_lb_placement_follows_measured_throughput():
+    """Load-balanced servers announce MEASURED throughput (batched compute probe, network term
+    from a measured link): a 2-block span measures slower than a 1-block span, so the next
+    server fills the slow span's blocks, not the lowest uncovered-by-one index."""
+    extra = "--use_load_balancing --mean_balance_check_period 1000 --throughput_batch 4"
+    a = ServerThread(server_argv(MODEL, "1", 1, extra=extra + " --num_blocks 1")).wait()
+    b = ServerThread(server_argv(MODEL, "1", 1, peers=a.addr, extra=extra + " --num_blocks 2")).wait()
+    c = None
+    try:
+        assert (a.srv.ex.start, a.srv.ex.end) == (1, 2) and (b.srv.ex.start, b.srv.ex.end) == (2, 4)
+        assert a.srv.throughput > b.srv.throughput > 0, (a.srv.throughput, b.srv.throughput)
+        # the network term came from a measured link, not the 100 Mbit/s constant
+        assert a.srv.link_mbps is not None and b.srv.link_mbps is not None and b.srv.link_mbps > 100
+        assert wait_for(lambda: len(get_remote_module_infos(a.dht, MODEL, 4)) >= 3)
+        c = ServerThread(server_argv(MODEL, "1", 1, peers=a.addr, extra=extra + " --num_blocks 1")).wait()
+        assert c.srv.ex.start in (2, 3), (c.srv.ex.start, a.srv.throughput, b.srv.throughput)
+    finally:
+        for s in (a, b, c):
+            if s is not None:
+                s.close()

@@ -119,10 +119,10 @@ class ThroughputCache:
             return {}
 
     @staticmethod
-    def key(executor) -> str:
+    def key(executor, batch: int = 1) -> str:
         dev = executor.device
         name = torch.cuda.get_device_name(dev) if dev.type == "cuda" else "cpu"
-        return f"{executor.cfg.name}|{executor.start}-{executor.end}|{executor.dtype}|{name}"
+        return f"{executor.cfg.name}|{executor.start}-{executor.end}|{executor.dtype}|{name}|b{int(batch)}"
 
     def get(self, key: str) -> Optional[dict]:
         with self._locked():
@@ -157,7 +157,7 @@ def get_server_throughput(executor, network_bandwidth_mbps: Optional[float] = No
     is per token too, so the two stay comparable.  ``network_bandwidth_mbps`` is the MEASURED
     link rate when the caller has one (``measure_link_bandwidth``), else the 100 Mbit/s
     assumption of the reference."""
-    key = ThroughputCache.key(executor) + f"|b{batch}" if cache is not None else None
+    key = ThroughputCache.key(executor, batch) if cache is not None else None
     cached = cache.get(key) if (cache is not None and not force_eval) else None
     if cached and "compute_rps" in cached:
         compute = float(cached["compute_rps"])

@@ -264,22 +264,29 @@ def norm_stats_buffer(device, n: int = 1) -> torch.Tensor:
     return torch.zeros(n, ref.SS_SHARDS, 64, dtype=torch.int64, device=device)
 
 
-def rmsnorm(x, w, eps, out=None, residual=None, mode=0, rows=None, packed=False, ss=None):
+def rmsnorm(x, w, eps, out=None, residual=None, mode=0, rows=None, packed=False, ss=None, a8=None, a8_scale=None):
     """mode 0: y = norm(x)*w; 1: residual += x, y = norm(residual)*w; 2: residual = x, y = norm(x)*w;
     3: residual = x, y = x, ``ss`` = fixed-point row sums of squares (``norm_stats_buffer``; entry of
     the fused-norm decode path).
 
-    ``packed``: write y in the packed decode-GEMM activation layout (``out`` flat)."""
+    ``packed``: write y in the packed decode-GEMM activation layout (``out`` flat).
+    ``a8`` / ``a8_scale`` (with ``packed``): emit y quantized for the fp8 GEMM instead (the
+    ``quant_act_fp8`` layout and per-row scales; ``out`` is then not written)."""
     if not _native(x):
         y = ref.rmsnorm(x, w, eps, out=None if packed else out, residual=residual, mode=mode, rows=rows, ss=ss)
+        if a8 is not None:
+            q, s = ref.quant_act_fp8(ref.pack_act(y), y.shape[0], y.shape[1])
+            a8[: q.numel()].copy_(q)
+            a8_scale[: y.shape[0]].copy_(s[: y.shape[0]])
+            return a8
         return ref.pack_act(y, out=out) if packed else y
     n = rows.numel() if rows is not None else x.shape[0]
     if out is None:
         out = (torch.empty(packed_numel(n, x.shape[1]), dtype=x.dtype, device=x.device) if packed
                else torch.empty(n, x.shape[1], dtype=x.dtype, device=x.device))
     torch.ops.mpamd.rmsnorm(x, residual if residual is not None else x, w, out, float(eps), int(mode), rows,
-                            int(bool(packed)), ss)
-    return out
+                            int(bool(packed)), ss, a8, a8_scale)
+    return a8 if a8 is not None else out
 
 
 def rope_kv_write(qkv, positions, cos, sin, k_cache, v_cache, slots, nh, nkv):

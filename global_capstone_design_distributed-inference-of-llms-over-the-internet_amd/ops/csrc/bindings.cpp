@@ -12,7 +12,7 @@
 extern "C" {
 int mp_rmsnorm(const void* x, int64_t x_stride, void* res, int64_t res_stride, const void* w, void* y,
                int64_t y_stride, const int32_t* rows, int nrows, int H, float eps, int mode, int packed_mt,
-               void* ss_out, hipStream_t stream);
+               void* ss_out, void* a8, float* a8_scale, hipStream_t stream);
 int mp_rope_kv_write(void* qkv, int64_t qkv_stride, const int64_t* pos, const float* cos_t, const float* sin_t,
                      void* kc, void* vc, const int64_t* slots, int T, int nh, int nkv, int D, int page_size,
                      hipStream_t stream);
@@ -81,7 +81,8 @@ inline void* opt_ss(const c10::optional<at::Tensor>& t, const char* name) {
 }
 
 void rmsnorm(const at::Tensor& x, at::Tensor& residual, const at::Tensor& w, at::Tensor& y, double eps, int64_t mode,
-             const c10::optional<at::Tensor>& rows, int64_t packed, const c10::optional<at::Tensor>& ss) {
+             const c10::optional<at::Tensor>& rows, int64_t packed, const c10::optional<at::Tensor>& ss,
+             const c10::optional<at::Tensor>& a8, const c10::optional<at::Tensor>& a8_scale) {
   check_bf16_cuda(x, "x");
   check_bf16_cuda(w, "w");
   check_bf16_cuda(y, "y");
@@ -115,9 +116,20 @@ void rmsnorm(const at::Tensor& x, at::Tensor& residual, const at::Tensor& w, at:
   } else {
     MP_CHECK(y.size(0) >= nrows, "y rows");
   }
+  void* a8p = nullptr;
+  float* a8s = nullptr;
+  if (a8.has_value()) {  // fp8 output (W8A8 decode path): A8 [K/64][MT][64][16 B] + per-row scales
+    MP_CHECK(packed && a8_scale.has_value(), "fp8 output needs packed=1 and a8_scale");
+    MP_CHECK(a8->is_cuda() && a8->scalar_type() == at::kByte && a8->is_contiguous() &&
+                 a8->numel() >= packed_numel(nrows, H) && H % 64 == 0, "a8: uint8 [packed_numel(rows, H)], H % 64");
+    MP_CHECK(a8_scale->is_cuda() && a8_scale->scalar_type() == at::kFloat && a8_scale->numel() >= nrows,
+             "a8_scale: fp32 [rows]");
+    a8p = a8->data_ptr();
+    a8s = a8_scale->data_ptr<float>();
+  }
   check_launch(mp_rmsnorm(x.data_ptr(), x.stride(0), mode ? residual.data_ptr() : nullptr,
                           mode ? residual.stride(0) : 0, w.data_ptr(), y.data_ptr(), packed ? 0 : y.stride(0), rp,
-                          nrows, H, (float)eps, (int)mode, pmt, ssp, cur_stream()),
+                          nrows, H, (float)eps, (int)mode, pmt, ssp, a8p, a8s, cur_stream()),
                "rmsnorm");
 }
 
@@ -492,7 +504,7 @@ TORCH_LIBRARY(mpamd, m) {
   m.def("gemm_workspace_bytes() -> int", &gemm_workspace_bytes);
   m.def(
       "rmsnorm(Tensor x, Tensor(a!) residual, Tensor w, Tensor(b!) y, float eps, int mode, Tensor? rows, "
-      "int packed, Tensor(c!)? ss=None) -> ()");
+      "int packed, Tensor(c!)? ss=None, Tensor(d!)? a8=None, Tensor(e!)? a8_scale=None) -> ()");
   m.def(
       "rope_kv_write(Tensor(a!) qkv, Tensor positions, Tensor cos, Tensor sin, Tensor(b!) k_cache, "
       "Tensor(c!) v_cache, Tensor slots, int nh, int nkv) -> ()");

@@ -11,6 +11,10 @@
 //            ss[1..31][row] = 0   (stage entry of the fused-norm decode path: the GEMMs apply
 //            the norm themselves and keep these fixed-point statistics, see gemm.hip EpiArgs)
 // packed_mt > 0 writes y in the packed decode-GEMM activation layout (common.h apk_off).
+// a8 != null (fp8 W8A8 decode path): y is instead quantized to OCP e4m3 with a per-row scale
+// max|y| / 448 into the fp8 GEMM's A layout A8[K/64][MT][64][16 B] (fp8.hip) and a8_scale[row]:
+// the norm owns whole rows, so the absmax needs no cross-workgroup pass (round 1 ran a
+// separate two-launch quantization after every norm).
 //
 // `rows` (optional) gathers input rows (e.g. the last token of each prompt for
 // the final norm before lm_head), so the output has one row per index.
@@ -26,8 +30,9 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(
     const bf16_t* __restrict__ x, int64_t x_stride, bf16_t* __restrict__ res, int64_t res_stride,
     const bf16_t* __restrict__ w, bf16_t* __restrict__ y, int64_t y_stride,
     const int32_t* __restrict__ rows, int H, float eps, int mode, int packed_mt,
-    unsigned long long* __restrict__ ss_out) {
+    unsigned long long* __restrict__ ss_out, uint8_t* __restrict__ a8, float* __restrict__ a8_scale) {
   __shared__ float red[16];
+  __shared__ float redm[16];
   __shared__ unsigned long long redq[16];
   const int orow = blockIdx.x;
   const int irow = rows ? rows[orow] : orow;
@@ -84,6 +89,7 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(
     if (threadIdx.x < 32) ss_out[threadIdx.x * 64 + orow] = threadIdx.x == 0 ? ssq : 0ull;
   }
   bf16_t* yr = y + (int64_t)orow * y_stride;
+  float amax = 0.f;
 #pragma unroll
   for (int k = 0; k < MAXC; ++k) {
     const int c = threadIdx.x + k * NT;
@@ -92,10 +98,39 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(
       u16x8 o;
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = mode == 3 ? v[k][j] : f2bf(round_bf(bf2f(v[k][j]) * r) * bf2f(wv_[j]));
-      if (packed_mt > 0)
+      if (a8 != nullptr) {
+        v[k] = o;  // kept for the quantization pass below
+#pragma unroll
+        for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(bf2f(o[j])));
+      } else if (packed_mt > 0) {
         *reinterpret_cast<u16x8*>(y + apk_off(orow, c * 8, packed_mt)) = o;
-      else
+      } else {
         *reinterpret_cast<u16x8*>(yr + c * 8) = o;
+      }
+    }
+  }
+  if (a8 == nullptr) return;
+  amax = NT == 64 ? wave_max(amax) : block_max(amax, redm);
+  const float sc = amax > 0.f ? amax * (1.f / 448.f) : 1.f;
+  const float inv = 1.f / sc;
+  if (threadIdx.x == 0) a8_scale[orow] = sc;
+  const int mt = orow >> 4, r16 = orow & 15;
+#pragma unroll
+  for (int k = 0; k < MAXC; ++k) {
+    const int c = threadIdx.x + k * NT;  // 8 columns 8c .. 8c+7
+    if (c < nch) {
+      float f[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] = fminf(fmaxf(bf2f(v[k][j]) * inv, -448.f), 448.f);
+      int lo = __builtin_amdgcn_cvt_pk_fp8_f32(f[0], f[1], 0, false);
+      lo = __builtin_amdgcn_cvt_pk_fp8_f32(f[2], f[3], lo, true);
+      int hi = __builtin_amdgcn_cvt_pk_fp8_f32(f[4], f[5], 0, false);
+      hi = __builtin_amdgcn_cvt_pk_fp8_f32(f[6], f[7], hi, true);
+      const int col = c * 8, ch = col >> 6, half = (col >> 5) & 1, q = (col >> 3) & 3;
+      int2 o2;
+      o2.x = lo;
+      o2.y = hi;
+      *reinterpret_cast<int2*>(a8 + (((int64_t)ch * packed_mt + mt) * 64 + q * 16 + r16) * 16 + half * 8) = o2;
     }
   }
 }
@@ -104,10 +139,11 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(
 
 extern "C" int mp_rmsnorm(const void* x, int64_t x_stride, void* res, int64_t res_stride, const void* w,
                           void* y, int64_t y_stride, const int32_t* rows, int nrows, int H, float eps,
-                          int mode, int packed_mt, void* ss_out, hipStream_t stream) {
+                          int mode, int packed_mt, void* ss_out, void* a8, float* a8_scale, hipStream_t stream) {
   using namespace mp;
   if (H % 8 != 0 || H > 8 * 256 * 8) return -1;
   if (mode == 3 && (ss_out == nullptr || nrows > 64)) return -2;
+  if (a8 != nullptr && (packed_mt <= 0 || H % 64 || a8_scale == nullptr || mode == 3)) return -3;
   if (nrows == 0) return 0;
   const int nch = H / 8;
   // threads per row: 512 (one 16-B chunk per thread at H = 4096) measured best in the decode
@@ -123,7 +159,7 @@ extern "C" int mp_rmsnorm(const void* x, int64_t x_stride, void* res, int64_t re
   auto args = [&](auto kern) {
     hipLaunchKernelGGL(kern, grid, block, 0, stream, (const bf16_t*)x, x_stride, (bf16_t*)res, res_stride,
                        (const bf16_t*)w, (bf16_t*)y, y_stride, rows, H, eps, mode, packed_mt,
-                       (unsigned long long*)ss_out);
+                       (unsigned long long*)ss_out, (uint8_t*)a8, a8_scale);
   };
   // MAXC = chunks of 8 per thread; nch <= MAXC * nt
   const int per = (nch + nt - 1) / nt;

@@ -1,4 +1,5 @@
 """fp8 (OCP e4m3fn) W8A8 path: packing/quantization references on CPU, executor on CPU."""
+import pytest
 import torch
 
 from src import ops
@@ -61,3 +62,31 @@ def test_fp8_stage_executor_matches_dequantized_reference():
         logits = ex.forward([("s", 1)], torch.tensor([got[-1]]))
         got.append(int(torch.argmax(logits[-1])))
     assert got == want
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M", [1, 17, 64])
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_rmsnorm_fp8_output_equals_norm_then_quant(M, mode):
+    """norm.hip a8 output (the fp8 path's norm sites) == bf16 packed norm + quant_act_fp8, bit for
+    bit: same per-row absmax / 448 scale, same e4m3 bytes in the fp8 GEMM's A layout."""
+    from src import ops
+
+    H = 1024
+    g = torch.Generator(device="cuda").manual_seed(M + 10 * mode)
+    x = (torch.randn(M, H, device="cuda", generator=g) * 2).to(torch.bfloat16)
+    w = (torch.rand(H, device="cuda", generator=g) + 0.5).to(torch.bfloat16)
+    res0 = (torch.randn(M, H, device="cuda", generator=g)).to(torch.bfloat16)
+    r1, r2 = res0.clone(), res0.clone()
+    xp = torch.zeros(ops.packed_numel(M, H), dtype=torch.bfloat16, device="cuda")
+    ops.rmsnorm(x, w, 1e-5, out=xp, residual=r1, mode=mode, packed=True)
+    a8_ref, s_ref = ops.quant_act_fp8(xp, M, H)
+    a8 = torch.zeros(ops.packed_numel(M, H), dtype=torch.uint8, device="cuda")
+    sc = torch.zeros(((M + 15) // 16) * 16, dtype=torch.float32, device="cuda")
+    ops.rmsnorm(x, w, 1e-5, out=xp, residual=r2, mode=mode, packed=True, a8=a8, a8_scale=sc)
+    assert torch.equal(r1, r2)
+    assert torch.equal(sc[:M], s_ref[:M])
+    # compare the valid rows' bytes (padding rows of the last 16-row tile are don't-care)
+    ar = ops.reference.dequant_act_fp8(a8_ref, s_ref, M, H)
+    an = ops.reference.dequant_act_fp8(a8, sc, M, H)
+    assert torch.equal(ar, an)

@@ -10,6 +10,9 @@ rejects).  Each stage is its own OS process; on a multi-GPU host stage k uses GP
 
     python scripts/run_all.py --model gpt2 --splits 6 --max_new_tokens 16
     python scripts/run_all.py --model llama2-7b --splits 8,16,24 --gpus
+    # one GPU, 4 stage processes sharing it, 8 concurrent sessions, TCP path vs device channel:
+    python scripts/run_all.py --model llama2-7b --splits 8,16,24 --gpus --extra "--kv_cache_gb 8" \
+        --client_extra "--num_sessions 8 --device_channel off"
 """
 from __future__ import annotations
 
@@ -48,7 +51,9 @@ def main():
     ap.add_argument("--max_new_tokens", type=int, default=16)
     ap.add_argument("--prompt", default="Hello, how are you?")
     ap.add_argument("--temperature", type=float, default=0.0)
-    ap.add_argument("--gpus", action="store_true", help="stage k on cuda:k-1 (client on cuda:N)")
+    ap.add_argument("--gpus", action="store_true",
+                    help="stage k on cuda:(k-1) mod #GPUs, client on cuda:N mod #GPUs (one GPU: all share cuda:0)")
+    ap.add_argument("--client_extra", default="", help="extra args for the stage-0 client only")
     ap.add_argument("--log_dir", default=os.path.join(ROOT, "gpurun_out", "run_all"))
     ap.add_argument("--extra", default="", help="extra args for every stage")
     a = ap.parse_args()
@@ -58,12 +63,17 @@ def main():
     from src.partition import parse_splits
 
     n_servers = len(parse_splits(a.splits, resolve_model(a.model).num_hidden_layers))
+    n_gpu = 1
+    if a.gpus:
+        import torch
+
+        n_gpu = max(1, torch.cuda.device_count())  # does not initialise the GPU in this process
     procs = []
     first_maddr = None
     env = dict(os.environ)
     try:
         for k in range(1, n_servers + 1):
-            dev = f"cuda:{k - 1}" if a.gpus else "cpu"
+            dev = f"cuda:{(k - 1) % n_gpu}" if a.gpus else "cpu"
             cmd = [sys.executable, "-m", "src.main", "--model", a.model, "--splits", a.splits, "--stage", str(k),
                    "--host", a.host, "--dht_port", str(a.base_port + 2 * k), "--rpc_port", str(a.base_port + 2 * k + 1),
                    "--device", dev] + a.extra.split()
@@ -76,10 +86,10 @@ def main():
                 first_maddr = m.group(1)
             wait_log(log, READY_RE, 600, procs[-1])
             print(f"stage {k} ready ({log})", flush=True)
-        dev = f"cuda:{n_servers}" if a.gpus else "cpu"
+        dev = f"cuda:{n_servers % n_gpu}" if a.gpus else "cpu"
         cmd = [sys.executable, "-m", "src.main", "--model", a.model, "--splits", a.splits, "--stage", "0",
                "--dht_initial_peers", first_maddr, "--max_new_tokens", str(a.max_new_tokens), "--prompt", a.prompt,
-               "--temperature", str(a.temperature), "--device", dev] + a.extra.split()
+               "--temperature", str(a.temperature), "--device", dev] + a.extra.split() + a.client_extra.split()
         log = os.path.join(a.log_dir, "stage0.log")
         with open(log, "w") as f:
             rc = subprocess.call(cmd, cwd=ROOT, stdout=f, stderr=subprocess.STDOUT, env=env)

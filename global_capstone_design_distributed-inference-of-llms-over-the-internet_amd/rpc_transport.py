@@ -338,6 +338,32 @@ class RpcTransport:
         self._get_route(session_id)
         self._last_token = self._run(self._send(session_id, hidden, md, "decode"))
 
+    def send_steps(self, steps: Sequence[Tuple[str, torch.Tensor, int, int, int, Optional[List[int]]]]) -> List[int]:
+        """Concurrent sessions over TCP: one step (prefill when ``seq_len == cur_len``, else
+        decode) for each ``(session_id, hidden, seq_len, cur_len, max_length, generated)``,
+        all in flight at once so each server's batching window (rpc_handler ``_drain``) runs
+        them as one ragged step.  Returns the sessions' next tokens, in order.  Per-session
+        recovery is unchanged (every ``_send`` excludes, re-routes and replays on its own)."""
+        if self.stage != 0:
+            raise RuntimeError("send_steps should only be called by stage0")
+
+        async def _all():
+            coros = []
+            for sid, hidden, L, cur, mx, gen in steps:
+                pre = int(L) == int(cur)
+                if pre:
+                    self.client_cache.pop(sid, None)
+                md = {"session_id": sid, "seq_len": int(L), "cur_len": int(cur), "is_prefill": pre,
+                      "max_length": int(mx), **self.sampling}
+                if not pre:
+                    md["generated_tokens"] = list(gen or [])[-50:]
+                coros.append(self._send(sid, hidden, md, "prefill" if pre else "decode"))
+            return await asyncio.gather(*coros)
+
+        for sid, *_ in steps:
+            self._get_route(sid)
+        return [int(t) for t in self._run(_all())]
+
     def recv_token(self) -> int:
         if self.stage != 0:
             raise RuntimeError("recv_token should only be called by stage0")

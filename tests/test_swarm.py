@@ -281,6 +281,31 @@ def test_cli_client_over_device_channel_matches_reference(capsys):
         s2.close()
 
 
+@pytest.mark.timeout(180)
+def test_cli_client_concurrent_tcp_sessions_batch_on_servers():
+    """``--num_sessions 4 --device_channel off``: four sessions go over TCP concurrently; each
+    server's batching window runs them as ragged multi-session steps, every session's greedy
+    output equals the reference, and all sessions are closed afterwards."""
+    from src import main as M
+
+    s1 = ServerThread(server_argv(MODEL, "1,2", 1, extra="--batch_window_ms 20")).wait()
+    s2 = ServerThread(server_argv(MODEL, "1,2", 2, peers=s1.addr, extra="--batch_window_ms 20")).wait()
+    try:
+        assert wait_for(lambda: s1.dht.get(get_stage_key(2)) is not None)
+        seen = []
+        orig = s1.srv.handler._run_batch
+        s1.srv.handler._run_batch = lambda batch: (seen.append(len(batch)), orig(batch))[1]
+        args = client_args(MODEL, "1,2", s1.addr, "--device_channel off --temperature 0 --max_new_tokens 6 "
+                                                  "--num_sessions 4")
+        gen = M.run_rank0(args, M.pick_device(args), [1, 2])
+        assert gen == _reference(6)
+        assert max(seen) > 1  # concurrent sessions shared a server step
+        assert wait_for(lambda: not s1.srv.ex.sessions.sessions and not s2.srv.ex.sessions.sessions)
+    finally:
+        s1.close()
+        s2.close()
+
+
 @pytest.mark.timeout(240)
 def test_lb_placement_follows_measured_throughput():
     """Load-balanced servers announce MEASURED throughput (batched compute probe, network term

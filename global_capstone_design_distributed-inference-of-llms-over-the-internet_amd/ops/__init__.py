@@ -91,8 +91,9 @@ _GEMM_SK = os.environ.get("MPAMD_GEMM_SK", "auto")
 _GEMM_WS = {}
 _SK_CHOICE = {}  # (m_bucket, N, K, epilogue) -> kernel name (see _KERNEL_FLAGS)
 # decode-GEMM kernels (csrc/gemm.hip): one-group-per-workgroup, stream-K, and the shared-A (LDS)
-# form with (NT column tiles per wave, CH column waves sharing each k-split's A) = (2,2)/(2,4)/(4,2)
-_KERNEL_FLAGS = {"pk": 0, "sk": 4, "lds22": 16, "lds24": 16 | 32, "lds42": 16 | 96}
+# form with (NT column tiles per wave, CH column waves sharing each k-split's A) = (2,2)/(2,4)/(4,2),
+# and the balanced ring form "rw" (every CU one workgroup with ceil/floor of tiles / CUs; M > 16)
+_KERNEL_FLAGS = {"pk": 0, "sk": 4, "lds22": 16, "lds24": 16 | 32, "lds42": 16 | 96, "rw": 128}
 _LDS_CFG = {"lds22": (2, 2), "lds24": (2, 4), "lds42": (4, 2)}
 
 
@@ -144,6 +145,8 @@ def _covered(name: str, M: int, N: int, K: int, epilogue: int) -> bool:
         return True
     if name == "sk":
         return _sk_covered(N, K)
+    if name == "rw":  # widths the launcher does not build fall back to the other kernels by itself
+        return M > 16
     return _lds_covered(name, M, N, K, epilogue)
 
 
@@ -616,6 +619,16 @@ def quant_act_fp8(xp: torch.Tensor, M: int, K: int, out=None, scale=None):
         scale = torch.empty(((M + 15) // 16) * 16 * 33, dtype=torch.float32, device=xp.device)
     torch.ops.mpamd.quant_act_fp8(xp, out, scale, int(M), int(K))
     return out, scale
+
+
+_FP8_KERNELS = {"pk": 0, "rw": 1}
+
+
+def set_fp8_kernel(name: str) -> None:
+    """fp8 decode GEMM form (csrc/fp8.hip): "rw" (balanced ring, default, M > 16) or "pk"
+    (one-group-per-workgroup) - for A/B measurements and tests."""
+    require_native()
+    torch.ops.mpamd.fp8_gemm_kernel(_FP8_KERNELS[name])
 
 
 def linear_fp8(a8, a_scale, wq, w_scale, M: int, out=None, epilogue: int = 0, residual=None,

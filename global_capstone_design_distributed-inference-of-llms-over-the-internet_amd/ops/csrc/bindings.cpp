@@ -39,6 +39,7 @@ int mp_attention_mfma(const void* q, int64_t q_stride, const void* kc, const voi
 int mp_quant_act_fp8(const void* ap, void* a8, float* scale, float* part, int M, int K, hipStream_t stream);
 int mp_gemm_fp8(const void* a8, const float* as, const void* wq, const float* ws, void* y, int64_t ys, const void* res,
                 int64_t rs, int M, int N, int K, int epilogue, int out_packed, hipStream_t stream);
+void mp_fp8_set_kernel(int kind);
 int mp_gemm_bf16(const void* x, int64_t x_stride, const void* w, void* y, int64_t y_stride, const void* res,
                  int64_t res_stride, int M, int N, int K, int epilogue, int flags, void* ws, const int* gate,
                  void* ap, void* ss_out, void* ss_zero, const void* ss_in, float inv_k, float eps,
@@ -449,6 +450,7 @@ at::Tensor pack_weight(const at::Tensor& w) {
 }
 
 int64_t gemm_workspace_bytes() { return mp_gemm_workspace_bytes(); }
+void fp8_gemm_kernel(int64_t kind) { mp_fp8_set_kernel((int)kind); }
 
 // packed bf16 decode activation (M rows) -> fp8 A8 [K/64][MT][64][16] (uint8) + row scales (fp32, >= MT*16)
 void quant_act_fp8(const at::Tensor& ap, at::Tensor& a8, at::Tensor& scale, int64_t M, int64_t K) {
@@ -502,6 +504,7 @@ void gemm_fp8(const at::Tensor& a8, const at::Tensor& as, const at::Tensor& wq, 
 
 TORCH_LIBRARY(mpamd, m) {
   m.def("gemm_workspace_bytes() -> int", &gemm_workspace_bytes);
+  m.def("fp8_gemm_kernel(int kind) -> ()", &fp8_gemm_kernel);
   m.def(
       "rmsnorm(Tensor x, Tensor(a!) residual, Tensor w, Tensor(b!) y, float eps, int mode, Tensor? rows, "
       "int packed, Tensor(c!)? ss=None, Tensor(d!)? a8=None, Tensor(e!)? a8_scale=None) -> ()");

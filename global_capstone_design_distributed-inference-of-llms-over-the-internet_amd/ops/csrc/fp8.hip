@@ -17,6 +17,7 @@
 //     (gemm.hip): 8 waves interleave k-groups, ping-pong weight registers, LDS combine,
 //     fused epilogues (scales, SwiGLU on 16-row-interleaved gate/up, residual).
 #include "common.h"
+#include <stdlib.h>
 
 namespace mp {
 
@@ -215,7 +216,198 @@ static int launch_gemm_fp8(const void* a8, const float* as, const void* wq, cons
   return 0;
 }
 
+// ---------------------------------------------------------------------------------------
+// Balanced ring form (the fp8 twin of gemm.hip's "rw" kernel): one 4-wave workgroup per CU owns
+// a contiguous run of ceil / floor (tiles / CUs) column tiles (SwiGLU: gate/up tile PAIRS) and
+// all of K; the waves take interleaved 64-k chunks through a 2-deep register ring holding both
+// operands, then the 4 partial tiles are summed through LDS (in passes of at most 32 quads:
+// the Llama-3-70B gate/up workgroup owns 14 tiles = 56 quads) and the scale / SwiGLU /
+// residual epilogue runs.  The one-group kernel above gives the 70B gate/up (3584 tiles) 1792
+// two-tile workgroups in 7 rounds over the CUs; here each CU streams its 7 pairs in one go.
+constexpr int F8RW_WAVES = 4;
+constexpr int F8RW_QC = 32;  // quads per combine pass (LDS: 4 waves x 32 x 1 KiB)
+
+template <int MT, int NT, int EPI, bool OPK>
+__device__ __forceinline__ void f8rw_body(const uint8_t* __restrict__ a8, const float* __restrict__ ascale,
+                                          const uint8_t* __restrict__ wq, const float* __restrict__ wscale,
+                                          bf16_t* __restrict__ y, int64_t ys, const bf16_t* __restrict__ res,
+                                          int64_t rs, int M, int K, int tile0, f32x4* red) {
+  constexpr int R = 2;
+  constexpr int Q = MT * NT;
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int c = lane & 15, q = lane >> 4;
+  const int nch = K >> 6;
+  const int cnt = (nch + F8RW_WAVES - 1) / F8RW_WAVES;
+  const uint8_t* wb = wq + ((int64_t)tile0 * nch) * 1024 + lane * 16;
+  const uint8_t* ab = a8 + lane * 16;
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[mt][t] = (f32x4)(0.f);
+  u16x8 ra[R][MT], rb[R][NT];
+#define F8RW_LOAD(s, i)                                                                                      \
+  {                                                                                                          \
+    const int k_ = min(wid + F8RW_WAVES * (i), nch - 1);                                                     \
+    _Pragma("unroll") for (int t = 0; t < NT; ++t) rb[s][t] =                                                \
+        __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(wb + ((int64_t)t * nch + k_) * 1024));    \
+    _Pragma("unroll") for (int mt = 0; mt < MT; ++mt) ra[s][mt] =                                            \
+        *reinterpret_cast<const u16x8*>(ab + ((int64_t)k_ * MT + mt) * 1024);                                \
+  }
+#pragma unroll
+  for (int s = 0; s < R; ++s) F8RW_LOAD(s, s)
+  for (int i0 = 0; i0 < cnt; i0 += R) {
+#pragma unroll
+    for (int s = 0; s < R; ++s) {
+      if (wid + F8RW_WAVES * (i0 + s) < nch) {
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int t = 0; t < NT; ++t) acc[mt][t] = mfma_fp8x2(ra[s][mt], rb[s][t], acc[mt][t]);
+      }
+      F8RW_LOAD(s, i0 + s + R)
+    }
+  }
+#undef F8RW_LOAD
+  // combine + epilogue in passes of QC quads (EPI 1: gate/up quads pair up inside a pass)
+  constexpr int QC = Q < F8RW_QC ? Q : F8RW_QC;
+#pragma unroll
+  for (int p0 = 0; p0 < Q; p0 += QC) {
+    if (p0 > 0) __syncthreads();  // the previous pass finished reading red
+#pragma unroll
+    for (int qd = p0; qd < p0 + QC && qd < Q; ++qd) red[(wid * QC + qd - p0) * 64 + lane] = acc[qd / NT][qd % NT];
+    __syncthreads();
+    for (int qd = p0 + wid; qd < p0 + QC && qd < Q; qd += F8RW_WAVES) {
+      const int mt = qd / NT, t = qd % NT, tile = tile0 + t;
+      if (EPI == 1 && (t & 1)) continue;  // up tile: consumed with its gate tile
+      f32x4 v = red[(qd - p0) * 64 + lane], up = (f32x4)(0.f);
+#pragma unroll
+      for (int w = 1; w < F8RW_WAVES; ++w) v += red[(w * QC + qd - p0) * 64 + lane];
+      if constexpr (EPI == 1) {
+#pragma unroll
+        for (int w = 0; w < F8RW_WAVES; ++w) up += red[(w * QC + qd + 1 - p0) * 64 + lane];
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = mt * 16 + q * 4 + r;
+        if (row >= M) continue;
+        const float as = ascale[row];
+        if constexpr (EPI == 1) {
+          const int gcol = tile * 16 + c;
+          const float gg = round_bf(v[r] * as * wscale[gcol]);
+          const float uu = round_bf(up[r] * as * wscale[gcol + 16]);
+          const float act = round_bf(gg / (1.f + __expf(-gg)));
+          const int ncol = (tile >> 1) * 16 + c;
+          const int64_t yo = OPK ? apk_off(row, ncol, MT) : (int64_t)row * ys + ncol;
+          y[yo] = f2bf(act * uu);
+        } else {
+          const int col = tile * 16 + c;
+          float o = v[r] * as * wscale[col];
+          if constexpr (EPI == 2) o = round_bf(o) + bf2f(res[(int64_t)row * rs + col]);
+          y[(int64_t)row * ys + col] = f2bf(o);
+        }
+      }
+    }
+  }
+}
+
+template <int MT, int NTB, int NTS, int EPI, bool OPK>
+__global__ __launch_bounds__(256) void gemm_fp8_rw_kernel(const uint8_t* __restrict__ a8,
+                                                          const float* __restrict__ ascale,
+                                                          const uint8_t* __restrict__ wq,
+                                                          const float* __restrict__ wscale, bf16_t* __restrict__ y,
+                                                          int64_t ys, const bf16_t* __restrict__ res, int64_t rs,
+                                                          int M, int K, int n_big) {
+  constexpr int QB = MT * NTB < F8RW_QC ? MT * NTB : F8RW_QC;
+  __shared__ __attribute__((aligned(16))) f32x4 red[F8RW_WAVES * QB * 64];
+  const int b = blockIdx.x;
+  if (b < n_big) {
+    f8rw_body<MT, NTB, EPI, OPK>(a8, ascale, wq, wscale, y, ys, res, rs, M, K, b * NTB, red);
+  } else {
+    f8rw_body<MT, NTS, EPI, OPK>(a8, ascale, wq, wscale, y, ys, res, rs, M, K, n_big * NTB + (b - n_big) * NTS, red);
+  }
+}
+
+static int f8_num_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+      v = 256;
+    n = v;
+  }
+  return n;
+}
+
+template <int MT, int NTB, int NTS>
+static int launch_gemm_fp8_rw_cfg(const void* a8, const float* as, const void* wq, const float* ws, void* y, int64_t ys,
+                                  const void* res, int64_t rs, int M, int K, int epi, bool opk, int G, int n_big,
+                                  hipStream_t stream) {
+#define F8RW(EPI_, OPK_)                                                                                          \
+  hipLaunchKernelGGL((gemm_fp8_rw_kernel<MT, NTB, NTS, EPI_, OPK_>), dim3(G), dim3(256), 0, stream,               \
+                     (const uint8_t*)a8, as, (const uint8_t*)wq, ws, (bf16_t*)y, ys, (const bf16_t*)res, rs, M, K, \
+                     n_big)
+  if (epi == 1) {
+    if constexpr (NTB % 2 == 0 && NTS % 2 == 0) {
+      if (opk) { F8RW(1, true); } else { F8RW(1, false); }
+    } else {
+      return 1;
+    }
+  } else if (opk) {
+    return -3;
+  } else if (epi == 2) {
+    F8RW(2, false);
+  } else {
+    F8RW(0, false);
+  }
+#undef F8RW
+  return 0;
+}
+
+// Widths built: SwiGLU 2..14 tiles in pairs (7 pairs = the 70B gate/up on 256 CUs), plain 1..4.
+template <int MT>
+static int launch_gemm_fp8_rw(const void* a8, const float* as, const void* wq, const float* ws, void* y, int64_t ys,
+                              const void* res, int64_t rs, int M, int N, int K, int epi, int opk, hipStream_t stream) {
+  const int step = epi == 1 ? 2 : 1;
+  const int units = (N / 16) / step;
+  if ((N / 16) % step || units == 0) return 1;
+  const int G = units < f8_num_cus() ? units : f8_num_cus();
+  const int base = units / G, rem = units % G;
+  const int ntb = (base + (rem ? 1 : 0)) * step;
+  const int n_big = rem ? rem : G;
+#define F8RWC(B_, S_) \
+  return launch_gemm_fp8_rw_cfg<MT, B_, S_>(a8, as, wq, ws, y, ys, res, rs, M, K, epi, opk, G, n_big, stream)
+  if (epi == 1) {
+    switch (ntb) {
+      case 2: if (rem) return 1; F8RWC(2, 2);
+      case 4: F8RWC(4, 2);
+      case 6: F8RWC(6, 4);
+      case 8: F8RWC(8, 6);
+      case 14: if (rem) return 1; F8RWC(14, 14);
+      default: return 1;
+    }
+  }
+  switch (ntb) {
+    case 1: F8RWC(1, 1);
+    case 2: F8RWC(2, 1);
+    case 3: F8RWC(3, 2);
+    case 4: F8RWC(4, 3);
+    default: return 1;
+  }
+#undef F8RWC
+}
+
+// 0 = one-group kernel, 1 = balanced ring kernel where it applies (M > 16; default);
+// MPAMD_FP8_GEMM=pk selects the one-group kernel at start-up (A/B runs of bench.py)
+static int g_fp8_kernel = [] {
+  const char* v = getenv("MPAMD_FP8_GEMM");
+  return (v && v[0] == 'p') ? 0 : 1;
+}();
+
 }  // namespace mp
+
+extern "C" void mp_fp8_set_kernel(int kind) { mp::g_fp8_kernel = kind; }
 
 // part: >= ceil(M/16) * 16 * Q_NS floats of scratch
 extern "C" int mp_quant_act_fp8(const void* ap, void* a8, float* scale, float* part, int M, int K,
@@ -238,6 +430,13 @@ extern "C" int mp_gemm_fp8(const void* a8, const float* as, const void* wq, cons
   if (M == 0) return 0;
   if (M > 64 || K % (64 * F8_GU_MAX) || N % 16) return -1;
   int rc;
+  if (g_fp8_kernel == 1 && M > 16) {
+    if (M <= 32) rc = launch_gemm_fp8_rw<2>(a8, as, wq, ws, y, ys, res, rs, M, N, K, epilogue, out_packed, stream);
+    else if (M <= 48) rc = launch_gemm_fp8_rw<3>(a8, as, wq, ws, y, ys, res, rs, M, N, K, epilogue, out_packed, stream);
+    else rc = launch_gemm_fp8_rw<4>(a8, as, wq, ws, y, ys, res, rs, M, N, K, epilogue, out_packed, stream);
+    if (rc < 0) return rc;
+    if (rc == 0) return (int)hipGetLastError();
+  }
   if (M <= 16) rc = launch_gemm_fp8<1>(a8, as, wq, ws, y, ys, res, rs, M, N, K, epilogue, out_packed, stream);
   else if (M <= 32) rc = launch_gemm_fp8<2>(a8, as, wq, ws, y, ys, res, rs, M, N, K, epilogue, out_packed, stream);
   else if (M <= 48) rc = launch_gemm_fp8<3>(a8, as, wq, ws, y, ys, res, rs, M, N, K, epilogue, out_packed, stream);

@@ -82,7 +82,7 @@ __device__ __forceinline__ void clear_other(const EpiArgs& ep) {
 // for them costs nothing beyond the first weight chunk the loop waits for anyway, and only 2
 // VGPRs stay live through the loop); the partials are reduced through LDS in the epilogue,
 // after the main loop's last barrier.
-template <bool ON>
+template <bool ON, int NW = 8>
 struct RowScale {
   u64 v = 0;
   __device__ __forceinline__ void load(const EpiArgs& ep, const void* any_valid) {
@@ -91,7 +91,7 @@ struct RowScale {
       const int tid = threadIdx.x;
       u64 t = 0;
 #pragma unroll
-      for (int j = 0; j < SS_NSH / 8; ++j) t += src[ep.ss_in != nullptr ? ((tid >> 6) + 8 * j) * 64 + (tid & 63) : 0];
+      for (int j = 0; j < SS_NSH / NW; ++j) t += src[ep.ss_in != nullptr ? ((tid >> 6) + NW * j) * 64 + (tid & 63) : 0];
       v = t;
     }
   }
@@ -105,7 +105,7 @@ struct RowScale {
       if (tid < 64) {
         u64 s = 0;
 #pragma unroll
-        for (int w = 0; w < 8; ++w) s += part[w][tid];
+        for (int w = 0; w < NW; ++w) s += part[w][tid];
         rs[tid] = rsqrtf((float)s * (1.f / SS_FX) * ep.inv_k + ep.eps);
       }
       __syncthreads();
@@ -374,12 +374,13 @@ __device__ __forceinline__ u16x4 res_quad(const bf16_t* __restrict__ res, int64_
   return o;
 }
 
-template <int MT, int NT, int EPI, bool OPK>
-__device__ __forceinline__ void sk_epilogue(int qd, int g, const f32x4& v, const f32x4& up, bf16_t* __restrict__ y,
-                                            int64_t ys, const bf16_t* __restrict__ res, int64_t rs, int M, int lane,
-                                            const EpiArgs& ep, const float* rsl, const u16x4* rpv = nullptr) {
-  const int mt = qd / NT, t = qd % NT, c = lane & 15, q = lane >> 4;
-  const int tile = g * NT + t;
+// Epilogue of one accumulator quad (rows mt*16 + 4q .. +3 of column tile ``tile``, this lane's
+// column); ``up`` is the matching up-projection quad for EPI 1.
+template <int MT, int EPI, bool OPK>
+__device__ __forceinline__ void tile_epilogue(int mt, int tile, const f32x4& v, const f32x4& up, bf16_t* __restrict__ y,
+                                              int64_t ys, const bf16_t* __restrict__ res, int64_t rs, int M, int lane,
+                                              const EpiArgs& ep, const float* rsl, const u16x4* rpv) {
+  const int c = lane & 15, q = lane >> 4;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int row = mt * 16 + q * 4 + r;
@@ -401,6 +402,13 @@ __device__ __forceinline__ void sk_epilogue(int qd, int g, const f32x4& v, const
       y[(int64_t)row * ys + col] = f2bf(o);
     }
   }
+}
+
+template <int MT, int NT, int EPI, bool OPK>
+__device__ __forceinline__ void sk_epilogue(int qd, int g, const f32x4& v, const f32x4& up, bf16_t* __restrict__ y,
+                                            int64_t ys, const bf16_t* __restrict__ res, int64_t rs, int M, int lane,
+                                            const EpiArgs& ep, const float* rsl, const u16x4* rpv = nullptr) {
+  tile_epilogue<MT, EPI, OPK>(qd / NT, g * NT + qd % NT, v, up, y, ys, res, rs, M, lane, ep, rsl, rpv);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -861,6 +869,189 @@ static int launch_gemm_sk(const void* x, void* y, int64_t ys, const void* w, con
   return launch_gemm_sk_cfg<MT, 4, DW>(x, y, ys, w, res, rs, M, N, K, epi, flags, ws, C, ep, stream);
 }
 
+// ---------------------------------------------------------------------------------------
+// Balanced ring form ("rw"): every CU gets one workgroup of 4 waves (one per SIMD) that owns a
+// CONTIGUOUS run of column tiles and all of K, with no split-K hand-off.  The tile count per
+// workgroup is ceil or floor of tiles / CUs (SwiGLU: of gate/up tile PAIRS), so every CU streams
+// about the same weight bytes.  This is what the layer shapes need: gate/up (1376 tiles =
+// 32 x 43) gives the fixed-width kernels 172 workgroups of 8 tiles (84 CUs idle) or ragged
+// waves of workgroups; here it is 176 x 6 + 80 x 4 tiles on 256 CUs.  The two widths are two
+// template bodies behind one uniform branch.
+// Inside a workgroup the waves take interleaved k-slices (k = wave + 4 i) through an R-deep
+// register ring holding BOTH operands of a slice, loads issued R slices ahead in consumption
+// order (in-order vmcnt never drains the ring; loads past the end are clamped to a valid slice
+// and their MFMAs skipped), then the 4 partial tiles are summed through LDS and the shared
+// epilogues run (row scale, SwiGLU, residual, the fused-norm producer).
+constexpr int RW_WAVES = 4;
+
+// Ring slots: a power of two (K / 32 / 4 waves is a multiple of it at K = 4096, 11008: no
+// clamped tail turn); 4 (MT + NT) VGPRs each (one wave per SIMD: the accumulators go to AGPRs).
+// Measured at M = 64 (lab, us): qkv depth 2 / 4 / 6 = 21.2 / 21.7 / 22.7, gate/up 35.1 / 35.3 /
+// 35.4, o 14.3 / 13.7 / 14.1: two slots of 4 waves already cover the latency where tiles are wide.
+template <int MT, int NT>
+constexpr int rw_depth() {
+  return 190 / (4 * (MT + NT)) >= 8 ? 4 : 2;
+}
+
+template <int MT, int NT, int EPI, bool OPK>
+__device__ __forceinline__ void rw_body(const bf16_t* __restrict__ x, const bf16_t* __restrict__ wp,
+                                        bf16_t* __restrict__ y, int64_t ys, const bf16_t* __restrict__ res, int64_t rs,
+                                        int M, int K, int tile0, const EpiArgs& ep, f32x4* red, u64 (*rs_part)[64],
+                                        float* rs_lds) {
+  constexpr int R = rw_depth<MT, NT>();
+  constexpr int Q = MT * NT;
+  constexpr int NQ = (Q + RW_WAVES - 1) / RW_WAVES;  // epilogue quads per wave
+  RowScale<EPI < 2, RW_WAVES> rsc;
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nks = K >> 5;
+  const int cnt = (nks + RW_WAVES - 1) / RW_WAVES;  // ring steps of the busiest wave
+  const bf16_t* wb = wp + ((int64_t)tile0 * nks) * 512 + lane * 8;
+  const bf16_t* xl = x + lane * 8;
+
+  // EPI 3: the residual quads this wave finalises, in flight during the main loop
+  u16x4 rpre[NQ];
+  if constexpr (EPI == 3) {
+#pragma unroll
+    for (int j = 0; j < NQ; ++j) {
+      const int qd = min(wid + RW_WAVES * j, Q - 1), mt = qd / NT, t = qd % NT;
+      const int col = (tile0 + t) * 16 + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) rpre[j][r] = res[(int64_t)min(mt * 16 + (lane >> 4) * 4 + r, M - 1) * rs + col];
+    }
+  }
+
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[mt][t] = (f32x4)(0.f);
+  u16x8 ra[R][MT], rb[R][NT];
+#define RW_LOAD(s, i)                                                                                        \
+  {                                                                                                          \
+    const int k_ = min(wid + RW_WAVES * (i), nks - 1);                                                       \
+    _Pragma("unroll") for (int t = 0; t < NT; ++t) rb[s][t] =                                                \
+        __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(wb + (((int64_t)t * nks + k_) << 9)));    \
+    _Pragma("unroll") for (int mt = 0; mt < MT; ++mt) ra[s][mt] =                                            \
+        MP_LOAD_A_FRAG(xl + (((int64_t)k_ * MT + mt) << 9));                                                 \
+  }
+#pragma unroll
+  for (int s = 0; s < R; ++s) RW_LOAD(s, s)
+  rsc.load(ep, wp);
+  for (int i0 = 0; i0 < cnt; i0 += R) {
+#pragma unroll
+    for (int s = 0; s < R; ++s) {
+      if (wid + RW_WAVES * (i0 + s) < nks) {
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int t = 0; t < NT; ++t) acc[mt][t] = mfma16(ra[s][mt], rb[s][t], acc[mt][t]);
+      }
+      RW_LOAD(s, i0 + s + R)
+    }
+  }
+#undef RW_LOAD
+  // ---- sum the 4 waves' partial tiles through LDS, then the epilogue ----
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) red[(wid * Q + mt * NT + t) * 64 + lane] = acc[mt][t];
+  __syncthreads();
+  rsc.finish(ep, rs_part, rs_lds);
+#pragma unroll
+  for (int j = 0; j < NQ; ++j) {
+    const int qd = wid + RW_WAVES * j;
+    if (qd >= Q) break;
+    if (EPI == 1 && (qd % NT) & 1) continue;  // up tile: consumed with its gate tile
+    f32x4 v = red[qd * 64 + lane], up = (f32x4)(0.f);
+#pragma unroll
+    for (int w = 1; w < RW_WAVES; ++w) v += red[(w * Q + qd) * 64 + lane];
+    if constexpr (EPI == 1) {
+#pragma unroll
+      for (int w = 0; w < RW_WAVES; ++w) up += red[(w * Q + qd + 1) * 64 + lane];
+    }
+    tile_epilogue<MT, EPI, OPK>(qd / NT, tile0 + qd % NT, v, up, y, ys, res, rs, M, lane, ep, rs_lds,
+                                EPI == 3 ? &rpre[j] : nullptr);
+  }
+}
+
+template <int MT, int NTB, int NTS, int EPI, bool OPK>
+__global__ __launch_bounds__(256) void gemm_rw_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ wp,
+                                                      bf16_t* __restrict__ y, int64_t ys,
+                                                      const bf16_t* __restrict__ res, int64_t rs, int M, int K,
+                                                      int n_big, const EpiArgs ep) {
+  clear_other(ep);
+  __shared__ u64 rs_part[8][64];
+  __shared__ float rs_lds[64];
+  __shared__ __attribute__((aligned(16))) f32x4 red[RW_WAVES * MT * NTB * 64];
+  const int b = blockIdx.x;
+  if (b < n_big) {
+    rw_body<MT, NTB, EPI, OPK>(x, wp, y, ys, res, rs, M, K, b * NTB, ep, red, rs_part, rs_lds);
+  } else {
+    rw_body<MT, NTS, EPI, OPK>(x, wp, y, ys, res, rs, M, K, n_big * NTB + (b - n_big) * NTS, ep, red, rs_part,
+                               rs_lds);
+  }
+}
+
+template <int MT, int NTB, int NTS>
+static int launch_gemm_rw_cfg(const void* x, const void* w, void* y, int64_t ys, const void* res, int64_t rs, int M,
+                              int K, int epi, bool opk, int G, int n_big, const EpiArgs& ep, hipStream_t stream) {
+#define MP_RW(EPI_, OPK_)                                                                                          \
+  hipLaunchKernelGGL((gemm_rw_kernel<MT, NTB, NTS, EPI_, OPK_>), dim3(G), dim3(256), 0, stream, (const bf16_t*)x, \
+                     (const bf16_t*)w, (bf16_t*)y, ys, (const bf16_t*)res, rs, M, K, n_big, ep)
+  if (epi == 1) {
+    if constexpr (NTB % 2 == 0 && NTS % 2 == 0) {
+      if (opk) { MP_RW(1, true); } else { MP_RW(1, false); }
+    } else {
+      return 1;
+    }
+  } else if (opk) {
+    return -3;
+  } else if (epi == 2) {
+    MP_RW(2, false);
+  } else if (epi == 3) {
+    MP_RW(3, false);
+  } else {
+    MP_RW(0, false);
+  }
+#undef MP_RW
+  return 0;
+}
+
+// Split the column units (tiles, or gate/up tile pairs) over G = min(#CUs, units) workgroups:
+// n_big of them take ceil, the rest floor.  Returns 1 (caller falls back) for widths not built.
+template <int MT>
+static int launch_gemm_rw(const void* x, const void* w, void* y, int64_t ys, const void* res, int64_t rs, int M,
+                          int N, int K, int epi, int flags, const EpiArgs& ep, hipStream_t stream) {
+  const int step = epi == 1 ? 2 : 1;
+  const int units = (N / 16) / step;
+  if ((N / 16) % step || units == 0) return 1;
+  const int G = units < sk_num_cus() ? units : sk_num_cus();
+  const int base = units / G, rem = units % G;
+  const int ntb = (base + (rem ? 1 : 0)) * step;
+  const int n_big = rem ? rem : G;
+  const bool opk = flags & 2;
+#define MP_RWC(B_, S_) return launch_gemm_rw_cfg<MT, B_, S_>(x, w, y, ys, res, rs, M, K, epi, opk, G, n_big, ep, stream)
+  if (epi == 1) {
+    switch (ntb) {
+      case 2: if (rem) return 1; MP_RWC(2, 2);
+      case 4: MP_RWC(4, 2);
+      case 6: MP_RWC(6, 4);
+      case 8: MP_RWC(8, 6);
+      default: return 1;
+    }
+  }
+  switch (ntb) {
+    case 1: MP_RWC(1, 1);
+    case 2: MP_RWC(2, 1);
+    case 3: MP_RWC(3, 2);
+    case 4: MP_RWC(4, 3);
+    case 6: if (rem) return 1; MP_RWC(6, 6);
+    case 8: MP_RWC(8, 7);
+    default: return 1;
+  }
+#undef MP_RWC
+}
+
 // Pack W[N, K] (row-major) into the fragment-native layout Wp[N/16][K/32][64][8].
 __global__ __launch_bounds__(256) void pack_weight_kernel(const bf16_t* __restrict__ w, bf16_t* __restrict__ wp,
                                                           int N, int K) {
@@ -890,7 +1081,8 @@ extern "C" int64_t mp_gemm_workspace_bytes() {
 // flags: bit 0 = x is packed (Ap[K/32][ceil(M/16)][64][8]); bit 1 = SwiGLU output packed;
 //        bit 2 = use the stream-K kernel (needs ws: mp_gemm_workspace_bytes(), zero-initialised,
 //        used by one stream at a time); bit 3 = force the one-group-per-workgroup kernel;
-//        bit 4 = shared-A (LDS-staged activation) kernel when the shape allows it.
+//        bit 4 = shared-A (LDS-staged activation) kernel when the shape allows it;
+//        bit 7 = balanced ring kernel (M > 16).
 //        epilogue 3 / ss_in: the fused-norm decode path (EpiArgs above; ap / ss_out / ss_zero /
 //        ss_in may be null when unused).
 extern "C" int mp_gemm_bf16(const void* x, int64_t x_stride, const void* w, void* y, int64_t y_stride,
@@ -903,7 +1095,14 @@ extern "C" int mp_gemm_bf16(const void* x, int64_t x_stride, const void* w, void
   const EpiArgs ep{(bf16_t*)ap, (u64*)ss_out, (u64*)ss_zero, (const u64*)ss_in, inv_k, eps, (M + 15) / 16};
   if (M > 64 || K % (32 * GU_MAX) || N % 16 || ((flags & 1) == 0 && x_stride % 8)) return -1;
   int rc;
-  if (gate != nullptr) flags &= ~(4 | 16);  // gated (MoE expert) GEMMs use the one-group kernel
+  if (gate != nullptr) flags &= ~(4 | 16 | 128);  // gated (MoE expert) GEMMs use the one-group kernel
+  if ((flags & 1) && (flags & 128) && !(flags & 8) && M > 16) {  // balanced ring kernel
+    if (M <= 32) rc = launch_gemm_rw<2>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, ep, stream);
+    else if (M <= 48) rc = launch_gemm_rw<3>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, ep, stream);
+    else rc = launch_gemm_rw<4>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, ep, stream);
+    if (rc < 0) return rc;
+    if (rc == 0) return (int)hipGetLastError();
+  }
   if ((flags & 1) && (flags & 16) && !(flags & 8)) {  // shared-A kernel
     if (M <= 16) rc = launch_gemm_lds<1>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, ep, stream);
     else if (M <= 32) rc = launch_gemm_lds<2>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, ep, stream);

@@ -35,6 +35,21 @@ def main():
               ("down+res3", 4096, 11008, 3, False), ("o+res3-noatomic", 4096, 4096, 3, None),
               ("down+res3-noatomic", 4096, 11008, 3, None)]
     for M in a.m:
+        # library baseline: hipBLASLt through torch (row-major bf16 weight, same rotation)
+        for name, N, K in (("qkv", 12288, 4096), ("o", 4096, 4096), ("gate_up", 22016, 4096), ("down", 4096, 11008)):
+            ws = [pool[i * N * K:(i + 1) * N * K].view(N, K) for i in range(min(16, pool.numel() // (N * K)))]
+            xa = (torch.randn(M, K, device=dev) * 0.5).to(torch.bfloat16)
+            for i in range(3):
+                torch.nn.functional.linear(xa, ws[i % len(ws)])
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for i in range(a.iters):
+                torch.nn.functional.linear(xa, ws[i % len(ws)])
+            e1.record()
+            e1.synchronize()
+            us = e0.elapsed_time(e1) / a.iters * 1000
+            print(json.dumps({"M": M, "shape": name, "N": N, "K": K, "kernel": "hipblaslt", "us": round(us, 2),
+                              "TBps": round(N * K * 2 / us / 1e6, 2)}), flush=True)
         ss = ops.norm_stats_buffer(dev, 3)
         for name, N, K, epi, rs in shapes:
             n = N * K

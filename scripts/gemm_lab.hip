@@ -86,17 +86,18 @@ int main(int argc, char** argv) {
   unsigned short* yref;
   CK(hipMalloc(&yref, (size_t)64 * 32768 * 2));
   std::vector<unsigned short> h0(64 * 32768), h1(64 * 32768);
-  const char* kname[6] = {"pk ", "sk ", "l22", "l24", "l14", "l42"};
+  const char* kname[7] = {"pk ", "sk ", "l22", "l24", "l14", "l42", "rw "};
   for (const Shape& s : shapes) {
     const size_t wbytes = (size_t)s.N * s.K * 2;
     const int copies = (int)(pool_bytes / wbytes);
     const int ncols = s.epi == 1 ? s.N / 2 : s.N;
     for (int M : Ms) {
-      for (int kind = 0; kind < 6; ++kind) {
-        const int flags = 1 | (kind == 0 ? 8 : kind == 1 ? 4 : 16 | ((kind - 2) << 5));
+      for (int kind = 0; kind < 7; ++kind) {
+        const int flags = 1 | (kind == 0 ? 8 : kind == 1 ? 4 : kind == 6 ? 128 : 16 | ((kind - 2) << 5));
         auto run = [&](int i, unsigned short* out) {
           const unsigned short* w = pool + (size_t)(i % copies) * (wbytes / 2);
-          return mp_gemm_bf16(x, s.K, w, out, ncols, nullptr, 0, M, s.N, s.K, s.epi, flags, ws, nullptr, 0);
+          return mp_gemm_bf16(x, s.K, w, out, ncols, nullptr, 0, M, s.N, s.K, s.epi, flags, ws, nullptr, nullptr,
+                              nullptr, nullptr, nullptr, 0.f, 0.f, 0);
         };
         int rc = run(0, kind == 0 ? yref : y);
         if (rc) {

@@ -211,12 +211,13 @@ def test_gemm_stream_k(M, N, K, sk):
     assert int(ops.gemm_workspace(DEV)[:4 * 4096].view(torch.int32).abs().sum()) == 0  # counters re-zeroed
 
 
-@pytest.mark.parametrize("kern", ["lds22", "lds24", "lds42"])
+@pytest.mark.parametrize("kern", ["lds22", "lds24", "lds42", "rw"])
 @pytest.mark.parametrize("M", [1, 16, 20, 40, 64])
 @pytest.mark.parametrize("N,K,epi", [(4096, 4096, 0), (12288, 4096, 2), (4096, 11008, 0), (22016, 4096, 1),
                                      (32000, 4096, 0), (1024, 1024, 1)])
 def test_gemm_shared_a(kern, M, N, K, epi):
-    """Shared-A (LDS-staged activation) decode GEMM, every epilogue, vs fp32; deterministic."""
+    """Shared-A (LDS-staged activation) and balanced-ring decode GEMMs, every epilogue, vs fp32;
+    deterministic."""
     from src.models.weights import interleave_gate_up
 
     x = bf(torch.randn(M, K, device=DEV))
@@ -390,12 +391,24 @@ def test_fp8_quant_act_kernel_matches_reference(M):
     assert a8.numel() >= MT * 16 * K
 
 
+@pytest.mark.parametrize("kern", ["pk", "rw"])
 @pytest.mark.parametrize("M", [1, 30, 64])
 @pytest.mark.parametrize("N,K,epi", [(1024, 1024, 0), (10240, 8192, 0), (8192, 28672, 0), (2048, 4096, 1),
-                                     (4096, 11008, 2)])
-def test_fp8_gemm_kernel_matches_reference(M, N, K, epi):
+                                     (4096, 11008, 2), (57344, 512, 1)])
+def test_fp8_gemm_kernel_matches_reference(kern, M, N, K, epi):
+    """Both fp8 GEMM forms vs the CPU reference; (57344, 512, 1) is the Llama-3-70B gate/up width
+    (7 gate/up pairs per CU in the balanced ring form) at a short K."""
     from src.ops import reference as ref
     from src.models.weights import interleave_gate_up
+
+    ops.set_fp8_kernel(kern)
+    try:
+        _fp8_gemm_case(M, N, K, epi, ref, interleave_gate_up)
+    finally:
+        ops.set_fp8_kernel("rw")
+
+
+def _fp8_gemm_case(M, N, K, epi, ref, interleave_gate_up):
 
     x = bf(torch.randn(M, K, device=DEV))
     if epi == 1:

@@ -621,6 +621,26 @@ def quant_act_fp8(xp: torch.Tensor, M: int, K: int, out=None, scale=None):
     return out, scale
 
 
+def quant_rows_fp8(x: torch.Tensor, out=None, scale=None):
+    """Row-major bf16 x[M, K] -> (fp8 A8 in the fp8 GEMM's A layout, per-row scales)."""
+    M, K = x.shape
+    if not _native(x):
+        a8, s = ref.quant_act_fp8(ref.pack_act(x), M, K)
+        if out is not None:
+            out[: a8.numel()].copy_(a8)
+            a8 = out
+        if scale is not None:
+            scale[: s.numel()].copy_(s)
+            s = scale
+        return a8, s
+    if out is None:
+        out = torch.empty(packed_numel(M, K), dtype=torch.uint8, device=x.device)
+    if scale is None:
+        scale = torch.empty(((M + 15) // 16) * 16, dtype=torch.float32, device=x.device)
+    torch.ops.mpamd.quant_rows_fp8(x, out, scale)
+    return out, scale
+
+
 _FP8_KERNELS = {"pk": 0, "rw": 1}
 
 

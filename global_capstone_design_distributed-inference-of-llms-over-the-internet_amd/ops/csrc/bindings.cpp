@@ -40,6 +40,7 @@ int mp_quant_act_fp8(const void* ap, void* a8, float* scale, float* part, int M,
 int mp_gemm_fp8(const void* a8, const float* as, const void* wq, const float* ws, void* y, int64_t ys, const void* res,
                 int64_t rs, int M, int N, int K, int epilogue, int out_packed, hipStream_t stream);
 void mp_fp8_set_kernel(int kind);
+int mp_quant_rows_fp8(const void* x, int64_t xs, void* a8, float* scale, int M, int K, hipStream_t stream);
 int mp_gemm_bf16(const void* x, int64_t x_stride, const void* w, void* y, int64_t y_stride, const void* res,
                  int64_t res_stride, int M, int N, int K, int epilogue, int flags, void* ws, const int* gate,
                  void* ap, void* ss_out, void* ss_zero, const void* ss_in, float inv_k, float eps,
@@ -467,6 +468,20 @@ void quant_act_fp8(const at::Tensor& ap, at::Tensor& a8, at::Tensor& scale, int6
                "quant_act_fp8");
 }
 
+// row-major bf16 x[M, K] -> fp8 A8 (the fp8 GEMM's A layout) + per-row scales
+void quant_rows_fp8(const at::Tensor& x, at::Tensor& a8, at::Tensor& scale) {
+  check_bf16_cuda(x, "x");
+  MP_CHECK(x.dim() == 2 && x.stride(1) == 1, "x: [M, K] with unit column stride");
+  const int64_t M = x.size(0), K = x.size(1);
+  MP_CHECK(a8.is_cuda() && a8.scalar_type() == at::kByte && a8.is_contiguous() && a8.numel() >= packed_numel(M, K),
+           "a8: uint8 [packed_numel(M, K)]");
+  MP_CHECK(scale.is_cuda() && scale.scalar_type() == at::kFloat && scale.numel() >= M, "scale: fp32 [>= M]");
+  MP_CHECK(K % 64 == 0 && K <= 65536, "K % 64 == 0 and K <= 65536");
+  check_launch(mp_quant_rows_fp8(x.data_ptr(), x.stride(0), a8.data_ptr(), scale.data_ptr<float>(), (int)M, (int)K,
+                                 cur_stream()),
+               "quant_rows_fp8");
+}
+
 // y = epilogue((a8 * as) . (wq * ws)^T); wq: [N/16, K/64, 64, 16] uint8 (ops.pack_weight_fp8)
 void gemm_fp8(const at::Tensor& a8, const at::Tensor& as, const at::Tensor& wq, const at::Tensor& ws, at::Tensor& y,
               const c10::optional<at::Tensor>& residual, int64_t epilogue, int64_t M, int64_t out_packed) {
@@ -542,6 +557,7 @@ TORCH_LIBRARY(mpamd, m) {
   m.def("pack_act(Tensor x, Tensor(a!) ap) -> ()");
   m.def("pack_weight(Tensor w) -> Tensor");
   m.def("quant_act_fp8(Tensor ap, Tensor(a!) a8, Tensor(b!) scale, int M, int K) -> ()");
+  m.def("quant_rows_fp8(Tensor x, Tensor(a!) a8, Tensor(b!) scale) -> ()");
   m.def(
       "gemm_fp8(Tensor a8, Tensor a_scale, Tensor wq, Tensor w_scale, Tensor(a!) y, Tensor? residual, int epilogue, "
       "int M, int out_packed) -> ()");
@@ -564,5 +580,6 @@ TORCH_LIBRARY_IMPL(mpamd, CUDA, m) {
   m.impl("pack_weight", &pack_weight);
   m.impl("pack_act", &pack_act);
   m.impl("quant_act_fp8", &quant_act_fp8);
+  m.impl("quant_rows_fp8", &quant_rows_fp8);
   m.impl("gemm_fp8", &gemm_fp8);
 }

@@ -93,6 +93,102 @@ __global__ __launch_bounds__(256) void quant_apply_kernel(const bf16_t* __restri
   }
 }
 
+// One launch instead of the two above: a 1024-thread workgroup per row loads the whole row
+// (16-B pieces of the packed layout, all in flight at once), reduces its absmax in the block and
+// writes the row's e4m3 bytes + scale.  Same scale and rounding as the pair above, bit for bit.
+// The decode rows are few (M <= 64), so the two-phase grid's extra launch and its second read of
+// the activation cost more than the 64-CU width of this one (r2 70B profile: 4.8 + 5.3 us per
+// site for the pair).
+template <int MAXC>
+__global__ __launch_bounds__(1024) void quant_row_kernel(const bf16_t* __restrict__ ap, uint8_t* __restrict__ a8,
+                                                        float* __restrict__ scale, int K, int MT) {
+  __shared__ float red[16];
+  const int row = blockIdx.x, tid = threadIdx.x;
+  const int nc = K >> 3;  // 8-element pieces of the row
+  const int mt = row >> 4, r16 = row & 15;
+  u16x8 v[MAXC];
+#pragma unroll
+  for (int j = 0; j < MAXC; ++j) {
+    const int i = min(tid + 1024 * j, nc - 1);  // piece i = k-slice i / 4, quarter i % 4
+    v[j] = *reinterpret_cast<const u16x8*>(ap + apk_off(row, i * 8, MT));
+  }
+  float m = 0.f;
+#pragma unroll
+  for (int j = 0; j < MAXC; ++j)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) m = fmaxf(m, fabsf(bf2f(v[j][e])));
+  m = block_max(m, red);
+  const float sc = m > 0.f ? m * (1.f / 448.f) : 1.f;
+  const float inv = 1.f / sc;
+  if (tid == 0) scale[row] = sc;
+#pragma unroll
+  for (int j = 0; j < MAXC; ++j) {
+    const int i = tid + 1024 * j;
+    if (i < nc) {
+      float f[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] = fminf(fmaxf(bf2f(v[j][e]) * inv, -448.f), 448.f);
+      int2 o;
+      o.x = pack4_fp8(f[0], f[1], f[2], f[3]);
+      o.y = pack4_fp8(f[4], f[5], f[6], f[7]);
+      const int sl = i >> 2, q = i & 3;
+      *reinterpret_cast<int2*>(a8 + (((int64_t)(sl >> 1) * MT + mt) * 64 + q * 16 + r16) * 16 + (sl & 1) * 8) = o;
+    }
+  }
+}
+
+// Row-major bf16 x[M, K] (stride xs) -> fp8 A8 + row scales, one 1024-thread workgroup per row.
+// The fp8 decode path has its producers (attention, the gate/up SwiGLU epilogue) write row-major
+// activations for this kernel: a row is one contiguous run (coalesced 16-B loads; the packed
+// layout scatters a row over 16-B pieces 256 B apart, and the packed-input kernel above spends
+// ~10 us per 28672-wide row set on that), and each thread writes one whole 16-B A8 lane slot
+// (k 64c + 8q .. +7 and 64c + 32 + 8q .. +7 of its row).
+template <int MAXC>
+__global__ __launch_bounds__(1024) void quant_rows_kernel(const bf16_t* __restrict__ x, int64_t xs,
+                                                         uint8_t* __restrict__ a8, float* __restrict__ scale, int K,
+                                                         int MT) {
+  __shared__ float red[16];
+  const int row = blockIdx.x, tid = threadIdx.x;
+  const int np = K >> 4;  // (64-k chunk, quarter) pieces: 2 x 8 elements each
+  const bf16_t* xr = x + (int64_t)row * xs;
+  u16x8 v0[MAXC], v1[MAXC];
+#pragma unroll
+  for (int j = 0; j < MAXC; ++j) {
+    const int p = min(tid + 1024 * j, np - 1), c = p >> 2, q = p & 3;
+    v0[j] = *reinterpret_cast<const u16x8*>(xr + c * 64 + q * 8);
+    v1[j] = *reinterpret_cast<const u16x8*>(xr + c * 64 + 32 + q * 8);
+  }
+  float m = 0.f;
+#pragma unroll
+  for (int j = 0; j < MAXC; ++j)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) m = fmaxf(m, fmaxf(fabsf(bf2f(v0[j][e])), fabsf(bf2f(v1[j][e]))));
+  m = block_max(m, red);
+  const float sc = m > 0.f ? m * (1.f / 448.f) : 1.f;
+  const float inv = 1.f / sc;
+  if (tid == 0) scale[row] = sc;
+  const int mt = row >> 4, r16 = row & 15;
+#pragma unroll
+  for (int j = 0; j < MAXC; ++j) {
+    const int p = tid + 1024 * j;
+    if (p < np) {
+      float f[16];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        f[e] = fminf(fmaxf(bf2f(v0[j][e]) * inv, -448.f), 448.f);
+        f[8 + e] = fminf(fmaxf(bf2f(v1[j][e]) * inv, -448.f), 448.f);
+      }
+      int4 o;
+      o.x = pack4_fp8(f[0], f[1], f[2], f[3]);
+      o.y = pack4_fp8(f[4], f[5], f[6], f[7]);
+      o.z = pack4_fp8(f[8], f[9], f[10], f[11]);
+      o.w = pack4_fp8(f[12], f[13], f[14], f[15]);
+      const int c = p >> 2, q = p & 3;
+      *reinterpret_cast<int4*>(a8 + (((int64_t)c * MT + mt) * 64 + q * 16 + r16) * 16) = o;
+    }
+  }
+}
+
 constexpr int F8_GU_MAX = 4;  // 64-k chunks per wave group
 
 template <int MT, int NT, int EPI, bool OPK>
@@ -227,12 +323,19 @@ static int launch_gemm_fp8(const void* a8, const float* as, const void* wq, cons
 constexpr int F8RW_WAVES = 4;
 constexpr int F8RW_QC = 32;  // quads per combine pass (LDS: 4 waves x 32 x 1 KiB)
 
+// ring depth: the largest of 8 / 4 / 2 slots (powers of two divide the per-wave chunk counts
+// of the 70B shapes, 32 and 112) whose operands fit ~200 VGPRs (accumulators sit in AGPRs)
+template <int MT, int NT>
+constexpr int f8rw_depth() {
+  return 4 * (MT + NT) * 8 <= 200 ? 8 : (4 * (MT + NT) * 4 <= 200 ? 4 : 2);
+}
+
 template <int MT, int NT, int EPI, bool OPK>
 __device__ __forceinline__ void f8rw_body(const uint8_t* __restrict__ a8, const float* __restrict__ ascale,
                                           const uint8_t* __restrict__ wq, const float* __restrict__ wscale,
                                           bf16_t* __restrict__ y, int64_t ys, const bf16_t* __restrict__ res,
                                           int64_t rs, int M, int K, int tile0, f32x4* red) {
-  constexpr int R = 2;
+  constexpr int R = f8rw_depth<MT, NT>();
   constexpr int Q = MT * NT;
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int c = lane & 15, q = lane >> 4;
@@ -416,9 +519,36 @@ extern "C" int mp_quant_act_fp8(const void* ap, void* a8, float* scale, float* p
   if (M <= 0) return 0;
   if (K % 64) return -1;
   const int MT = (M + 15) / 16;
+  const int per = (K / 8 + 1023) / 1024;
+  if (per <= 4) {
+    auto launch = [&](auto kern) {
+      hipLaunchKernelGGL(kern, dim3(M), dim3(1024), 0, stream, (const bf16_t*)ap, (uint8_t*)a8, scale, K, MT);
+    };
+    if (per <= 1) launch(quant_row_kernel<1>);
+    else if (per <= 2) launch(quant_row_kernel<2>);
+    else launch(quant_row_kernel<4>);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(quant_absmax_kernel, dim3(MT, Q_NS), dim3(256), 0, stream, (const bf16_t*)ap, part, K, MT);
   hipLaunchKernelGGL(quant_apply_kernel, dim3(MT, Q_NS), dim3(256), 0, stream, (const bf16_t*)ap, part, (uint8_t*)a8,
                      scale, K, MT);
+  return (int)hipGetLastError();
+}
+
+extern "C" int mp_quant_rows_fp8(const void* x, int64_t xs, void* a8, float* scale, int M, int K,
+                                 hipStream_t stream) {
+  using namespace mp;
+  if (M <= 0) return 0;
+  if (K % 64 || xs % 8) return -1;
+  const int MT = (M + 15) / 16;
+  const int per = (K / 16 + 1023) / 1024;
+  auto launch = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(M), dim3(1024), 0, stream, (const bf16_t*)x, xs, (uint8_t*)a8, scale, K, MT);
+  };
+  if (per <= 1) launch(quant_rows_kernel<1>);
+  else if (per <= 2) launch(quant_rows_kernel<2>);
+  else if (per <= 4) launch(quant_rows_kernel<4>);
+  else return -2;
   return (int)hipGetLastError();
 }
 

@@ -468,11 +468,12 @@ class StageExecutor:
             # each GEMM (csrc/fp8.hip); weights stream at 1 byte per parameter
             pk = ops.packed_numel
             xn = e("xn_p", (pk(T, H),))
-            attn = e("attn_p", (pk(T, cfg.q_dim),))
-            act = e("act_p", (pk(T, cfg.intermediate_size),))
+            F = cfg.intermediate_size
+            # row-major: their only reader is the row quantization kernel (coalesced rows)
+            attn = e("attn", (T, cfg.q_dim))
+            act = e("act", (T, F))
             a8 = e("a8", (pk(T, max(H, cfg.q_dim, cfg.intermediate_size)),), torch.uint8)
             asc = e("a8_scale", (((T + 15) // 16) * 16 * 33,), torch.float32)
-            F = cfg.intermediate_size
             # the two norm sites emit fp8 + row scales themselves (norm.hip a8 output): only the
             # attention output and the SwiGLU output still take a separate quantization pass
             for li, L in enumerate(w.layers):
@@ -483,14 +484,14 @@ class StageExecutor:
                                 a8_scale=asc)
                 ops.linear_fp8(a8, asc, L.qkv_q, L.qkv_s, T, out=qkv)
                 kc, vc = self.cache.layer(li)
-                self._rope_attend(qkv, positions, slots, kc, vc, q_seq, q_ctx, attn, ws, ps, np_, True, qblocks,
+                self._rope_attend(qkv, positions, slots, kc, vc, q_seq, q_ctx, attn, ws, ps, np_, False, qblocks,
                                   max_ctx, decode)
-                ops.quant_act_fp8(attn, T, cfg.q_dim, out=a8, scale=asc)
+                ops.quant_rows_fp8(attn, out=a8, scale=asc)
                 ops.linear_fp8(a8, asc, L.o_q, L.o_s, T, out=o)
                 self._ar(o)
                 ops.rmsnorm(o, L.post_norm, eps, out=xn, residual=res, mode=1, packed=True, a8=a8, a8_scale=asc)
-                ops.linear_fp8(a8, asc, L.gate_up_q, L.gate_up_s, T, out=act, epilogue=1, out_packed=True)
-                ops.quant_act_fp8(act, T, F, out=a8, scale=asc)
+                ops.linear_fp8(a8, asc, L.gate_up_q, L.gate_up_s, T, out=act, epilogue=1)
+                ops.quant_rows_fp8(act, out=a8, scale=asc)
                 ops.linear_fp8(a8, asc, L.down_q, L.down_s, T, out=mlp)
                 self._ar(mlp)
         elif prompt is None and self._fused and self._packed_ok(T):

@@ -4,7 +4,7 @@ import torch
 
 from src import ops
 from src.models.config import resolve_model
-from src.models.reference_model import greedy_generate
+from src.models.reference_model import greedy_generate, reference_forward
 from src.models.weights import random_stage_weights
 from src.ops import reference as ref
 from src.runtime.executor import StageExecutor
@@ -90,3 +90,46 @@ def test_rmsnorm_fp8_output_equals_norm_then_quant(M, mode):
     ar = ops.reference.dequant_act_fp8(a8_ref, s_ref, M, H)
     an = ops.reference.dequant_act_fp8(a8, sc, M, H)
     assert torch.equal(ar, an)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("graphs", [False, True])
+def test_fp8_executor_gpu_decode_tracks_dequantized_oracle(graphs):
+    """The GPU fp8 decode path (norm-emitted fp8, row-major attention / SwiGLU outputs through
+    the row quantization kernel, balanced-ring fp8 GEMMs at 17 rows, one-group at 1 row) stays
+    within the W8A8 error budget of the fp32 oracle on the dequantized weights, with and without
+    hipGraphs (which must agree bit for bit with each other)."""
+    cfg = resolve_model("small-llama")
+    L = cfg.num_hidden_layers
+    w = random_stage_weights(cfg, 0, L, has_embed=True, has_head=True, device="cuda", seed=5)
+    wd = random_stage_weights(cfg, 0, L, has_embed=True, has_head=True, device="cuda", seed=5, dtype=torch.float32)
+    w.quantize_fp8(drop_dense=True)
+    for Lq, Ld in zip(w.layers, wd.layers):
+        for name in Lq.PROJ:
+            setattr(Ld, name, Lq.dense(name, torch.float32))
+    gen = torch.Generator().manual_seed(7)
+    outs = {}
+    for g in sorted({False, graphs}):
+        ex = StageExecutor(cfg, w, "cuda", kv_cache_bytes=64 << 20, max_sessions=32, max_seq_len=128, use_graphs=g)
+        assert ex._fp8_ok(17)
+        n = 17
+        prompts = [torch.randint(0, cfg.vocab_size, (5 + i % 7,), generator=torch.Generator().manual_seed(i))
+                   for i in range(n)]
+        seqs = [(f"s{i}", len(p)) for i, p in enumerate(prompts)]
+        ex.forward(seqs, torch.cat(prompts).cuda(), reset=[True] * n)
+        cur = [p.clone() for p in prompts]
+        steps = []
+        for _ in range(3):
+            tok = torch.tensor([int(c[-1]) * 7 % cfg.vocab_size for c in cur])
+            cur = [torch.cat([c, tok[i:i + 1]]) for i, c in enumerate(cur)]
+            steps.append(ex.forward([(s, 1) for s, _ in seqs], tok.cuda()).float())
+        outs[g] = (steps, cur)
+    steps, cur = outs[graphs]
+    if graphs:
+        for a, b in zip(outs[False][0], steps):
+            assert torch.equal(a, b)
+    for i in (0, 5, 16):
+        ref_logits = reference_forward([wd], cur[i].cuda())[-1].float()
+        got = steps[-1][i]
+        cos = torch.nn.functional.cosine_similarity(got, ref_logits, dim=0)
+        assert float(cos) > 0.99, (i, float(cos))

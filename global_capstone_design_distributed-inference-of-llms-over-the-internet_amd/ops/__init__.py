@@ -510,8 +510,25 @@ def sample(logits, temps, top_ps, top_ks, rep_pens, recent, recent_len, seeds, w
     return out
 
 
-def native_gemm_ok(M: int, N: int, K: int, epilogue: int = 0) -> bool:
-    return 0 < M <= 64 and K % 128 == 0 and N % (32 if epilogue == 1 else 16) == 0
+_RW_OK = {}
+
+
+def wide_gemm_ok(M: int, N: int, K: int, epilogue: int = 0, out_packed: bool = False) -> bool:
+    """65..128 decode rows: the balanced ring kernel covers (packed A; epilogue 0 or packed SwiGLU,
+    the widths it is built for)."""
+    key = (M, N, K, int(epilogue), bool(out_packed))
+    if key not in _RW_OK:
+        _RW_OK[key] = bool(native_available() and
+                           torch.ops.mpamd.gemm_rw_ok(int(M), int(N), int(K), int(epilogue), int(bool(out_packed))))
+    return _RW_OK[key]
+
+
+def native_gemm_ok(M: int, N: int, K: int, epilogue: int = 0, out_packed: bool = False) -> bool:
+    if not (K % 128 == 0 and N % (32 if epilogue == 1 else 16) == 0):
+        return False
+    if 64 < M <= 128:
+        return wide_gemm_ok(M, N, K, epilogue, out_packed)
+    return 0 < M <= 64
 
 
 def pack_weight(w: torch.Tensor) -> torch.Tensor:
@@ -554,7 +571,7 @@ def linear(x, w, out=None, epilogue=0, residual=None, policy=None, wp=None, a_ro
         M, K = x.shape
     N = w.shape[0] if w is not None else 16 * wp.shape[0]
     policy = policy or _GEMM_POLICY
-    ok = wp is not None and native_gemm_ok(M, N, K, epilogue) and (
+    ok = wp is not None and native_gemm_ok(M, N, K, epilogue, out_packed) and (
         a_rows is not None or (x.stride(0) % 8 == 0 and x.stride(1) == 1))
     if ok and (policy in ("auto", "native") or a_rows is not None or out_packed):
         ncols = N // 2 if epilogue == 1 else N
@@ -563,7 +580,7 @@ def linear(x, w, out=None, epilogue=0, residual=None, policy=None, wp=None, a_ro
         if out is None:
             out = (torch.empty(packed_numel(M, ncols), dtype=x.dtype, device=x.device) if out_packed
                    else torch.empty(M, ncols, dtype=x.dtype, device=x.device))
-        kern = "pk" if gate is not None else _kernel_for(M, N, K, epilogue)
+        kern = "pk" if gate is not None else ("rw" if M > 64 else _kernel_for(M, N, K, epilogue))
         flags = 1 | (2 if out_packed else 0) | _KERNEL_FLAGS[kern]
         ws = gemm_workspace(x.device) if kern == "sk" else None
         torch.ops.mpamd.gemm(x, wp, out, residual, int(epilogue), M, flags, ws, gate, ap_out, ss_out, ss_zero, ss_in,
@@ -642,13 +659,66 @@ def quant_rows_fp8(x: torch.Tensor, out=None, scale=None):
 
 
 _FP8_KERNELS = {"pk": 0, "rw": 1}
+_FP8_CHOICE = {}  # (m_bucket, N, K, epilogue) -> fp8 kernel name, from autotune_fp8
+_FP8_MODE = "auto"
 
 
 def set_fp8_kernel(name: str) -> None:
-    """fp8 decode GEMM form (csrc/fp8.hip): "rw" (balanced ring, default, M > 16) or "pk"
-    (one-group-per-workgroup) - for A/B measurements and tests."""
+    """fp8 decode GEMM form (csrc/fp8.hip): "auto" (autotuned table, else the balanced ring),
+    "rw" (balanced ring, M > 16) or "pk" (one-group-per-workgroup) everywhere."""
+    global _FP8_MODE
+    assert name == "auto" or name in _FP8_KERNELS
+    _FP8_MODE = name
+
+
+def _fp8_kind(M: int, N: int, K: int, epilogue: int) -> int:
+    if _FP8_MODE != "auto":
+        return _FP8_KERNELS[_FP8_MODE]
+    name = _FP8_CHOICE.get((_m_bucket(M), N, K, int(epilogue)))
+    return -1 if name is None else _FP8_KERNELS[name]
+
+
+def autotune_fp8(shapes, device, ms=(32, 48, 64), iters: int = 12, rounds: int = 3) -> dict:
+    """``autotune_gemm`` for the fp8 GEMM: time both forms on each (N, K, epilogue) per M bucket
+    (M <= 16 always runs the one-group form) on weights rotated over ~1 GiB, keep the faster."""
+    global _FP8_MODE
+    device = torch.device(device)
+    if device.type != "cuda":
+        return {}
     require_native()
-    torch.ops.mpamd.fp8_gemm_kernel(_FP8_KERNELS[name])
+    saved = _FP8_MODE
+    try:
+        for (N, K, epi) in shapes:
+            todo = [M for M in ms if (_m_bucket(M), N, K, int(epi)) not in _FP8_CHOICE]
+            if not todo:
+                continue
+            copies = max(1, min(8, (1 << 30) // (N * K)))
+            wqs = [torch.randint(0, 0x77, (N // 16, K // 64, 64, 16), dtype=torch.uint8, device=device)
+                   for _ in range(copies)]
+            wsc = torch.full((N,), 1e-3, dtype=torch.float32, device=device)
+            ncols = N // 2 if epi == 1 else N
+            for M in todo:
+                a8 = torch.randint(0, 0x77, (packed_numel(M, K),), dtype=torch.uint8, device=device)
+                asc = torch.ones(((M + 15) // 16) * 16, dtype=torch.float32, device=device)
+                out = torch.empty(M, ncols, dtype=torch.bfloat16, device=device)
+                t = {k: float("inf") for k in _FP8_KERNELS}
+                for _ in range(rounds):
+                    for name in _FP8_KERNELS:
+                        _FP8_MODE = name
+                        for i in range(2):
+                            linear_fp8(a8, asc, wqs[i % copies], wsc, M, out=out, epilogue=epi)
+                        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                        e0.record()
+                        for i in range(iters):
+                            linear_fp8(a8, asc, wqs[i % copies], wsc, M, out=out, epilogue=epi)
+                        e1.record()
+                        e1.synchronize()
+                        t[name] = min(t[name], e0.elapsed_time(e1) / iters)
+                _FP8_CHOICE[(_m_bucket(M), N, K, int(epi))] = min(t, key=t.get)
+            del wqs
+    finally:
+        _FP8_MODE = saved
+    return dict(_FP8_CHOICE)
 
 
 def linear_fp8(a8, a_scale, wq, w_scale, M: int, out=None, epilogue: int = 0, residual=None,
@@ -667,5 +737,6 @@ def linear_fp8(a8, a_scale, wq, w_scale, M: int, out=None, epilogue: int = 0, re
     if out is None:
         out = (torch.empty(packed_numel(M, ncols), dtype=torch.bfloat16, device=a8.device) if out_packed
                else torch.empty(M, ncols, dtype=torch.bfloat16, device=a8.device))
-    torch.ops.mpamd.gemm_fp8(a8, a_scale, wq, w_scale, out, residual, int(epilogue), int(M), int(bool(out_packed)))
+    torch.ops.mpamd.gemm_fp8(a8, a_scale, wq, w_scale, out, residual, int(epilogue), int(M), int(bool(out_packed)),
+                             _fp8_kind(M, N, 64 * wq.shape[1], epilogue))
     return out

@@ -38,8 +38,9 @@ int mp_attention_mfma(const void* q, int64_t q_stride, const void* kc, const voi
                       const int64_t* slots, hipStream_t stream);
 int mp_quant_act_fp8(const void* ap, void* a8, float* scale, float* part, int M, int K, hipStream_t stream);
 int mp_gemm_fp8(const void* a8, const float* as, const void* wq, const float* ws, void* y, int64_t ys, const void* res,
-                int64_t rs, int M, int N, int K, int epilogue, int out_packed, hipStream_t stream);
+                int64_t rs, int M, int N, int K, int epilogue, int out_packed, int kind, hipStream_t stream);
 void mp_fp8_set_kernel(int kind);
+int mp_gemm_rw_ok(int M, int N, int K, int epilogue, int out_packed);
 int mp_quant_rows_fp8(const void* x, int64_t xs, void* a8, float* scale, int M, int K, hipStream_t stream);
 int mp_gemm_bf16(const void* x, int64_t x_stride, const void* w, void* y, int64_t y_stride, const void* res,
                  int64_t res_stride, int M, int N, int K, int epilogue, int flags, void* ws, const int* gate,
@@ -452,6 +453,9 @@ at::Tensor pack_weight(const at::Tensor& w) {
 
 int64_t gemm_workspace_bytes() { return mp_gemm_workspace_bytes(); }
 void fp8_gemm_kernel(int64_t kind) { mp_fp8_set_kernel((int)kind); }
+bool gemm_rw_ok(int64_t M, int64_t N, int64_t K, int64_t epilogue, int64_t out_packed) {
+  return mp_gemm_rw_ok((int)M, (int)N, (int)K, (int)epilogue, (int)out_packed) != 0;
+}
 
 // packed bf16 decode activation (M rows) -> fp8 A8 [K/64][MT][64][16] (uint8) + row scales (fp32, >= MT*16)
 void quant_act_fp8(const at::Tensor& ap, at::Tensor& a8, at::Tensor& scale, int64_t M, int64_t K) {
@@ -484,7 +488,8 @@ void quant_rows_fp8(const at::Tensor& x, at::Tensor& a8, at::Tensor& scale) {
 
 // y = epilogue((a8 * as) . (wq * ws)^T); wq: [N/16, K/64, 64, 16] uint8 (ops.pack_weight_fp8)
 void gemm_fp8(const at::Tensor& a8, const at::Tensor& as, const at::Tensor& wq, const at::Tensor& ws, at::Tensor& y,
-              const c10::optional<at::Tensor>& residual, int64_t epilogue, int64_t M, int64_t out_packed) {
+              const c10::optional<at::Tensor>& residual, int64_t epilogue, int64_t M, int64_t out_packed,
+              int64_t kind) {
   MP_CHECK(wq.is_cuda() && wq.scalar_type() == at::kByte && wq.dim() == 4 && wq.size(2) == 64 && wq.size(3) == 16 &&
                wq.is_contiguous(),
            "wq must be a packed fp8 weight [N/16, K/64, 64, 16]");
@@ -511,7 +516,7 @@ void gemm_fp8(const at::Tensor& a8, const at::Tensor& as, const at::Tensor& wq, 
   MP_CHECK(epilogue != 2 || rp != nullptr, "residual epilogue needs residual");
   check_launch(mp_gemm_fp8(a8.data_ptr(), as.data_ptr<float>(), wq.data_ptr(), ws.data_ptr<float>(), y.data_ptr(),
                            out_packed ? 0 : y.stride(0), rp, rs, (int)M, N, K, (int)epilogue, (int)out_packed,
-                           cur_stream()),
+                           (int)kind, cur_stream()),
                "gemm_fp8");
 }
 
@@ -520,6 +525,7 @@ void gemm_fp8(const at::Tensor& a8, const at::Tensor& as, const at::Tensor& wq, 
 TORCH_LIBRARY(mpamd, m) {
   m.def("gemm_workspace_bytes() -> int", &gemm_workspace_bytes);
   m.def("fp8_gemm_kernel(int kind) -> ()", &fp8_gemm_kernel);
+  m.def("gemm_rw_ok(int M, int N, int K, int epilogue, int out_packed) -> bool", &gemm_rw_ok);
   m.def(
       "rmsnorm(Tensor x, Tensor(a!) residual, Tensor w, Tensor(b!) y, float eps, int mode, Tensor? rows, "
       "int packed, Tensor(c!)? ss=None, Tensor(d!)? a8=None, Tensor(e!)? a8_scale=None) -> ()");
@@ -560,7 +566,7 @@ TORCH_LIBRARY(mpamd, m) {
   m.def("quant_rows_fp8(Tensor x, Tensor(a!) a8, Tensor(b!) scale) -> ()");
   m.def(
       "gemm_fp8(Tensor a8, Tensor a_scale, Tensor wq, Tensor w_scale, Tensor(a!) y, Tensor? residual, int epilogue, "
-      "int M, int out_packed) -> ()");
+      "int M, int out_packed, int kind=-1) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(mpamd, CUDA, m) {

@@ -321,6 +321,10 @@ static int launch_gemm_fp8(const void* a8, const float* as, const void* wq, cons
 // residual epilogue runs.  The one-group kernel above gives the 70B gate/up (3584 tiles) 1792
 // two-tile workgroups in 7 rounds over the CUs; here each CU streams its 7 pairs in one go.
 constexpr int F8RW_WAVES = 4;
+// A-fragment load; scripts/fp8_lab.hip overrides it to ablate the activation stream
+#ifndef MP_F8_LOAD_A
+#define MP_F8_LOAD_A(p) (*reinterpret_cast<const u16x8*>(p))
+#endif
 constexpr int F8RW_QC = 32;  // quads per combine pass (LDS: 4 waves x 32 x 1 KiB)
 
 // ring depth: the largest of 8 / 4 / 2 slots (powers of two divide the per-wave chunk counts
@@ -355,7 +359,7 @@ __device__ __forceinline__ void f8rw_body(const uint8_t* __restrict__ a8, const 
     _Pragma("unroll") for (int t = 0; t < NT; ++t) rb[s][t] =                                                \
         __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(wb + ((int64_t)t * nch + k_) * 1024));    \
     _Pragma("unroll") for (int mt = 0; mt < MT; ++mt) ra[s][mt] =                                            \
-        *reinterpret_cast<const u16x8*>(ab + ((int64_t)k_ * MT + mt) * 1024);                                \
+        MP_F8_LOAD_A(ab + ((int64_t)k_ * MT + mt) * 1024);                                                   \
   }
 #pragma unroll
   for (int s = 0; s < R; ++s) F8RW_LOAD(s, s)
@@ -553,14 +557,15 @@ extern "C" int mp_quant_rows_fp8(const void* x, int64_t xs, void* a8, float* sca
 }
 
 // a8/as: quant_act_fp8 output for M rows; wq/ws: pack_weight_fp8 output for W[N, K].
+// kind: 0 = one-group kernel, 1 = balanced ring kernel (M > 16), -1 = the start-up default
 extern "C" int mp_gemm_fp8(const void* a8, const float* as, const void* wq, const float* ws, void* y, int64_t ys,
-                           const void* res, int64_t rs, int M, int N, int K, int epilogue, int out_packed,
+                           const void* res, int64_t rs, int M, int N, int K, int epilogue, int out_packed, int kind,
                            hipStream_t stream) {
   using namespace mp;
   if (M == 0) return 0;
   if (M > 64 || K % (64 * F8_GU_MAX) || N % 16) return -1;
   int rc;
-  if (g_fp8_kernel == 1 && M > 16) {
+  if ((kind < 0 ? g_fp8_kernel : kind) == 1 && M > 16) {
     if (M <= 32) rc = launch_gemm_fp8_rw<2>(a8, as, wq, ws, y, ys, res, rs, M, N, K, epilogue, out_packed, stream);
     else if (M <= 48) rc = launch_gemm_fp8_rw<3>(a8, as, wq, ws, y, ys, res, rs, M, N, K, epilogue, out_packed, stream);
     else rc = launch_gemm_fp8_rw<4>(a8, as, wq, ws, y, ys, res, rs, M, N, K, epilogue, out_packed, stream);

@@ -883,6 +883,7 @@ static int launch_gemm_sk(const void* x, void* y, int64_t ys, const void* w, con
 // and their MFMAs skipped), then the 4 partial tiles are summed through LDS and the shared
 // epilogues run (row scale, SwiGLU, residual, the fused-norm producer).
 constexpr int RW_WAVES = 4;
+constexpr int RW_QC = 32;  // quads per LDS combine pass (4 waves x 32 x 1 KiB = 128 KiB)
 
 // Ring slots: a power of two (K / 32 / 4 waves is a multiple of it at K = 4096, 11008: no
 // clamped tail turn); 4 (MT + NT) VGPRs each (one wave per SIMD: the accumulators go to AGPRs).
@@ -950,27 +951,32 @@ __device__ __forceinline__ void rw_body(const bf16_t* __restrict__ x, const bf16
     }
   }
 #undef RW_LOAD
-  // ---- sum the 4 waves' partial tiles through LDS, then the epilogue ----
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-    for (int t = 0; t < NT; ++t) red[(wid * Q + mt * NT + t) * 64 + lane] = acc[mt][t];
-  __syncthreads();
+  // ---- sum the 4 waves' partial tiles through LDS (passes of at most RW_QC quads: 128-row
+  //      workgroups own up to 48), then the epilogue ----
   rsc.finish(ep, rs_part, rs_lds);
+  constexpr int QC = Q < RW_QC ? Q : RW_QC;
 #pragma unroll
-  for (int j = 0; j < NQ; ++j) {
-    const int qd = wid + RW_WAVES * j;
-    if (qd >= Q) break;
-    if (EPI == 1 && (qd % NT) & 1) continue;  // up tile: consumed with its gate tile
-    f32x4 v = red[qd * 64 + lane], up = (f32x4)(0.f);
+  for (int p0 = 0; p0 < Q; p0 += QC) {
+    if (p0 > 0) __syncthreads();  // the previous pass has finished reading red
 #pragma unroll
-    for (int w = 1; w < RW_WAVES; ++w) v += red[(w * Q + qd) * 64 + lane];
-    if constexpr (EPI == 1) {
+    for (int qd = p0; qd < p0 + QC && qd < Q; ++qd) red[(wid * QC + qd - p0) * 64 + lane] = acc[qd / NT][qd % NT];
+    __syncthreads();
+    // quad qd = wid + 4 j lies in this pass exactly when j does (p0, QC are multiples of 4)
 #pragma unroll
-      for (int w = 0; w < RW_WAVES; ++w) up += red[(w * Q + qd + 1) * 64 + lane];
+    for (int j = p0 / RW_WAVES; j < (p0 + QC) / RW_WAVES && j < NQ; ++j) {
+      const int qd = wid + RW_WAVES * j;
+      if (qd >= Q) break;
+      if (EPI == 1 && (qd % NT) & 1) continue;  // up tile: consumed with its gate tile
+      f32x4 v = red[(qd - p0) * 64 + lane], up = (f32x4)(0.f);
+#pragma unroll
+      for (int w = 1; w < RW_WAVES; ++w) v += red[(w * QC + qd - p0) * 64 + lane];
+      if constexpr (EPI == 1) {
+#pragma unroll
+        for (int w = 0; w < RW_WAVES; ++w) up += red[(w * QC + qd + 1 - p0) * 64 + lane];
+      }
+      tile_epilogue<MT, EPI, OPK>(qd / NT, tile0 + qd % NT, v, up, y, ys, res, rs, M, lane, ep, rs_lds,
+                                  EPI == 3 ? &rpre[j] : nullptr);
     }
-    tile_epilogue<MT, EPI, OPK>(qd / NT, tile0 + qd % NT, v, up, y, ys, res, rs, M, lane, ep, rs_lds,
-                                EPI == 3 ? &rpre[j] : nullptr);
   }
 }
 
@@ -982,7 +988,7 @@ __global__ __launch_bounds__(256) void gemm_rw_kernel(const bf16_t* __restrict__
   clear_other(ep);
   __shared__ u64 rs_part[8][64];
   __shared__ float rs_lds[64];
-  __shared__ __attribute__((aligned(16))) f32x4 red[RW_WAVES * MT * NTB * 64];
+  __shared__ __attribute__((aligned(16))) f32x4 red[RW_WAVES * (MT * NTB < RW_QC ? MT * NTB : RW_QC) * 64];
   const int b = blockIdx.x;
   if (b < n_big) {
     rw_body<MT, NTB, EPI, OPK>(x, wp, y, ys, res, rs, M, K, b * NTB, ep, red, rs_part, rs_lds);
@@ -994,7 +1000,29 @@ __global__ __launch_bounds__(256) void gemm_rw_kernel(const bf16_t* __restrict__
 
 template <int MT, int NTB, int NTS>
 static int launch_gemm_rw_cfg(const void* x, const void* w, void* y, int64_t ys, const void* res, int64_t rs, int M,
-                              int K, int epi, bool opk, int G, int n_big, const EpiArgs& ep, hipStream_t stream) {
+                              int K, int epi, bool opk, int G, int n_big, const EpiArgs& ep, hipStream_t stream,
+                              bool dry) {
+  if constexpr (MT > 4) {
+    // M = 65..128 (the unfused packed decode path at 96 / 128 sessions): plain and packed-SwiGLU
+    // epilogues only, accumulators within 192 AGPRs
+    if constexpr (4 * MT * NTB > 192) {
+      return 1;
+    } else {
+      if (!(epi == 0 || (epi == 1 && opk)) || (epi == 1 && (NTB % 2 || NTS % 2))) return 1;
+      if (dry) return 0;
+      if (epi == 1) {
+        if constexpr (NTB % 2 == 0 && NTS % 2 == 0)
+          hipLaunchKernelGGL((gemm_rw_kernel<MT, NTB, NTS, 1, true>), dim3(G), dim3(256), 0, stream, (const bf16_t*)x,
+                             (const bf16_t*)w, (bf16_t*)y, ys, (const bf16_t*)res, rs, M, K, n_big, ep);
+      } else {
+        hipLaunchKernelGGL((gemm_rw_kernel<MT, NTB, NTS, 0, false>), dim3(G), dim3(256), 0, stream, (const bf16_t*)x,
+                           (const bf16_t*)w, (bf16_t*)y, ys, (const bf16_t*)res, rs, M, K, n_big, ep);
+      }
+      return 0;
+    }
+  } else {
+  if (epi == 1 && (NTB % 2 || NTS % 2)) return 1;
+  if (dry) return 0;
 #define MP_RW(EPI_, OPK_)                                                                                          \
   hipLaunchKernelGGL((gemm_rw_kernel<MT, NTB, NTS, EPI_, OPK_>), dim3(G), dim3(256), 0, stream, (const bf16_t*)x, \
                      (const bf16_t*)w, (bf16_t*)y, ys, (const bf16_t*)res, rs, M, K, n_big, ep)
@@ -1015,13 +1043,14 @@ static int launch_gemm_rw_cfg(const void* x, const void* w, void* y, int64_t ys,
   }
 #undef MP_RW
   return 0;
+  }
 }
 
 // Split the column units (tiles, or gate/up tile pairs) over G = min(#CUs, units) workgroups:
 // n_big of them take ceil, the rest floor.  Returns 1 (caller falls back) for widths not built.
 template <int MT>
 static int launch_gemm_rw(const void* x, const void* w, void* y, int64_t ys, const void* res, int64_t rs, int M,
-                          int N, int K, int epi, int flags, const EpiArgs& ep, hipStream_t stream) {
+                          int N, int K, int epi, int flags, const EpiArgs& ep, hipStream_t stream, bool dry = false) {
   const int step = epi == 1 ? 2 : 1;
   const int units = (N / 16) / step;
   if ((N / 16) % step || units == 0) return 1;
@@ -1030,7 +1059,8 @@ static int launch_gemm_rw(const void* x, const void* w, void* y, int64_t ys, con
   const int ntb = (base + (rem ? 1 : 0)) * step;
   const int n_big = rem ? rem : G;
   const bool opk = flags & 2;
-#define MP_RWC(B_, S_) return launch_gemm_rw_cfg<MT, B_, S_>(x, w, y, ys, res, rs, M, K, epi, opk, G, n_big, ep, stream)
+#define MP_RWC(B_, S_) \
+  return launch_gemm_rw_cfg<MT, B_, S_>(x, w, y, ys, res, rs, M, K, epi, opk, G, n_big, ep, stream, dry)
   if (epi == 1) {
     switch (ntb) {
       case 2: if (rem) return 1; MP_RWC(2, 2);
@@ -1072,6 +1102,21 @@ __global__ __launch_bounds__(256) void pack_weight_kernel(const bf16_t* __restri
 
 extern "C" int mp_gemm_ss_elems() { return mp::SS_NSH * 64; }
 
+// 1 if mp_gemm_bf16 covers a packed-activation decode GEMM of M = 65..128 rows (balanced ring
+// kernel: the widths built, epilogue 0 or packed SwiGLU), else 0.  No launch.
+extern "C" int mp_gemm_rw_ok(int M, int N, int K, int epilogue, int out_packed) {
+  using namespace mp;
+  if (M <= 64 || M > 128 || K % (32 * GU_MAX) || N % 16) return 0;
+  const EpiArgs ep{};
+  const int flags = 1 | (out_packed ? 2 : 0) | 128;
+  int rc;
+  if (M <= 80) rc = launch_gemm_rw<5>(nullptr, nullptr, nullptr, 0, nullptr, 0, M, N, K, epilogue, flags, ep, 0, true);
+  else if (M <= 96) rc = launch_gemm_rw<6>(nullptr, nullptr, nullptr, 0, nullptr, 0, M, N, K, epilogue, flags, ep, 0, true);
+  else if (M <= 112) rc = launch_gemm_rw<7>(nullptr, nullptr, nullptr, 0, nullptr, 0, M, N, K, epilogue, flags, ep, 0, true);
+  else rc = launch_gemm_rw<8>(nullptr, nullptr, nullptr, 0, nullptr, 0, M, N, K, epilogue, flags, ep, 0, true);
+  return rc == 0;
+}
+
 extern "C" int64_t mp_gemm_workspace_bytes() {
   using namespace mp;
   return (int64_t)SK_MAX_GROUPS * sizeof(int) + SK_ZERO_BYTES +
@@ -1093,8 +1138,17 @@ extern "C" int mp_gemm_bf16(const void* x, int64_t x_stride, const void* w, void
   if (M == 0) return 0;
   if (epilogue == 3 && (ap == nullptr || res == nullptr)) return -5;
   const EpiArgs ep{(bf16_t*)ap, (u64*)ss_out, (u64*)ss_zero, (const u64*)ss_in, inv_k, eps, (M + 15) / 16};
-  if (M > 64 || K % (32 * GU_MAX) || N % 16 || ((flags & 1) == 0 && x_stride % 8)) return -1;
+  if (M > 128 || K % (32 * GU_MAX) || N % 16 || ((flags & 1) == 0 && x_stride % 8)) return -1;
   int rc;
+  if (M > 64) {  // 65..128 rows: the balanced ring kernel only (packed A, no gate), or nothing
+    if (!(flags & 1) || gate != nullptr) return -1;
+    if (M <= 80) rc = launch_gemm_rw<5>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, ep, stream);
+    else if (M <= 96) rc = launch_gemm_rw<6>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, ep, stream);
+    else if (M <= 112) rc = launch_gemm_rw<7>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, ep, stream);
+    else rc = launch_gemm_rw<8>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, ep, stream);
+    if (rc != 0) return rc < 0 ? rc : -1;
+    return (int)hipGetLastError();
+  }
   if (gate != nullptr) flags &= ~(4 | 16 | 128);  // gated (MoE expert) GEMMs use the one-group kernel
   if ((flags & 1) && (flags & 128) && !(flags & 8) && M > 16) {  // balanced ring kernel
     if (M <= 32) rc = launch_gemm_rw<2>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, ep, stream);

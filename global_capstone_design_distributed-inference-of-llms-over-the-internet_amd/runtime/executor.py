@@ -203,6 +203,9 @@ class StageExecutor:
                        os.environ.get("MPAMD_FUSED_NORM", "1") != "0" and
                        all(d % 128 == 0 for d in (cfg.hidden_size, cfg.q_dim, cfg.intermediate_size)))
         self._ss = ops.norm_stats_buffer(self.device, 2) if self._fused else None
+        # unit RMSNorm weight for > 64-row decode steps over norm-folded packed weights (made
+        # here, not inside a hipGraph capture)
+        self._ones = torch.ones(cfg.hidden_size, dtype=self.dtype, device=self.device) if self._fused else None
         if self.device.type == "cuda":
             ops.require_native()
             if cfg.model_type != "gpt2" and ops.gemm_policy() != "hipblaslt":
@@ -221,6 +224,9 @@ class StageExecutor:
                     if weights.lm_head_p is not None:
                         shapes.append((16 * weights.lm_head_p.shape[0], H, 0))
                     ops.autotune_gemm(shapes, self.device)
+                    if weights.fp8 and weights.layers:
+                        ops.autotune_fp8([(cfg.q_dim + 2 * cfg.kv_dim, H, 0), (H, cfg.q_dim, 0), (2 * F, H, 1),
+                                          (H, F, 0)], self.device)
         self._streamer, self._n_stream = None, self.n_layers
         if offload and self.device.type == "cuda":
             self._setup_offload(keep_layers_on_gpu)
@@ -494,7 +500,7 @@ class StageExecutor:
                 ops.quant_rows_fp8(act, out=a8, scale=asc)
                 ops.linear_fp8(a8, asc, L.down_q, L.down_s, T, out=mlp)
                 self._ar(mlp)
-        elif prompt is None and self._fused and self._packed_ok(T):
+        elif prompt is None and self._fused and T <= 64 and self._packed_ok(T):
             # fused-norm decode path: 5 launches per layer (qkv, attention, o, gate/up, down).
             # The residual stream r lives row-major in ``res`` and packed in ``xr``; o / down add
             # their product into it in their epilogue and accumulate sum(r^2) per row, and qkv /
@@ -527,17 +533,21 @@ class StageExecutor:
             attn = e("attn_p", (pk(T, cfg.q_dim),))
             act = e("act_p", (pk(T, cfg.intermediate_size),))
             for li, L in self._iter_layers(_PACKED_FIELDS):
+                # weights packed for the fused path (> 64 rows here) carry the norm weights in
+                # their columns: normalise with a unit weight
+                g_in, g_post = (self._unit_norm(), self._unit_norm()) if getattr(L, "folded", False) else \
+                    (L.input_norm, L.post_norm)
                 if li == 0:
-                    ops.rmsnorm(h, L.input_norm, eps, out=xn, residual=res, mode=2, packed=True)
+                    ops.rmsnorm(h, g_in, eps, out=xn, residual=res, mode=2, packed=True)
                 else:
-                    ops.rmsnorm(mlp, L.input_norm, eps, out=xn, residual=res, mode=1, packed=True)
+                    ops.rmsnorm(mlp, g_in, eps, out=xn, residual=res, mode=1, packed=True)
                 ops.linear(xn, L.qkv, out=qkv, wp=L.qkv_p, a_rows=T)
                 kc, vc = self.cache.layer(li)
                 self._rope_attend(qkv, positions, slots, kc, vc, q_seq, q_ctx, attn, ws, ps, np_, True, qblocks,
                                   max_ctx, decode)
                 ops.linear(attn, L.o, out=o, wp=L.o_p, a_rows=T)
                 self._ar(o)
-                ops.rmsnorm(o, L.post_norm, eps, out=xn, residual=res, mode=1, packed=True)
+                ops.rmsnorm(o, g_post, eps, out=xn, residual=res, mode=1, packed=True)
                 if L.moe:
                     self._moe_mlp(L, xn, T, mlp, act, e, packed=True)
                     continue
@@ -583,6 +593,12 @@ class StageExecutor:
             return logits[:, :V]
         fn = ops.rmsnorm(hout, w.final_norm, eps, out=e("fn", (S, H)), rows=last_rows)
         return ops.linear(fn, w.lm_head, out=e("logits", (S, V)))
+
+    def _unit_norm(self) -> torch.Tensor:
+        u = getattr(self, "_ones", None)
+        if u is None:
+            u = self._ones = torch.ones(self.cfg.hidden_size, dtype=self.dtype, device=self.device)
+        return u
 
     def _moe_mlp(self, L, xn, T, mlp, act, e, packed: bool) -> None:
         """Mixtral sparse-MoE MLP into ``mlp`` (ops/moe.py has the routing math and the
@@ -691,14 +707,23 @@ class StageExecutor:
             (cfg.q_dim + 2 * cfg.kv_dim) % 32 == 0
 
     def _packed_ok(self, M: int) -> bool:
-        """Packed-activation decode path: GPU, native GEMM allowed, all projections packed."""
-        if self.device.type != "cuda" or ops.gemm_policy() == "hipblaslt" or not 0 < M <= 64:
+        """Packed-activation decode path: GPU, native GEMM allowed, all projections packed; 65..128
+        rows when the balanced ring kernel covers every projection of the layer (dense Llama)."""
+        if self.device.type != "cuda" or ops.gemm_policy() == "hipblaslt" or not 0 < M <= 128:
             return False
         if getattr(self, "_packed_ready", None) is None:
             cfg = self.cfg
             dims_ok = all(d % 128 == 0 for d in (cfg.hidden_size, cfg.q_dim, cfg.intermediate_size))
             self._packed_ready = dims_ok and all(getattr(L, "qkv_p", None) is not None for L in self.w.layers)
-        return self._packed_ready
+        if not self._packed_ready:
+            return False
+        if M > 64:
+            cfg = self.cfg
+            H, F = cfg.hidden_size, cfg.intermediate_size
+            return not cfg.is_moe and self._tp is None and all(
+                ops.wide_gemm_ok(M, N, K, epi, epi == 1) for N, K, epi in
+                ((cfg.q_dim + 2 * cfg.kv_dim, H, 0), (H, cfg.q_dim, 0), (2 * F, H, 1), (H, F, 0)))
+        return True
 
     # ------------------------------------------------------------------ gpt2 (plumbing family)
     def _forward_gpt2(self, plan: Plan, x, prompt=None):

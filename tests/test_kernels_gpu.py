@@ -405,7 +405,7 @@ def test_fp8_gemm_kernel_matches_reference(kern, M, N, K, epi):
     try:
         _fp8_gemm_case(M, N, K, epi, ref, interleave_gate_up)
     finally:
-        ops.set_fp8_kernel("rw")
+        ops.set_fp8_kernel("auto")
 
 
 def _fp8_gemm_case(M, N, K, epi, ref, interleave_gate_up):
@@ -596,3 +596,62 @@ def test_attention_mfma_rope_fused_matches_two_kernels(nh, nkv, D, parts, packed
     torch.testing.assert_close(o1.float(), o2.float(), atol=2e-2, rtol=2e-2)
     o_ref = ref.paged_attention(q2.float(), k2.float(), v2.float(), bt, q_seq, q_ctx, nh, nkv, scale)
     torch.testing.assert_close(o1.float(), o_ref.float(), atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("M", [65, 96, 113, 128])
+@pytest.mark.parametrize("N,K,epi", [(4096, 4096, 0), (12288, 4096, 0), (4096, 11008, 0), (22016, 4096, 1),
+                                     (1536, 512, 0), (2048, 512, 1)])
+def test_gemm_wide_rows_65_to_128(M, N, K, epi):
+    """65..128 decode rows (96 / 128 sessions) stay on the hand-written balanced ring kernel:
+    plain and packed-SwiGLU epilogues vs fp32 x @ w.T; deterministic."""
+    from src.models.weights import interleave_gate_up
+
+    assert ops.native_gemm_ok(M, N, K, epi, epi == 1)
+    x = bf(torch.randn(M, K, device=DEV))
+    if epi == 1:
+        w = bf(interleave_gate_up(torch.randn(N // 2, K, device=DEV) * 0.02, torch.randn(N // 2, K, device=DEV) * 0.02))
+    else:
+        w = bf(torch.randn(N, K, device=DEV) * 0.02)
+    wp = ops.pack_weight(w)
+    xp = ops.pack_act(x)
+    y1 = ops.linear(xp, None, wp=wp, a_rows=M, epilogue=epi, out_packed=epi == 1)
+    y2 = ops.linear(xp, None, wp=wp, a_rows=M, epilogue=epi, out_packed=epi == 1)
+    torch.cuda.synchronize()
+    if epi == 1:
+        y1, y2 = ops.unpack_act(y1, M, N // 2), ops.unpack_act(y2, M, N // 2)
+    assert torch.equal(y1, y2)
+    yr = x.float() @ w.float().t()
+    if epi == 1:
+        gt = w.view(N // 32, 2, 16, K)
+        g = x.float() @ gt[:, 0].reshape(-1, K).float().t()
+        u = x.float() @ gt[:, 1].reshape(-1, K).float().t()
+        yr = torch.nn.functional.silu(g) * u
+    torch.testing.assert_close(y1.float(), yr, atol=4e-2, rtol=3e-2)
+
+
+def test_executor_wide_decode_batch_packed_path_matches_hipblaslt():
+    """A 80-session decode step takes the packed path (ring kernel at MT = 5) and matches the
+    row-major hipBLASLt path of the same executor weights."""
+    from src.models.config import resolve_model
+    from src.models.weights import random_stage_weights
+    from src.runtime.executor import StageExecutor
+
+    cfg = resolve_model("small-llama")
+    w = random_stage_weights(cfg, 0, cfg.num_hidden_layers, has_embed=True, has_head=True, device=DEV, seed=9)
+    n = 80
+    gen = torch.Generator().manual_seed(1)
+    prompts = [torch.randint(0, cfg.vocab_size, (3 + i % 5,), generator=gen) for i in range(n)]
+    outs = []
+    for policy in ("auto", "hipblaslt"):
+        ops.set_gemm_policy(policy)
+        try:
+            ex = StageExecutor(cfg, w, DEV, kv_cache_bytes=64 << 20, max_sessions=96, max_seq_len=64, use_graphs=False)
+            if policy == "auto":
+                assert ex._packed_ok(n)
+            seqs = [(f"s{i}", len(p)) for i, p in enumerate(prompts)]
+            ex.forward(seqs, torch.cat(prompts).to(DEV), reset=[True] * n)
+            tok = torch.arange(n, device=DEV) % cfg.vocab_size
+            outs.append(ex.forward([(s, 1) for s, _ in seqs], tok).float())
+        finally:
+            ops.set_gemm_policy("auto")
+    torch.testing.assert_close(outs[0], outs[1], atol=0.08, rtol=0.05)

@@ -961,11 +961,12 @@ __device__ __forceinline__ void rw_body(const bf16_t* __restrict__ x, const bf16
 #pragma unroll
     for (int qd = p0; qd < p0 + QC && qd < Q; ++qd) red[(wid * QC + qd - p0) * 64 + lane] = acc[qd / NT][qd % NT];
     __syncthreads();
-    // quad qd = wid + 4 j lies in this pass exactly when j does (p0, QC are multiples of 4)
+    // quad qd = wid + 4 j lies in this pass exactly when j does (with several passes p0 and QC
+    // are multiples of 4; a single pass has QC = Q)
 #pragma unroll
-    for (int j = p0 / RW_WAVES; j < (p0 + QC) / RW_WAVES && j < NQ; ++j) {
+    for (int j = p0 / RW_WAVES; j < (p0 + QC + RW_WAVES - 1) / RW_WAVES && j < NQ; ++j) {
       const int qd = wid + RW_WAVES * j;
-      if (qd >= Q) break;
+      if (qd >= Q || qd >= p0 + QC) break;
       if (EPI == 1 && (qd % NT) & 1) continue;  // up tile: consumed with its gate tile
       f32x4 v = red[(qd - p0) * 64 + lane], up = (f32x4)(0.f);
 #pragma unroll

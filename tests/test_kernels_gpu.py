@@ -645,7 +645,7 @@ def test_executor_wide_decode_batch_packed_path_matches_hipblaslt():
     for policy in ("auto", "hipblaslt"):
         ops.set_gemm_policy(policy)
         try:
-            ex = StageExecutor(cfg, w, DEV, kv_cache_bytes=64 << 20, max_sessions=96, max_seq_len=64, use_graphs=False)
+            ex = StageExecutor(cfg, w, DEV, kv_cache_bytes=512 << 20, max_sessions=96, max_seq_len=64, use_graphs=False)
             if policy == "auto":
                 assert ex._packed_ok(n)
             seqs = [(f"s{i}", len(p)) for i, p in enumerate(prompts)]

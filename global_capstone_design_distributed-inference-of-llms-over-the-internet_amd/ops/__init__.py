@@ -400,6 +400,31 @@ def attention_mfma_rope(qkv, k_cache, v_cache, block_tables, q_seq, q_ctx, qbloc
     return out
 
 
+_ATTN_CNT = {}
+
+
+def attention_counters(device) -> torch.Tensor:
+    """Per-device zeroed int32 arrival counters of the flash-decoding kernel's in-launch split-K
+    combine (csrc/attention.hip split_combine): one per (query, head group) of a step; the
+    last-arriving slice re-zeroes its counter.  Steps with more (query, group) pairs than this
+    holds fall back to the separate reduce launch.  Call before a hipGraph capture."""
+    device = torch.device(device)
+    key = (device.type, device.index if device.index is not None else torch.cuda.current_device())
+    c = _ATTN_CNT.get(key)
+    if c is None:
+        c = _ATTN_CNT[key] = torch.zeros(1 << 16, dtype=torch.int32, device=device)
+    return c
+
+
+def _attn_cnt(device):
+    # off by default: measured at batch 1 (Llama-2-7B, 1 MI355X) 2.984 ms/step with the in-launch
+    # combine vs 2.921 with the separate reduce launch - the release / ticket / acquire chain of
+    # the last-arriving slice costs more than the launch it removes (profiles/r2_attn_combine)
+    if os.environ.get("MPAMD_ATTN_INLAUNCH_REDUCE", "0") == "0":
+        return None
+    return attention_counters(device)
+
+
 def attention_workspace(num_queries: int, nh: int, head_dim: int, num_parts: int, device) -> torch.Tensor:
     return torch.empty(max(1, num_queries * nh * num_parts * (head_dim + 2)), dtype=torch.float32, device=device)
 
@@ -422,7 +447,7 @@ def paged_attention(q, k_cache, v_cache, block_tables, q_seq, q_ctx, nh, nkv, sc
     if workspace is None:
         workspace = attention_workspace(T, nh, D, num_parts, q.device)
     torch.ops.mpamd.paged_attention(q, k_cache, v_cache, block_tables, q_seq, q_ctx, out, workspace, int(nh), int(nkv),
-                                    float(scale), int(part_size), int(num_parts), int(bool(packed)))
+                                    float(scale), int(part_size), int(num_parts), int(bool(packed)), _attn_cnt(q.device))
     return out
 
 
@@ -451,7 +476,7 @@ def paged_attention_rope(qkv, k_cache, v_cache, block_tables, q_seq, q_ctx, posi
         workspace = attention_workspace(T, nh, D, num_parts, qkv.device)
     torch.ops.mpamd.paged_attention_rope(qkv, k_cache, v_cache, block_tables, q_seq, q_ctx, positions, cos, sin,
                                          slots, out, workspace, int(nh), int(nkv), float(scale), int(part_size),
-                                         int(num_parts), int(bool(packed)))
+                                         int(num_parts), int(bool(packed)), _attn_cnt(qkv.device))
     return out
 
 

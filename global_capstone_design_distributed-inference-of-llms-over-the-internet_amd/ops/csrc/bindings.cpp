@@ -22,7 +22,7 @@ int mp_paged_attention(const void* q, int64_t q_stride, const void* kc, const vo
                        int bt_stride, const int32_t* q_seq, const int32_t* q_ctx, void* out, float* workspace, int T,
                        int nh, int nkv, int D, int page_size, int PS, int NP, float scale, int packed_mt,
                        const int64_t* rope_pos, const float* cos_t, const float* sin_t, const int64_t* slots,
-                       hipStream_t stream);
+                       int* counters, int n_counters, hipStream_t stream);
 int mp_embedding(const int64_t* ids, const void* table, void* out, int T, int H, int64_t vocab, hipStream_t stream);
 int mp_swiglu(const void* gu, void* out, int64_t T, int F, hipStream_t stream);
 int mp_add(const void* a, const void* b, void* y, int64_t n, hipStream_t stream);
@@ -178,7 +178,8 @@ static void paged_attention_impl(const at::Tensor& q, const at::Tensor& k_cache,
                                  const at::Tensor& block_tables, const at::Tensor& q_seq, const at::Tensor& q_ctx,
                                  at::Tensor& out, at::Tensor& workspace, int64_t nh, int64_t nkv, double scale,
                                  int64_t part_size, int64_t num_parts, int64_t packed, const int64_t* rope_pos,
-                                 const float* cos_t, const float* sin_t, const int64_t* slots) {
+                                 const float* cos_t, const float* sin_t, const int64_t* slots,
+                                 const c10::optional<at::Tensor>& counters) {
   check_bf16_cuda(q, "q");
   check_rows(q, "q");
   check_bf16_cuda(out, "out");
@@ -198,20 +199,29 @@ static void paged_attention_impl(const at::Tensor& q, const at::Tensor& k_cache,
   MP_CHECK(q_ctx.scalar_type() == at::kInt && q_ctx.numel() == T, "q_ctx");
   MP_CHECK(workspace.scalar_type() == at::kFloat, "workspace fp32");
   if (num_parts > 1) MP_CHECK(workspace.numel() >= (int64_t)T * nh * num_parts * (D + 2), "workspace too small");
+  int* cp = nullptr;
+  int ncnt = 0;
+  if (counters.has_value()) {
+    MP_CHECK(counters->is_cuda() && counters->scalar_type() == at::kInt && counters->is_contiguous(),
+             "counters: zero-initialised cuda int32");
+    cp = counters->data_ptr<int32_t>();
+    ncnt = (int)counters->numel();
+  }
   check_launch(mp_paged_attention(q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
                                   block_tables.data_ptr<int32_t>(), block_tables.stride(0), q_seq.data_ptr<int32_t>(),
                                   q_ctx.data_ptr<int32_t>(), out.data_ptr(), workspace.data_ptr<float>(), T, nh, nkv,
                                   D, k_cache.size(2), part_size, num_parts, (float)scale,
-                                  packed ? (int)((T + 15) / 16) : 0, rope_pos, cos_t, sin_t, slots, cur_stream()),
+                                  packed ? (int)((T + 15) / 16) : 0, rope_pos, cos_t, sin_t, slots, cp, ncnt,
+                                  cur_stream()),
                "paged_attention");
 }
 
 void paged_attention(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
                      const at::Tensor& block_tables, const at::Tensor& q_seq, const at::Tensor& q_ctx,
                      at::Tensor& out, at::Tensor& workspace, int64_t nh, int64_t nkv, double scale, int64_t part_size,
-                     int64_t num_parts, int64_t packed) {
+                     int64_t num_parts, int64_t packed, const c10::optional<at::Tensor>& counters) {
   paged_attention_impl(q, k_cache, v_cache, block_tables, q_seq, q_ctx, out, workspace, nh, nkv, scale, part_size,
-                       num_parts, packed, nullptr, nullptr, nullptr, nullptr);
+                       num_parts, packed, nullptr, nullptr, nullptr, nullptr, counters);
 }
 
 // Decode attention with RoPE + KV write fused in (attention.hip ROPE path): q is the unrotated
@@ -220,7 +230,8 @@ void paged_attention_rope(const at::Tensor& qkv, at::Tensor& k_cache, at::Tensor
                           const at::Tensor& block_tables, const at::Tensor& q_seq, const at::Tensor& q_ctx,
                           const at::Tensor& positions, const at::Tensor& cos, const at::Tensor& sin,
                           const at::Tensor& slots, at::Tensor& out, at::Tensor& workspace, int64_t nh, int64_t nkv,
-                          double scale, int64_t part_size, int64_t num_parts, int64_t packed) {
+                          double scale, int64_t part_size, int64_t num_parts, int64_t packed,
+                          const c10::optional<at::Tensor>& counters) {
   check_bf16_cuda(k_cache, "k_cache");
   check_bf16_cuda(v_cache, "v_cache");
   MP_CHECK(k_cache.dim() == 4 && k_cache.sizes() == v_cache.sizes(), "cache [pages, nkv, page, D]");
@@ -234,7 +245,7 @@ void paged_attention_rope(const at::Tensor& qkv, at::Tensor& k_cache, at::Tensor
   MP_CHECK(D % 16 == 0, "head dim");
   paged_attention_impl(qkv, k_cache, v_cache, block_tables, q_seq, q_ctx, out, workspace, nh, nkv, scale, part_size,
                        num_parts, packed, positions.data_ptr<int64_t>(), cos.data_ptr<float>(), sin.data_ptr<float>(),
-                       slots.data_ptr<int64_t>());
+                       slots.data_ptr<int64_t>(), counters);
 }
 
 static void attention_mfma_impl(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
@@ -536,11 +547,11 @@ TORCH_LIBRARY(mpamd, m) {
   m.def(
       "paged_attention(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor q_seq, Tensor q_ctx, "
       "Tensor(a!) out, Tensor(b!) workspace, int nh, int nkv, float scale, int part_size, int num_parts, "
-      "int packed) -> ()");
+      "int packed, Tensor(c!)? counters=None) -> ()");
   m.def(
       "paged_attention_rope(Tensor qkv, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor block_tables, Tensor q_seq, "
       "Tensor q_ctx, Tensor positions, Tensor cos, Tensor sin, Tensor slots, Tensor(c!) out, Tensor(d!) workspace, "
-      "int nh, int nkv, float scale, int part_size, int num_parts, int packed) -> ()");
+      "int nh, int nkv, float scale, int part_size, int num_parts, int packed, Tensor(e!)? counters=None) -> ()");
   m.def(
       "attention_mfma(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor q_seq, Tensor q_ctx, "
       "Tensor qblocks, Tensor(a!) out, Tensor(b!) workspace, int nh, int nkv, float scale, int part_size, "

@@ -213,6 +213,7 @@ class StageExecutor:
                 if self._fused and not all(getattr(L, "folded", False) for L in weights.layers):
                     self._fused = False  # packed before (e.g. a shared weights object): norm kernels
                 ops.gemm_workspace(self.device)  # allocated before any hipGraph capture
+                ops.attention_counters(self.device)
                 if os.environ.get("MPAMD_GEMM_AUTOTUNE", "1") != "0":
                     H, F = cfg.hidden_size, cfg.intermediate_size
                     shapes = [] if (weights.fp8 or not weights.layers) else \

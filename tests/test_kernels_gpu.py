@@ -114,6 +114,29 @@ def test_paged_attention_explicit_partitions(parts):
     torch.testing.assert_close(out.float(), o_ref.float(), atol=2e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("packed", [False, True])
+@pytest.mark.parametrize("ctxs,parts", [([300, 17, 1, 0], (64, 5)), ([150], (64, 3)), ([4097, 2], (128, 33))])
+def test_paged_attention_inlaunch_combine_equals_reduce_kernel(ctxs, parts, packed, monkeypatch):
+    """The in-launch split-K combine (last-arriving slice sums the partials) gives exactly the
+    separate reduce kernel's output (same arithmetic, slice order), with empty slices (short
+    contexts, ctx = 0 rows) arriving too; the counters are left at zero for the next launch."""
+    nh, nkv, D = 32, 8, 128
+    q, kc, vc, bt, q_seq, q_ctx = _attn_case(nh, nkv, D, ctxs)
+    ps, np_ = parts
+    outs = []
+    for flag in ("0", "1", "1"):
+        monkeypatch.setenv("MPAMD_ATTN_INLAUNCH_REDUCE", flag)
+        outs.append(ops.paged_attention(q, kc, vc, bt, q_seq, q_ctx, nh, nkv, 0.088, part_size=ps, num_parts=np_,
+                                        packed=packed))
+    torch.cuda.synchronize()
+    if packed:  # padding rows of the last 16-row tile are never written: compare the real rows
+        outs = [ops.unpack_act(o, len(ctxs), nh * D) for o in outs]
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[1], outs[2])
+    assert int(ops.attention_counters(DEV).abs().sum()) == 0
+    o_ref = ref.paged_attention(q.float(), kc.float(), vc.float(), bt, q_seq, q_ctx, nh, nkv, 0.088)
+    torch.testing.assert_close(outs[1].float(), o_ref.float(), atol=2e-2, rtol=2e-2)
+
+
 def test_paged_attention_prefill_causal_and_padding():
     nh, nkv, D = 16, 4, 128
     q, kc, vc, bt, q_seq, q_ctx = _attn_case(nh, nkv, D, [70, 9], multi_q=True)

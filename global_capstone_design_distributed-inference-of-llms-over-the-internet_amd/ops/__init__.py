@@ -93,7 +93,7 @@ _SK_CHOICE = {}  # (m_bucket, N, K, epilogue) -> kernel name (see _KERNEL_FLAGS)
 # decode-GEMM kernels (csrc/gemm.hip): one-group-per-workgroup, stream-K, and the shared-A (LDS)
 # form with (NT column tiles per wave, CH column waves sharing each k-split's A) = (2,2)/(2,4)/(4,2),
 # and the balanced ring form "rw" (every CU one workgroup with ceil/floor of tiles / CUs; M > 16)
-_KERNEL_FLAGS = {"pk": 0, "sk": 4, "lds22": 16, "lds24": 16 | 32, "lds42": 16 | 96, "rw": 128}
+_KERNEL_FLAGS = {"pk": 0, "sk": 4, "lds22": 16, "lds24": 16 | 32, "lds42": 16 | 96, "rw": 128, "rwk": 256}
 _LDS_CFG = {"lds22": (2, 2), "lds24": (2, 4), "lds42": (4, 2)}
 
 
@@ -147,6 +147,8 @@ def _covered(name: str, M: int, N: int, K: int, epilogue: int) -> bool:
         return _sk_covered(N, K)
     if name == "rw":  # widths the launcher does not build fall back to the other kernels by itself
         return M > 16
+    if name == "rwk":  # split-K ring + reduce launch: plain / residual / fused-norm producer epilogues
+        return M > 16 and epilogue != 1 and N % 2048 == 0
     return _lds_covered(name, M, N, K, epilogue)
 
 
@@ -605,9 +607,15 @@ def linear(x, w, out=None, epilogue=0, residual=None, policy=None, wp=None, a_ro
         if out is None:
             out = (torch.empty(packed_numel(M, ncols), dtype=x.dtype, device=x.device) if out_packed
                    else torch.empty(M, ncols, dtype=x.dtype, device=x.device))
-        kern = "pk" if gate is not None else ("rw" if M > 64 else _kernel_for(M, N, K, epilogue))
+        if gate is not None:
+            kern = "pk"
+        elif M > 64:  # 65..128 rows: split-K ring where it applies (o, down), else the ring kernel
+            kern = "rwk" if (not out_packed and _covered("rwk", M, N, K, epilogue)
+                             and os.environ.get("MPAMD_WIDE_SPLITK", "1") != "0") else "rw"
+        else:
+            kern = _kernel_for(M, N, K, epilogue)
         flags = 1 | (2 if out_packed else 0) | _KERNEL_FLAGS[kern]
-        ws = gemm_workspace(x.device) if kern == "sk" else None
+        ws = gemm_workspace(x.device) if kern in ("sk", "rwk") else None
         torch.ops.mpamd.gemm(x, wp, out, residual, int(epilogue), M, flags, ws, gate, ap_out, ss_out, ss_zero, ss_in,
                              1.0 / K, float(eps))
         return out

@@ -1083,6 +1083,183 @@ static int launch_gemm_rw(const void* x, const void* w, void* y, int64_t ys, con
 #undef MP_RWC
 }
 
+// ---------------------------------------------------------------------------------------
+// Split-K ring form ("rwk") for the narrow projections (o, down: N = 4096 -> 256 column tiles,
+// one per CU): with every CU owning all of K, each CU streams ALL of the activation block
+// (M x K) for just 16 weight columns - at M = 64 that is 4x the weight bytes through the
+// texture path (the lab: down 29 us, 16 us with the A loads removed).  Here a workgroup owns NT
+// column tiles and 1/S of K (C x S = #CUs), so A per CU drops S-fold, and writes an fp32 partial
+// slab; the sum over the S slabs and the epilogue (residual, packed copy, row sums of squares)
+// run in a small second launch - a kernel boundary instead of an in-launch seam (the stream-K
+// kernel's end-of-range hand-off costs ~7 us at these sizes).
+constexpr int64_t RWK_SLAB_BYTES = (int64_t)16 << 20;  // S x M x N fp32 partials (workspace tail)
+
+template <int MT, int NT>
+__global__ __launch_bounds__(256) void gemm_rwk_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ wp,
+                                                       float* __restrict__ part, int M, int N, int K, int S,
+                                                       const EpiArgs ep) {
+  clear_other(ep);
+  constexpr int R = rw_depth<MT, NT>();
+  constexpr int Q = MT * NT;
+  constexpr int QC = Q < RW_QC ? Q : RW_QC;
+  __shared__ __attribute__((aligned(16))) f32x4 red[RW_WAVES * QC * 64];
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int c = blockIdx.x / S, sp = blockIdx.x - c * S;
+  const int tile0 = c * NT;
+  const int nks = K >> 5;
+  const int ks0 = (int)((int64_t)sp * nks / S), ks1 = (int)((int64_t)(sp + 1) * nks / S);
+  const int cnt = (ks1 - ks0 + RW_WAVES - 1) / RW_WAVES;
+  const bf16_t* wb = wp + ((int64_t)tile0 * nks) * 512 + lane * 8;
+  const bf16_t* xl = x + lane * 8;
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[mt][t] = (f32x4)(0.f);
+  u16x8 ra[R][MT], rb[R][NT];
+#define RWK_LOAD(s, i)                                                                                       \
+  {                                                                                                          \
+    const int k_ = min(ks0 + wid + RW_WAVES * (i), ks1 - 1);                                                 \
+    _Pragma("unroll") for (int t = 0; t < NT; ++t) rb[s][t] =                                                \
+        __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(wb + (((int64_t)t * nks + k_) << 9)));    \
+    _Pragma("unroll") for (int mt = 0; mt < MT; ++mt) ra[s][mt] =                                            \
+        MP_LOAD_A_FRAG(xl + (((int64_t)k_ * MT + mt) << 9));                                                 \
+  }
+#pragma unroll
+  for (int s = 0; s < R; ++s) RWK_LOAD(s, s)
+  for (int i0 = 0; i0 < cnt; i0 += R) {
+#pragma unroll
+    for (int s = 0; s < R; ++s) {
+      if (ks0 + wid + RW_WAVES * (i0 + s) < ks1) {
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int t = 0; t < NT; ++t) acc[mt][t] = mfma16(ra[s][mt], rb[s][t], acc[mt][t]);
+      }
+      RWK_LOAD(s, i0 + s + R)
+    }
+  }
+#undef RWK_LOAD
+  // sum the 4 waves' partial tiles through LDS and store this split's fp32 slab [M][N]
+  float* slab = part + (int64_t)sp * M * N;
+  const int cl = lane & 15, q = lane >> 4;
+#pragma unroll
+  for (int p0 = 0; p0 < Q; p0 += QC) {
+    if (p0 > 0) __syncthreads();
+#pragma unroll
+    for (int qd = p0; qd < p0 + QC && qd < Q; ++qd) red[(wid * QC + qd - p0) * 64 + lane] = acc[qd / NT][qd % NT];
+    __syncthreads();
+    for (int qd = p0 + wid; qd < p0 + QC && qd < Q; qd += RW_WAVES) {
+      f32x4 v = red[(qd - p0) * 64 + lane];
+#pragma unroll
+      for (int w = 1; w < RW_WAVES; ++w) v += red[(w * QC + qd - p0) * 64 + lane];
+      const int mt = qd / NT, col = (tile0 + qd % NT) * 16 + cl;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = mt * 16 + q * 4 + r;
+        if (row < M) slab[(int64_t)row * N + col] = v[r];
+      }
+    }
+  }
+}
+
+// Sum the S fp32 slabs (fixed order: deterministic) + epilogue.  One thread per 8 consecutive
+// columns of a row; a workgroup covers 2048 columns of one row (EPI 3: its row's sum of squares
+// is reduced in the workgroup and added to one shard with a single atomic).
+template <int EPI>
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ part, int S, int M, int N,
+                                                            bf16_t* __restrict__ y, int64_t ys,
+                                                            const bf16_t* __restrict__ res, int64_t rs,
+                                                            const EpiArgs ep) {
+  __shared__ u64 red[4];
+  __shared__ float s_rs;
+  const int row = blockIdx.y;
+  const int col = (blockIdx.x * 256 + threadIdx.x) * 8;
+  u64 sq = 0;
+  float sc = 1.f;
+  if constexpr (EPI == 0) {  // fused-norm consumer (qkv): row scale rsqrt(sum of squares / K + eps)
+    if (ep.ss_in != nullptr) {
+      if (threadIdx.x < 64) {
+        u64 t = threadIdx.x < SS_NSH ? ep.ss_in[threadIdx.x * 64 + row] : 0ull;
+#pragma unroll
+        for (int o2 = 32; o2 > 0; o2 >>= 1) t += __shfl_xor(t, o2, 64);
+        if (threadIdx.x == 0) s_rs = rsqrtf((float)t * (1.f / SS_FX) * ep.inv_k + ep.eps);
+      }
+      __syncthreads();
+      sc = s_rs;
+    }
+  }
+  if (col < N) {
+    f32x4 a0 = (f32x4)(0.f), a1 = (f32x4)(0.f);
+    for (int s = 0; s < S; ++s) {
+      const float* pp = part + ((int64_t)s * M + row) * N + col;
+      a0 += *reinterpret_cast<const f32x4*>(pp);
+      a1 += *reinterpret_cast<const f32x4*>(pp + 4);
+    }
+    u16x8 o;
+    if constexpr (EPI == 0) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = f2bf((j < 4 ? a0[j] : a1[j - 4]) * sc);
+    } else {
+      const u16x8 rv = *reinterpret_cast<const u16x8*>(res + (int64_t)row * rs + col);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        o[j] = f2bf(round_bf(j < 4 ? a0[j] : a1[j - 4]) + bf2f(rv[j]));
+        if constexpr (EPI == 3) sq += fx_sq(bf2f(o[j]));
+      }
+    }
+    *reinterpret_cast<u16x8*>(y + (int64_t)row * ys + col) = o;
+    if constexpr (EPI == 3) *reinterpret_cast<u16x8*>(ep.ap + apk_off(row, col, ep.mt_out)) = o;
+  }
+  if constexpr (EPI == 3) {
+    if (ep.ss_out == nullptr) return;
+#pragma unroll
+    for (int o2 = 32; o2 > 0; o2 >>= 1) sq += __shfl_xor(sq, o2, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sq;
+    __syncthreads();
+    if (threadIdx.x == 0)
+      atomicAdd(ep.ss_out + ((blockIdx.y * gridDim.x + blockIdx.x) % SS_NSH) * 64 + row,
+                red[0] + red[1] + red[2] + red[3]);
+  }
+}
+
+// Column-group width NT and split count S with C x S <= #CUs (prefer NT = 4, then 2, 8, 1;
+// 2 <= S <= 8); returns 1 when no split applies (the caller falls back).
+template <int MT>
+static int launch_gemm_rwk(const void* x, const void* w, void* y, int64_t ys, const void* res, int64_t rs, int M,
+                           int N, int K, int epi, const EpiArgs& ep, void* ws, hipStream_t stream) {
+  if (epi == 1 || ws == nullptr || N % 2048 != 0) return 1;
+  const int tiles = N / 16, C0 = sk_num_cus(), nks = K / 32;
+  int nt = 0, S = 0;
+  for (int cand : {4, 2, 8, 1}) {
+    if (tiles % cand) continue;
+    const int C = tiles / cand, s = C0 / C;
+    if (s >= 2 && s <= 8 && nks >= 4 * s) { nt = cand; S = s; break; }
+  }
+  if (nt == 0) return 1;
+  if ((int64_t)S * M * N * 4 > RWK_SLAB_BYTES) return 1;
+  if constexpr (4 * MT * 8 > 192) {
+    if (nt == 8) return 1;
+  }
+  float* part = (float*)((char*)ws + (int64_t)SK_MAX_GROUPS * sizeof(int) + SK_ZERO_BYTES +
+                         (int64_t)SK_MAX_BLOCKS * 2 * SK_MAX_S * 64 * sizeof(float));
+  const dim3 g1((tiles / nt) * S);
+  switch (nt) {
+    case 1: hipLaunchKernelGGL((gemm_rwk_kernel<MT, 1>), g1, dim3(256), 0, stream, (const bf16_t*)x, (const bf16_t*)w, part, M, N, K, S, ep); break;
+    case 2: hipLaunchKernelGGL((gemm_rwk_kernel<MT, 2>), g1, dim3(256), 0, stream, (const bf16_t*)x, (const bf16_t*)w, part, M, N, K, S, ep); break;
+    case 4: hipLaunchKernelGGL((gemm_rwk_kernel<MT, 4>), g1, dim3(256), 0, stream, (const bf16_t*)x, (const bf16_t*)w, part, M, N, K, S, ep); break;
+    default:
+      if constexpr (4 * MT * 8 <= 192)
+        hipLaunchKernelGGL((gemm_rwk_kernel<MT, 8>), g1, dim3(256), 0, stream, (const bf16_t*)x, (const bf16_t*)w, part, M, N, K, S, ep);
+      break;
+  }
+  const dim3 g2(N / 2048, M);
+  if (epi == 3) hipLaunchKernelGGL(splitk_reduce_kernel<3>, g2, dim3(256), 0, stream, part, S, M, N, (bf16_t*)y, ys, (const bf16_t*)res, rs, ep);
+  else if (epi == 2) hipLaunchKernelGGL(splitk_reduce_kernel<2>, g2, dim3(256), 0, stream, part, S, M, N, (bf16_t*)y, ys, (const bf16_t*)res, rs, ep);
+  else hipLaunchKernelGGL(splitk_reduce_kernel<0>, g2, dim3(256), 0, stream, part, S, M, N, (bf16_t*)y, ys, (const bf16_t*)res, rs, ep);
+  return 0;
+}
+
 // Pack W[N, K] (row-major) into the fragment-native layout Wp[N/16][K/32][64][8].
 __global__ __launch_bounds__(256) void pack_weight_kernel(const bf16_t* __restrict__ w, bf16_t* __restrict__ wp,
                                                           int N, int K) {
@@ -1121,14 +1298,15 @@ extern "C" int mp_gemm_rw_ok(int M, int N, int K, int epilogue, int out_packed) 
 extern "C" int64_t mp_gemm_workspace_bytes() {
   using namespace mp;
   return (int64_t)SK_MAX_GROUPS * sizeof(int) + SK_ZERO_BYTES +
-         (int64_t)SK_MAX_BLOCKS * 2 * SK_MAX_S * 64 * sizeof(float);
+         (int64_t)SK_MAX_BLOCKS * 2 * SK_MAX_S * 64 * sizeof(float) + RWK_SLAB_BYTES;
 }
 
 // flags: bit 0 = x is packed (Ap[K/32][ceil(M/16)][64][8]); bit 1 = SwiGLU output packed;
 //        bit 2 = use the stream-K kernel (needs ws: mp_gemm_workspace_bytes(), zero-initialised,
 //        used by one stream at a time); bit 3 = force the one-group-per-workgroup kernel;
 //        bit 4 = shared-A (LDS-staged activation) kernel when the shape allows it;
-//        bit 7 = balanced ring kernel (M > 16).
+//        bit 7 = balanced ring kernel (M > 16); bit 8 = split-K ring kernel + reduce launch
+//        (M > 16, epilogue 0 / 2 / 3, needs ws).
 //        epilogue 3 / ss_in: the fused-norm decode path (EpiArgs above; ap / ss_out / ss_zero /
 //        ss_in may be null when unused).
 extern "C" int mp_gemm_bf16(const void* x, int64_t x_stride, const void* w, void* y, int64_t y_stride,
@@ -1141,6 +1319,21 @@ extern "C" int mp_gemm_bf16(const void* x, int64_t x_stride, const void* w, void
   const EpiArgs ep{(bf16_t*)ap, (u64*)ss_out, (u64*)ss_zero, (const u64*)ss_in, inv_k, eps, (M + 15) / 16};
   if (M > 128 || K % (32 * GU_MAX) || N % 16 || ((flags & 1) == 0 && x_stride % 8)) return -1;
   int rc;
+  if ((flags & 1) && (flags & 256) && !(flags & 2) && gate == nullptr && ws != nullptr && M > 16) {  // split-K ring
+#define MP_RWK(MT_) rc = launch_gemm_rwk<MT_>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, ep, ws, stream)
+    switch ((M + 15) / 16) {  // the packed layout's row-tile count is part of its strides
+      case 2: MP_RWK(2); break;
+      case 3: MP_RWK(3); break;
+      case 4: MP_RWK(4); break;
+      case 5: MP_RWK(5); break;
+      case 6: MP_RWK(6); break;
+      case 7: MP_RWK(7); break;
+      default: MP_RWK(8); break;
+    }
+#undef MP_RWK
+    if (rc < 0) return rc;
+    if (rc == 0) return (int)hipGetLastError();
+  }
   if (M > 64) {  // 65..128 rows: the balanced ring kernel only (packed A, no gate), or nothing
     if (!(flags & 1) || gate != nullptr) return -1;
     if (M <= 80) rc = launch_gemm_rw<5>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, ep, stream);

@@ -68,32 +68,38 @@ int main(int argc, char** argv) {
     Ms.clear();
     for (char* t = strtok(argv[1], ","); t; t = strtok(nullptr, ",")) Ms.push_back(atoi(t));
   }
+  for (int M : Ms)
+    if (M < 1 || M > 128) {
+      fprintf(stderr, "M must be in 1..128 (buffer sizes)\n");
+      return 1;
+    }
   const size_t pool_bytes = (size_t)1536 << 20;
   unsigned short *pool, *x, *y;
   CK(hipMalloc(&pool, pool_bytes));
-  CK(hipMalloc(&x, (size_t)64 * 11008 * 2));
-  CK(hipMalloc(&y, (size_t)64 * 32768 * 2));
+  // sized for the largest M the kernels take (128 rows) and the widest shape
+  CK(hipMalloc(&x, (size_t)128 * 11008 * 2));
+  CK(hipMalloc(&y, (size_t)128 * 32768 * 2));
   void* ws;
   const int64_t wsb = mp_gemm_workspace_bytes();
   CK(hipMalloc(&ws, wsb));
   CK(hipMemset(ws, 0, wsb));
   hipLaunchKernelGGL(fill_bf16, dim3(4096), dim3(256), 0, 0, pool, pool_bytes / 2, 1u);
-  hipLaunchKernelGGL(fill_bf16, dim3(1024), dim3(256), 0, 0, x, (size_t)64 * 11008, 7u);
+  hipLaunchKernelGGL(fill_bf16, dim3(1024), dim3(256), 0, 0, x, (size_t)128 * 11008, 7u);
   CK(hipDeviceSynchronize());
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   unsigned short* yref;
-  CK(hipMalloc(&yref, (size_t)64 * 32768 * 2));
-  std::vector<unsigned short> h0(64 * 32768), h1(64 * 32768);
-  const char* kname[7] = {"pk ", "sk ", "l22", "l24", "l14", "l42", "rw "};
+  CK(hipMalloc(&yref, (size_t)128 * 32768 * 2));
+  std::vector<unsigned short> h0(128 * 32768), h1(128 * 32768);
+  const char* kname[8] = {"pk ", "sk ", "l22", "l24", "l14", "l42", "rw ", "rwk"};
   for (const Shape& s : shapes) {
     const size_t wbytes = (size_t)s.N * s.K * 2;
     const int copies = (int)(pool_bytes / wbytes);
     const int ncols = s.epi == 1 ? s.N / 2 : s.N;
     for (int M : Ms) {
-      for (int kind = 0; kind < 7; ++kind) {
-        const int flags = 1 | (kind == 0 ? 8 : kind == 1 ? 4 : kind == 6 ? 128 : 16 | ((kind - 2) << 5));
+      for (int kind = 0; kind < 8; ++kind) {
+        const int flags = 1 | (kind == 0 ? 8 : kind == 1 ? 4 : kind == 6 ? 128 : kind == 7 ? 256 : 16 | ((kind - 2) << 5));
         auto run = [&](int i, unsigned short* out) {
           const unsigned short* w = pool + (size_t)(i % copies) * (wbytes / 2);
           return mp_gemm_bf16(x, s.K, w, out, ncols, nullptr, 0, M, s.N, s.K, s.epi, flags, ws, nullptr, nullptr,

@@ -50,7 +50,7 @@ def test_reference_fold_identity_cpu():
     assert int(ssz.abs().sum()) == 0
 
 
-KERNELS = ["pk", "sk", "lds22", "lds24", "lds42", "rw"]
+KERNELS = ["pk", "sk", "lds22", "lds24", "lds42", "rw", "rwk"]
 
 
 @pytest.mark.gpu
@@ -59,7 +59,7 @@ KERNELS = ["pk", "sk", "lds22", "lds24", "lds42", "rw"]
 def test_consumer_row_scale_matches_rmsnorm_then_gemm(kern, M):
     dev = "cuda"
     g = torch.Generator(device=dev).manual_seed(M)
-    K, N = 1024, 2048
+    K, N = 1024, 2048  # N % 2048 == 0: the split-K ring form applies too (plain-epilogue consumer)
     x = (torch.randn(M, K, device=dev, generator=g) * 0.7).to(torch.bfloat16)
     gw = (torch.rand(K, device=dev, generator=g) + 0.5).to(torch.bfloat16)
     w = (torch.randn(N, K, device=dev, generator=g) * 0.03).to(torch.bfloat16)
@@ -93,7 +93,7 @@ def test_consumer_row_scale_matches_rmsnorm_then_gemm(kern, M):
 def test_producer_epilogue_residual_pack_and_sumsq(kern, M):
     dev = "cuda"
     g = torch.Generator(device=dev).manual_seed(100 + M)
-    K, N = 2048, 1024
+    K, N = 2048, 2048
     a = (torch.randn(M, K, device=dev, generator=g) * 0.5).to(torch.bfloat16)
     w = (torch.randn(N, K, device=dev, generator=g) * 0.03).to(torch.bfloat16)
     res = (torch.randn(M, N, device=dev, generator=g)).to(torch.bfloat16)

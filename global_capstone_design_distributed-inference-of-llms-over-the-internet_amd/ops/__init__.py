@@ -691,7 +691,7 @@ def quant_rows_fp8(x: torch.Tensor, out=None, scale=None):
     return out, scale
 
 
-_FP8_KERNELS = {"pk": 0, "rw": 1}
+_FP8_KERNELS = {"pk": 0, "rw": 1, "rwk": 2}
 _FP8_CHOICE = {}  # (m_bucket, N, K, epilogue) -> fp8 kernel name, from autotune_fp8
 _FP8_MODE = "auto"
 
@@ -770,6 +770,7 @@ def linear_fp8(a8, a_scale, wq, w_scale, M: int, out=None, epilogue: int = 0, re
     if out is None:
         out = (torch.empty(packed_numel(M, ncols), dtype=torch.bfloat16, device=a8.device) if out_packed
                else torch.empty(M, ncols, dtype=torch.bfloat16, device=a8.device))
+    kind = _fp8_kind(M, N, 64 * wq.shape[1], epilogue)
     torch.ops.mpamd.gemm_fp8(a8, a_scale, wq, w_scale, out, residual, int(epilogue), int(M), int(bool(out_packed)),
-                             _fp8_kind(M, N, 64 * wq.shape[1], epilogue))
+                             kind, gemm_workspace(a8.device) if kind == 2 else None)
     return out

@@ -38,7 +38,10 @@ int mp_attention_mfma(const void* q, int64_t q_stride, const void* kc, const voi
                       const int64_t* slots, hipStream_t stream);
 int mp_quant_act_fp8(const void* ap, void* a8, float* scale, float* part, int M, int K, hipStream_t stream);
 int mp_gemm_fp8(const void* a8, const float* as, const void* wq, const float* ws, void* y, int64_t ys, const void* res,
-                int64_t rs, int M, int N, int K, int epilogue, int out_packed, int kind, hipStream_t stream);
+                int64_t rs, int M, int N, int K, int epilogue, int out_packed, int kind, float* part,
+                int64_t part_bytes, hipStream_t stream);
+int64_t mp_gemm_slab_offset();
+int64_t mp_gemm_slab_bytes();
 void mp_fp8_set_kernel(int kind);
 int mp_gemm_rw_ok(int M, int N, int K, int epilogue, int out_packed);
 int mp_quant_rows_fp8(const void* x, int64_t xs, void* a8, float* scale, int M, int K, hipStream_t stream);
@@ -500,7 +503,7 @@ void quant_rows_fp8(const at::Tensor& x, at::Tensor& a8, at::Tensor& scale) {
 // y = epilogue((a8 * as) . (wq * ws)^T); wq: [N/16, K/64, 64, 16] uint8 (ops.pack_weight_fp8)
 void gemm_fp8(const at::Tensor& a8, const at::Tensor& as, const at::Tensor& wq, const at::Tensor& ws, at::Tensor& y,
               const c10::optional<at::Tensor>& residual, int64_t epilogue, int64_t M, int64_t out_packed,
-              int64_t kind) {
+              int64_t kind, const c10::optional<at::Tensor>& workspace) {
   MP_CHECK(wq.is_cuda() && wq.scalar_type() == at::kByte && wq.dim() == 4 && wq.size(2) == 64 && wq.size(3) == 16 &&
                wq.is_contiguous(),
            "wq must be a packed fp8 weight [N/16, K/64, 64, 16]");
@@ -525,9 +528,18 @@ void gemm_fp8(const at::Tensor& a8, const at::Tensor& as, const at::Tensor& wq, 
     rs = residual->stride(0);
   }
   MP_CHECK(epilogue != 2 || rp != nullptr, "residual epilogue needs residual");
+  float* part = nullptr;
+  int64_t part_bytes = 0;
+  if (workspace.has_value()) {  // the GEMM workspace (ops.gemm_workspace): its split-K slab region
+    MP_CHECK(workspace->is_cuda() && workspace->is_contiguous() &&
+                 workspace->numel() * workspace->element_size() >= mp_gemm_workspace_bytes(),
+             "workspace: ops.gemm_workspace");
+    part = (float*)((char*)workspace->data_ptr() + mp_gemm_slab_offset());
+    part_bytes = mp_gemm_slab_bytes();
+  }
   check_launch(mp_gemm_fp8(a8.data_ptr(), as.data_ptr<float>(), wq.data_ptr(), ws.data_ptr<float>(), y.data_ptr(),
                            out_packed ? 0 : y.stride(0), rp, rs, (int)M, N, K, (int)epilogue, (int)out_packed,
-                           (int)kind, cur_stream()),
+                           (int)kind, part, part_bytes, cur_stream()),
                "gemm_fp8");
 }
 
@@ -577,7 +589,7 @@ TORCH_LIBRARY(mpamd, m) {
   m.def("quant_rows_fp8(Tensor x, Tensor(a!) a8, Tensor(b!) scale) -> ()");
   m.def(
       "gemm_fp8(Tensor a8, Tensor a_scale, Tensor wq, Tensor w_scale, Tensor(a!) y, Tensor? residual, int epilogue, "
-      "int M, int out_packed, int kind=-1) -> ()");
+      "int M, int out_packed, int kind=-1, Tensor(b!)? workspace=None) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(mpamd, CUDA, m) {

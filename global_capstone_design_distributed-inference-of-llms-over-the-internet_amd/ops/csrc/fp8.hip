@@ -505,6 +505,142 @@ static int launch_gemm_fp8_rw(const void* a8, const float* as, const void* wq, c
 #undef F8RWC
 }
 
+// ---------------------------------------------------------------------------------------
+// Split-K ring form (kind 2; the fp8 twin of gemm.hip's "rwk"): for the narrow 70B projections
+// (o, down: N = 8192 -> 512 tiles, two per CU with all of K) every CU streams the whole fp8
+// activation block (down: 64 x 28672 B) for 32 weight columns.  A workgroup here owns NT tiles
+// and 1/S of K (C x S = #CUs) and writes an unscaled fp32 partial slab; a second launch sums the
+// S slabs in order and applies a_scale[row] * w_scale[col] (+ residual).
+template <int MT, int NT>
+__global__ __launch_bounds__(256) void gemm_fp8_rwk_kernel(const uint8_t* __restrict__ a8,
+                                                           const uint8_t* __restrict__ wq, float* __restrict__ part,
+                                                           int M, int N, int K, int S) {
+  constexpr int R = f8rw_depth<MT, NT>();
+  constexpr int Q = MT * NT;
+  constexpr int QC = Q < F8RW_QC ? Q : F8RW_QC;
+  __shared__ __attribute__((aligned(16))) f32x4 red[F8RW_WAVES * QC * 64];
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int cg = blockIdx.x / S, sp = blockIdx.x - cg * S;
+  const int tile0 = cg * NT;
+  const int nch = K >> 6;
+  const int k0 = (int)((int64_t)sp * nch / S), k1 = (int)((int64_t)(sp + 1) * nch / S);
+  const int cnt = (k1 - k0 + F8RW_WAVES - 1) / F8RW_WAVES;
+  const uint8_t* wb = wq + ((int64_t)tile0 * nch) * 1024 + lane * 16;
+  const uint8_t* ab = a8 + lane * 16;
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[mt][t] = (f32x4)(0.f);
+  u16x8 ra[R][MT], rb[R][NT];
+#define F8K_LOAD(s, i)                                                                                       \
+  {                                                                                                          \
+    const int k_ = min(k0 + wid + F8RW_WAVES * (i), k1 - 1);                                                 \
+    _Pragma("unroll") for (int t = 0; t < NT; ++t) rb[s][t] =                                                \
+        __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(wb + ((int64_t)t * nch + k_) * 1024));    \
+    _Pragma("unroll") for (int mt = 0; mt < MT; ++mt) ra[s][mt] =                                            \
+        MP_F8_LOAD_A(ab + ((int64_t)k_ * MT + mt) * 1024);                                                   \
+  }
+#pragma unroll
+  for (int s = 0; s < R; ++s) F8K_LOAD(s, s)
+  for (int i0 = 0; i0 < cnt; i0 += R) {
+#pragma unroll
+    for (int s = 0; s < R; ++s) {
+      if (k0 + wid + F8RW_WAVES * (i0 + s) < k1) {
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int t = 0; t < NT; ++t) acc[mt][t] = mfma_fp8x2(ra[s][mt], rb[s][t], acc[mt][t]);
+      }
+      F8K_LOAD(s, i0 + s + R)
+    }
+  }
+#undef F8K_LOAD
+  float* slab = part + (int64_t)sp * M * N;
+  const int cl = lane & 15, q = lane >> 4;
+#pragma unroll
+  for (int p0 = 0; p0 < Q; p0 += QC) {
+    if (p0 > 0) __syncthreads();
+#pragma unroll
+    for (int qd = p0; qd < p0 + QC && qd < Q; ++qd) red[(wid * QC + qd - p0) * 64 + lane] = acc[qd / NT][qd % NT];
+    __syncthreads();
+    for (int qd = p0 + wid; qd < p0 + QC && qd < Q; qd += F8RW_WAVES) {
+      f32x4 v = red[(qd - p0) * 64 + lane];
+#pragma unroll
+      for (int w = 1; w < F8RW_WAVES; ++w) v += red[(w * QC + qd - p0) * 64 + lane];
+      const int mt = qd / NT, col = (tile0 + qd % NT) * 16 + cl;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = mt * 16 + q * 4 + r;
+        if (row < M) slab[(int64_t)row * N + col] = v[r];
+      }
+    }
+  }
+}
+
+template <int EPI>
+__global__ __launch_bounds__(256) void fp8_splitk_reduce_kernel(const float* __restrict__ part, int S, int M, int N,
+                                                                const float* __restrict__ ascale,
+                                                                const float* __restrict__ wscale,
+                                                                bf16_t* __restrict__ y, int64_t ys,
+                                                                const bf16_t* __restrict__ res, int64_t rs) {
+  const int row = blockIdx.y;
+  const int col = (blockIdx.x * 256 + threadIdx.x) * 8;
+  if (col >= N) return;
+  f32x4 a0 = (f32x4)(0.f), a1 = (f32x4)(0.f);
+  for (int s = 0; s < S; ++s) {
+    const float* pp = part + ((int64_t)s * M + row) * N + col;
+    a0 += *reinterpret_cast<const f32x4*>(pp);
+    a1 += *reinterpret_cast<const f32x4*>(pp + 4);
+  }
+  const float as = ascale[row];
+  const f32x4 w0 = *reinterpret_cast<const f32x4*>(wscale + col), w1 = *reinterpret_cast<const f32x4*>(wscale + col + 4);
+  u16x8 o;
+  u16x8 rv = (u16x8)(0);
+  if constexpr (EPI == 2) rv = *reinterpret_cast<const u16x8*>(res + (int64_t)row * rs + col);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float v = (j < 4 ? a0[j] : a1[j - 4]) * as * (j < 4 ? w0[j] : w1[j - 4]);
+    if constexpr (EPI == 2) v = round_bf(v) + bf2f(rv[j]);
+    o[j] = f2bf(v);
+  }
+  *reinterpret_cast<u16x8*>(y + (int64_t)row * ys + col) = o;
+}
+
+template <int MT>
+static int launch_gemm_fp8_rwk(const void* a8, const float* as, const void* wq, const float* ws, void* y, int64_t ys,
+                               const void* res, int64_t rs, int M, int N, int K, int epi, int opk, float* part,
+                               int64_t part_bytes, hipStream_t stream) {
+  if (epi == 1 || opk || part == nullptr || N % 2048) return 1;
+  const int tiles = N / 16, C0 = f8_num_cus(), nch = K / 64;
+  int nt = 0, S = 0;
+  for (int cand : {8, 4, 2}) {
+    if (tiles % cand || (cand == 8 && 4 * MT * 8 > 128)) continue;
+    const int C = tiles / cand, sp = C0 / C;
+    if (sp >= 2 && sp <= 8 && nch >= 4 * sp) { nt = cand; S = sp; break; }
+  }
+  if (nt == 0 || (int64_t)S * M * N * 4 > part_bytes) return 1;
+  const dim3 g1((tiles / nt) * S);
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, g1, dim3(256), 0, stream, (const uint8_t*)a8, (const uint8_t*)wq, part, M, N, K, S);
+  };
+  if (nt == 8) {
+    if constexpr (4 * MT * 8 <= 128) go(gemm_fp8_rwk_kernel<MT, 8>);
+  } else if (nt == 4) {
+    go(gemm_fp8_rwk_kernel<MT, 4>);
+  } else {
+    go(gemm_fp8_rwk_kernel<MT, 2>);
+  }
+  const dim3 g2(N / 2048, M);
+  if (epi == 2)
+    hipLaunchKernelGGL(fp8_splitk_reduce_kernel<2>, g2, dim3(256), 0, stream, part, S, M, N, as, ws, (bf16_t*)y, ys,
+                       (const bf16_t*)res, rs);
+  else
+    hipLaunchKernelGGL(fp8_splitk_reduce_kernel<0>, g2, dim3(256), 0, stream, part, S, M, N, as, ws, (bf16_t*)y, ys,
+                       (const bf16_t*)res, rs);
+  return 0;
+}
+
 // 0 = one-group kernel, 1 = balanced ring kernel where it applies (M > 16; default);
 // MPAMD_FP8_GEMM=pk selects the one-group kernel at start-up (A/B runs of bench.py)
 static int g_fp8_kernel = [] {
@@ -557,14 +693,23 @@ extern "C" int mp_quant_rows_fp8(const void* x, int64_t xs, void* a8, float* sca
 }
 
 // a8/as: quant_act_fp8 output for M rows; wq/ws: pack_weight_fp8 output for W[N, K].
-// kind: 0 = one-group kernel, 1 = balanced ring kernel (M > 16), -1 = the start-up default
+// kind: 0 = one-group kernel, 1 = balanced ring kernel (M > 16), 2 = split-K ring kernel + reduce
+// launch (M > 16, epilogue 0 / 2, needs part: fp32 scratch of part_bytes), -1 = the start-up default
 extern "C" int mp_gemm_fp8(const void* a8, const float* as, const void* wq, const float* ws, void* y, int64_t ys,
                            const void* res, int64_t rs, int M, int N, int K, int epilogue, int out_packed, int kind,
-                           hipStream_t stream) {
+                           float* part, int64_t part_bytes, hipStream_t stream) {
   using namespace mp;
   if (M == 0) return 0;
   if (M > 64 || K % (64 * F8_GU_MAX) || N % 16) return -1;
   int rc;
+  if (kind == 2 && M > 16) {
+    if (M <= 32) rc = launch_gemm_fp8_rwk<2>(a8, as, wq, ws, y, ys, res, rs, M, N, K, epilogue, out_packed, part, part_bytes, stream);
+    else if (M <= 48) rc = launch_gemm_fp8_rwk<3>(a8, as, wq, ws, y, ys, res, rs, M, N, K, epilogue, out_packed, part, part_bytes, stream);
+    else rc = launch_gemm_fp8_rwk<4>(a8, as, wq, ws, y, ys, res, rs, M, N, K, epilogue, out_packed, part, part_bytes, stream);
+    if (rc < 0) return rc;
+    if (rc == 0) return (int)hipGetLastError();
+    kind = 1;  // not covered: the balanced ring kernel
+  }
   if ((kind < 0 ? g_fp8_kernel : kind) == 1 && M > 16) {
     if (M <= 32) rc = launch_gemm_fp8_rw<2>(a8, as, wq, ws, y, ys, res, rs, M, N, K, epilogue, out_packed, stream);
     else if (M <= 48) rc = launch_gemm_fp8_rw<3>(a8, as, wq, ws, y, ys, res, rs, M, N, K, epilogue, out_packed, stream);

@@ -1280,6 +1280,14 @@ __global__ __launch_bounds__(256) void pack_weight_kernel(const bf16_t* __restri
 
 extern "C" int mp_gemm_ss_elems() { return mp::SS_NSH * 64; }
 
+// byte offset / size of the split-K partial-slab region inside the GEMM workspace (shared with
+// the fp8 split-K kernel, fp8.hip)
+extern "C" int64_t mp_gemm_slab_offset() {
+  using namespace mp;
+  return (int64_t)SK_MAX_GROUPS * sizeof(int) + SK_ZERO_BYTES + (int64_t)SK_MAX_BLOCKS * 2 * SK_MAX_S * 64 * sizeof(float);
+}
+extern "C" int64_t mp_gemm_slab_bytes() { return mp::RWK_SLAB_BYTES; }
+
 // 1 if mp_gemm_bf16 covers a packed-activation decode GEMM of M = 65..128 rows (balanced ring
 // kernel: the widths built, epilogue 0 or packed SwiGLU), else 0.  No launch.
 extern "C" int mp_gemm_rw_ok(int M, int N, int K, int epilogue, int out_packed) {

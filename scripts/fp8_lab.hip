@@ -50,6 +50,8 @@ int main() {
   CK(hipMalloc(&ws, (size_t)57344 * 4));
   CK(hipMalloc(&as, 64 * 4));
   CK(hipMalloc(&y, (size_t)64 * 57344 * 2));
+  float* part;
+  CK(hipMalloc(&part, (size_t)16 << 20));
   hipLaunchKernelGGL(fill_u8, dim3(4096), dim3(256), 0, 0, pool, pool_bytes, 1u);
   hipLaunchKernelGGL(fill_u8, dim3(1024), dim3(256), 0, 0, a8, (size_t)64 * 28672, 7u);
   std::vector<float> one(57344, 1e-3f);
@@ -62,10 +64,10 @@ int main() {
   for (const Shape& s : shapes) {
     const size_t wbytes = (size_t)s.N * s.K;
     const int copies = (int)(pool_bytes / wbytes);
-    for (int kind = 0; kind < 2; ++kind) {
+    for (int kind = 0; kind < 3; ++kind) {
       auto run = [&](int i) {
         return mp_gemm_fp8(a8, as, pool + (size_t)(i % copies) * wbytes, ws, y, s.epi == 1 ? s.N / 2 : s.N, nullptr,
-                           0, M, s.N, s.K, s.epi, 0, kind, 0);
+                           0, M, s.N, s.K, s.epi, 0, kind, part, (int64_t)16 << 20, 0);
       };
       if (int rc = run(0)) {
         printf("%-8s rc=%d\n", s.name, rc);
@@ -84,7 +86,7 @@ int main() {
         best = ms < best ? ms : best;
       }
       const double us = best * 1000.0 / iters;
-      printf("%-8s M=%d N=%5d K=%5d %s %7.2f us %5.2f TB/s\n", s.name, M, s.N, s.K, kind ? "rw" : "pk", us,
+      printf("%-8s M=%d N=%5d K=%5d %s %7.2f us %5.2f TB/s\n", s.name, M, s.N, s.K, kind == 2 ? "rwk" : kind ? "rw " : "pk ", us,
              wbytes / us / 1e6);
       fflush(stdout);
     }

@@ -416,7 +416,7 @@ def test_fp8_quant_act_kernel_matches_reference(M):
     assert a8.numel() >= MT * 16 * K
 
 
-@pytest.mark.parametrize("kern", ["pk", "rw"])
+@pytest.mark.parametrize("kern", ["pk", "rw", "rwk"])
 @pytest.mark.parametrize("M", [1, 30, 64])
 @pytest.mark.parametrize("N,K,epi", [(1024, 1024, 0), (10240, 8192, 0), (8192, 28672, 0), (2048, 4096, 1),
                                      (4096, 11008, 2), (57344, 512, 1)])

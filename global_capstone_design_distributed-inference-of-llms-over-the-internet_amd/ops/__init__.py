@@ -92,7 +92,8 @@ _GEMM_WS = {}
 _SK_CHOICE = {}  # (m_bucket, N, K, epilogue) -> kernel name (see _KERNEL_FLAGS)
 # decode-GEMM kernels (csrc/gemm.hip): one-group-per-workgroup, stream-K, and the shared-A (LDS)
 # form with (NT column tiles per wave, CH column waves sharing each k-split's A) = (2,2)/(2,4)/(4,2),
-# and the balanced ring form "rw" (every CU one workgroup with ceil/floor of tiles / CUs; M > 16)
+# the balanced ring form "rw" (every CU one workgroup with ceil/floor of tiles / CUs) and its
+# split-K variant "rwk" (+ a reduce / epilogue launch) for the narrow projections
 _KERNEL_FLAGS = {"pk": 0, "sk": 4, "lds22": 16, "lds24": 16 | 32, "lds42": 16 | 96, "rw": 128, "rwk": 256}
 _LDS_CFG = {"lds22": (2, 2), "lds24": (2, 4), "lds42": (4, 2)}
 
@@ -126,7 +127,9 @@ def gemm_workspace(device) -> torch.Tensor:
 
 
 def _m_bucket(M: int) -> int:
-    return 16 * ((M + 15) // 16)
+    """Autotune row buckets: 4 (batch-1..4 decode: latency-bound, its own winner), then 16-row
+    steps (the packed layout's row tiles)."""
+    return 4 if M <= 4 else 16 * ((M + 15) // 16)
 
 
 def _sk_covered(N: int, K: int) -> bool:
@@ -146,9 +149,9 @@ def _covered(name: str, M: int, N: int, K: int, epilogue: int) -> bool:
     if name == "sk":
         return _sk_covered(N, K)
     if name == "rw":  # widths the launcher does not build fall back to the other kernels by itself
-        return M > 16
+        return True
     if name == "rwk":  # split-K ring + reduce launch: plain / residual / fused-norm producer epilogues
-        return M > 16 and epilogue != 1 and N % 2048 == 0
+        return epilogue != 1 and N % 2048 == 0
     return _lds_covered(name, M, N, K, epilogue)
 
 
@@ -170,7 +173,7 @@ def _use_sk(M: int, N: int, K: int, epilogue: int) -> bool:
 _TUNE_POOL_BYTES = 1 << 30
 
 
-def autotune_gemm(shapes, device, ms=(16, 32, 48, 64), iters: int = 24, rounds: int = 3) -> dict:
+def autotune_gemm(shapes, device, ms=(4, 16, 32, 48, 64), iters: int = 24, rounds: int = 3) -> dict:
     """Time every applicable decode-GEMM kernel (one-group, stream-K, shared-A variants) on each
     (N, K, epilogue) for each M bucket and record the fastest for ``linear``.  Returns the table.
 

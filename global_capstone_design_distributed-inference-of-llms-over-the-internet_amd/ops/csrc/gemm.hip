@@ -1313,8 +1313,8 @@ extern "C" int64_t mp_gemm_workspace_bytes() {
 //        bit 2 = use the stream-K kernel (needs ws: mp_gemm_workspace_bytes(), zero-initialised,
 //        used by one stream at a time); bit 3 = force the one-group-per-workgroup kernel;
 //        bit 4 = shared-A (LDS-staged activation) kernel when the shape allows it;
-//        bit 7 = balanced ring kernel (M > 16); bit 8 = split-K ring kernel + reduce launch
-//        (M > 16, epilogue 0 / 2 / 3, needs ws).
+//        bit 7 = balanced ring kernel; bit 8 = split-K ring kernel + reduce launch (epilogue
+//        0 / 2 / 3, needs ws).
 //        epilogue 3 / ss_in: the fused-norm decode path (EpiArgs above; ap / ss_out / ss_zero /
 //        ss_in may be null when unused).
 extern "C" int mp_gemm_bf16(const void* x, int64_t x_stride, const void* w, void* y, int64_t y_stride,
@@ -1327,9 +1327,10 @@ extern "C" int mp_gemm_bf16(const void* x, int64_t x_stride, const void* w, void
   const EpiArgs ep{(bf16_t*)ap, (u64*)ss_out, (u64*)ss_zero, (const u64*)ss_in, inv_k, eps, (M + 15) / 16};
   if (M > 128 || K % (32 * GU_MAX) || N % 16 || ((flags & 1) == 0 && x_stride % 8)) return -1;
   int rc;
-  if ((flags & 1) && (flags & 256) && !(flags & 2) && gate == nullptr && ws != nullptr && M > 16) {  // split-K ring
+  if ((flags & 1) && (flags & 256) && !(flags & 2) && gate == nullptr && ws != nullptr) {  // split-K ring
 #define MP_RWK(MT_) rc = launch_gemm_rwk<MT_>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, ep, ws, stream)
     switch ((M + 15) / 16) {  // the packed layout's row-tile count is part of its strides
+      case 1: MP_RWK(1); break;
       case 2: MP_RWK(2); break;
       case 3: MP_RWK(3); break;
       case 4: MP_RWK(4); break;
@@ -1352,8 +1353,9 @@ extern "C" int mp_gemm_bf16(const void* x, int64_t x_stride, const void* w, void
     return (int)hipGetLastError();
   }
   if (gate != nullptr) flags &= ~(4 | 16 | 128);  // gated (MoE expert) GEMMs use the one-group kernel
-  if ((flags & 1) && (flags & 128) && !(flags & 8) && M > 16) {  // balanced ring kernel
-    if (M <= 32) rc = launch_gemm_rw<2>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, ep, stream);
+  if ((flags & 1) && (flags & 128) && !(flags & 8)) {  // balanced ring kernel
+    if (M <= 16) rc = launch_gemm_rw<1>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, ep, stream);
+    else if (M <= 32) rc = launch_gemm_rw<2>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, ep, stream);
     else if (M <= 48) rc = launch_gemm_rw<3>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, ep, stream);
     else rc = launch_gemm_rw<4>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, ep, stream);
     if (rc < 0) return rc;

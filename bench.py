@@ -142,8 +142,10 @@ def main(argv=None):
 
         link = HostLink(c10d._get_default_store(), "bench/all", rank, world, timeout_s=600.0)
         thr = gather_replica_throughput(link, ex, lane // TP, stage, R, batch=min(B, 16))
-        counts = [assign_sessions(M * B * R, thr).count(r) for r in range(R)]
-        n_sessions = min(M * B, counts[lane // TP])  # a slot holds B sessions: never over-admit
+        # M slots of B sessions per pipeline: a faster replica's overflow goes to the others
+        placed = assign_sessions(M * B * R, thr, capacity=M * B)
+        counts = [placed.count(r) for r in range(R)]
+        n_sessions = counts[lane // TP]
         link.close()
         if rank == 0:
             print(f"replica throughput (tok/s, probe batch {min(B, 16)}): {[round(t, 1) for t in thr]} -> "

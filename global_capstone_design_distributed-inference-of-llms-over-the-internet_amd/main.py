@@ -560,6 +560,7 @@ def run_stage_server_with_load_balancing(args, device, cuts: List[int], stop: Op
         srv.throughput = thr
         srv.link_mbps = mbps
         srv.store_once()
+        logger.info(f"Announced blocks [{s}, {e}) throughput={thr:.1f} rps link={mbps} Mbit/s")
         if on_ready is not None:
             on_ready(dht, srv)
         rebalance = False

@@ -22,6 +22,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from run_all import MADDR_RE, READY_RE, wait_log  # noqa: E402
 
 SEL_RE = re.compile(r"Selected blocks \[(\d+), (\d+)\)")
+ANN_RE = re.compile(r"Announced blocks \[(\d+), (\d+)\)")
 
 
 def main():
@@ -53,7 +54,10 @@ def main():
             wait_log(log, READY_RE, 600, procs[-1])
             sel = wait_log(log, SEL_RE, 60, procs[-1])
             print(f"server {k}: Selected blocks [{sel.group(1)}, {sel.group(2)})", flush=True)
-            time.sleep(1.0)  # let the registry replicate before the next server chooses
+            # the next server chooses only once this one's span (with its measured throughput)
+            # is in the registry: a fixed sleep raced the throughput probe on a loaded host
+            wait_log(log, ANN_RE, 300, procs[-1])
+            time.sleep(0.5)
         cmd = [sys.executable, "-m", "src.main", "--model", a.model, "--splits", a.splits, "--stage", "0",
                "--use_load_balancing", "--dht_initial_peers", first, "--max_new_tokens", str(a.max_new_tokens),
                "--temperature", "0", "--device", "cuda:0" if a.gpus else "cpu"]

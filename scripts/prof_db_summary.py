@@ -1,14 +1,19 @@
 #!/usr/bin/env python3
 """Summarise a rocprofv3 SQLite (rocpd) kernel trace: per-kernel time over the last third of the
-dispatches (decode steady state).  Usage: prof_db_summary.py run_results.db [fraction]"""
+dispatches (decode steady state).  Usage: prof_db_summary.py run_results.db [fraction | <N>ms]
+(``40ms``: the kernels that start in the trace's last 40 ms instead of a fraction of them)"""
 import collections
 import sqlite3
 import sys
 
 db = sqlite3.connect(sys.argv[1])
-frac = float(sys.argv[2]) if len(sys.argv) > 2 else 0.33
+arg = sys.argv[2] if len(sys.argv) > 2 else "0.33"
 rows = db.execute("select name, grid_x, grid_y, grid_z, start, end, vgpr_count from kernels order by start").fetchall()
-tail = rows[-int(len(rows) * frac):]
+if arg.endswith("ms"):
+    t_end = max(r[5] for r in rows)
+    tail = [r for r in rows if r[4] >= t_end - float(arg[:-2]) * 1e6]
+else:
+    tail = rows[-int(len(rows) * float(arg)):]
 d = collections.defaultdict(list)
 for name, gx, gy, gz, s, e, vg in tail:
     d[(name.split("(")[0][:60], f"{gx}x{gy}x{gz}", vg)].append(e - s)

@@ -22,3 +22,15 @@ def test_place_one_follows_throughput_and_skips_dead():
     plans = r.fail(1)
     assert {p.replica for p in plans} <= {0, 2} and len(plans) == 2
     assert all(r.place_one(f"t{i}", [1]) != 1 for i in range(5))
+
+
+def test_assign_sessions_capacity_redistributes_overflow():
+    a = assign_sessions(12, [7.0, 5.0], capacity=6)
+    assert a.count(0) == 6 and a.count(1) == 6
+    a = assign_sessions(12, [10.0, 1.0, 1.0], capacity=5)
+    assert [a.count(r) for r in range(3)] == [5, 4, 3] or sorted(a.count(r) for r in range(3)) == [3, 4, 5]
+    assert len(a) == 12 and max(a.count(r) for r in range(3)) <= 5
+    import pytest
+
+    with pytest.raises(ValueError):
+        assign_sessions(13, [1.0, 1.0], capacity=6)

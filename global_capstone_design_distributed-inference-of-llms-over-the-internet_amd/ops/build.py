@@ -70,18 +70,40 @@ def build(force: bool = False, jobs: int = 0, verbose: bool = False) -> str:
     common = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-I" + CSRC]
     objs = []
     cmds = []
+    hdr_tag = _digest(headers, extra=ARCH + HIPCC)
+
+    def stale(src, obj):
+        # per-object stamp: the source + every csrc header (a kernel edit rebuilds one object)
+        t = _digest([src], extra=hdr_tag)
+        st = obj + ".stamp"
+        if force or not os.path.exists(obj) or not os.path.exists(st) or open(st).read().strip() != t:
+            return t
+        return None
+
     for src in hips:
         obj = os.path.join(BUILD, os.path.basename(src) + ".o")
         objs.append(obj)
-        cmds.append([HIPCC] + common + ["-c", src, "-o", obj])
+        t = stale(src, obj)
+        if t is not None:
+            cmds.append(([HIPCC] + common + ["-c", src, "-o", obj], obj, t))
     bobj = os.path.join(BUILD, "bindings.o")
     objs.append(bobj)
-    # host-only translation unit (torch headers): plain C++, no device pass
-    cmds.append([HIPCC, "-x", "c++", "-O2", "-fPIC", "-std=c++17", "-DUSE_ROCM=1", "-D__HIP_PLATFORM_AMD__=1",
-                 "-I/opt/rocm/include"] + [f"-I{p}" for p in inc] + ["-c", binding, "-o", bobj])
-    jobs = jobs or min(len(cmds), os.cpu_count() or 4, 8)
+    t = stale(binding, bobj)
+    if t is not None:
+        # host-only translation unit (torch headers): plain C++, no device pass
+        cmds.append(([HIPCC, "-x", "c++", "-O2", "-fPIC", "-std=c++17", "-DUSE_ROCM=1", "-D__HIP_PLATFORM_AMD__=1",
+                      "-I/opt/rocm/include"] + [f"-I{p}" for p in inc] + ["-c", binding, "-o", bobj], bobj, t))
+
+    def run_one(job):
+        cmd, obj, t = job
+        out = _run(cmd)
+        with open(obj + ".stamp", "w") as f:
+            f.write(t)
+        return out
+
+    jobs = jobs or max(1, min(len(cmds), os.cpu_count() or 4, 8))
     with cf.ThreadPoolExecutor(jobs) as ex:
-        for out in ex.map(_run, cmds):
+        for out in ex.map(run_one, cmds):
             if verbose and out.strip():
                 print(out)
     tmp = LIB_PATH + ".tmp"

@@ -362,6 +362,239 @@ __global__ __launch_bounds__(256) void paged_attn_kernel(
                            packed_mt, s_red);
 }
 
+// Single-pass form of the kernel above (the default; MPAMD_ATTN_1PASS=0 selects the two-pass
+// one).  The two-pass kernel reads K, publishes scores to LDS, waits at a barrier, and only then
+// starts the V stream: every workgroup has ONE stream in flight at a time and the whole grid idles
+// at the barrier (at 64 sessions all 2048 workgroups are resident at once and hit it together).
+// Here each lane keeps an ONLINE softmax over the tokens it sees (running max m, sum l and the
+// 8-dim P.V accumulator, exp2 domain), so the K and V loads of an iteration are issued together
+// (8 x 16 B per lane in flight) and the page ids of the next iteration are fetched into registers
+// while the current one computes (no dependent page-table round trip on the critical path).  The
+// 4 token groups of a wave merge by xor shuffles, the 4 waves through LDS (rescaled by their
+// maxima), and the output / split-K partials (o, m, l) have the two-pass kernel's format.
+template <int D, int NREP, bool ROPE>
+__global__ __launch_bounds__(256) void paged_attn1_kernel(
+    const bf16_t* __restrict__ q, int64_t q_stride, const bf16_t* __restrict__ kc,
+    const bf16_t* __restrict__ vc, const int32_t* __restrict__ block_tables, int bt_stride,
+    const int32_t* __restrict__ q_seq, const int32_t* __restrict__ q_ctx, bf16_t* __restrict__ out,
+    float* __restrict__ part_o, float* __restrict__ part_ml, int nkv, int nh, int page_log2, int PS, int NP,
+    float scale_log2, int packed_mt, RopeFuse rf, int* __restrict__ cnt) {
+  constexpr int LPT = D / 8;
+  constexpr int TPI = 64 / LPT;
+  constexpr int U = 4;
+  constexpr int TPW = TPI * U;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* s_o = smem;                  // [4][NREP][D] per-wave accumulators
+  float* s_m = smem + 4 * NREP * D;   // [4][NREP] per-wave maxima
+  float* s_l = s_m + 4 * NREP;        // [4][NREP] per-wave sums
+
+  const int t = blockIdx.z, p = blockIdx.x;
+  const int hbase = blockIdx.y * NREP;
+  const int g = hbase / (nh / nkv);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int sl = lane % LPT, tg = lane / LPT;
+  const int ctx = q_ctx[t];
+  const int start = p * PS;
+  const int end = min(start + PS, ctx);
+  const int64_t obase = ((int64_t)t * nh + hbase) * D;
+  if (start >= end) {
+    if (NP == 1) {
+      for (int i = tid; i < NREP * D; i += 256)
+        out[packed_mt > 0 ? apk_off(t, hbase * D + i, packed_mt) : obase + i] = 0;
+    } else {
+      if (tid < NREP) {
+        float* ml = part_ml + (((int64_t)t * nh + hbase + tid) * NP + p) * 2;
+        ml[0] = -INFINITY;
+        ml[1] = 0.f;
+      }
+      if (cnt != nullptr)
+        split_combine<D, NREP>(cnt + (int64_t)t * (nh / NREP) + blockIdx.y, NP, part_o, part_ml, t, hbase, nh, out,
+                               packed_mt, smem);
+    }
+    return;
+  }
+  const int page_size = 1 << page_log2;
+  const int32_t* bt = block_tables + (int64_t)q_seq[t] * bt_stride;
+  const int64_t head_off = (int64_t)g * page_size * D + sl * 8;
+  const int64_t page_stride = (int64_t)nkv * page_size * D;
+  // page ids of this wave's first iteration (then prefetched one iteration ahead)
+  int pgn[U];
+  {
+    const int b0 = start + w * TPW;
+#pragma unroll
+    for (int u = 0; u < U; ++u) pgn[u] = bt[min(b0 + u * TPI + tg, end - 1) >> page_log2];
+  }
+
+  float qf[NREP][8];
+  u16x8 kn = (u16x8)(0), vn = (u16x8)(0);
+  int tnew = -1;
+  if constexpr (ROPE) {
+    constexpr int HALF = D / 2;
+    const bf16_t* row = q + (int64_t)t * q_stride;
+    const int c0 = (sl * 8) & (HALF - 1);
+    const bool lo = sl * 8 < HALF;
+    const int po = lo ? HALF : -HALF;
+    const int64_t ps_ = rf.pos[t];
+    const f32x4 ca = *reinterpret_cast<const f32x4*>(rf.cos_t + ps_ * HALF + c0);
+    const f32x4 cb = *reinterpret_cast<const f32x4*>(rf.cos_t + ps_ * HALF + c0 + 4);
+    const f32x4 sa = *reinterpret_cast<const f32x4*>(rf.sin_t + ps_ * HALF + c0);
+    const f32x4 sb = *reinterpret_cast<const f32x4*>(rf.sin_t + ps_ * HALF + c0 + 4);
+    auto rot = [&](const bf16_t* hp) {
+      const u16x8 me = *reinterpret_cast<const u16x8*>(hp + sl * 8);
+      const u16x8 ot = *reinterpret_cast<const u16x8*>(hp + sl * 8 + po);
+      u16x8 r;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float c = j < 4 ? ca[j] : cb[j - 4], s = j < 4 ? sa[j] : sb[j - 4];
+        const float x = bf2f(me[j]), y = bf2f(ot[j]);
+        r[j] = lo ? f2bf(x * c - y * s) : f2bf(x * c + y * s);
+      }
+      return r;
+    };
+#pragma unroll
+    for (int r = 0; r < NREP; ++r) {
+      const u16x8 v = rot(row + (hbase + r) * D);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qf[r][j] = bf2f(v[j]) * scale_log2;
+    }
+    kn = rot(row + (nh + g) * D);
+    vn = *reinterpret_cast<const u16x8*>(row + (nh + nkv + g) * D + sl * 8);
+    tnew = ctx - 1;
+    const int64_t slot = rf.slots[t];
+    if (tnew >= start && tnew < end && slot >= 0 && tid < LPT && hbase % (nh / nkv) == 0) {
+      const int64_t pg = slot >> page_log2, off = slot & (page_size - 1);
+      const int64_t dst = pg * page_stride + head_off + off * D;
+      *reinterpret_cast<u16x8*>(rf.kw + dst) = kn;
+      *reinterpret_cast<u16x8*>(rf.vw + dst) = vn;
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < NREP; ++r) {
+      const u16x8 v = *reinterpret_cast<const u16x8*>(q + (int64_t)t * q_stride + (hbase + r) * D + sl * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qf[r][j] = bf2f(v[j]) * scale_log2;
+    }
+  }
+
+  float m[NREP], l[NREP], acc[NREP][8];
+#pragma unroll
+  for (int r = 0; r < NREP; ++r) {
+    m[r] = -INFINITY;
+    l[r] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[r][j] = 0.f;
+  }
+  for (int base = start + w * TPW; base < end; base += 4 * TPW) {
+    u16x8 kv[U], vv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int tc = min(base + u * TPI + tg, end - 1);
+      const int64_t off = (int64_t)pgn[u] * page_stride + head_off + (int64_t)(tc & (page_size - 1)) * D;
+      kv[u] = *reinterpret_cast<const u16x8*>(kc + off);
+      vv[u] = *reinterpret_cast<const u16x8*>(vc + off);
+    }
+    // next iteration's page ids, in flight behind the K / V loads
+    const int nb = base + 4 * TPW;
+#pragma unroll
+    for (int u = 0; u < U; ++u) pgn[u] = bt[min(nb + u * TPI + tg, end - 1) >> page_log2];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      asm volatile("" : "+v"(kv[u]));
+      asm volatile("" : "+v"(vv[u]));
+    }
+    if constexpr (ROPE) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int tok = base + u * TPI + tg;
+        kv[u] = tok == tnew ? kn : kv[u];
+        vv[u] = tok == tnew ? vn : vv[u];
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < NREP; ++r) {
+      float s[U];
+      float mx = m[r];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        float d = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) d += qf[r][j] * bf2f(kv[u][j]);
+        d = group_sum<LPT>(d);
+        s[u] = base + u * TPI + tg < end ? d : -INFINITY;
+        mx = fmaxf(mx, s[u]);
+      }
+      const float mref = mx == -INFINITY ? 0.f : mx;
+      const float sc = exp2f(m[r] - mref);
+      l[r] *= sc;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[r][j] *= sc;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const float pr = exp2f(s[u] - mref);
+        l[r] += pr;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[r][j] += pr * bf2f(vv[u][j]);
+      }
+      m[r] = mx;
+    }
+  }
+  // merge the token groups of the wave (lanes sl, sl + LPT, ...)
+#pragma unroll
+  for (int o = LPT; o < 64; o <<= 1) {
+#pragma unroll
+    for (int r = 0; r < NREP; ++r) {
+      const float mo = __shfl_xor(m[r], o, 64);
+      const float lo = __shfl_xor(l[r], o, 64);
+      const float M = fmaxf(m[r], mo);
+      const float mref = M == -INFINITY ? 0.f : M;
+      const float a = exp2f(m[r] - mref), b = exp2f(mo - mref);
+      l[r] = l[r] * a + lo * b;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[r][j] = acc[r][j] * a + __shfl_xor(acc[r][j], o, 64) * b;
+      m[r] = M;
+    }
+  }
+  if (tg == 0) {
+#pragma unroll
+    for (int r = 0; r < NREP; ++r) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s_o[(w * NREP + r) * D + sl * 8 + j] = acc[r][j];
+      if (sl == 0) {
+        s_m[w * NREP + r] = m[r];
+        s_l[w * NREP + r] = l[r];
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < NREP * D; i += 256) {
+    const int r = i / D, d = i - r * D;
+    float M = s_m[r];
+#pragma unroll
+    for (int ww = 1; ww < 4; ++ww) M = fmaxf(M, s_m[ww * NREP + r]);
+    const float mref = M == -INFINITY ? 0.f : M;
+    float o = 0.f, L = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < 4; ++ww) {
+      const float a = exp2f(s_m[ww * NREP + r] - mref);
+      o += a * s_o[(ww * NREP + r) * D + d];
+      L += a * s_l[ww * NREP + r];
+    }
+    if (NP == 1) {
+      out[packed_mt > 0 ? apk_off(t, hbase * D + i, packed_mt) : obase + i] = f2bf(o / L);
+    } else {
+      const int64_t hp = ((int64_t)t * nh + hbase + r) * NP + p;
+      part_o[hp * D + d] = o;
+      if (d == 0) {
+        part_ml[hp * 2] = M;
+        part_ml[hp * 2 + 1] = L;
+      }
+    }
+  }
+  if (NP > 1 && cnt != nullptr)
+    split_combine<D, NREP>(cnt + (int64_t)t * (nh / NREP) + blockIdx.y, NP, part_o, part_ml, t, hbase, nh, out,
+                           packed_mt, s_m);
+}
+
 // Combine split-K partials: one workgroup (D threads) per (query row, head).
 __global__ void paged_attn_reduce_kernel(const float* __restrict__ part_o, const float* __restrict__ part_ml,
                                          bf16_t* __restrict__ out, int NP, int D, int nh, int packed_mt) {
@@ -393,14 +626,25 @@ static void launch_attn(const void* q, int64_t q_stride, const void* kc, const v
                         int bt_stride, const int32_t* q_seq, const int32_t* q_ctx, void* out, float* ws_o,
                         float* ws_ml, int T, int nkv, int nh, int page_log2, int PS, int NP, float scale_log2,
                         int packed_mt, const RopeFuse& rf, int* cnt, hipStream_t stream) {
-  const size_t lds = (size_t)(NREP * PS + 8 * NREP + 4 * NREP * D) * sizeof(float);
+  static const bool one_pass = [] {
+    const char* v = getenv("MPAMD_ATTN_1PASS");
+    return !(v && v[0] == '0');
+  }();
+  const size_t lds = one_pass ? (size_t)(4 * NREP * D + 8 * NREP + 4) * sizeof(float)
+                              : (size_t)(NREP * PS + 8 * NREP + 4 * NREP * D) * sizeof(float);
   auto go = [&](auto kern) {
     hipLaunchKernelGGL(kern, dim3(NP, nh / NREP, T), dim3(256), lds, stream, (const bf16_t*)q, q_stride,
                        (const bf16_t*)kc, (const bf16_t*)vc, bt, bt_stride, q_seq, q_ctx, (bf16_t*)out, ws_o, ws_ml,
                        nkv, nh, page_log2, PS, NP, scale_log2, packed_mt, rf, cnt);
   };
-  if (rf.pos) go(paged_attn_kernel<D, NREP, true>);
-  else go(paged_attn_kernel<D, NREP, false>);
+  if (one_pass) {
+    if (rf.pos) go(paged_attn1_kernel<D, NREP, true>);
+    else go(paged_attn1_kernel<D, NREP, false>);
+  } else if (rf.pos) {
+    go(paged_attn_kernel<D, NREP, true>);
+  } else {
+    go(paged_attn_kernel<D, NREP, false>);
+  }
 }
 
 }  // namespace mp

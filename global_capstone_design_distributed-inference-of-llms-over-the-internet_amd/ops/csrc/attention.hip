@@ -372,8 +372,10 @@ __global__ __launch_bounds__(256) void paged_attn_kernel(
 // while the current one computes (no dependent page-table round trip on the critical path).  The
 // 4 token groups of a wave merge by xor shuffles, the 4 waves through LDS (rescaled by their
 // maxima), and the output / split-K partials (o, m, l) have the two-pass kernel's format.
-template <int D, int NREP, bool ROPE>
-__global__ __launch_bounds__(256) void paged_attn1_kernel(
+// NW = waves per workgroup: 4, or 16 when the grid is small (batch 1: one workgroup per head
+// over the whole context, each wave a 16-token slice; no split-K, no reduce launch).
+template <int D, int NREP, bool ROPE, int NW>
+__global__ __launch_bounds__(NW * 64) void paged_attn1_kernel(
     const bf16_t* __restrict__ q, int64_t q_stride, const bf16_t* __restrict__ kc,
     const bf16_t* __restrict__ vc, const int32_t* __restrict__ block_tables, int bt_stride,
     const int32_t* __restrict__ q_seq, const int32_t* __restrict__ q_ctx, bf16_t* __restrict__ out,
@@ -384,9 +386,10 @@ __global__ __launch_bounds__(256) void paged_attn1_kernel(
   constexpr int U = 4;
   constexpr int TPW = TPI * U;
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* s_o = smem;                  // [4][NREP][D] per-wave accumulators
-  float* s_m = smem + 4 * NREP * D;   // [4][NREP] per-wave maxima
-  float* s_l = s_m + 4 * NREP;        // [4][NREP] per-wave sums
+  constexpr int NT_ = NW * 64;
+  float* s_o = smem;                   // [NW][NREP][D] per-wave accumulators
+  float* s_m = smem + NW * NREP * D;   // [NW][NREP] per-wave maxima
+  float* s_l = s_m + NW * NREP;        // [NW][NREP] per-wave sums
 
   const int t = blockIdx.z, p = blockIdx.x;
   const int hbase = blockIdx.y * NREP;
@@ -399,7 +402,7 @@ __global__ __launch_bounds__(256) void paged_attn1_kernel(
   const int64_t obase = ((int64_t)t * nh + hbase) * D;
   if (start >= end) {
     if (NP == 1) {
-      for (int i = tid; i < NREP * D; i += 256)
+      for (int i = tid; i < NREP * D; i += NT_)
         out[packed_mt > 0 ? apk_off(t, hbase * D + i, packed_mt) : obase + i] = 0;
     } else {
       if (tid < NREP) {
@@ -484,7 +487,7 @@ __global__ __launch_bounds__(256) void paged_attn1_kernel(
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[r][j] = 0.f;
   }
-  for (int base = start + w * TPW; base < end; base += 4 * TPW) {
+  for (int base = start + w * TPW; base < end; base += NW * TPW) {
     u16x8 kv[U], vv[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -494,7 +497,7 @@ __global__ __launch_bounds__(256) void paged_attn1_kernel(
       vv[u] = *reinterpret_cast<const u16x8*>(vc + off);
     }
     // next iteration's page ids, in flight behind the K / V loads
-    const int nb = base + 4 * TPW;
+    const int nb = base + NW * TPW;
 #pragma unroll
     for (int u = 0; u < U; ++u) pgn[u] = bt[min(nb + u * TPI + tg, end - 1) >> page_log2];
 #pragma unroll
@@ -566,15 +569,15 @@ __global__ __launch_bounds__(256) void paged_attn1_kernel(
     }
   }
   __syncthreads();
-  for (int i = tid; i < NREP * D; i += 256) {
+  for (int i = tid; i < NREP * D; i += NT_) {
     const int r = i / D, d = i - r * D;
     float M = s_m[r];
 #pragma unroll
-    for (int ww = 1; ww < 4; ++ww) M = fmaxf(M, s_m[ww * NREP + r]);
+    for (int ww = 1; ww < NW; ++ww) M = fmaxf(M, s_m[ww * NREP + r]);
     const float mref = M == -INFINITY ? 0.f : M;
     float o = 0.f, L = 0.f;
 #pragma unroll
-    for (int ww = 0; ww < 4; ++ww) {
+    for (int ww = 0; ww < NW; ++ww) {
       const float a = exp2f(s_m[ww * NREP + r] - mref);
       o += a * s_o[(ww * NREP + r) * D + d];
       L += a * s_l[ww * NREP + r];
@@ -630,16 +633,26 @@ static void launch_attn(const void* q, int64_t q_stride, const void* kc, const v
     const char* v = getenv("MPAMD_ATTN_1PASS");
     return !(v && v[0] == '0');
   }();
-  const size_t lds = one_pass ? (size_t)(4 * NREP * D + 8 * NREP + 4) * sizeof(float)
+  // 16-wave workgroups when the grid cannot fill the chip with 4-wave ones
+  static const int wide_max = [] {
+    const char* v = getenv("MPAMD_ATTN_WIDE_WGS");
+    return v ? atoi(v) : 512;
+  }();
+  const bool wide = one_pass && (int64_t)NP * (nh / NREP) * T <= wide_max;
+  const int nw = wide ? 16 : 4;
+  const size_t lds = one_pass ? (size_t)(nw * NREP * D + 2 * nw * NREP + 4) * sizeof(float)
                               : (size_t)(NREP * PS + 8 * NREP + 4 * NREP * D) * sizeof(float);
   auto go = [&](auto kern) {
-    hipLaunchKernelGGL(kern, dim3(NP, nh / NREP, T), dim3(256), lds, stream, (const bf16_t*)q, q_stride,
+    hipLaunchKernelGGL(kern, dim3(NP, nh / NREP, T), dim3(64 * nw), lds, stream, (const bf16_t*)q, q_stride,
                        (const bf16_t*)kc, (const bf16_t*)vc, bt, bt_stride, q_seq, q_ctx, (bf16_t*)out, ws_o, ws_ml,
                        nkv, nh, page_log2, PS, NP, scale_log2, packed_mt, rf, cnt);
   };
-  if (one_pass) {
-    if (rf.pos) go(paged_attn1_kernel<D, NREP, true>);
-    else go(paged_attn1_kernel<D, NREP, false>);
+  if (one_pass && wide) {
+    if (rf.pos) go(paged_attn1_kernel<D, NREP, true, 16>);
+    else go(paged_attn1_kernel<D, NREP, false, 16>);
+  } else if (one_pass) {
+    if (rf.pos) go(paged_attn1_kernel<D, NREP, true, 4>);
+    else go(paged_attn1_kernel<D, NREP, false, 4>);
   } else if (rf.pos) {
     go(paged_attn_kernel<D, NREP, true>);
   } else {

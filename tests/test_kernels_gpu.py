@@ -93,7 +93,7 @@ def _attn_case(nh, nkv, D, ctxs, ps=64, multi_q=False):
 
 @pytest.mark.parametrize("nh,nkv,D", [(32, 32, 128), (32, 8, 128), (64, 8, 128), (16, 8, 128), (12, 12, 64),
                                       (8, 2, 64)])
-@pytest.mark.parametrize("ctxs", [[1, 5, 64, 200], [1000, 3], [4097]])
+@pytest.mark.parametrize("ctxs", [[1, 5, 64, 200], [1000, 3], [4097], [150] * 40])
 def test_paged_attention_decode(nh, nkv, D, ctxs):
     q, kc, vc, bt, q_seq, q_ctx = _attn_case(nh, nkv, D, ctxs)
     scale = 1 / math.sqrt(D)

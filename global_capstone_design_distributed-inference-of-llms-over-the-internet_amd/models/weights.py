@@ -66,6 +66,16 @@ class LlamaLayer:
     gate_up_s: Optional[torch.Tensor] = None
     down_q: Optional[torch.Tensor] = None
     down_s: Optional[torch.Tensor] = None
+    # fp8 W8A16 copies (ops.w8_from_fp8: the bf16 fragment order at 1 byte per weight) + fp32
+    # per-output-channel scales, for the fused-norm decode GEMMs of an fp8 stage
+    qkv_w8: Optional[torch.Tensor] = None
+    qkv_ws: Optional[torch.Tensor] = None
+    o_w8: Optional[torch.Tensor] = None
+    o_ws: Optional[torch.Tensor] = None
+    gate_up_w8: Optional[torch.Tensor] = None
+    gate_up_ws: Optional[torch.Tensor] = None
+    down_w8: Optional[torch.Tensor] = None
+    down_ws: Optional[torch.Tensor] = None
     # Mixtral sparse-MoE block (HF MixtralSparseMoeBlock): ``router`` [E, H]; gate_up / down
     # (and their packed copies) are then stacked per expert: [E, 2F, H] / [E, H, F]
     router: Optional[torch.Tensor] = None
@@ -80,15 +90,22 @@ class LlamaLayer:
 
     @property
     def fp8(self) -> bool:
-        return self.qkv_q is not None
+        return self.qkv_q is not None or self.qkv_w8 is not None
+
+    @property
+    def w8(self) -> bool:
+        return self.qkv_w8 is not None
 
     def dense(self, name: str, dtype=torch.bfloat16) -> torch.Tensor:
-        """Row-major weight ``name`` (dequantized on the fly when only the fp8 copy is kept)."""
+        """Row-major weight ``name`` (dequantized on the fly when only an fp8 copy is kept; a
+        W8A16 layer's qkv / gate_up then carry the folded norm weights, see ``folded``)."""
         w = getattr(self, name)
         if w is not None:
             return w
         from .. import ops
 
+        if getattr(self, name + "_w8") is not None:
+            return ops.unpack_weight_w8(getattr(self, name + "_w8"), getattr(self, name + "_ws"), dtype)
         return ops.unpack_weight_fp8(getattr(self, name + "_q"), getattr(self, name + "_s"), dtype)
 
 
@@ -197,9 +214,36 @@ class StageWeights:
                     setattr(lay, name, None)
                     setattr(lay, name + "_p", None)
 
+    def prepare_w8a16(self, fold_norms: bool = True) -> None:
+        """Convert every fp8 layer to the W8A16 layout (ops.w8_from_fp8) and drop the W8A8
+        copies.  ``fold_norms``: qkv / gate_up are dequantized, multiplied by the input /
+        post-attention RMSNorm weight along K and re-quantized (W' = W diag(g), per-output-channel
+        scales), as the bf16 fused-norm path folds them into its packed weights; ``folded`` is set
+        and every path over these weights normalises with a unit RMSNorm weight."""
+        from .. import ops
+
+        for lay in self.layers:
+            if not isinstance(lay, LlamaLayer) or lay.w8 or lay.qkv_q is None:
+                continue
+            for name, g in (("qkv", lay.input_norm), ("o", None), ("gate_up", lay.post_norm), ("down", None)):
+                q, sc = getattr(lay, name + "_q"), getattr(lay, name + "_s")
+                if fold_norms and g is not None:
+                    w = ops.unpack_weight_fp8(q, sc, torch.float32) * g.float()[None, :]
+                    q, sc = ops.pack_weight_fp8(w)
+                    del w
+                setattr(lay, name + "_w8", ops.w8_from_fp8(q))
+                setattr(lay, name + "_ws", sc)
+                setattr(lay, name + "_q", None)
+                setattr(lay, name + "_s", None)
+            lay.folded = bool(fold_norms)
+
     @property
     def fp8(self) -> bool:
         return bool(self.layers) and all(isinstance(L, LlamaLayer) and L.fp8 for L in self.layers)
+
+    @property
+    def w8(self) -> bool:
+        return bool(self.layers) and all(isinstance(L, LlamaLayer) and L.w8 for L in self.layers)
 
     def tensors(self):
         seen = set()

@@ -781,3 +781,108 @@ def linear_fp8(a8, a_scale, wq, w_scale, M: int, out=None, epilogue: int = 0, re
     torch.ops.mpamd.gemm_fp8(a8, a_scale, wq, w_scale, out, residual, int(epilogue), int(M), int(bool(out_packed)),
                              kind, gemm_workspace(a8.device) if kind == 2 else None)
     return out
+
+
+# ---------------------------------------------------------------------------------------
+# W8A16 decode GEMM (csrc/gemm.hip mp_gemm_w8): fp8 weights dequantized in registers into the
+# bf16 MFMA, bf16 activations - the fused-norm decode path of an fp8 stage (no activation
+# quantization launches).  Weight layout: the bf16 fragment order at 1 byte per element.
+def w8_from_fp8(wq: torch.Tensor) -> torch.Tensor:
+    """W8A8 layout uint8 [N/16, K/64, 64, 16] -> W8A16 layout [N/16, K/32, 64, 8] (same bytes:
+    the two 32-deep k-slices of a 16-byte lane chunk become consecutive k-slices)."""
+    n16, k64 = wq.shape[0], wq.shape[1]
+    return wq.view(n16, k64, 64, 2, 8).permute(0, 1, 3, 2, 4).reshape(n16, 2 * k64, 64, 8).contiguous()
+
+
+def fp8_from_w8(w8: torch.Tensor) -> torch.Tensor:
+    n16, k32 = w8.shape[0], w8.shape[1]
+    return w8.view(n16, k32 // 2, 2, 64, 8).permute(0, 1, 3, 2, 4).reshape(n16, k32 // 2, 64, 16)
+
+
+def unpack_weight_w8(w8: torch.Tensor, w_scale: torch.Tensor, dtype=torch.bfloat16) -> torch.Tensor:
+    return ref.unpack_weight_fp8(fp8_from_w8(w8), w_scale, dtype)
+
+
+_W8_KERNELS = {"rw": 128, "rwk": 256}
+_W8_CHOICE = {}  # (m_bucket, N, K, epilogue) -> "rw" / "rwk", from autotune_w8
+_W8_MODE = os.environ.get("MPAMD_W8_KERNEL", "auto")
+
+
+def _w8_kernel(M: int, N: int, K: int, epilogue: int) -> str:
+    rwk_ok = epilogue != 1 and N % 2048 == 0
+    mode = _W8_MODE if _W8_MODE != "auto" else _W8_CHOICE.get((_m_bucket(M), N, K, int(epilogue)), "rw")
+    return "rwk" if (mode == "rwk" and rwk_ok) else "rw"
+
+
+def linear_w8(x, w8, w_scale, a_rows: int, out=None, epilogue: int = 0, residual=None, out_packed: bool = False,
+              ss_in=None, eps: float = 0.0, ap_out=None, ss_out=None, ss_zero=None):
+    """``linear`` with an fp8 weight (``w8_from_fp8`` layout + per-column scales) and a PACKED
+    bf16 activation of ``a_rows`` rows (M <= 64): same epilogues as the bf16 decode GEMM
+    (0 with optional ``ss_in`` row scale, packed SwiGLU, 3 = residual-stream producer)."""
+    M = int(a_rows)
+    N, K = 16 * w8.shape[0], 32 * w8.shape[1]
+    if not _native(x):
+        return linear(x, None, out=out, epilogue=epilogue, residual=residual, wp=pack_weight(
+            unpack_weight_w8(w8, w_scale, x.dtype)), a_rows=M, out_packed=out_packed, ss_in=ss_in, eps=eps,
+            ap_out=ap_out, ss_out=ss_out, ss_zero=ss_zero)
+    ncols = N // 2 if epilogue == 1 else N
+    if out is None:
+        out = (torch.empty(packed_numel(M, ncols), dtype=x.dtype, device=x.device) if out_packed
+               else torch.empty(M, ncols, dtype=x.dtype, device=x.device))
+    kern = _w8_kernel(M, N, K, epilogue)
+    flags = 1 | (2 if out_packed else 0) | _W8_KERNELS[kern]
+    torch.ops.mpamd.gemm_w8(x, w8, w_scale, out, residual, int(epilogue), M, flags,
+                            gemm_workspace(x.device) if kern == "rwk" else None, ap_out, ss_out, ss_zero, ss_in,
+                            1.0 / K, float(eps))
+    return out
+
+
+def autotune_w8(shapes, device, ms=(4, 16, 32, 48, 64), iters: int = 12, rounds: int = 3) -> dict:
+    """``autotune_gemm`` for the W8A16 GEMM: ring vs split-K ring per (N, K, epilogue) and M
+    bucket, on fp8 weights rotated over ~1 GiB (decode never finds them in the Infinity Cache)."""
+    global _W8_MODE
+    device = torch.device(device)
+    if device.type != "cuda":
+        return {}
+    require_native()
+    gemm_workspace(device)
+    saved = _W8_MODE
+    try:
+        for (N, K, epi) in shapes:
+            todo = [M for M in ms if (_m_bucket(M), N, K, int(epi)) not in _W8_CHOICE]
+            if not todo:
+                continue
+            if epi == 1 or N % 2048:
+                for M in todo:
+                    _W8_CHOICE[(_m_bucket(M), N, K, int(epi))] = "rw"
+                continue
+            copies = max(1, min(8, (1 << 30) // (N * K)))
+            wqs = [torch.randint(0, 0x77, (N // 16, K // 32, 64, 8), dtype=torch.uint8, device=device)
+                   for _ in range(copies)]
+            wsc = torch.full((N,), 1e-3, dtype=torch.float32, device=device)
+            for M in todo:
+                xp = pack_act(torch.randn(M, K, device=device).to(torch.bfloat16))
+                res = torch.zeros(M, N, dtype=torch.bfloat16, device=device) if epi == 3 else None
+                extra = {}
+                if epi == 3:
+                    extra = dict(ap_out=torch.zeros(packed_numel(M, N), dtype=torch.bfloat16, device=device),
+                                 ss_out=norm_stats_buffer(device)[0], ss_zero=norm_stats_buffer(device)[0])
+                out = res if epi == 3 else torch.empty(M, N, dtype=torch.bfloat16, device=device)
+                t = {k: float("inf") for k in _W8_KERNELS}
+                for _ in range(rounds):
+                    for name in _W8_KERNELS:
+                        _W8_MODE = name
+                        for i in range(2):
+                            linear_w8(xp, wqs[i % copies], wsc, M, out=out, epilogue=epi, residual=res, **extra)
+                        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                        e0.record()
+                        for i in range(iters):
+                            linear_w8(xp, wqs[i % copies], wsc, M, out=out, epilogue=epi, residual=res, **extra)
+                        e1.record()
+                        e1.synchronize()
+                        t[name] = min(t[name], e0.elapsed_time(e1) / iters)
+                _W8_CHOICE[(_m_bucket(M), N, K, int(epi))] = min(t, key=t.get)
+            del wqs
+    finally:
+        _W8_MODE = saved
+    return dict(_W8_CHOICE)

@@ -50,6 +50,9 @@ int mp_gemm_bf16(const void* x, int64_t x_stride, const void* w, void* y, int64_
                  void* ap, void* ss_out, void* ss_zero, const void* ss_in, float inv_k, float eps,
                  hipStream_t stream);
 int mp_gemm_ss_elems();
+int mp_gemm_w8(const void* x, const void* wq, const float* wsc, void* y, int64_t y_stride, const void* res,
+               int64_t res_stride, int M, int N, int K, int epilogue, int flags, void* ws, void* ap, void* ss_out,
+               void* ss_zero, const void* ss_in, float inv_k, float eps, hipStream_t stream);
 int mp_pack_act(const void* x, int64_t xs, void* ap, int M, int K, hipStream_t stream);
 int mp_pack_weight(const void* w, void* wp, int N, int K, hipStream_t stream);
 }
@@ -465,6 +468,65 @@ at::Tensor pack_weight(const at::Tensor& w) {
   return wp;
 }
 
+// W8A16 decode GEMM (gemm.hip mp_gemm_w8): packed bf16 x (M rows), fp8 weight Wq uint8
+// [N/16, K/32, 64, 8] + per-column fp32 scales; flags as mp_gemm_w8 (bit 1 packed SwiGLU out,
+// bit 7 ring, bit 8 split-K ring)
+void gemm_w8(const at::Tensor& x, const at::Tensor& wq, const at::Tensor& wsc, at::Tensor& y,
+             const c10::optional<at::Tensor>& residual, int64_t epilogue, int64_t M_, int64_t flags,
+             const c10::optional<at::Tensor>& workspace, const c10::optional<at::Tensor>& ap,
+             const c10::optional<at::Tensor>& ss_out, const c10::optional<at::Tensor>& ss_zero,
+             const c10::optional<at::Tensor>& ss_in, double inv_k, double eps) {
+  check_bf16_cuda(x, "x");
+  check_bf16_cuda(y, "y");
+  MP_CHECK(wq.is_cuda() && wq.scalar_type() == at::kByte && wq.dim() == 4 && wq.size(2) == 64 && wq.size(3) == 8 &&
+               wq.is_contiguous(),
+           "wq must be an fp8 weight uint8 [N/16, K/32, 64, 8] (ops.pack_weight_w8)");
+  const int N = 16 * wq.size(0), K = 32 * wq.size(1);
+  MP_CHECK(wsc.is_cuda() && wsc.scalar_type() == at::kFloat && wsc.is_contiguous() && wsc.numel() == N,
+           "wsc: fp32 [N] column scales");
+  const int M = (int)M_;
+  const bool opk = flags & 2;
+  MP_CHECK(M >= 0 && M <= 64, "gemm_w8: 0 <= M <= 64");
+  MP_CHECK(x.is_contiguous() && x.numel() >= packed_numel(M, K), "packed x too small");
+  const int ncols = epilogue == 1 ? N / 2 : N;
+  if (opk) {
+    MP_CHECK(epilogue == 1 && y.is_contiguous() && y.numel() >= packed_numel(M, ncols), "packed y");
+  } else {
+    check_rows(y, "y");
+    MP_CHECK(y.size(0) == M && y.size(1) == ncols, "y shape");
+  }
+  MP_CHECK(epilogue == 0 || epilogue == 3 || (epilogue == 1 && opk), "gemm_w8: epilogue 0, 3 or packed SwiGLU");
+  const void* rp = nullptr;
+  int64_t rs = 0;
+  if (residual.has_value()) {
+    check_bf16_cuda(*residual, "residual");
+    check_rows(*residual, "residual");
+    MP_CHECK(residual->size(0) == M && residual->size(1) == N, "residual shape");
+    rp = residual->data_ptr();
+    rs = residual->stride(0);
+  }
+  void* app = nullptr;
+  if (ap.has_value()) {
+    check_bf16_cuda(*ap, "ap");
+    MP_CHECK(ap->is_contiguous() && ap->numel() >= packed_numel(M, N), "ap: packed [ceil(M/16)*16*N]");
+    app = ap->data_ptr();
+  }
+  MP_CHECK(epilogue != 3 || (app != nullptr && rp != nullptr), "epilogue 3 needs residual and ap");
+  void* ws = nullptr;
+  if (workspace.has_value()) {
+    MP_CHECK(workspace->is_cuda() && workspace->is_contiguous() &&
+                 workspace->numel() * workspace->element_size() >= mp_gemm_workspace_bytes(),
+             "gemm workspace too small (ops.gemm_workspace)");
+    ws = workspace->data_ptr();
+  }
+  const int rc = mp_gemm_w8(x.data_ptr(), wq.data_ptr(), wsc.data_ptr<float>(), y.data_ptr(), opk ? 0 : y.stride(0),
+                            rp, rs, M, N, K, (int)epilogue, (int)flags, ws, app, opt_ss(ss_out, "ss_out"),
+                            opt_ss(ss_zero, "ss_zero"), opt_ss(ss_in, "ss_in"), (float)inv_k, (float)eps, cur_stream());
+  TORCH_CHECK(rc != 1, "mpamd: gemm_w8: no fp8-weight kernel covers M=", M, " N=", N, " K=", K, " epilogue=",
+              epilogue);
+  check_launch(rc, "gemm_w8");
+}
+
 int64_t gemm_workspace_bytes() { return mp_gemm_workspace_bytes(); }
 void fp8_gemm_kernel(int64_t kind) { mp_fp8_set_kernel((int)kind); }
 bool gemm_rw_ok(int64_t M, int64_t N, int64_t K, int64_t epilogue, int64_t out_packed) {
@@ -583,6 +645,10 @@ TORCH_LIBRARY(mpamd, m) {
       "gemm(Tensor x, Tensor wp, Tensor(a!) y, Tensor? residual, int epilogue, int M, int flags, "
       "Tensor(b!)? workspace=None, Tensor? gate=None, Tensor(c!)? ap=None, Tensor(d!)? ss_out=None, "
       "Tensor(e!)? ss_zero=None, Tensor? ss_in=None, float inv_k=0., float eps=0.) -> ()");
+  m.def(
+      "gemm_w8(Tensor x, Tensor wq, Tensor wsc, Tensor(a!) y, Tensor? residual, int epilogue, int M, int flags, "
+      "Tensor(b!)? workspace=None, Tensor(c!)? ap=None, Tensor(d!)? ss_out=None, Tensor(e!)? ss_zero=None, "
+      "Tensor? ss_in=None, float inv_k=0., float eps=0.) -> ()");
   m.def("pack_act(Tensor x, Tensor(a!) ap) -> ()");
   m.def("pack_weight(Tensor w) -> Tensor");
   m.def("quant_act_fp8(Tensor ap, Tensor(a!) a8, Tensor(b!) scale, int M, int K) -> ()");
@@ -606,6 +672,7 @@ TORCH_LIBRARY_IMPL(mpamd, CUDA, m) {
   m.impl("argmax", &argmax);
   m.impl("sample", &sample);
   m.impl("gemm", &gemm);
+  m.impl("gemm_w8", &gemm_w8);
   m.impl("pack_weight", &pack_weight);
   m.impl("pack_act", &pack_act);
   m.impl("quant_act_fp8", &quant_act_fp8);

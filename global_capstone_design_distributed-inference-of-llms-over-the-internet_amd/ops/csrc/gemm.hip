@@ -66,7 +66,30 @@ struct EpiArgs {
   float inv_k;
   float eps;
   int mt_out;
+  const float* wsc;    // fp8 weights (W8A16 kernels): per-output-column dequantization scales
 };
+
+// fp8 (OCP e4m3) weight fragment -> bf16 MFMA B operand (exact: every e4m3 value is a bf16
+// value): the W8A16 form of the ring kernels streams 1 byte per weight and keeps bf16
+// activations (no activation quantization launches between the layer's GEMMs).  8 bytes per lane
+// per k-slice: byte j = W[col][32 ks + 8 q + j], the bf16 fragment's element order.  Four
+// v_cvt_scalef32_pk_bf16_fp8 (unit scale) per fragment; the per-column dequantization scale
+// multiplies the accumulators once, after the K loop.
+typedef __attribute__((ext_vector_type(2))) unsigned u32x2;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
+__device__ __forceinline__ u16x8 f8w_to_bf16(const u32x2& raw) {
+  u16x8 r;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const u16x2 lo = __builtin_bit_cast(u16x2, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(raw[h], 1.0f, false));
+    const u16x2 hi = __builtin_bit_cast(u16x2, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(raw[h], 1.0f, true));
+    r[4 * h + 0] = lo[0];
+    r[4 * h + 1] = lo[1];
+    r[4 * h + 2] = hi[0];
+    r[4 * h + 3] = hi[1];
+  }
+  return r;
+}
 
 __device__ __forceinline__ u64 fx_sq(float f) { return (u64)__float2ull_rn(f * f * SS_FX); }
 
@@ -893,21 +916,33 @@ template <int MT, int NT>
 constexpr int rw_depth() {
   return 190 / (4 * (MT + NT)) >= 8 ? 4 : 2;
 }
+template <int MT, int NT, bool F8>
+constexpr int rw_depth2() {
+  return F8 ? (190 / (4 * MT + 2 * NT) >= 8 ? 4 : 2) : rw_depth<MT, NT>();
+}
 
-template <int MT, int NT, int EPI, bool OPK>
+template <int MT, int NT, int EPI, bool OPK, bool F8 = false>
 __device__ __forceinline__ void rw_body(const bf16_t* __restrict__ x, const bf16_t* __restrict__ wp,
                                         bf16_t* __restrict__ y, int64_t ys, const bf16_t* __restrict__ res, int64_t rs,
                                         int M, int K, int tile0, const EpiArgs& ep, f32x4* red, u64 (*rs_part)[64],
                                         float* rs_lds) {
-  constexpr int R = rw_depth<MT, NT>();
+  constexpr int R = rw_depth2<MT, NT, F8>();
   constexpr int Q = MT * NT;
   constexpr int NQ = (Q + RW_WAVES - 1) / RW_WAVES;  // epilogue quads per wave
   RowScale<EPI < 2, RW_WAVES> rsc;
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nks = K >> 5;
   const int cnt = (nks + RW_WAVES - 1) / RW_WAVES;  // ring steps of the busiest wave
-  const bf16_t* wb = wp + ((int64_t)tile0 * nks) * 512 + lane * 8;
+  // F8: the same fragment order at 1 byte per weight (offsets below count elements)
+  using WT = std::conditional_t<F8, uint8_t, bf16_t>;
+  using BT = std::conditional_t<F8, u32x2, u16x8>;
+  const WT* wb = reinterpret_cast<const WT*>(wp) + ((int64_t)tile0 * nks) * 512 + lane * 8;
   const bf16_t* xl = x + lane * 8;
+  float wsc[NT];
+  if constexpr (F8) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) wsc[t] = ep.wsc[(tile0 + t) * 16 + (lane & 15)];
+  }
 
   // EPI 3: the residual quads this wave finalises, in flight during the main loop
   u16x4 rpre[NQ];
@@ -926,12 +961,13 @@ __device__ __forceinline__ void rw_body(const bf16_t* __restrict__ x, const bf16
   for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[mt][t] = (f32x4)(0.f);
-  u16x8 ra[R][MT], rb[R][NT];
+  u16x8 ra[R][MT];
+  BT rb[R][NT];
 #define RW_LOAD(s, i)                                                                                        \
   {                                                                                                          \
     const int k_ = min(wid + RW_WAVES * (i), nks - 1);                                                       \
     _Pragma("unroll") for (int t = 0; t < NT; ++t) rb[s][t] =                                                \
-        __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(wb + (((int64_t)t * nks + k_) << 9)));    \
+        __builtin_nontemporal_load(reinterpret_cast<const BT*>(wb + (((int64_t)t * nks + k_) << 9)));       \
     _Pragma("unroll") for (int mt = 0; mt < MT; ++mt) ra[s][mt] =                                            \
         MP_LOAD_A_FRAG(xl + (((int64_t)k_ * MT + mt) << 9));                                                 \
   }
@@ -942,15 +978,30 @@ __device__ __forceinline__ void rw_body(const bf16_t* __restrict__ x, const bf16
 #pragma unroll
     for (int s = 0; s < R; ++s) {
       if (wid + RW_WAVES * (i0 + s) < nks) {
+        if constexpr (F8) {
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt)
+          for (int t = 0; t < NT; ++t) {
+            const u16x8 b = f8w_to_bf16(rb[s][t]);
 #pragma unroll
-          for (int t = 0; t < NT; ++t) acc[mt][t] = mfma16(ra[s][mt], rb[s][t], acc[mt][t]);
+            for (int mt = 0; mt < MT; ++mt) acc[mt][t] = mfma16(ra[s][mt], b, acc[mt][t]);
+          }
+        } else {
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+            for (int t = 0; t < NT; ++t) acc[mt][t] = mfma16(ra[s][mt], rb[s][t], acc[mt][t]);
+        }
       }
       RW_LOAD(s, i0 + s + R)
     }
   }
 #undef RW_LOAD
+  if constexpr (F8) {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[mt][t] *= wsc[t];
+  }
   // ---- sum the 4 waves' partial tiles through LDS (passes of at most RW_QC quads: 128-row
   //      workgroups own up to 48), then the epilogue ----
   rsc.finish(ep, rs_part, rs_lds);
@@ -981,7 +1032,7 @@ __device__ __forceinline__ void rw_body(const bf16_t* __restrict__ x, const bf16
   }
 }
 
-template <int MT, int NTB, int NTS, int EPI, bool OPK>
+template <int MT, int NTB, int NTS, int EPI, bool OPK, bool F8 = false>
 __global__ __launch_bounds__(256) void gemm_rw_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ wp,
                                                       bf16_t* __restrict__ y, int64_t ys,
                                                       const bf16_t* __restrict__ res, int64_t rs, int M, int K,
@@ -992,18 +1043,39 @@ __global__ __launch_bounds__(256) void gemm_rw_kernel(const bf16_t* __restrict__
   __shared__ __attribute__((aligned(16))) f32x4 red[RW_WAVES * (MT * NTB < RW_QC ? MT * NTB : RW_QC) * 64];
   const int b = blockIdx.x;
   if (b < n_big) {
-    rw_body<MT, NTB, EPI, OPK>(x, wp, y, ys, res, rs, M, K, b * NTB, ep, red, rs_part, rs_lds);
+    rw_body<MT, NTB, EPI, OPK, F8>(x, wp, y, ys, res, rs, M, K, b * NTB, ep, red, rs_part, rs_lds);
   } else {
-    rw_body<MT, NTS, EPI, OPK>(x, wp, y, ys, res, rs, M, K, n_big * NTB + (b - n_big) * NTS, ep, red, rs_part,
-                               rs_lds);
+    rw_body<MT, NTS, EPI, OPK, F8>(x, wp, y, ys, res, rs, M, K, n_big * NTB + (b - n_big) * NTS, ep, red, rs_part,
+                                   rs_lds);
   }
 }
 
-template <int MT, int NTB, int NTS>
+template <int MT, int NTB, int NTS, bool F8 = false>
 static int launch_gemm_rw_cfg(const void* x, const void* w, void* y, int64_t ys, const void* res, int64_t rs, int M,
                               int K, int epi, bool opk, int G, int n_big, const EpiArgs& ep, hipStream_t stream,
                               bool dry) {
-  if constexpr (MT > 4) {
+  if constexpr (F8) {
+    // fp8-weight (W8A16) forms, M <= 64: the fused-norm decode epilogues (0 with row scale,
+    // packed SwiGLU, residual-stream producer)
+    if constexpr (MT > 4 || 4 * MT * NTB > 256) {
+      return 1;
+    } else {
+      if (!(epi == 0 || epi == 3 || (epi == 1 && opk)) || (epi == 1 && (NTB % 2 || NTS % 2))) return 1;
+      if (dry) return 0;
+      if (epi == 1) {
+        if constexpr (NTB % 2 == 0 && NTS % 2 == 0)
+          hipLaunchKernelGGL((gemm_rw_kernel<MT, NTB, NTS, 1, true, true>), dim3(G), dim3(256), 0, stream,
+                             (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, ys, (const bf16_t*)res, rs, M, K, n_big, ep);
+      } else if (epi == 3) {
+        hipLaunchKernelGGL((gemm_rw_kernel<MT, NTB, NTS, 3, false, true>), dim3(G), dim3(256), 0, stream,
+                           (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, ys, (const bf16_t*)res, rs, M, K, n_big, ep);
+      } else {
+        hipLaunchKernelGGL((gemm_rw_kernel<MT, NTB, NTS, 0, false, true>), dim3(G), dim3(256), 0, stream,
+                           (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, ys, (const bf16_t*)res, rs, M, K, n_big, ep);
+      }
+      return 0;
+    }
+  } else if constexpr (MT > 4) {
     // M = 65..128 (the unfused packed decode path at 96 / 128 sessions): plain and packed-SwiGLU
     // epilogues only, accumulators within 192 AGPRs
     if constexpr (4 * MT * NTB > 192) {
@@ -1049,7 +1121,7 @@ static int launch_gemm_rw_cfg(const void* x, const void* w, void* y, int64_t ys,
 
 // Split the column units (tiles, or gate/up tile pairs) over G = min(#CUs, units) workgroups:
 // n_big of them take ceil, the rest floor.  Returns 1 (caller falls back) for widths not built.
-template <int MT>
+template <int MT, bool F8 = false>
 static int launch_gemm_rw(const void* x, const void* w, void* y, int64_t ys, const void* res, int64_t rs, int M,
                           int N, int K, int epi, int flags, const EpiArgs& ep, hipStream_t stream, bool dry = false) {
   const int step = epi == 1 ? 2 : 1;
@@ -1061,13 +1133,16 @@ static int launch_gemm_rw(const void* x, const void* w, void* y, int64_t ys, con
   const int n_big = rem ? rem : G;
   const bool opk = flags & 2;
 #define MP_RWC(B_, S_) \
-  return launch_gemm_rw_cfg<MT, B_, S_>(x, w, y, ys, res, rs, M, K, epi, opk, G, n_big, ep, stream, dry)
+  return launch_gemm_rw_cfg<MT, B_, S_, F8>(x, w, y, ys, res, rs, M, K, epi, opk, G, n_big, ep, stream, dry)
   if (epi == 1) {
     switch (ntb) {
       case 2: if (rem) return 1; MP_RWC(2, 2);
       case 4: MP_RWC(4, 2);
       case 6: MP_RWC(6, 4);
       case 8: MP_RWC(8, 6);
+      case 14:  // Llama-3-70B gate/up (3584 tiles on 256 CUs), fp8 weights only
+        if constexpr (F8) { if (rem) return 1; MP_RWC(14, 14); }
+        return 1;
       default: return 1;
     }
   }
@@ -1094,12 +1169,14 @@ static int launch_gemm_rw(const void* x, const void* w, void* y, int64_t ys, con
 // kernel's end-of-range hand-off costs ~7 us at these sizes).
 constexpr int64_t RWK_SLAB_BYTES = (int64_t)16 << 20;  // S x M x N fp32 partials (workspace tail)
 
-template <int MT, int NT>
+template <int MT, int NT, bool F8 = false>
 __global__ __launch_bounds__(256) void gemm_rwk_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ wp,
                                                        float* __restrict__ part, int M, int N, int K, int S,
                                                        const EpiArgs ep) {
   clear_other(ep);
-  constexpr int R = rw_depth<MT, NT>();
+  constexpr int R = rw_depth2<MT, NT, F8>();
+  using WT = std::conditional_t<F8, uint8_t, bf16_t>;
+  using BT = std::conditional_t<F8, u32x2, u16x8>;
   constexpr int Q = MT * NT;
   constexpr int QC = Q < RW_QC ? Q : RW_QC;
   __shared__ __attribute__((aligned(16))) f32x4 red[RW_WAVES * QC * 64];
@@ -1109,19 +1186,25 @@ __global__ __launch_bounds__(256) void gemm_rwk_kernel(const bf16_t* __restrict_
   const int nks = K >> 5;
   const int ks0 = (int)((int64_t)sp * nks / S), ks1 = (int)((int64_t)(sp + 1) * nks / S);
   const int cnt = (ks1 - ks0 + RW_WAVES - 1) / RW_WAVES;
-  const bf16_t* wb = wp + ((int64_t)tile0 * nks) * 512 + lane * 8;
+  const WT* wb = reinterpret_cast<const WT*>(wp) + ((int64_t)tile0 * nks) * 512 + lane * 8;
   const bf16_t* xl = x + lane * 8;
+  float wsc[NT];
+  if constexpr (F8) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) wsc[t] = ep.wsc[(tile0 + t) * 16 + (lane & 15)];
+  }
   f32x4 acc[MT][NT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[mt][t] = (f32x4)(0.f);
-  u16x8 ra[R][MT], rb[R][NT];
+  u16x8 ra[R][MT];
+  BT rb[R][NT];
 #define RWK_LOAD(s, i)                                                                                       \
   {                                                                                                          \
     const int k_ = min(ks0 + wid + RW_WAVES * (i), ks1 - 1);                                                 \
     _Pragma("unroll") for (int t = 0; t < NT; ++t) rb[s][t] =                                                \
-        __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(wb + (((int64_t)t * nks + k_) << 9)));    \
+        __builtin_nontemporal_load(reinterpret_cast<const BT*>(wb + (((int64_t)t * nks + k_) << 9)));       \
     _Pragma("unroll") for (int mt = 0; mt < MT; ++mt) ra[s][mt] =                                            \
         MP_LOAD_A_FRAG(xl + (((int64_t)k_ * MT + mt) << 9));                                                 \
   }
@@ -1131,15 +1214,30 @@ __global__ __launch_bounds__(256) void gemm_rwk_kernel(const bf16_t* __restrict_
 #pragma unroll
     for (int s = 0; s < R; ++s) {
       if (ks0 + wid + RW_WAVES * (i0 + s) < ks1) {
+        if constexpr (F8) {
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt)
+          for (int t = 0; t < NT; ++t) {
+            const u16x8 b = f8w_to_bf16(rb[s][t]);
 #pragma unroll
-          for (int t = 0; t < NT; ++t) acc[mt][t] = mfma16(ra[s][mt], rb[s][t], acc[mt][t]);
+            for (int mt = 0; mt < MT; ++mt) acc[mt][t] = mfma16(ra[s][mt], b, acc[mt][t]);
+          }
+        } else {
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+            for (int t = 0; t < NT; ++t) acc[mt][t] = mfma16(ra[s][mt], rb[s][t], acc[mt][t]);
+        }
       }
       RWK_LOAD(s, i0 + s + R)
     }
   }
 #undef RWK_LOAD
+  if constexpr (F8) {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[mt][t] *= wsc[t];
+  }
   // sum the 4 waves' partial tiles through LDS and store this split's fp32 slab [M][N]
   float* slab = part + (int64_t)sp * M * N;
   const int cl = lane & 15, q = lane >> 4;
@@ -1225,13 +1323,16 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 
 // Column-group width NT and split count S with C x S <= #CUs (prefer NT = 4, then 2, 8, 1;
 // 2 <= S <= 8); returns 1 when no split applies (the caller falls back).
-template <int MT>
+template <int MT, bool F8 = false>
 static int launch_gemm_rwk(const void* x, const void* w, void* y, int64_t ys, const void* res, int64_t rs, int M,
                            int N, int K, int epi, const EpiArgs& ep, void* ws, hipStream_t stream) {
   if (epi == 1 || ws == nullptr || N % 2048 != 0) return 1;
   const int tiles = N / 16, C0 = sk_num_cus(), nks = K / 32;
   int nt = 0, S = 0;
-  for (int cand : {4, 2, 8, 1}) {
+  // fp8 weights: the bf16 activation block costs 2M / (16 NT) x the weight bytes per CU - the
+  // widest column group first (NT = 8: A and W bytes equal at M = 64)
+  static constexpr int kOrderBf16[4] = {4, 2, 8, 1}, kOrderF8[4] = {8, 4, 2, 1};
+  for (int cand : (F8 ? kOrderF8 : kOrderBf16)) {
     if (tiles % cand) continue;
     const int C = tiles / cand, s = C0 / C;
     if (s >= 2 && s <= 8 && nks >= 4 * s) { nt = cand; S = s; break; }
@@ -1245,12 +1346,12 @@ static int launch_gemm_rwk(const void* x, const void* w, void* y, int64_t ys, co
                          (int64_t)SK_MAX_BLOCKS * 2 * SK_MAX_S * 64 * sizeof(float));
   const dim3 g1((tiles / nt) * S);
   switch (nt) {
-    case 1: hipLaunchKernelGGL((gemm_rwk_kernel<MT, 1>), g1, dim3(256), 0, stream, (const bf16_t*)x, (const bf16_t*)w, part, M, N, K, S, ep); break;
-    case 2: hipLaunchKernelGGL((gemm_rwk_kernel<MT, 2>), g1, dim3(256), 0, stream, (const bf16_t*)x, (const bf16_t*)w, part, M, N, K, S, ep); break;
-    case 4: hipLaunchKernelGGL((gemm_rwk_kernel<MT, 4>), g1, dim3(256), 0, stream, (const bf16_t*)x, (const bf16_t*)w, part, M, N, K, S, ep); break;
+    case 1: hipLaunchKernelGGL((gemm_rwk_kernel<MT, 1, F8>), g1, dim3(256), 0, stream, (const bf16_t*)x, (const bf16_t*)w, part, M, N, K, S, ep); break;
+    case 2: hipLaunchKernelGGL((gemm_rwk_kernel<MT, 2, F8>), g1, dim3(256), 0, stream, (const bf16_t*)x, (const bf16_t*)w, part, M, N, K, S, ep); break;
+    case 4: hipLaunchKernelGGL((gemm_rwk_kernel<MT, 4, F8>), g1, dim3(256), 0, stream, (const bf16_t*)x, (const bf16_t*)w, part, M, N, K, S, ep); break;
     default:
       if constexpr (4 * MT * 8 <= 192)
-        hipLaunchKernelGGL((gemm_rwk_kernel<MT, 8>), g1, dim3(256), 0, stream, (const bf16_t*)x, (const bf16_t*)w, part, M, N, K, S, ep);
+        hipLaunchKernelGGL((gemm_rwk_kernel<MT, 8, F8>), g1, dim3(256), 0, stream, (const bf16_t*)x, (const bf16_t*)w, part, M, N, K, S, ep);
       break;
   }
   const dim3 g2(N / 2048, M);
@@ -1388,6 +1489,41 @@ extern "C" int mp_gemm_bf16(const void* x, int64_t x_stride, const void* w, void
                                         ep, stream);
   else rc = launch_gemm<4>(x, x_stride, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, gate, ep, stream);
   if (rc) return rc;
+  return (int)hipGetLastError();
+}
+
+// W8A16 decode GEMM: fp8 (e4m3) weights in the bf16 fragment order at 1 byte per element
+// (Wq[N/16][K/32][64][8], per-output-column scales wsc[N]), packed bf16 activations, M <= 64.
+// flags: bit 1 = packed SwiGLU output; bit 7 = balanced ring kernel; bit 8 = split-K ring +
+// reduce launch (epilogue 0 / 3, needs ws).  Same epilogues / EpiArgs as mp_gemm_bf16.
+// Returns 1 when neither form covers the shape (nothing launched).
+extern "C" int mp_gemm_w8(const void* x, const void* wq, const float* wsc, void* y, int64_t y_stride,
+                          const void* res, int64_t res_stride, int M, int N, int K, int epilogue, int flags, void* ws,
+                          void* ap, void* ss_out, void* ss_zero, const void* ss_in, float inv_k, float eps,
+                          hipStream_t stream) {
+  using namespace mp;
+  if (M == 0) return 0;
+  if (M > 64 || K % (32 * GU_MAX) || N % 16 || wsc == nullptr) return -1;
+  if (epilogue == 3 && (ap == nullptr || res == nullptr)) return -5;
+  EpiArgs ep{(bf16_t*)ap, (u64*)ss_out, (u64*)ss_zero, (const u64*)ss_in, inv_k, eps, (M + 15) / 16};
+  ep.wsc = wsc;
+  int rc = 1;
+  if ((flags & 256) && !(flags & 2) && ws != nullptr) {
+    switch ((M + 15) / 16) {
+      case 1: rc = launch_gemm_rwk<1, true>(x, wq, y, y_stride, res, res_stride, M, N, K, epilogue, ep, ws, stream); break;
+      case 2: rc = launch_gemm_rwk<2, true>(x, wq, y, y_stride, res, res_stride, M, N, K, epilogue, ep, ws, stream); break;
+      case 3: rc = launch_gemm_rwk<3, true>(x, wq, y, y_stride, res, res_stride, M, N, K, epilogue, ep, ws, stream); break;
+      default: rc = launch_gemm_rwk<4, true>(x, wq, y, y_stride, res, res_stride, M, N, K, epilogue, ep, ws, stream); break;
+    }
+    if (rc < 0) return rc;
+    if (rc == 0) return (int)hipGetLastError();
+  }
+  const int fl = flags | 1;
+  if (M <= 16) rc = launch_gemm_rw<1, true>(x, wq, y, y_stride, res, res_stride, M, N, K, epilogue, fl, ep, stream);
+  else if (M <= 32) rc = launch_gemm_rw<2, true>(x, wq, y, y_stride, res, res_stride, M, N, K, epilogue, fl, ep, stream);
+  else if (M <= 48) rc = launch_gemm_rw<3, true>(x, wq, y, y_stride, res, res_stride, M, N, K, epilogue, fl, ep, stream);
+  else rc = launch_gemm_rw<4, true>(x, wq, y, y_stride, res, res_stride, M, N, K, epilogue, fl, ep, stream);
+  if (rc != 0) return rc;
   return (int)hipGetLastError();
 }
 

@@ -196,10 +196,21 @@ class StageExecutor:
         # one executor may be driven by the TCP handler's GPU worker AND a device-channel
         # engine thread: every device step (incl. hipGraph capture) runs under this lock
         self.exec_lock = threading.RLock()
+        # fp8 weights: W8A16 (ops.linear_w8: fp8 weights dequantized into the bf16 MFMA, bf16
+        # activations, the fused-norm path below; default) or W8A8 (MPAMD_FP8_MODE=w8a8: fp8 MFMA,
+        # activations quantized per row before every GEMM, RMSNorm kernels; also under TP)
+        self._w8 = (self.device.type == "cuda" and weights.fp8 and cfg.model_type != "gpt2" and not cfg.is_moe and
+                    self._tp is None and os.environ.get("MPAMD_FP8_MODE", "w8a16") == "w8a16" and
+                    os.environ.get("MPAMD_FUSED_NORM", "1") != "0" and
+                    all(d % 256 == 0 for d in (cfg.hidden_size, cfg.q_dim, cfg.intermediate_size)) and
+                    (cfg.q_dim + 2 * cfg.kv_dim) % 32 == 0)
+        if self._w8:
+            weights.prepare_w8a16(fold_norms=True)
         # fused-norm decode path (ops/csrc/gemm.hip EpiArgs): no RMSNorm kernels between the
-        # layers' GEMMs - dense bf16 Llama stages without TP (MoE / fp8 / TP keep the norm kernels)
+        # layers' GEMMs - dense bf16 or W8A16 Llama stages without TP (MoE / W8A8 / TP keep the
+        # norm kernels)
         self._fused = (self.device.type == "cuda" and cfg.model_type != "gpt2" and not cfg.is_moe and
-                       self._tp is None and not weights.fp8 and ops.gemm_policy() != "hipblaslt" and
+                       self._tp is None and (not weights.fp8 or self._w8) and ops.gemm_policy() != "hipblaslt" and
                        os.environ.get("MPAMD_FUSED_NORM", "1") != "0" and
                        all(d % 128 == 0 for d in (cfg.hidden_size, cfg.q_dim, cfg.intermediate_size)))
         self._ss = ops.norm_stats_buffer(self.device, 2) if self._fused else None
@@ -225,7 +236,10 @@ class StageExecutor:
                     if weights.lm_head_p is not None:
                         shapes.append((16 * weights.lm_head_p.shape[0], H, 0))
                     ops.autotune_gemm(shapes, self.device)
-                    if weights.fp8 and weights.layers:
+                    if self._w8 and weights.layers:
+                        ops.autotune_w8([(cfg.q_dim + 2 * cfg.kv_dim, H, 0), (H, cfg.q_dim, 3), (2 * F, H, 1),
+                                         (H, F, 3)], self.device)
+                    elif weights.fp8 and weights.layers:
                         ops.autotune_fp8([(cfg.q_dim + 2 * cfg.kv_dim, H, 0), (H, cfg.q_dim, 0), (2 * F, H, 1),
                                           (H, F, 0)], self.device)
         self._streamer, self._n_stream = None, self.n_layers
@@ -501,7 +515,7 @@ class StageExecutor:
                 ops.quant_rows_fp8(act, out=a8, scale=asc)
                 ops.linear_fp8(a8, asc, L.down_q, L.down_s, T, out=mlp)
                 self._ar(mlp)
-        elif prompt is None and self._fused and T <= 64 and self._packed_ok(T):
+        elif prompt is None and self._fused and T <= 64 and (self._w8 or self._packed_ok(T)):
             # fused-norm decode path: 5 launches per layer (qkv, attention, o, gate/up, down).
             # The residual stream r lives row-major in ``res`` and packed in ``xr``; o / down add
             # their product into it in their epilogue and accumulate sum(r^2) per row, and qkv /
@@ -513,19 +527,22 @@ class StageExecutor:
             attn = e("attn_p", (pk(T, cfg.q_dim),))
             act = e("act_p", (pk(T, cfg.intermediate_size),))
             ss_in, ss_post = self._ss[0], self._ss[1]
+            if self._w8:  # fp8 weights (W8A16): same launches, 1 byte per weight streamed
+                def gemm(a, L, name, **kw):
+                    return ops.linear_w8(a, getattr(L, name + "_w8"), getattr(L, name + "_ws"), T, **kw)
+            else:
+                def gemm(a, L, name, **kw):
+                    return ops.linear(a, None, wp=getattr(L, name + "_p"), a_rows=T, **kw)
             for li, L in self._iter_layers(_PACKED_FIELDS):
                 if li == 0:
                     ops.rmsnorm(h, L.input_norm, eps, out=xr, residual=res, mode=3, packed=True, ss=ss_in)
-                ops.linear(xr, None, out=qkv, wp=L.qkv_p, a_rows=T, ss_in=ss_in, eps=eps)
+                gemm(xr, L, "qkv", out=qkv, ss_in=ss_in, eps=eps)
                 kc, vc = self.cache.layer(li)
                 self._rope_attend(qkv, positions, slots, kc, vc, q_seq, q_ctx, attn, ws, ps, np_, True, qblocks,
                                   max_ctx, decode)
-                ops.linear(attn, None, out=res, epilogue=3, residual=res, wp=L.o_p, a_rows=T, ap_out=xr,
-                           ss_out=ss_post, ss_zero=ss_in)
-                ops.linear(xr, None, out=act, epilogue=1, wp=L.gate_up_p, a_rows=T, out_packed=True, ss_in=ss_post,
-                           eps=eps)
-                ops.linear(act, None, out=res, epilogue=3, residual=res, wp=L.down_p, a_rows=T, ap_out=xr,
-                           ss_out=ss_in, ss_zero=ss_post)
+                gemm(attn, L, "o", out=res, epilogue=3, residual=res, ap_out=xr, ss_out=ss_post, ss_zero=ss_in)
+                gemm(xr, L, "gate_up", out=act, epilogue=1, out_packed=True, ss_in=ss_post, eps=eps)
+                gemm(act, L, "down", out=res, epilogue=3, residual=res, ap_out=xr, ss_out=ss_in, ss_zero=ss_post)
             mlp = None
         elif prompt is None and self._packed_ok(T):
             # decode path: activations feeding a GEMM stay in the packed MFMA-fragment layout
@@ -560,21 +577,24 @@ class StageExecutor:
             attn = e("attn", (T, cfg.q_dim))
             act = e("act", (T, cfg.intermediate_size))
             for li, L in self._iter_layers(_DENSE_FIELDS):
+                # W8A16 layers' only weights carry the norm weights folded in (prepare_w8a16)
+                g_in, g_post = (self._unit_norm(), self._unit_norm()) if (L.folded and L.w8) else \
+                    (L.input_norm, L.post_norm)
                 if prompt is not None:  # deep prompt: the block input (residual stream) += prompt[li]
                     cur = h.clone() if li == 0 else ops.add(res, mlp)
                     cur.index_add_(0, prompt[0], prompt[1][li])
-                    ops.rmsnorm(cur, L.input_norm, eps, out=xn, residual=res, mode=2)
+                    ops.rmsnorm(cur, g_in, eps, out=xn, residual=res, mode=2)
                 elif li == 0:
-                    ops.rmsnorm(h, L.input_norm, eps, out=xn, residual=res, mode=2)
+                    ops.rmsnorm(h, g_in, eps, out=xn, residual=res, mode=2)
                 else:
-                    ops.rmsnorm(mlp, L.input_norm, eps, out=xn, residual=res, mode=1)
+                    ops.rmsnorm(mlp, g_in, eps, out=xn, residual=res, mode=1)
                 ops.linear(xn, L.dense("qkv"), out=qkv, wp=L.qkv_p)
                 kc, vc = self.cache.layer(li)
                 self._rope_attend(qkv, positions, slots, kc, vc, q_seq, q_ctx, attn, ws, ps, np_, False, qblocks,
                                   max_ctx, decode)
                 ops.linear(attn, L.dense("o"), out=o, wp=L.o_p)
                 self._ar(o)
-                ops.rmsnorm(o, L.post_norm, eps, out=xn, residual=res, mode=1)
+                ops.rmsnorm(o, g_post, eps, out=xn, residual=res, mode=1)
                 if L.moe:
                     self._moe_mlp(L, xn, T, mlp, act, e, packed=False)
                     continue
@@ -701,7 +721,7 @@ class StageExecutor:
 
     def _fp8_ok(self, M: int) -> bool:
         """fp8 W8A8 decode path: GPU, fp8 weights, fp8 GEMM shape constraints."""
-        if self.device.type != "cuda" or not 0 < M <= 64 or not self.w.fp8:
+        if self.device.type != "cuda" or not 0 < M <= 64 or not self.w.fp8 or self._w8:
             return False
         cfg = self.cfg
         return all(d % 256 == 0 for d in (cfg.hidden_size, cfg.q_dim, cfg.intermediate_size)) and \

@@ -93,25 +93,36 @@ def test_rmsnorm_fp8_output_equals_norm_then_quant(M, mode):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["w8a8", "w8a16"])
 @pytest.mark.parametrize("graphs", [False, True])
-def test_fp8_executor_gpu_decode_tracks_dequantized_oracle(graphs):
-    """The GPU fp8 decode path (norm-emitted fp8, row-major attention / SwiGLU outputs through
-    the row quantization kernel, balanced-ring fp8 GEMMs at 17 rows, one-group at 1 row) stays
-    within the W8A8 error budget of the fp32 oracle on the dequantized weights, with and without
-    hipGraphs (which must agree bit for bit with each other)."""
+def test_fp8_executor_gpu_decode_tracks_dequantized_oracle(graphs, mode, monkeypatch):
+    """The GPU fp8 decode paths stay within the fp8 error budget of the fp32 oracle on the
+    dequantized weights, with and without hipGraphs (which must agree bit for bit):
+    w8a8 - norm-emitted fp8, row-major attention / SwiGLU outputs through the row quantization
+    kernel, fp8 MFMA GEMMs; w8a16 - the fused-norm path with fp8 weights dequantized into the
+    bf16 MFMA (norm weights folded into qkv / gate_up and re-quantized: non-unit norms here)."""
+    monkeypatch.setenv("MPAMD_FP8_MODE", mode)
     cfg = resolve_model("small-llama")
     L = cfg.num_hidden_layers
     w = random_stage_weights(cfg, 0, L, has_embed=True, has_head=True, device="cuda", seed=5)
     wd = random_stage_weights(cfg, 0, L, has_embed=True, has_head=True, device="cuda", seed=5, dtype=torch.float32)
     w.quantize_fp8(drop_dense=True)
+    gn = torch.Generator(device="cuda").manual_seed(11)
     for Lq, Ld in zip(w.layers, wd.layers):
         for name in Lq.PROJ:
             setattr(Ld, name, Lq.dense(name, torch.float32))
+        for nm in ("input_norm", "post_norm"):
+            g = (0.5 + torch.rand(cfg.hidden_size, device="cuda", generator=gn)).to(torch.bfloat16)
+            setattr(Lq, nm, g)
+            setattr(Ld, nm, g.float())
     gen = torch.Generator().manual_seed(7)
     outs = {}
     for g in sorted({False, graphs}):
         ex = StageExecutor(cfg, w, "cuda", kv_cache_bytes=64 << 20, max_sessions=32, max_seq_len=128, use_graphs=g)
-        assert ex._fp8_ok(17)
+        if mode == "w8a8":
+            assert ex._fp8_ok(17) and not ex._w8
+        else:
+            assert ex._w8 and ex._fused and not ex._fp8_ok(17)
         n = 17
         prompts = [torch.randint(0, cfg.vocab_size, (5 + i % 7,), generator=torch.Generator().manual_seed(i))
                    for i in range(n)]

@@ -434,6 +434,64 @@ def test_fp8_gemm_kernel_matches_reference(kern, M, N, K, epi):
         ops.set_fp8_kernel("auto")
 
 
+@pytest.mark.parametrize("kern", ["rw", "rwk"])
+@pytest.mark.parametrize("M", [1, 30, 64])
+@pytest.mark.parametrize("N,K,epi", [(1024, 1024, 0), (10240, 8192, 0), (8192, 8192, 3), (8192, 28672, 3),
+                                     (2048, 4096, 1), (57344, 512, 1), (4096, 1024, 0)])
+def test_w8a16_gemm_matches_dequantized_reference(kern, M, N, K, epi, monkeypatch):
+    """W8A16 decode GEMM (fp8 weights dequantized into the bf16 MFMA) vs x @ dequant(W)^T in fp32;
+    epilogue 0 with and without the fused-norm row scale, packed SwiGLU (57344 = the Llama-3-70B
+    gate/up width: 14 tiles per CU), and the residual-stream producer (residual, packed copy, row
+    sums of squares) in both the ring and the split-K ring forms."""
+    from src.models.weights import interleave_gate_up
+
+    monkeypatch.setattr(ops, "_W8_MODE", kern)
+    x = bf(torch.randn(M, K, device=DEV))
+    if epi == 1:
+        w = interleave_gate_up(torch.randn(N // 2, K, device=DEV) * 0.02, torch.randn(N // 2, K, device=DEV) * 0.02)
+    else:
+        w = torch.randn(N, K, device=DEV) * 0.02
+    wq, ws = ops.pack_weight_fp8(w)
+    w8 = ops.w8_from_fp8(wq)
+    wdq = ops.unpack_weight_w8(w8, ws, torch.float32)
+    wbf = wdq.to(torch.bfloat16).float()  # the kernel rounds the dequantized weight to bf16
+    xp = ops.pack_act(x)
+    exact = x.float() @ wbf.t()
+    if epi == 0:
+        y = ops.linear_w8(xp, w8, ws, M)
+        torch.testing.assert_close(y.float(), exact, atol=5e-2, rtol=2e-2)
+        assert float((y.float() - exact).norm() / exact.norm()) < 1e-2  # bf16 outputs: 2^-8 relative
+        # fused-norm consumer: row scale rsqrt(ss / K + eps) from the fixed-point row statistics
+        ss = ops.norm_stats_buffer(DEV)[0]
+        ss.zero_()
+        sq = (x.float() ** 2).sum(1)
+        ss[0, :M] = torch.round(sq * 2.0 ** 20).long()
+        y2 = ops.linear_w8(xp, w8, ws, M, ss_in=ss, eps=1e-5)
+        want = exact * torch.rsqrt(sq / K + 1e-5)[:, None]
+        torch.testing.assert_close(y2.float(), want, atol=5e-2, rtol=2e-2)
+        assert float((y2.float() - want).norm() / want.norm()) < 1e-2  # bf16 outputs: 2^-8 relative
+    elif epi == 1:
+        yp = ops.linear_w8(xp, w8, ws, M, epilogue=1, out_packed=True)
+        y = ops.unpack_act(yp, M, N // 2).float()
+        g, u = exact.view(M, N // 32, 2, 16)[:, :, 0].reshape(M, N // 2), \
+            exact.view(M, N // 32, 2, 16)[:, :, 1].reshape(M, N // 2)
+        want = torch.nn.functional.silu(g) * u
+        torch.testing.assert_close(y, want, atol=5e-2, rtol=2e-2)
+        assert float((y - want).norm() / want.norm()) < 1e-2  # bf16 outputs: 2^-8 relative
+    else:
+        res = bf(torch.randn(M, N, device=DEV))
+        r0 = res.clone()
+        ap = torch.zeros(ops.packed_numel(M, N), dtype=torch.bfloat16, device=DEV)
+        ss_out, ss_zero = ops.norm_stats_buffer(DEV, 2)
+        ss_out.zero_()
+        ops.linear_w8(xp, w8, ws, M, out=res, epilogue=3, residual=res, ap_out=ap, ss_out=ss_out, ss_zero=ss_zero)
+        want = exact + r0.float()
+        torch.testing.assert_close(res.float(), want, atol=6e-2, rtol=2e-2)  # two bf16 roundings of ~|8|
+        assert torch.equal(ops.unpack_act(ap, M, N), res)
+        got_ss = ss_out.view(-1, 64).sum(0)[:M].double() / 2.0 ** 20
+        torch.testing.assert_close(got_ss, (res.double() ** 2).sum(1), rtol=1e-4, atol=1e-3)
+
+
 def _fp8_gemm_case(M, N, K, epi, ref, interleave_gate_up):
 
     x = bf(torch.randn(M, K, device=DEV))

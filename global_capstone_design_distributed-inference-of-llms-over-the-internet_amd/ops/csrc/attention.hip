@@ -374,7 +374,7 @@ __global__ __launch_bounds__(256) void paged_attn_kernel(
 // maxima), and the output / split-K partials (o, m, l) have the two-pass kernel's format.
 // NW = waves per workgroup: 4, or 16 when the grid is small (batch 1: one workgroup per head
 // over the whole context, each wave a 16-token slice; no split-K, no reduce launch).
-template <int D, int NREP, bool ROPE, int NW>
+template <int D, int NREP, bool ROPE, int NW, bool PIPE>
 __global__ __launch_bounds__(NW * 64) void paged_attn1_kernel(
     const bf16_t* __restrict__ q, int64_t q_stride, const bf16_t* __restrict__ kc,
     const bf16_t* __restrict__ vc, const int32_t* __restrict__ block_tables, int bt_stride,
@@ -487,24 +487,20 @@ __global__ __launch_bounds__(NW * 64) void paged_attn1_kernel(
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[r][j] = 0.f;
   }
-  for (int base = start + w * TPW; base < end; base += NW * TPW) {
-    u16x8 kv[U], vv[U];
+  auto issue = [&](int b, const int* pg, u16x8* kd, u16x8* vd) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int tc = min(base + u * TPI + tg, end - 1);
-      const int64_t off = (int64_t)pgn[u] * page_stride + head_off + (int64_t)(tc & (page_size - 1)) * D;
-      kv[u] = *reinterpret_cast<const u16x8*>(kc + off);
-      vv[u] = *reinterpret_cast<const u16x8*>(vc + off);
+      const int tc = min(b + u * TPI + tg, end - 1);
+      const int64_t off = (int64_t)pg[u] * page_stride + head_off + (int64_t)(tc & (page_size - 1)) * D;
+      kd[u] = *reinterpret_cast<const u16x8*>(kc + off);
+      vd[u] = *reinterpret_cast<const u16x8*>(vc + off);
     }
-    // next iteration's page ids, in flight behind the K / V loads
-    const int nb = base + NW * TPW;
+  };
+  auto page_ids = [&](int b, int* pg) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) pgn[u] = bt[min(nb + u * TPI + tg, end - 1) >> page_log2];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      asm volatile("" : "+v"(kv[u]));
-      asm volatile("" : "+v"(vv[u]));
-    }
+    for (int u = 0; u < U; ++u) pg[u] = bt[min(b + u * TPI + tg, end - 1) >> page_log2];
+  };
+  auto compute = [&](int base, u16x8 (&kv)[U], u16x8 (&vv)[U]) {
     if constexpr (ROPE) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -514,31 +510,65 @@ __global__ __launch_bounds__(NW * 64) void paged_attn1_kernel(
       }
     }
 #pragma unroll
-    for (int r = 0; r < NREP; ++r) {
-      float s[U];
-      float mx = m[r];
+      for (int r = 0; r < NREP; ++r) {
+        float s[U];
+        float mx = m[r];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          float d = 0.f;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) d += qf[r][j] * bf2f(kv[u][j]);
+          d = group_sum<LPT>(d);
+          s[u] = base + u * TPI + tg < end ? d : -INFINITY;
+          mx = fmaxf(mx, s[u]);
+        }
+        const float mref = mx == -INFINITY ? 0.f : mx;
+        const float sc = exp2f(m[r] - mref);
+        l[r] *= sc;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[r][j] *= sc;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const float pr = exp2f(s[u] - mref);
+          l[r] += pr;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[r][j] += pr * bf2f(vv[u][j]);
+        }
+        m[r] = mx;
+      }
+
+  };
+  u16x8 kv[U], vv[U];
+  if constexpr (PIPE) {
+    // software-pipelined: iteration i+1's K / V (and i+2's page ids) are in flight while
+    // iteration i computes, so the stream never stops between iterations
+    int pgm[U];
+    page_ids(start + w * TPW + NW * TPW, pgm);
+    issue(start + w * TPW, pgn, kv, vv);
+    for (int base = start + w * TPW; base < end; base += NW * TPW) {
+      const int nb = base + NW * TPW;
+      u16x8 kx[U], vx[U];
+      page_ids(nb + NW * TPW, pgn);
+      if (nb < end) issue(nb, pgm, kx, vx);
+      compute(base, kv, vv);
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        float d = 0.f;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) d += qf[r][j] * bf2f(kv[u][j]);
-        d = group_sum<LPT>(d);
-        s[u] = base + u * TPI + tg < end ? d : -INFINITY;
-        mx = fmaxf(mx, s[u]);
+        kv[u] = kx[u];
+        vv[u] = vx[u];
+        pgm[u] = pgn[u];
       }
-      const float mref = mx == -INFINITY ? 0.f : mx;
-      const float sc = exp2f(m[r] - mref);
-      l[r] *= sc;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc[r][j] *= sc;
+    }
+  } else {
+    for (int base = start + w * TPW; base < end; base += NW * TPW) {
+      issue(base, pgn, kv, vv);
+      // next iteration's page ids, in flight behind the K / V loads
+      page_ids(base + NW * TPW, pgn);
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const float pr = exp2f(s[u] - mref);
-        l[r] += pr;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc[r][j] += pr * bf2f(vv[u][j]);
+        asm volatile("" : "+v"(kv[u]));
+        asm volatile("" : "+v"(vv[u]));
       }
-      m[r] = mx;
+      compute(base, kv, vv);
     }
   }
   // merge the token groups of the wave (lanes sl, sl + LPT, ...)
@@ -647,12 +677,19 @@ static void launch_attn(const void* q, int64_t q_stride, const void* kc, const v
                        (const bf16_t*)kc, (const bf16_t*)vc, bt, bt_stride, q_seq, q_ctx, (bf16_t*)out, ws_o, ws_ml,
                        nkv, nh, page_log2, PS, NP, scale_log2, packed_mt, rf, cnt);
   };
+  static const bool pipe = [] {
+    const char* v = getenv("MPAMD_ATTN_PIPE");
+    return !(v && v[0] == '0');
+  }();
   if (one_pass && wide) {
-    if (rf.pos) go(paged_attn1_kernel<D, NREP, true, 16>);
-    else go(paged_attn1_kernel<D, NREP, false, 16>);
+    if (rf.pos) go(paged_attn1_kernel<D, NREP, true, 16, false>);
+    else go(paged_attn1_kernel<D, NREP, false, 16, false>);
+  } else if (one_pass && pipe) {
+    if (rf.pos) go(paged_attn1_kernel<D, NREP, true, 4, true>);
+    else go(paged_attn1_kernel<D, NREP, false, 4, true>);
   } else if (one_pass) {
-    if (rf.pos) go(paged_attn1_kernel<D, NREP, true, 4>);
-    else go(paged_attn1_kernel<D, NREP, false, 4>);
+    if (rf.pos) go(paged_attn1_kernel<D, NREP, true, 4, false>);
+    else go(paged_attn1_kernel<D, NREP, false, 4, false>);
   } else if (rf.pos) {
     go(paged_attn_kernel<D, NREP, true>);
   } else {

@@ -1169,10 +1169,17 @@ static int launch_gemm_rw(const void* x, const void* w, void* y, int64_t ys, con
 // kernel's end-of-range hand-off costs ~7 us at these sizes).
 constexpr int64_t RWK_SLAB_BYTES = (int64_t)16 << 20;  // S x M x N fp32 partials (workspace tail)
 
-template <int MT, int NT, bool F8 = false>
+// INL >= 0: in-launch combine instead of the reduce launch - every split stores its summed
+// tiles as write-through (sc1) fp32 slabs in fragment order, takes an arrival ticket on its
+// column group, and the LAST of the S splits reads the S slabs back (sc1 loads, slab order:
+// deterministic) and runs epilogue INL (0 with the optional row scale, 2, 3) itself - the
+// stream-K kernel's hand-off protocol (guide: splitk-seam, publish-large).
+template <int MT, int NT, bool F8 = false, int INL = -1>
 __global__ __launch_bounds__(256) void gemm_rwk_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ wp,
                                                        float* __restrict__ part, int M, int N, int K, int S,
-                                                       const EpiArgs ep) {
+                                                       const EpiArgs ep, bf16_t* __restrict__ y, int64_t ys,
+                                                       const bf16_t* __restrict__ res, int64_t rs,
+                                                       int* __restrict__ tick) {
   clear_other(ep);
   constexpr int R = rw_depth2<MT, NT, F8>();
   using WT = std::conditional_t<F8, uint8_t, bf16_t>;
@@ -1237,6 +1244,49 @@ __global__ __launch_bounds__(256) void gemm_rwk_kernel(const bf16_t* __restrict_
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
       for (int t = 0; t < NT; ++t) acc[mt][t] *= wsc[t];
+  }
+  if constexpr (INL >= 0) {
+    __shared__ u64 rs_part[RW_WAVES][64];
+    __shared__ float rs_lds[64];
+    __shared__ int s_last;
+    RowScale<INL < 2, RW_WAVES> rsc;
+    rsc.load(ep, wp);
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc(part, (short)0, (int)RWK_SLAB_BYTES, 0x00020000);
+#pragma unroll
+    for (int p0 = 0; p0 < Q; p0 += QC) {
+      if (p0 > 0) __syncthreads();
+#pragma unroll
+      for (int qd = p0; qd < p0 + QC && qd < Q; ++qd) red[(wid * QC + qd - p0) * 64 + lane] = acc[qd / NT][qd % NT];
+      __syncthreads();
+      for (int qd = p0 + wid; qd < p0 + QC && qd < Q; qd += RW_WAVES) {
+        f32x4 v = red[(qd - p0) * 64 + lane];
+#pragma unroll
+        for (int w = 1; w < RW_WAVES; ++w) v += red[(w * QC + qd - p0) * 64 + lane];
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rsrc,
+                                               (((c * S + sp) * Q + qd) * 64 + lane) * 16, 0, 16);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 slab stores landed
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const int old = __hip_atomic_fetch_add(tick + c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_last = old == S - 1;
+      if (old == S - 1) __hip_atomic_store(tick + c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (!s_last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keep the slab loads below the ticket
+    rsc.finish(ep, rs_part, rs_lds);
+    for (int qd = wid; qd < Q; qd += RW_WAVES) {
+      f32x4 v = (f32x4)(0.f);
+      for (int s2 = 0; s2 < S; ++s2)
+        v += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                           rsrc, (((c * S + s2) * Q + qd) * 64 + lane) * 16, 0, 16));
+      tile_epilogue<MT, INL, false>(qd / NT, tile0 + qd % NT, v, (f32x4)(0.f), y, ys, res, rs, M, lane, ep, rs_lds,
+                                    nullptr);
+    }
+    return;
   }
   // sum the 4 waves' partial tiles through LDS and store this split's fp32 slab [M][N]
   float* slab = part + (int64_t)sp * M * N;
@@ -1325,7 +1375,8 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 // 2 <= S <= 8); returns 1 when no split applies (the caller falls back).
 template <int MT, bool F8 = false>
 static int launch_gemm_rwk(const void* x, const void* w, void* y, int64_t ys, const void* res, int64_t rs, int M,
-                           int N, int K, int epi, const EpiArgs& ep, void* ws, hipStream_t stream) {
+                           int N, int K, int epi, const EpiArgs& ep, void* ws, hipStream_t stream,
+                           bool inl = false) {
   if (epi == 1 || ws == nullptr || N % 2048 != 0) return 1;
   const int tiles = N / 16, C0 = sk_num_cus(), nks = K / 32;
   int nt = 0, S = 0;
@@ -1345,13 +1396,32 @@ static int launch_gemm_rwk(const void* x, const void* w, void* y, int64_t ys, co
   float* part = (float*)((char*)ws + (int64_t)SK_MAX_GROUPS * sizeof(int) + SK_ZERO_BYTES +
                          (int64_t)SK_MAX_BLOCKS * 2 * SK_MAX_S * 64 * sizeof(float));
   const dim3 g1((tiles / nt) * S);
+  int* tick = (int*)ws + SK_MAX_GROUPS / 2;  // rwk arrival tickets (the stream-K kernel uses the low half)
+  if (inl && MT <= 4 && nt >= 2 && tiles / nt <= SK_MAX_GROUPS / 2 &&
+      (int64_t)tiles * MT * S * 1024 <= RWK_SLAB_BYTES) {
+    if constexpr (MT <= 4) {
+#define MP_RWKI(NT_, E_)                                                                                       \
+  hipLaunchKernelGGL((gemm_rwk_kernel<MT, NT_, F8, E_>), g1, dim3(256), 0, stream, (const bf16_t*)x,            \
+                     (const bf16_t*)w, part, M, N, K, S, ep, (bf16_t*)y, ys, (const bf16_t*)res, rs, tick)
+#define MP_RWKI_E(NT_) \
+  { if (epi == 3) MP_RWKI(NT_, 3); else if (epi == 2) MP_RWKI(NT_, 2); else MP_RWKI(NT_, 0); }
+      switch (nt) {
+        case 2: MP_RWKI_E(2); break;
+        case 4: MP_RWKI_E(4); break;
+        default: MP_RWKI_E(8); break;
+      }
+#undef MP_RWKI_E
+#undef MP_RWKI
+      return 0;
+    }
+  }
   switch (nt) {
-    case 1: hipLaunchKernelGGL((gemm_rwk_kernel<MT, 1, F8>), g1, dim3(256), 0, stream, (const bf16_t*)x, (const bf16_t*)w, part, M, N, K, S, ep); break;
-    case 2: hipLaunchKernelGGL((gemm_rwk_kernel<MT, 2, F8>), g1, dim3(256), 0, stream, (const bf16_t*)x, (const bf16_t*)w, part, M, N, K, S, ep); break;
-    case 4: hipLaunchKernelGGL((gemm_rwk_kernel<MT, 4, F8>), g1, dim3(256), 0, stream, (const bf16_t*)x, (const bf16_t*)w, part, M, N, K, S, ep); break;
+    case 1: hipLaunchKernelGGL((gemm_rwk_kernel<MT, 1, F8>), g1, dim3(256), 0, stream, (const bf16_t*)x, (const bf16_t*)w, part, M, N, K, S, ep, nullptr, 0, nullptr, 0, nullptr); break;
+    case 2: hipLaunchKernelGGL((gemm_rwk_kernel<MT, 2, F8>), g1, dim3(256), 0, stream, (const bf16_t*)x, (const bf16_t*)w, part, M, N, K, S, ep, nullptr, 0, nullptr, 0, nullptr); break;
+    case 4: hipLaunchKernelGGL((gemm_rwk_kernel<MT, 4, F8>), g1, dim3(256), 0, stream, (const bf16_t*)x, (const bf16_t*)w, part, M, N, K, S, ep, nullptr, 0, nullptr, 0, nullptr); break;
     default:
       if constexpr (4 * MT * 8 <= 192)
-        hipLaunchKernelGGL((gemm_rwk_kernel<MT, 8, F8>), g1, dim3(256), 0, stream, (const bf16_t*)x, (const bf16_t*)w, part, M, N, K, S, ep);
+        hipLaunchKernelGGL((gemm_rwk_kernel<MT, 8, F8>), g1, dim3(256), 0, stream, (const bf16_t*)x, (const bf16_t*)w, part, M, N, K, S, ep, nullptr, 0, nullptr, 0, nullptr);
       break;
   }
   const dim3 g2(N / 2048, M);
@@ -1415,7 +1485,7 @@ extern "C" int64_t mp_gemm_workspace_bytes() {
 //        used by one stream at a time); bit 3 = force the one-group-per-workgroup kernel;
 //        bit 4 = shared-A (LDS-staged activation) kernel when the shape allows it;
 //        bit 7 = balanced ring kernel; bit 8 = split-K ring kernel + reduce launch (epilogue
-//        0 / 2 / 3, needs ws).
+//        0 / 2 / 3, needs ws); bits 8 + 9 = split-K ring kernel with the in-launch combine.
 //        epilogue 3 / ss_in: the fused-norm decode path (EpiArgs above; ap / ss_out / ss_zero /
 //        ss_in may be null when unused).
 extern "C" int mp_gemm_bf16(const void* x, int64_t x_stride, const void* w, void* y, int64_t y_stride,
@@ -1429,7 +1499,8 @@ extern "C" int mp_gemm_bf16(const void* x, int64_t x_stride, const void* w, void
   if (M > 128 || K % (32 * GU_MAX) || N % 16 || ((flags & 1) == 0 && x_stride % 8)) return -1;
   int rc;
   if ((flags & 1) && (flags & 256) && !(flags & 2) && gate == nullptr && ws != nullptr) {  // split-K ring
-#define MP_RWK(MT_) rc = launch_gemm_rwk<MT_>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, ep, ws, stream)
+#define MP_RWK(MT_) \
+  rc = launch_gemm_rwk<MT_>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, ep, ws, stream, (flags & 512) != 0)
     switch ((M + 15) / 16) {  // the packed layout's row-tile count is part of its strides
       case 1: MP_RWK(1); break;
       case 2: MP_RWK(2); break;
@@ -1510,10 +1581,10 @@ extern "C" int mp_gemm_w8(const void* x, const void* wq, const float* wsc, void*
   int rc = 1;
   if ((flags & 256) && !(flags & 2) && ws != nullptr) {
     switch ((M + 15) / 16) {
-      case 1: rc = launch_gemm_rwk<1, true>(x, wq, y, y_stride, res, res_stride, M, N, K, epilogue, ep, ws, stream); break;
-      case 2: rc = launch_gemm_rwk<2, true>(x, wq, y, y_stride, res, res_stride, M, N, K, epilogue, ep, ws, stream); break;
-      case 3: rc = launch_gemm_rwk<3, true>(x, wq, y, y_stride, res, res_stride, M, N, K, epilogue, ep, ws, stream); break;
-      default: rc = launch_gemm_rwk<4, true>(x, wq, y, y_stride, res, res_stride, M, N, K, epilogue, ep, ws, stream); break;
+      case 1: rc = launch_gemm_rwk<1, true>(x, wq, y, y_stride, res, res_stride, M, N, K, epilogue, ep, ws, stream, (flags & 512) != 0); break;
+      case 2: rc = launch_gemm_rwk<2, true>(x, wq, y, y_stride, res, res_stride, M, N, K, epilogue, ep, ws, stream, (flags & 512) != 0); break;
+      case 3: rc = launch_gemm_rwk<3, true>(x, wq, y, y_stride, res, res_stride, M, N, K, epilogue, ep, ws, stream, (flags & 512) != 0); break;
+      default: rc = launch_gemm_rwk<4, true>(x, wq, y, y_stride, res, res_stride, M, N, K, epilogue, ep, ws, stream, (flags & 512) != 0); break;
     }
     if (rc < 0) return rc;
     if (rc == 0) return (int)hipGetLastError();

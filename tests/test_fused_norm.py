@@ -50,7 +50,7 @@ def test_reference_fold_identity_cpu():
     assert int(ssz.abs().sum()) == 0
 
 
-KERNELS = ["pk", "sk", "lds22", "lds24", "lds42", "rw", "rwk"]
+KERNELS = ["pk", "sk", "lds22", "lds24", "lds42", "rw", "rwk", "rwki"]
 
 
 @pytest.mark.gpu

@@ -45,6 +45,17 @@ typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
 #define MP_LOAD_A_FRAG(p) (*reinterpret_cast<const u16x8*>(p))
 #endif
 
+// A fragment of a packed-activation lane whose row (lane & 15 of its m-tile) may lie past the M
+// real rows: such a lane loads its tile's row-0 chunk instead (the address lane 16 q of the same
+// wave-instruction reads), so at batch 1 a fragment load touches 4 x 16 B instead of 1 KiB of
+// L2 lines (the 16-row tile otherwise streams as many activation bytes as the N = 4096
+// projections stream weights).  Rows >= M of the accumulators then hold row-0 products, which
+// no epilogue stores (every epilogue, slab and row statistic is limited to rows < M).  No
+// branch, no select on the loaded value: the ring's vmcnt accounting is unchanged.
+__device__ __forceinline__ u16x8 load_a_rows(const bf16_t* p, int lane, bool row_ok) {
+  return MP_LOAD_A_FRAG(row_ok ? p : p - (lane & 15) * 8);
+}
+
 // Epilogue side inputs/outputs of the fused-norm decode path (see the header).
 //
 // Row statistics travel as FIXED-POINT sums of squares: every element contributes
@@ -240,8 +251,8 @@ __global__ __launch_bounds__(512) void gemm_packed_kernel(const bf16_t* __restri
       __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(wbase[t] + (int64_t)((grp) * GU + u) * 512));
 #define MP_LOAD_A(grp)                                                                                        \
   _Pragma("unroll") for (int mt = 0; mt < MT; ++mt) _Pragma("unroll") for (int u = 0; u < GU; ++u) a[mt][u] =  \
-      MP_LOAD_A_FRAG(xrow[mt] + (APK ? (int64_t)((grp) * GU + u) * MT * 512                                    \
-                                     : (int64_t)((grp) * GU * 32 + 32 * u)));
+      (APK ? load_a_rows(xrow[mt] + (int64_t)((grp) * GU + u) * MT * 512, lane, mt * 16 + (lane & 15) < M)     \
+           : MP_LOAD_A_FRAG(xrow[mt] + (int64_t)((grp) * GU * 32 + 32 * u)));
 #define MP_MMA(bb)                                                                                            \
   _Pragma("unroll") for (int mt = 0; mt < MT; ++mt) _Pragma("unroll") for (int u = 0; u < GU; ++u)            \
       _Pragma("unroll") for (int t = 0; t < NT; ++t) acc[mt][t] = mfma16(a[mt][u], bb[t][u], acc[mt][t]);
@@ -649,7 +660,8 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(const bf16_t* __restrict__
     _Pragma("unroll") for (int t = 0; t < NT; ++t) rb[s][t] = __builtin_nontemporal_load(                   \
         reinterpret_cast<const u16x8*>(wp + (((int64_t)(g_ * NT + t) * nks + k_) << 9) + lane * 8));        \
     const bf16_t* xa_ = act_ ? x + (((int64_t)k_ * MT) << 9) : zero_a;                                      \
-    _Pragma("unroll") for (int mt = 0; mt < MT; ++mt) ra[s][mt] = MP_LOAD_A_FRAG(xa_ + (mt << 9) + lane * 8); \
+    _Pragma("unroll") for (int mt = 0; mt < MT; ++mt) ra[s][mt] =                                            \
+        load_a_rows(xa_ + (mt << 9) + lane * 8, lane, mt * 16 + (lane & 15) < M);                           \
   }
 
   // sum of the 8 waves' parked partials for quad qd (this lane)
@@ -969,7 +981,7 @@ __device__ __forceinline__ void rw_body(const bf16_t* __restrict__ x, const bf16
     _Pragma("unroll") for (int t = 0; t < NT; ++t) rb[s][t] =                                                \
         __builtin_nontemporal_load(reinterpret_cast<const BT*>(wb + (((int64_t)t * nks + k_) << 9)));       \
     _Pragma("unroll") for (int mt = 0; mt < MT; ++mt) ra[s][mt] =                                            \
-        MP_LOAD_A_FRAG(xl + (((int64_t)k_ * MT + mt) << 9));                                                 \
+        load_a_rows(xl + (((int64_t)k_ * MT + mt) << 9), lane, mt * 16 + (lane & 15) < M);                  \
   }
 #pragma unroll
   for (int s = 0; s < R; ++s) RW_LOAD(s, s)
@@ -1213,7 +1225,7 @@ __global__ __launch_bounds__(256) void gemm_rwk_kernel(const bf16_t* __restrict_
     _Pragma("unroll") for (int t = 0; t < NT; ++t) rb[s][t] =                                                \
         __builtin_nontemporal_load(reinterpret_cast<const BT*>(wb + (((int64_t)t * nks + k_) << 9)));       \
     _Pragma("unroll") for (int mt = 0; mt < MT; ++mt) ra[s][mt] =                                            \
-        MP_LOAD_A_FRAG(xl + (((int64_t)k_ * MT + mt) << 9));                                                 \
+        load_a_rows(xl + (((int64_t)k_ * MT + mt) << 9), lane, mt * 16 + (lane & 15) < M);                  \
   }
 #pragma unroll
   for (int s = 0; s < R; ++s) RWK_LOAD(s, s)

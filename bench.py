@@ -165,14 +165,20 @@ def main(argv=None):
         if device.type == "cuda":
             torch.cuda.synchronize()
 
-    # prefill (TTFT of the whole batch through the pipeline) + first decode round (graph capture)
+    # prefill (TTFT of the whole batch through the pipeline) + first decode round (graph capture),
+    # timed separately as well
     pdist.barrier(device)
     sync()
     tp0 = time.perf_counter()
-    eng.run_rounds(2)
+    eng.run_rounds(1)
+    sync()
+    pdist.barrier(device)
+    tp1 = time.perf_counter()
+    eng.run_rounds(1)
     sync()
     pdist.barrier(device)
     prefill_s = time.perf_counter() - tp0
+    prefill_only_s = pdist.all_max(tp1 - tp0, device)
 
     eng.run_rounds(a.warmup)
     sync()
@@ -202,6 +208,7 @@ def main(argv=None):
     counted = float(n_sessions) if (stage == 0 and lane % TP == 0) else 0.0  # TP lanes mirror one replica
     per_stage = pdist.all_gather_floats([stage_ms, float(end - start), counted], device)
     global_batch = int(sum(p[2] for p in per_stage))
+    n_sessions_total = global_batch
     tokens = a.steps * global_batch  # every session advances one token per round
     value = tokens / dt
     base = baseline_value() if a.model == "llama2-7b" else None  # the baseline is a Llama-2-7B number
@@ -238,6 +245,10 @@ def main(argv=None):
             "per_stage_ms": [round(p[0], 3) for p in per_stage],
             "per_stage_blocks": [int(p[1]) for p in per_stage],
             "prefill_plus_first_token_s": round(prefill_s, 3),
+            # the prefill round alone: every session's prompt through the whole pipeline
+            # (micro-batch slots x batch x prompt-len tokens), max over ranks
+            "prefill_round_s": round(prefill_only_s, 4),
+            "prefill_tokens_per_s": round(n_sessions_total * a.prompt_len / max(prefill_only_s, 1e-9), 1),
             "load_s": round(load_s, 1),
         }
         print(json.dumps(rec), flush=True)

@@ -355,11 +355,29 @@ def query_blocks(ntoks, nrep: int):
     return np.stack([tok0, cnt]).astype(np.int32)
 
 
+def query_superblocks(ntoks, nrep: int, group: int = 4):
+    """Runs of <= ``group`` consecutive query blocks (``query_blocks`` order) of one sequence:
+    int32 [2, NSB] = (first block, count).  The grouped MFMA prefill kernel runs one workgroup
+    per run and streams each K/V step once for all of its blocks."""
+    import numpy as np
+
+    tb = 16 // min(max(int(nrep), 1), 16)
+    nb = (np.asarray(ntoks, dtype=np.int64) + tb - 1) // tb
+    first, cnt, b = [], [], 0
+    for n in nb.tolist():
+        for k in range(0, n, group):
+            first.append(b + k)
+            cnt.append(min(group, n - k))
+        b += n
+    return np.array([first, cnt], dtype=np.int32).reshape(2, -1)
+
+
 def attention_mfma(q, k_cache, v_cache, block_tables, q_seq, q_ctx, qblocks, nh, nkv, scale, out=None,
-                   workspace=None, part_size=None, num_parts=None, max_ctx=None, packed=False):
+                   workspace=None, part_size=None, num_parts=None, max_ctx=None, packed=False, superblocks=None):
     """MFMA flash attention (csrc/attention_mfma.hip): prefill blocks of 16 query rows and GQA
     decode.  Same semantics and output as ``paged_attention``; ``qblocks`` from
-    ``query_blocks`` (device int32 [2, NB])."""
+    ``query_blocks`` (device int32 [2, NB]); ``superblocks`` (``query_superblocks``, device)
+    selects the grouped prefill kernel (up to 4 blocks of a sequence per workgroup)."""
     if not _native(q):
         return paged_attention(q, k_cache, v_cache, block_tables, q_seq, q_ctx, nh, nkv, scale, out=out,
                                packed=packed)
@@ -368,7 +386,7 @@ def attention_mfma(q, k_cache, v_cache, block_tables, q_seq, q_ctx, qblocks, nh,
     if part_size is None:
         if max_ctx is None:
             max_ctx = int(q_ctx.max().item()) if T else 1
-        nblk = qblocks.shape[1] * (nh // min(nh // nkv, 16))
+        nblk = (superblocks.shape[1] if superblocks is not None else qblocks.shape[1]) * (nh // min(nh // nkv, 16))
         want = max(1, math.ceil(1024 / max(1, nblk)))
         num_parts = max(1, min(want, math.ceil(max_ctx / 128)))
         part_size = 128 * math.ceil(math.ceil(max_ctx / num_parts) / 128)
@@ -379,7 +397,7 @@ def attention_mfma(q, k_cache, v_cache, block_tables, q_seq, q_ctx, qblocks, nh,
     if workspace is None or (num_parts > 1 and workspace.numel() < T * nh * num_parts * (D + 2)):
         workspace = attention_workspace(T, nh, D, num_parts, q.device)
     torch.ops.mpamd.attention_mfma(q, k_cache, v_cache, block_tables, q_seq, q_ctx, qblocks, out, workspace, nh, nkv,
-                                   float(scale), int(part_size), int(num_parts), int(bool(packed)))
+                                   float(scale), int(part_size), int(num_parts), int(bool(packed)), superblocks)
     return out
 
 

@@ -288,12 +288,187 @@ __global__ __launch_bounds__(256) void attn_mfma_kernel(
   }
 }
 
+
+// Grouped prefill form: a workgroup owns up to 4 query blocks of ONE sequence (one per wave;
+// superblock table sb_first / sb_n) and streams each 32-token context step ONCE into LDS for
+// all of them - K as a [32][D] tile read back as MFMA A fragments, V transposed as above - so a
+// long prompt reads its K/V 4x less often than with one block per workgroup (the one-block
+// kernel re-streams the whole causal context for every 16 query rows: 2K-token MHA prefill was
+// K/V-bandwidth-bound at ~94 TFLOP/s).  Every wave runs every step (barriers); a wave's rows
+// only see tokens < their own ctx, and each wave finishes its own rows (no cross-wave merge).
+template <int D, int HB>
+__global__ __launch_bounds__(256) void attn_mfma_grp_kernel(
+    const bf16_t* __restrict__ q, int64_t q_stride, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
+    const int32_t* __restrict__ block_tables, int bt_stride, const int32_t* __restrict__ q_seq,
+    const int32_t* __restrict__ q_ctx, const int32_t* __restrict__ qb_tok0, const int32_t* __restrict__ qb_ntok,
+    const int32_t* __restrict__ sb_first, const int32_t* __restrict__ sb_n, bf16_t* __restrict__ out,
+    float* __restrict__ part_o, float* __restrict__ part_ml, int nkv, int nh, int page_log2, int PS, int NP,
+    float scale_log2, int packed_mt) {
+  constexpr int KD = D / 32;
+  constexpr int DT = D / 16;
+  constexpr int KP = D + 8;  // K tile row pitch (bf16): rows 272 B apart stagger the banks
+  __shared__ __attribute__((aligned(16))) bf16_t s_k[32 * KP];
+  __shared__ __attribute__((aligned(16))) bf16_t s_vt[D * VT_PITCH];
+
+  const int p = blockIdx.z;
+  const int hbase = blockIdx.y * HB;
+  const int g = hbase / (nh / nkv);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int c = lane & 15, qd = lane >> 4;
+  const int b_first = sb_first[blockIdx.x], nblk = sb_n[blockIdx.x];
+  const bool wave_ok = w < nblk;
+  const int b = b_first + (wave_ok ? w : 0);
+  const int tok0 = qb_tok0[b], ntok = qb_ntok[b];
+  const int32_t* bt = block_tables + (int64_t)q_seq[tok0] * bt_stride;
+  const int page_size = 1 << page_log2;
+  const int64_t page_stride = (int64_t)nkv * page_size * D;
+  const int64_t head_off = (int64_t)g * page_size * D;
+
+  const int my_t = c / HB, my_h = hbase + c % HB;
+  const bool row_ok = wave_ok && my_t < ntok;
+  const int my_ctx = row_ok ? q_ctx[tok0 + my_t] : 0;
+  int grp_ctx = 0;  // the context the workgroup streams: the largest ctx of any of its tokens
+  for (int bb = b_first; bb < b_first + nblk; ++bb)
+    for (int i = 0; i < qb_ntok[bb]; ++i) grp_ctx = max(grp_ctx, q_ctx[qb_tok0[bb] + i]);
+  const int start = p * PS, end = min(start + PS, grp_ctx);
+
+  u16x8 qf[KD];
+#pragma unroll
+  for (int kd = 0; kd < KD; ++kd) {
+    if (row_ok) qf[kd] = *reinterpret_cast<const u16x8*>(q + (int64_t)(tok0 + my_t) * q_stride + (int64_t)my_h * D +
+                                                         kd * 32 + qd * 8);
+    else qf[kd] = (u16x8)(0);
+  }
+  f32x4 o[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) o[dt] = (f32x4)(0.f);
+  float m = -INFINITY, l = 0.f;
+
+  // the step's K and V (32 tokens, one page: b0 % 32 == 0 and pages hold 32k tokens) are
+  // fetched into registers one step ahead, so the global loads of step i+1 are in flight while
+  // step i computes out of LDS
+  constexpr int CPT = (32 * D / 8 + 255) / 256;  // 16-B chunks per thread per tile
+  u16x8 kreg[CPT], vreg[CPT];
+  auto fetch = [&](int s0) {
+    const int64_t pg = bt[s0 >> page_log2];
+    const bf16_t* kpage = kc + pg * page_stride + head_off + (int64_t)(s0 & (page_size - 1)) * D;
+    const bf16_t* vpage = vc + pg * page_stride + head_off + (int64_t)(s0 & (page_size - 1)) * D;
+#pragma unroll
+    for (int j = 0; j < CPT; ++j) {
+      const int i = tid + 256 * j;
+      const int tk = i / (D / 8), d0 = (i % (D / 8)) * 8;
+      kreg[j] = *reinterpret_cast<const u16x8*>(kpage + (int64_t)tk * D + d0);
+      vreg[j] = *reinterpret_cast<const u16x8*>(vpage + (int64_t)tk * D + d0);
+    }
+  };
+  if (start < end) fetch(start);
+  for (int b0 = start; b0 < end; b0 += 32) {
+#pragma unroll
+    for (int j = 0; j < CPT; ++j) {
+      const int i = tid + 256 * j;
+      const int tk = i / (D / 8), d0 = (i % (D / 8)) * 8;
+      const bool past = b0 + tk >= end;  // past the context: stale cache bytes never meet a p = 0
+      *reinterpret_cast<u16x8*>(s_k + tk * KP + d0) = past ? (u16x8)(0) : kreg[j];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s_vt[(d0 + e) * VT_PITCH + tk] = past ? (bf16_t)0 : vreg[j][e];
+    }
+    __syncthreads();
+    if (b0 + 32 < end) fetch(b0 + 32);
+    if (wave_ok) {
+      f32x4 st[2];
+#pragma unroll
+      for (int sub = 0; sub < 2; ++sub) {
+        st[sub] = (f32x4)(0.f);
+#pragma unroll
+        for (int kd = 0; kd < KD; ++kd) {
+          const u16x8 kf = *reinterpret_cast<const u16x8*>(s_k + (sub * 16 + c) * KP + kd * 32 + qd * 8);
+          st[sub] = mfma_bf16(kf, qf[kd], st[sub]);
+        }
+      }
+      float s8[8];
+      float lm = -INFINITY;
+#pragma unroll
+      for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int tk = b0 + sub * 16 + qd * 4 + r;
+          const float v = (tk < my_ctx && tk < end) ? st[sub][r] * scale_log2 : -INFINITY;
+          s8[sub * 4 + r] = v;
+          lm = fmaxf(lm, v);
+        }
+      lm = fmaxf(lm, __shfl_xor(lm, 16, 64));
+      lm = fmaxf(lm, __shfl_xor(lm, 32, 64));
+      const float m_new = fmaxf(m, lm);
+      const float alpha = (m_new == -INFINITY) ? 1.f : exp2f(m - m_new);
+      u16x8 pa;
+      float ps = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float pv = (m_new == -INFINITY) ? 0.f : exp2f(s8[j] - m_new);
+        const bf16_t pb = f2bf(pv);
+        pa[j] = pb;
+        ps += bf2f(pb);
+      }
+      l = l * alpha + ps;
+      m = m_new;
+      float ar[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) ar[r] = __shfl(alpha, qd * 4 + r, 64);
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        const bf16_t* vrow = s_vt + (dt * 16 + c) * VT_PITCH;
+        const u16x4 lo = *reinterpret_cast<const u16x4*>(vrow + qd * 4);
+        const u16x4 hi = *reinterpret_cast<const u16x4*>(vrow + 16 + qd * 4);
+        const u16x8 vb = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[dt][r] *= ar[r];
+        o[dt] = mfma_bf16(pa, vb, o[dt]);
+      }
+    }
+    __syncthreads();  // the next step overwrites the tiles
+  }
+  if (!wave_ok) return;
+  l += __shfl_xor(l, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+  // this lane holds O rows 4 qd + r (columns dt * 16 + c); row rr's m / l live in lane rr
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int rr = qd * 4 + r;
+    const float lr = __shfl(l, rr, 64), mr = __shfl(m, rr, 64);
+    const int t = rr / HB, h = hbase + rr % HB;
+    if (t >= ntok) continue;
+    const int tok = tok0 + t;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      const int d = dt * 16 + c;
+      if (NP == 1) {
+        const float v = lr > 0.f ? o[dt][r] / lr : 0.f;
+        const int64_t col = (int64_t)h * D + d;
+        out[packed_mt > 0 ? apk_off(tok, (int)col, packed_mt) : (int64_t)tok * nh * D + col] = f2bf(v);
+      } else {
+        const int64_t hp = ((int64_t)tok * nh + h) * NP + p;
+        part_o[hp * D + d] = o[dt][r];
+        if (d == 0) {
+          part_ml[hp * 2] = mr;
+          part_ml[hp * 2 + 1] = lr;
+        }
+      }
+    }
+  }
+}
+
 template <int D, int HB>
 static void launch_attn_mfma(const void* q, int64_t q_stride, const void* kc, const void* vc, const int32_t* bt,
                              int bt_stride, const int32_t* q_seq, const int32_t* q_ctx, const int32_t* qb_tok0,
                              const int32_t* qb_ntok, int NB, void* out, float* ws_o, float* ws_ml, int nkv, int nh,
                              int page_log2, int PS, int NP, float scale_log2, int packed_mt, const RopeFuseM& rf,
-                             hipStream_t stream) {
+                             const int32_t* sb_first, const int32_t* sb_n, int NSB, hipStream_t stream) {
+  if (sb_first != nullptr && NSB > 0 && rf.pos == nullptr) {
+    hipLaunchKernelGGL((attn_mfma_grp_kernel<D, HB>), dim3(NSB, nh / HB, NP), dim3(256), 0, stream, (const bf16_t*)q,
+                       q_stride, (const bf16_t*)kc, (const bf16_t*)vc, bt, bt_stride, q_seq, q_ctx, qb_tok0, qb_ntok,
+                       sb_first, sb_n, (bf16_t*)out, ws_o, ws_ml, nkv, nh, page_log2, PS, NP, scale_log2, packed_mt);
+    return;
+  }
   auto go = [&](auto kern) {
     hipLaunchKernelGGL(kern, dim3(NB, nh / HB, NP), dim3(256), 0, stream, (const bf16_t*)q, q_stride,
                        (const bf16_t*)kc, (const bf16_t*)vc, bt, bt_stride, q_seq, q_ctx, qb_tok0, qb_ntok,
@@ -310,12 +485,15 @@ __global__ void paged_attn_reduce_kernel(const float* __restrict__ part_o, const
 
 // Query blocks: qb_tok0[i] = first flat token of block i, qb_ntok[i] = its token count
 // (<= 16 / heads_per_block, all from one sequence).  heads_per_block = min(nh / nkv, 16).
+// Superblocks (optional, prefill): sb_first[j] / sb_n[j] = runs of <= 4 consecutive query blocks
+// of one sequence, one workgroup each (attn_mfma_grp_kernel).
 extern "C" int mp_attention_mfma(const void* q, int64_t q_stride, const void* kc, const void* vc, const int32_t* bt,
                                  int bt_stride, const int32_t* q_seq, const int32_t* q_ctx, const int32_t* qb_tok0,
                                  const int32_t* qb_ntok, int NB, void* out, float* workspace, int T, int nh, int nkv,
                                  int D, int page_size, int PS, int NP, float scale, int packed_mt,
                                  const int64_t* rope_pos, const float* cos_t, const float* sin_t,
-                                 const int64_t* slots, hipStream_t stream) {
+                                 const int64_t* slots, const int32_t* sb_first, const int32_t* sb_n, int NSB,
+                                 hipStream_t stream) {
   using namespace mp;
   const RopeFuseM rf{rope_pos, cos_t, sin_t, slots, (bf16_t*)const_cast<void*>(kc), (bf16_t*)const_cast<void*>(vc)};
   if (NB == 0 || T == 0) return 0;
@@ -332,7 +510,8 @@ extern "C" int mp_attention_mfma(const void* q, int64_t q_stride, const void* kc
 #define MP_AM_CASE(DD, HH)                                                                                      \
   if (D == DD && hb == HH) {                                                                                    \
     launch_attn_mfma<DD, HH>(q, q_stride, kc, vc, bt, bt_stride, q_seq, q_ctx, qb_tok0, qb_ntok, NB, out, ws_o,  \
-                             ws_ml, nkv, nh, page_log2, PS, NP, scale_log2, packed_mt, rf, stream);             \
+                             ws_ml, nkv, nh, page_log2, PS, NP, scale_log2, packed_mt, rf, sb_first, sb_n, NSB, \
+                             stream);                                                                           \
     goto launched;                                                                                              \
   }
   MP_AM_CASE(128, 1)

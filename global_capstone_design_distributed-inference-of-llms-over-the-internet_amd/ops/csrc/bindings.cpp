@@ -35,7 +35,8 @@ int mp_attention_mfma(const void* q, int64_t q_stride, const void* kc, const voi
                       const int32_t* q_seq, const int32_t* q_ctx, const int32_t* qb_tok0, const int32_t* qb_ntok, int NB,
                       void* out, float* workspace, int T, int nh, int nkv, int D, int page_size, int PS, int NP,
                       float scale, int packed_mt, const int64_t* rope_pos, const float* cos_t, const float* sin_t,
-                      const int64_t* slots, hipStream_t stream);
+                      const int64_t* slots, const int32_t* sb_first, const int32_t* sb_n, int NSB,
+                      hipStream_t stream);
 int mp_quant_act_fp8(const void* ap, void* a8, float* scale, float* part, int M, int K, hipStream_t stream);
 int mp_gemm_fp8(const void* a8, const float* as, const void* wq, const float* ws, void* y, int64_t ys, const void* res,
                 int64_t rs, int M, int N, int K, int epilogue, int out_packed, int kind, float* part,
@@ -259,7 +260,7 @@ static void attention_mfma_impl(const at::Tensor& q, const at::Tensor& k_cache, 
                                 const at::Tensor& qblocks, at::Tensor& out, at::Tensor& workspace, int64_t nh,
                                 int64_t nkv, double scale, int64_t part_size, int64_t num_parts, int64_t packed,
                                 const int64_t* rope_pos, const float* cos_t, const float* sin_t,
-                                const int64_t* slots) {
+                                const int64_t* slots, const c10::optional<at::Tensor>& superblocks = c10::nullopt) {
   check_bf16_cuda(q, "q");
   check_rows(q, "q");
   check_bf16_cuda(out, "out");
@@ -282,21 +283,32 @@ static void attention_mfma_impl(const at::Tensor& q, const at::Tensor& k_cache, 
   MP_CHECK(qblocks.scalar_type() == at::kInt && qblocks.dim() == 2 && qblocks.size(0) == 2 && qblocks.is_contiguous(),
            "qblocks int32 [2, NB] (first token, token count)");
   const int NB = qblocks.size(1);
+  const int32_t* sbp = nullptr;
+  int NSB = 0;
+  if (superblocks.has_value()) {  // prefill superblocks: int32 [2, NSB] (first query block, count <= 4)
+    MP_CHECK(superblocks->is_cuda() && superblocks->scalar_type() == at::kInt && superblocks->dim() == 2 &&
+                 superblocks->size(0) == 2 && superblocks->is_contiguous() && superblocks->size(1) <= NB,
+             "superblocks int32 [2, NSB] (ops.query_superblocks)");
+    sbp = superblocks->data_ptr<int32_t>();
+    NSB = superblocks->size(1);
+  }
   check_launch(mp_attention_mfma(q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
                                  block_tables.data_ptr<int32_t>(), block_tables.stride(0), q_seq.data_ptr<int32_t>(),
                                  q_ctx.data_ptr<int32_t>(), qblocks.data_ptr<int32_t>(),
                                  qblocks.data_ptr<int32_t>() + NB, NB, out.data_ptr(), workspace.data_ptr<float>(), T,
                                  nh, nkv, D, k_cache.size(2), part_size, num_parts, (float)scale,
-                                 packed ? (int)((T + 15) / 16) : 0, rope_pos, cos_t, sin_t, slots, cur_stream()),
+                                 packed ? (int)((T + 15) / 16) : 0, rope_pos, cos_t, sin_t, slots, sbp,
+                                 sbp != nullptr ? sbp + NSB : nullptr, NSB, cur_stream()),
                "attention_mfma");
 }
 
 void attention_mfma(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
                     const at::Tensor& block_tables, const at::Tensor& q_seq, const at::Tensor& q_ctx,
                     const at::Tensor& qblocks, at::Tensor& out, at::Tensor& workspace, int64_t nh, int64_t nkv,
-                    double scale, int64_t part_size, int64_t num_parts, int64_t packed) {
+                    double scale, int64_t part_size, int64_t num_parts, int64_t packed,
+                    const c10::optional<at::Tensor>& superblocks) {
   attention_mfma_impl(q, k_cache, v_cache, block_tables, q_seq, q_ctx, qblocks, out, workspace, nh, nkv, scale,
-                      part_size, num_parts, packed, nullptr, nullptr, nullptr, nullptr);
+                      part_size, num_parts, packed, nullptr, nullptr, nullptr, nullptr, superblocks);
 }
 
 // GQA decode with RoPE + KV write fused (attention_mfma.hip ROPE path): one token per query block.
@@ -629,7 +641,7 @@ TORCH_LIBRARY(mpamd, m) {
   m.def(
       "attention_mfma(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor q_seq, Tensor q_ctx, "
       "Tensor qblocks, Tensor(a!) out, Tensor(b!) workspace, int nh, int nkv, float scale, int part_size, "
-      "int num_parts, int packed) -> ()");
+      "int num_parts, int packed, Tensor? superblocks=None) -> ()");
   m.def(
       "attention_mfma_rope(Tensor qkv, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor block_tables, Tensor q_seq, "
       "Tensor q_ctx, Tensor qblocks, Tensor positions, Tensor cos, Tensor sin, Tensor slots, Tensor(c!) out, "

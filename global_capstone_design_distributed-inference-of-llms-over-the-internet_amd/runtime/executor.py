@@ -62,6 +62,7 @@ class Plan:
     h64: np.ndarray                     # [2, T] positions, slots (pinned host view)
     h32: np.ndarray                     # [2*T + S] q_seq, q_ctx, last_rows (pinned host view)
     qblocks: Optional[torch.Tensor] = None  # [2, NB] MFMA-attention query blocks (prefill steps)
+    superblocks: Optional[torch.Tensor] = None  # [2, NSB] runs of <= 4 blocks (grouped prefill kernel)
     _dev: Optional[Tuple[torch.Tensor, torch.Tensor]] = None
     _upload: Optional[object] = None    # callable making the device copies
 
@@ -186,6 +187,10 @@ class StageExecutor:
         # sessions and 13847 vs 16248 at 128 (Llama-2-7B, profiles/r1_attn_mha_mfma_vs_simt/)
         self._attn_mfma_gqa = self._attn_mfma_prefill and (
             self.nh // self.nkv >= 4 or os.environ.get("MPAMD_ATTN_MFMA_DECODE", "0") == "1")
+        # prefill: up to 4 query blocks of a sequence per workgroup share each K/V step
+        # (csrc/attention_mfma.hip attn_mfma_grp_kernel); MPAMD_ATTN_GROUPED=0 = one block each
+        self._attn_grouped = os.environ.get("MPAMD_ATTN_GROUPED", "1") != "0"
+        self._cur_sb = None
         # decode steps on the flash-decoding kernel fold RoPE + the KV page write into it
         self._fuse_rope = os.environ.get("MPAMD_FUSE_ROPE", "1") != "0"
         # shortest split-K context slice (ops.attention_partition): longer on the MFMA GQA kernel
@@ -296,10 +301,13 @@ class StageExecutor:
                 d32 = h32[: 2 * T + S].clone()
             return d64, d32
 
-        qb = None
+        qb = sb = None
         if self.device.type == "cuda" and not is_decode and self._attn_mfma_prefill:
             qb = torch.from_numpy(ops.query_blocks(ntoks, self.nh // self.nkv)).to(self.device, non_blocking=True)
-        return Plan(sess, ntoks, st, T, max_ctx, is_decode, n64, n32, qb, _upload=upload)
+            if self._attn_grouped:
+                sb = torch.from_numpy(ops.query_superblocks(ntoks, self.nh // self.nkv)).to(self.device,
+                                                                                              non_blocking=True)
+        return Plan(sess, ntoks, st, T, max_ctx, is_decode, n64, n32, qb, sb, _upload=upload)
 
     def commit(self, plan: Plan) -> None:
         for s, n in zip(plan.sessions, plan.ntoks):
@@ -406,9 +414,13 @@ class StageExecutor:
         elif self.cfg.model_type == "gpt2":
             out = self._forward_gpt2(plan, x, prompt=prompt)
         else:
-            out = self._forward_llama(x, plan.positions, plan.slots, plan.q_seq, plan.q_ctx, plan.last_rows,
-                                      plan.T, plan.max_ctx, None, qblocks=plan.qblocks, prompt=prompt,
-                                      decode=plan.is_decode)
+            self._cur_sb = plan.superblocks
+            try:
+                out = self._forward_llama(x, plan.positions, plan.slots, plan.q_seq, plan.q_ctx, plan.last_rows,
+                                          plan.T, plan.max_ctx, None, qblocks=plan.qblocks, prompt=prompt,
+                                          decode=plan.is_decode)
+            finally:
+                self._cur_sb = None
         if ev is not None:
             ev[1].record()
             ev[1].synchronize()
@@ -440,7 +452,8 @@ class StageExecutor:
                                       packed=packed)
         if qblocks is not None:
             return ops.attention_mfma(qkv, kc, vc, table, q_seq, q_ctx, qblocks, self.nh, self.nkv, self.scale,
-                                      out=out, workspace=ws, max_ctx=max_ctx, packed=packed)
+                                      out=out, workspace=ws, max_ctx=max_ctx, packed=packed,
+                                      superblocks=getattr(self, "_cur_sb", None))
         return ops.paged_attention(qkv, kc, vc, table, q_seq, q_ctx, self.nh, self.nkv, self.scale, out=out,
                                    workspace=ws, part_size=ps, num_parts=np_, packed=packed)
 

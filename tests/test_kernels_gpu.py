@@ -593,6 +593,37 @@ def test_attention_mfma_matches_reference(nh, nkv, D, ctxs, multi):
                                rtol=2e-2)
 
 
+@pytest.mark.parametrize("nh,nkv,D", [(32, 32, 128), (32, 8, 128), (12, 12, 64), (64, 8, 128)])
+@pytest.mark.parametrize("ntoks,prefix", [([70, 9, 1, 33, 130], [0, 0, 0, 0, 0]), ([300, 17], [64, 5]),
+                                          ([1000], [0]), ([48, 64], [1, 200])])
+@pytest.mark.parametrize("parts", [None, (128, 3)])
+def test_attention_mfma_grouped_prefill(nh, nkv, D, ntoks, prefix, parts):
+    """Grouped MFMA prefill (up to 4 query blocks of a sequence per workgroup sharing each K/V
+    step) vs the fp32 reference: ragged prompts, chunked prefill over an existing prefix
+    (ctx = prefix + i + 1), split-K partitions, packed output."""
+    ctxs = [p + n for p, n in zip(prefix, ntoks)]
+    q, kc, vc, bt, _, _ = _attn_case(nh, nkv, D, ctxs)
+    q_seq = torch.cat([torch.full((n,), i, dtype=torch.int32) for i, n in enumerate(ntoks)]).to(DEV)
+    q_ctx = torch.cat([torch.arange(p + 1, p + n + 1, dtype=torch.int32) for p, n in zip(prefix, ntoks)]).to(DEV)
+    T = q_seq.numel()
+    q = bf(torch.randn(T, (nh + 2 * nkv) * D, device=DEV))
+    qb = torch.from_numpy(ops.query_blocks(ntoks, nh // nkv)).to(DEV)
+    sb = torch.from_numpy(ops.query_superblocks(ntoks, nh // nkv)).to(DEV)
+    assert int(sb[1].sum()) == qb.shape[1] and int(sb[1].max()) <= 4
+    scale = 1 / math.sqrt(D)
+    kw = {} if parts is None else dict(part_size=parts[0], num_parts=math.ceil(max(ctxs) / parts[0]))
+    out = ops.attention_mfma(q, kc, vc, bt, q_seq, q_ctx, qb, nh, nkv, scale, superblocks=sb, **kw)
+    o_ref = ref.paged_attention(q.float(), kc.float(), vc.float(), bt, q_seq, q_ctx, nh, nkv, scale)
+    torch.testing.assert_close(out.float(), o_ref.float(), atol=2e-2, rtol=2e-2)
+    outp = ops.attention_mfma(q, kc, vc, bt, q_seq, q_ctx, qb, nh, nkv, scale, superblocks=sb, packed=True, **kw)
+    torch.testing.assert_close(ops.unpack_act(outp, T, nh * D).float(), o_ref.float(), atol=2e-2, rtol=2e-2)
+
+
+def test_query_superblocks():
+    assert ops.query_superblocks([5, 1, 70], 1).tolist() == [[0, 1, 2, 6], [1, 1, 4, 1]]
+    assert ops.query_superblocks([16], 4).tolist() == [[0], [4]]
+
+
 def test_query_blocks():
     qb = ops.query_blocks([5, 1, 17], 1)
     assert qb.tolist() == [[0, 5, 6, 22], [5, 1, 16, 1]]

@@ -355,7 +355,7 @@ def query_blocks(ntoks, nrep: int):
     return np.stack([tok0, cnt]).astype(np.int32)
 
 
-def query_superblocks(ntoks, nrep: int, group: int = 4):
+def query_superblocks(ntoks, nrep: int, group: int = 8):
     """Runs of <= ``group`` consecutive query blocks (``query_blocks`` order) of one sequence:
     int32 [2, NSB] = (first block, count).  The grouped MFMA prefill kernel runs one workgroup
     per run and streams each K/V step once for all of its blocks."""

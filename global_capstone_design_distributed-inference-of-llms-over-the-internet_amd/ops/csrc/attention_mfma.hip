@@ -289,15 +289,15 @@ __global__ __launch_bounds__(256) void attn_mfma_kernel(
 }
 
 
-// Grouped prefill form: a workgroup owns up to 4 query blocks of ONE sequence (one per wave;
+// Grouped prefill form: a workgroup owns up to NWG (8) query blocks of ONE sequence (one per wave;
 // superblock table sb_first / sb_n) and streams each 32-token context step ONCE into LDS for
 // all of them - K as a [32][D] tile read back as MFMA A fragments, V transposed as above - so a
 // long prompt reads its K/V 4x less often than with one block per workgroup (the one-block
 // kernel re-streams the whole causal context for every 16 query rows: 2K-token MHA prefill was
 // K/V-bandwidth-bound at ~94 TFLOP/s).  Every wave runs every step (barriers); a wave's rows
 // only see tokens < their own ctx, and each wave finishes its own rows (no cross-wave merge).
-template <int D, int HB>
-__global__ __launch_bounds__(256) void attn_mfma_grp_kernel(
+template <int D, int HB, int NWG>
+__global__ __launch_bounds__(NWG * 64) void attn_mfma_grp_kernel(
     const bf16_t* __restrict__ q, int64_t q_stride, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
     const int32_t* __restrict__ block_tables, int bt_stride, const int32_t* __restrict__ q_seq,
     const int32_t* __restrict__ q_ctx, const int32_t* __restrict__ qb_tok0, const int32_t* __restrict__ qb_ntok,
@@ -347,7 +347,8 @@ __global__ __launch_bounds__(256) void attn_mfma_grp_kernel(
   // the step's K and V (32 tokens, one page: b0 % 32 == 0 and pages hold 32k tokens) are
   // fetched into registers one step ahead, so the global loads of step i+1 are in flight while
   // step i computes out of LDS
-  constexpr int CPT = (32 * D / 8 + 255) / 256;  // 16-B chunks per thread per tile
+  constexpr int NCH = 32 * D / 8;                           // 16-B chunks per tile
+  constexpr int CPT = (NCH + NWG * 64 - 1) / (NWG * 64);  // per thread
   u16x8 kreg[CPT], vreg[CPT];
   auto fetch = [&](int s0) {
     const int64_t pg = bt[s0 >> page_log2];
@@ -355,7 +356,8 @@ __global__ __launch_bounds__(256) void attn_mfma_grp_kernel(
     const bf16_t* vpage = vc + pg * page_stride + head_off + (int64_t)(s0 & (page_size - 1)) * D;
 #pragma unroll
     for (int j = 0; j < CPT; ++j) {
-      const int i = tid + 256 * j;
+      const int i = tid + NWG * 64 * j;
+      if (NCH % (NWG * 64) != 0 && i >= NCH) break;
       const int tk = i / (D / 8), d0 = (i % (D / 8)) * 8;
       kreg[j] = *reinterpret_cast<const u16x8*>(kpage + (int64_t)tk * D + d0);
       vreg[j] = *reinterpret_cast<const u16x8*>(vpage + (int64_t)tk * D + d0);
@@ -365,7 +367,8 @@ __global__ __launch_bounds__(256) void attn_mfma_grp_kernel(
   for (int b0 = start; b0 < end; b0 += 32) {
 #pragma unroll
     for (int j = 0; j < CPT; ++j) {
-      const int i = tid + 256 * j;
+      const int i = tid + NWG * 64 * j;
+      if (NCH % (NWG * 64) != 0 && i >= NCH) break;
       const int tk = i / (D / 8), d0 = (i % (D / 8)) * 8;
       const bool past = b0 + tk >= end;  // past the context: stale cache bytes never meet a p = 0
       *reinterpret_cast<u16x8*>(s_k + tk * KP + d0) = past ? (u16x8)(0) : kreg[j];
@@ -464,7 +467,7 @@ static void launch_attn_mfma(const void* q, int64_t q_stride, const void* kc, co
                              int page_log2, int PS, int NP, float scale_log2, int packed_mt, const RopeFuseM& rf,
                              const int32_t* sb_first, const int32_t* sb_n, int NSB, hipStream_t stream) {
   if (sb_first != nullptr && NSB > 0 && rf.pos == nullptr) {
-    hipLaunchKernelGGL((attn_mfma_grp_kernel<D, HB>), dim3(NSB, nh / HB, NP), dim3(256), 0, stream, (const bf16_t*)q,
+    hipLaunchKernelGGL((attn_mfma_grp_kernel<D, HB, 8>), dim3(NSB, nh / HB, NP), dim3(512), 0, stream, (const bf16_t*)q,
                        q_stride, (const bf16_t*)kc, (const bf16_t*)vc, bt, bt_stride, q_seq, q_ctx, qb_tok0, qb_ntok,
                        sb_first, sb_n, (bf16_t*)out, ws_o, ws_ml, nkv, nh, page_log2, PS, NP, scale_log2, packed_mt);
     return;
@@ -485,7 +488,7 @@ __global__ void paged_attn_reduce_kernel(const float* __restrict__ part_o, const
 
 // Query blocks: qb_tok0[i] = first flat token of block i, qb_ntok[i] = its token count
 // (<= 16 / heads_per_block, all from one sequence).  heads_per_block = min(nh / nkv, 16).
-// Superblocks (optional, prefill): sb_first[j] / sb_n[j] = runs of <= 4 consecutive query blocks
+// Superblocks (optional, prefill): sb_first[j] / sb_n[j] = runs of <= 8 consecutive query blocks
 // of one sequence, one workgroup each (attn_mfma_grp_kernel).
 extern "C" int mp_attention_mfma(const void* q, int64_t q_stride, const void* kc, const void* vc, const int32_t* bt,
                                  int bt_stride, const int32_t* q_seq, const int32_t* q_ctx, const int32_t* qb_tok0,

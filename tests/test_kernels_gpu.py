@@ -609,7 +609,7 @@ def test_attention_mfma_grouped_prefill(nh, nkv, D, ntoks, prefix, parts):
     q = bf(torch.randn(T, (nh + 2 * nkv) * D, device=DEV))
     qb = torch.from_numpy(ops.query_blocks(ntoks, nh // nkv)).to(DEV)
     sb = torch.from_numpy(ops.query_superblocks(ntoks, nh // nkv)).to(DEV)
-    assert int(sb[1].sum()) == qb.shape[1] and int(sb[1].max()) <= 4
+    assert int(sb[1].sum()) == qb.shape[1] and int(sb[1].max()) <= 8
     scale = 1 / math.sqrt(D)
     kw = {} if parts is None else dict(part_size=parts[0], num_parts=math.ceil(max(ctxs) / parts[0]))
     out = ops.attention_mfma(q, kc, vc, bt, q_seq, q_ctx, qb, nh, nkv, scale, superblocks=sb, **kw)
@@ -620,8 +620,10 @@ def test_attention_mfma_grouped_prefill(nh, nkv, D, ntoks, prefix, parts):
 
 
 def test_query_superblocks():
-    assert ops.query_superblocks([5, 1, 70], 1).tolist() == [[0, 1, 2, 6], [1, 1, 4, 1]]
+    assert ops.query_superblocks([5, 1, 70], 1).tolist() == [[0, 1, 2], [1, 1, 5]]
+    assert ops.query_superblocks([5, 1, 70], 1, group=4).tolist() == [[0, 1, 2, 6], [1, 1, 4, 1]]
     assert ops.query_superblocks([16], 4).tolist() == [[0], [4]]
+    assert ops.query_superblocks([40], 4).tolist() == [[0, 8], [8, 2]]
 
 
 def test_query_blocks():

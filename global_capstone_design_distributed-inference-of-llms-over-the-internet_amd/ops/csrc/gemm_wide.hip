@@ -1,0 +1,45 @@
+// Decode GEMM for 65..128 rows (the unfused packed decode path at 96 / 128 sessions): split-K
+// ring (o, down) and balanced ring kernels at MT = 5..8 (kernels: gemm_kernels.h).
+#include "gemm_kernels.h"
+
+extern "C" int mp_gemm_bf16_wide(const void* x, const void* w, void* y, int64_t y_stride, const void* res,
+                                 int64_t res_stride, int M, int N, int K, int epilogue, int flags, void* ws,
+                                 const mp::EpiArgs& ep, hipStream_t stream) {
+  using namespace mp;
+  int rc = 1;
+  if ((flags & 256) && !(flags & 2) && ws != nullptr) {  // split-K ring
+#define MP_RWK(MT_) \
+  rc = launch_gemm_rwk<MT_>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, ep, ws, stream, (flags & 512) != 0)
+    switch ((M + 15) / 16) {
+      case 5: MP_RWK(5); break;
+      case 6: MP_RWK(6); break;
+      case 7: MP_RWK(7); break;
+      default: MP_RWK(8); break;
+    }
+#undef MP_RWK
+    if (rc < 0) return rc;
+    if (rc == 0) return (int)hipGetLastError();
+  }
+  if (M <= 80) rc = launch_gemm_rw<5>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, ep, stream);
+  else if (M <= 96) rc = launch_gemm_rw<6>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, ep, stream);
+  else if (M <= 112) rc = launch_gemm_rw<7>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, ep, stream);
+  else rc = launch_gemm_rw<8>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, ep, stream);
+  if (rc != 0) return rc < 0 ? rc : -1;
+  return (int)hipGetLastError();
+}
+
+// 1 if mp_gemm_bf16 covers a packed-activation decode GEMM of M = 65..128 rows (balanced ring
+// kernel: the widths built, epilogue 0 or packed SwiGLU), else 0.  No launch.
+extern "C" int mp_gemm_rw_ok(int M, int N, int K, int epilogue, int out_packed) {
+  using namespace mp;
+  if (M <= 64 || M > 128 || K % (32 * GU_MAX) || N % 16) return 0;
+  const EpiArgs ep{};
+  const int flags = 1 | (out_packed ? 2 : 0) | 128;
+  int rc;
+  if (M <= 80) rc = launch_gemm_rw<5>(nullptr, nullptr, nullptr, 0, nullptr, 0, M, N, K, epilogue, flags, ep, 0, true);
+  else if (M <= 96) rc = launch_gemm_rw<6>(nullptr, nullptr, nullptr, 0, nullptr, 0, M, N, K, epilogue, flags, ep, 0, true);
+  else if (M <= 112) rc = launch_gemm_rw<7>(nullptr, nullptr, nullptr, 0, nullptr, 0, M, N, K, epilogue, flags, ep, 0, true);
+  else rc = launch_gemm_rw<8>(nullptr, nullptr, nullptr, 0, nullptr, 0, M, N, K, epilogue, flags, ep, 0, true);
+  return rc == 0;
+}
+

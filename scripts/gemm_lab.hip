@@ -23,6 +23,8 @@
 #define MP_LOAD_A_FRAG(p) (*reinterpret_cast<const mp::u16x8*>((const char*)x + (((uintptr_t)(p) - (uintptr_t)x) & 4095)))
 #endif
 #include "gemm.hip"
+#include "gemm_wide.hip"  // 65..128-row entry point (mp_gemm_bf16 calls it)
+#include "gemm_w8.hip"
 
 #define CK(x)                                                                       \
   do {                                                                              \

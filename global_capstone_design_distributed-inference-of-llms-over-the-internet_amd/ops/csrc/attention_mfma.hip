@@ -360,7 +360,11 @@ __global__ __launch_bounds__(NWG * 64) void attn_mfma_grp_kernel(
       if (NCH % (NWG * 64) != 0 && i >= NCH) break;
       const int tk = i / (D / 8), d0 = (i % (D / 8)) * 8;
       kreg[j] = *reinterpret_cast<const u16x8*>(kpage + (int64_t)tk * D + d0);
-      vreg[j] = *reinterpret_cast<const u16x8*>(vpage + (int64_t)tk * D + d0);
+      // V: tokens vary fastest across lanes, so the transposed LDS writes below are 32
+      // consecutive bf16 of one d row per half-wave (no bank conflicts; token-major lanes put
+      // 16 lanes on 4 banks)
+      const int tv = i % 32, dv = (i / 32) * 8;
+      vreg[j] = *reinterpret_cast<const u16x8*>(vpage + (int64_t)tv * D + dv);
     }
   };
   if (start < end) fetch(start);
@@ -372,8 +376,10 @@ __global__ __launch_bounds__(NWG * 64) void attn_mfma_grp_kernel(
       const int tk = i / (D / 8), d0 = (i % (D / 8)) * 8;
       const bool past = b0 + tk >= end;  // past the context: stale cache bytes never meet a p = 0
       *reinterpret_cast<u16x8*>(s_k + tk * KP + d0) = past ? (u16x8)(0) : kreg[j];
+      const int tv = i % 32, dv = (i / 32) * 8;
+      const bool vpast = b0 + tv >= end;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) s_vt[(d0 + e) * VT_PITCH + tk] = past ? (bf16_t)0 : vreg[j][e];
+      for (int e = 0; e < 8; ++e) s_vt[(dv + e) * VT_PITCH + tv] = vpast ? (bf16_t)0 : vreg[j][e];
     }
     __syncthreads();
     if (b0 + 32 < end) fetch(b0 + 32);

@@ -174,10 +174,12 @@ __global__ __launch_bounds__(256) void attn_mfma_kernel(
       }
     }
     // ---- V tile -> LDS transposed [d][tok] (this wave only; in-order LDS needs no barrier) ----
+    // tokens vary fastest across lanes: each half-wave's transposed stores are 32 consecutive
+    // bf16 of one d row (token-major lanes would put 16 lanes on 4 banks, sub-dword)
 #pragma unroll
     for (int i = 0; i < (32 * D * 2) / 1024; ++i) {
-      const int byte = i * 1024 + lane * 16;
-      const int tk = byte / (D * 2), d0 = (byte % (D * 2)) / 2;
+      const int ci = i * 64 + lane;
+      const int tk = ci % 32, d0 = (ci / 32) * 8;
       u16x8 vv = *reinterpret_cast<const u16x8*>(vpage + (int64_t)tk * D + d0);
       if (b0 + tk >= end) vv = (u16x8)(0);
 #pragma unroll

@@ -44,6 +44,13 @@ def baseline_value():
         return None
 
 
+def fp8_label(ex) -> str:
+    """The precision path the executor actually runs for fp8 weights."""
+    if getattr(ex, "_w8", False):
+        return "fp8-w8a16 (e4m3 weights, bf16 activations/KV)"
+    return "fp8-w8a8 (e4m3 weights and activations, bf16 KV)"
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=None)
@@ -63,7 +70,12 @@ def main(argv=None):
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--tp", type=int, default=1,
                     help="tensor-parallel degree inside each stage (RCCL all-reduce after o / down)")
-    ap.add_argument("--fp8", action="store_true", help="fp8 (OCP e4m3) W8A8 projections (the 70B config)")
+    ap.add_argument("--fp8", action="store_true",
+                    help="fp8 (OCP e4m3) projection weights (the 70B config): W8A16 by default, W8A8 with "
+                         "MPAMD_FP8_MODE=w8a8")
+    ap.add_argument("--splits", default="auto",
+                    help="'auto' (cost-balanced: lm_head + sampler weigh on the tail, partition.balanced_splits), "
+                         "'even', or explicit cut points")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--device", default=None)
     a = ap.parse_args(argv)
@@ -75,7 +87,7 @@ def main(argv=None):
     from src.parallel.channel import Channel
     from src.parallel.engine import PipelineServingEngine, Request
     from src.parallel.tensor_parallel import make_tp_groups, shard_stage_weights
-    from src.partition import even_splits, stage_ranges
+    from src.partition import balanced_splits, even_splits, parse_splits, stage_ranges
     from src.runtime.executor import StageExecutor
     from src.runtime.sampler import SamplingParams
 
@@ -96,10 +108,17 @@ def main(argv=None):
     tpg = make_tp_groups(world, S, TP)
     stage = rank % S
     lane = rank // S                      # pipeline index: replica * TP + tensor-parallel shard
-    cuts = even_splits(cfg.num_hidden_layers, S)
-    start, end = stage_ranges(cuts, cfg.num_hidden_layers)[stage]
     M = a.micro or (S + 1 if S > 1 else 1)  # one slot of slack for the token-return hop
     B = a.batch
+    if a.splits == "auto":
+        cuts = balanced_splits(cfg, S, batch=B, ctx=a.prompt_len + (a.warmup + a.steps) // 2, fp8=a.fp8)
+    elif a.splits == "even":
+        cuts = even_splits(cfg.num_hidden_layers, S)
+    else:
+        cuts = parse_splits(a.splits, cfg.num_hidden_layers)
+        if len(cuts) != S - 1:
+            raise SystemExit(f"--splits {a.splits} defines {len(cuts) + 1} stages, the run has {S}")
+    start, end = stage_ranges(cuts, cfg.num_hidden_layers)[stage]
     dtype = torch.bfloat16
     t0 = time.time()
     w = random_stage_weights(cfg, start, end, has_embed=stage == 0, has_head=stage == S - 1, device=device,
@@ -184,6 +203,9 @@ def main(argv=None):
     sync()
     pdist.barrier(device)
     sync()
+    if ch is not None:
+        ch.stats(reset=True)
+        ch.timing = True
     t1 = time.perf_counter()
     eng.timing = True
     eng.run_rounds(a.steps)
@@ -192,7 +214,10 @@ def main(argv=None):
     sync()
     dt_local = time.perf_counter() - t1
     eng.timing = False
+    if ch is not None:
+        ch.timing = False
     stage_ms = eng.stage_ms() or 0.0
+    hop = ch.stats() if ch is not None else {"backend": "none", "bytes_sent": 0, "sends": 0, "recv_wait_ms": 0.0}
     n_tokens = 0
     if stage == 0:
         eng.drain()
@@ -206,7 +231,8 @@ def main(argv=None):
         ch.close()
     dt = pdist.all_max(dt_local, device)
     counted = float(n_sessions) if (stage == 0 and lane % TP == 0) else 0.0  # TP lanes mirror one replica
-    per_stage = pdist.all_gather_floats([stage_ms, float(end - start), counted], device)
+    per_stage = pdist.all_gather_floats([stage_ms, float(end - start), counted, float(hop["bytes_sent"]),
+                                         float(hop["sends"]), float(hop["recv_wait_ms"])], device)
     global_batch = int(sum(p[2] for p in per_stage))
     n_sessions_total = global_batch
     tokens = a.steps * global_batch  # every session advances one token per round
@@ -225,7 +251,7 @@ def main(argv=None):
             "scaling": "weak",
             "vs_baseline": (round(value / (base * world), 3) if base else None),
             "baseline_tokens_per_s_per_gpu": base,
-            "dtype": "fp8-w8a8 (bf16 activations/KV)" if a.fp8 else "bf16",
+            "dtype": fp8_label(ex) if a.fp8 else "bf16",
             "data": f"synthetic (random-init {cfg.name} weights, random prompt ids)",
             "config": {
                 "model": {"llama2-7b": "Llama-2-7B", "llama3-70b": "Llama-3-70B", "llama3-8b": "Llama-3-8B"}.get(
@@ -244,6 +270,13 @@ def main(argv=None):
             },
             "per_stage_ms": [round(p[0], 3) for p in per_stage],
             "per_stage_blocks": [int(p[1]) for p in per_stage],
+            # the device channel of every pipeline: which backend carried the hops (RCCL over
+            # xGMI on a multi-GPU node), payload bytes each rank sent during the timed steps,
+            # and how long each rank's stream waited for its incoming payload per step
+            "channel_backend": hop["backend"],
+            "hop_bytes_sent_per_rank": [int(p[3]) for p in per_stage],
+            "hop_sends_per_rank": [int(p[4]) for p in per_stage],
+            "hop_recv_wait_ms_per_rank": [round(p[5], 4) for p in per_stage],
             "prefill_plus_first_token_s": round(prefill_s, 3),
             # the prefill round alone: every session's prompt through the whole pipeline
             # (micro-batch slots x batch x prompt-len tokens), max over ranks

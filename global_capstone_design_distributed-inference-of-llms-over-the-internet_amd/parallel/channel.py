@@ -112,9 +112,41 @@ class _Pending:
                 w.wait(_td(timeout_s))
 
 
+class _SlabRing:
+    """Preallocated device byte slabs reused round-robin for RCCL payloads (no per-hop
+    ``clone`` / ``empty``: the caching allocator and its cross-stream bookkeeping stay off the
+    hop).  A slab is handed out again only after a stream dependency on the work that last
+    used it (``work.wait()`` = the current stream waits for the RCCL stream, no host block),
+    so a send is never overwritten in flight; a receive slab's readers were enqueued on the
+    current stream before the next receive into it is posted, and RCCL's stream waits for
+    them.  Slabs grow (per slot, lazily) to the largest payload seen."""
+
+    def __init__(self, device: torch.device, slots: int):
+        self.device = device
+        self.bufs: List[Optional[torch.Tensor]] = [None] * int(slots)
+        self.works: List[Optional[object]] = [None] * int(slots)
+        self.k = -1
+
+    def take(self, shape, dtype) -> Tuple[int, torch.Tensor]:
+        self.k = (self.k + 1) % len(self.bufs)
+        k = self.k
+        w = self.works[k]
+        if w is not None:
+            w.wait()
+            self.works[k] = None
+        n = int(np.prod(shape)) * torch.empty((), dtype=dtype).element_size()
+        buf = self.bufs[k]
+        if buf is None or buf.numel() < n:
+            buf = self.bufs[k] = torch.empty(max(n, 1 << 16), dtype=torch.uint8, device=self.device)
+        return k, buf[:n].view(dtype).view(shape)
+
+    def done(self, k: int, work) -> None:
+        self.works[k] = work
+
+
 class Channel:
     def __init__(self, store, prefix: str, rank: int, world: int, device, timeout_s: float = 120.0,
-                 data_backend: Optional[str] = None):
+                 data_backend: Optional[str] = None, ring_slots: int = 32):
         self.rank, self.world = int(rank), int(world)
         self.device = torch.device(device)
         self.timeout_s = float(timeout_s)
@@ -133,7 +165,17 @@ class Channel:
         self._sends = _Pending()
         self._msg_sends = _Pending()
         self.closed = False
+        # hop statistics (bench JSON / serving logs): payload bytes and sends, and how long this
+        # rank's compute stream waited for an incoming payload (device: HIP events around the
+        # stream wait; host paths: wall time of the blocking wait)
         self.bytes_sent = 0
+        self.sends = 0
+        self.timing = False
+        self._wait_events: List[Tuple[object, object]] = []
+        self._wait_host_s: List[float] = []
+        self._rings = {}
+        if data_backend == "nccl" and self.device.type == "cuda":
+            self._rings = {(w, d): _SlabRing(self.device, ring_slots) for w in ("data", "ret") for d in ("send", "recv")}
 
     # ------------------------------------------------------------------ host control messages
     def send_msg(self, dst: int, arr: np.ndarray) -> None:
@@ -180,12 +222,20 @@ class Channel:
         e.g. a hipGraph output buffer - while the send is in flight)."""
         pg = self._pg(which)
         try:
-            if self.staged:
+            ring = self._rings.get((which, "send"))
+            if ring is not None:
+                k, buf = ring.take(tuple(t.shape), t.dtype)
+                buf.copy_(t.detach())
+            elif self.staged:
                 buf = t.detach().to("cpu")
             else:
                 buf = t.detach().clone()
             self.bytes_sent += buf.numel() * buf.element_size()
-            self._sends.add(pg.send([buf], dst, 0), buf)
+            self.sends += 1
+            work = pg.send([buf], dst, 0)
+            if ring is not None:
+                ring.done(k, work)
+            self._sends.add(work, buf)
             self._sends.reap()
         except RuntimeError as e:
             raise ChannelError(f"{which} send to {dst} failed: {e}") from e
@@ -202,23 +252,55 @@ class Channel:
                 work = pg.recv([host], src, 0)
 
                 def waiter():
+                    t0 = time.perf_counter()
                     try:
                         work.wait(_td(t))
                     except RuntimeError as e:
                         raise ChannelError(f"{which} recv from {src} failed: {e}") from e
+                    if self.timing:
+                        self._wait_host_s.append(time.perf_counter() - t0)
                     return host.to(self.device, non_blocking=False) if self.staged else host
 
                 return None, waiter
-            buf = torch.empty(shape, dtype=dtype, device=self.device)
+            ring = self._rings.get((which, "recv"))
+            if ring is not None:
+                k, buf = ring.take(tuple(shape), dtype)
+            else:
+                buf = torch.empty(shape, dtype=dtype, device=self.device)
             work = pg.recv([buf], src, 0)
+            if ring is not None:
+                ring.done(k, work)
 
             def waiter():
+                e0 = None
+                if self.timing:
+                    e0 = torch.cuda.Event(enable_timing=True)
+                    e0.record()
                 work.wait()
+                if e0 is not None:
+                    e1 = torch.cuda.Event(enable_timing=True)
+                    e1.record()
+                    self._wait_events.append((e0, e1))
                 return buf
 
             return buf, waiter
         except RuntimeError as e:
             raise ChannelError(f"{which} recv from {src} failed: {e}") from e
+
+    def stats(self, reset: bool = True) -> dict:
+        """Hop statistics since the last reset: backend, payload bytes / sends, and the mean
+        ms this rank's stream (device) or host (gloo) waited for an incoming payload."""
+        waits = [1e3 * x for x in self._wait_host_s]
+        if self._wait_events:
+            self._wait_events[-1][1].synchronize()
+            waits += [a.elapsed_time(b) for a, b in self._wait_events]
+        out = {"backend": self.data_backend + ("(host-staged)" if self.staged else ""), "bytes_sent": self.bytes_sent,
+               "sends": self.sends, "recv_wait_ms": (sum(waits) / len(waits)) if waits else 0.0,
+               "recvs_timed": len(waits)}
+        if reset:
+            self._wait_events.clear()
+            self._wait_host_s.clear()
+        return out
 
     def flush(self, timeout_s: Optional[float] = None) -> None:
         self._sends.drain(timeout_s if timeout_s is not None else None)

@@ -117,6 +117,18 @@ def mix_seeds(base: np.ndarray, pos: np.ndarray) -> np.ndarray:
     return (z & np.uint64(0x7FFFFFFFFFFFFFFF)).astype(np.int64)
 
 
+def repeat_run(generated: Sequence[int]) -> int:
+    """The client's consecutive-repeat counter after ``generated`` (reference src/main.py:160,
+    197-205: ``last_token`` starts as None, so the first token - the prefill's - is never
+    compared; every later token equal to its predecessor extends the run, any other resets it)."""
+    n = 0
+    for i in range(len(generated) - 1, 1, -1):
+        if generated[i] != generated[i - 1]:
+            break
+        n += 1
+    return n
+
+
 def request_seed(seed: int, rid: str) -> int:
     import hashlib
 
@@ -340,9 +352,10 @@ class PipelineServingEngine:
             self._rid += 1
         if not req.prompt:
             raise ValueError("empty prompt")
-        need = len(req.prompt) + len(req.generated) + req.max_new_tokens + 2
+        need = self._need(req)
         if need > self.max_len:
             raise ValueError(f"request needs {need} tokens > max_seq_len {self.max_len}")
+        req._repeat = repeat_run(req.generated)  # a re-placed session resumes its stop counter
         req.t_submit = req.t_submit or time.perf_counter()
         self.queue.append(req)
         return req
@@ -354,8 +367,14 @@ class PipelineServingEngine:
     def _key(self, h: int) -> str:
         return f"{self.name}:{h}"
 
+    @staticmethod
+    def _need(req: Request) -> int:
+        """KV tokens a request can ever hold: ``max_new_tokens`` is the TOTAL generation budget,
+        so tokens a failed-over session already generated are part of it, not extra."""
+        return len(req.prompt) + max(req.max_new_tokens, len(req.generated)) + 2
+
     def _reserve(self, req: Request) -> int:
-        n = len(req.prompt) + len(req.generated) + req.max_new_tokens + 2
+        n = self._need(req)
         return self.page * ((n + self.page - 1) // self.page)
 
     def _admit(self, m: int, budget: int) -> List[Tuple[_Live, int]]:

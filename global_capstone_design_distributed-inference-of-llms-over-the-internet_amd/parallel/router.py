@@ -130,7 +130,11 @@ def serve_replica_head(engine: PipelineServingEngine, link: HostLink, timeout_s:
             return "failed"
         stop, adm = decode_cmd(link.recv_msg(0, timeout_s))
         for r in adm:
-            engine.submit(r)
+            try:
+                engine.submit(r)
+            except ValueError as e:  # cannot fit this pipeline: report it finished, keep serving
+                logger.error(f"replica head: session {r.rid} rejected: {e}")
+                fin.append((int(r.rid), REASONS["max_length"]))
         if stop:
             engine.drain()
             engine.stop()
@@ -241,9 +245,13 @@ class ReplicaFrontend:
 
     def _feed_local(self) -> None:
         for rid, m in self._take(0):
-            self.local.submit(Request(list(m.prompt), max_new_tokens=m.max_new_tokens, params=m.params,
-                                      eos_token_id=m.eos_token_id, stop_on_repeat=m.stop_on_repeat, seed=m.seed,
-                                      rid=str(rid), generated=list(m.generated)))
+            try:
+                self.local.submit(Request(list(m.prompt), max_new_tokens=m.max_new_tokens, params=m.params,
+                                          eos_token_id=m.eos_token_id, stop_on_repeat=m.stop_on_repeat, seed=m.seed,
+                                          rid=str(rid), generated=list(m.generated)))
+            except ValueError as e:  # cannot fit this pipeline: finish it instead of killing the front end
+                logger.error(f"session {rid} rejected by the local pipeline: {e}")
+                self._finish(0, rid, "max_length")
 
     def _fail(self, r: int, why: str) -> None:
         with self.lock:

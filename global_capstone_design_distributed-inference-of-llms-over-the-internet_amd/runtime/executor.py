@@ -589,10 +589,17 @@ class StageExecutor:
             xn = e("xn", (T, H))
             attn = e("attn", (T, cfg.q_dim))
             act = e("act", (T, cfg.intermediate_size))
+            fold_native = self._folded_native(T)
             for li, L in self._iter_layers(_DENSE_FIELDS):
-                # W8A16 layers' only weights carry the norm weights folded in (prepare_w8a16)
-                g_in, g_post = (self._unit_norm(), self._unit_norm()) if (L.folded and L.w8) else \
-                    (L.input_norm, L.post_norm)
+                # W8A16 layers' only weights carry the norm weights folded in (prepare_w8a16).
+                # bf16 layers packed for the fused path carry them in qkv_p / gate_up_p only: when
+                # the native GEMM would pick those up, normalise with a unit weight; otherwise
+                # keep the real norm weights and hand the GEMM the unfolded row-major weight only
+                folded_bf16 = L.folded and not L.w8
+                unit = (L.folded and L.w8) or (folded_bf16 and fold_native)
+                g_in, g_post = (self._unit_norm(), self._unit_norm()) if unit else (L.input_norm, L.post_norm)
+                qkv_p = None if (folded_bf16 and not fold_native) else L.qkv_p
+                gu_p = None if (folded_bf16 and not fold_native) else L.gate_up_p
                 if prompt is not None:  # deep prompt: the block input (residual stream) += prompt[li]
                     cur = h.clone() if li == 0 else ops.add(res, mlp)
                     cur.index_add_(0, prompt[0], prompt[1][li])
@@ -601,7 +608,7 @@ class StageExecutor:
                     ops.rmsnorm(h, g_in, eps, out=xn, residual=res, mode=2)
                 else:
                     ops.rmsnorm(mlp, g_in, eps, out=xn, residual=res, mode=1)
-                ops.linear(xn, L.dense("qkv"), out=qkv, wp=L.qkv_p)
+                ops.linear(xn, L.dense("qkv"), out=qkv, wp=qkv_p)
                 kc, vc = self.cache.layer(li)
                 self._rope_attend(qkv, positions, slots, kc, vc, q_seq, q_ctx, attn, ws, ps, np_, False, qblocks,
                                   max_ctx, decode)
@@ -611,7 +618,7 @@ class StageExecutor:
                 if L.moe:
                     self._moe_mlp(L, xn, T, mlp, act, e, packed=False)
                     continue
-                ops.linear(xn, L.dense("gate_up"), out=act, epilogue=1, wp=L.gate_up_p)
+                ops.linear(xn, L.dense("gate_up"), out=act, epilogue=1, wp=gu_p)
                 ops.linear(act, L.dense("down"), out=mlp, wp=L.down_p)
                 self._ar(mlp)
         hout = res if mlp is None else ops.add(res, mlp, out=e("hout", (T, H)))
@@ -627,6 +634,18 @@ class StageExecutor:
             return logits[:, :V]
         fn = ops.rmsnorm(hout, w.final_norm, eps, out=e("fn", (S, H)), rows=last_rows)
         return ops.linear(fn, w.lm_head, out=e("logits", (S, V)))
+
+    def _folded_native(self, T: int) -> bool:
+        """Would ``ops.linear`` run BOTH norm-consuming projections (qkv, gate/up) of a T-row
+        row-major step on the native GEMM (i.e. over the norm-folded packed weights)?  The
+        row-major branch must then normalise with a unit weight, else with the real one and
+        the unfolded weights (one decision per step, so the two never mix)."""
+        if self.device.type != "cuda" or ops.gemm_policy() == "hipblaslt":
+            return False
+        cfg = self.cfg
+        H, F = cfg.hidden_size, cfg.intermediate_size
+        return ops.native_gemm_ok(T, cfg.q_dim + 2 * cfg.kv_dim, H, 0) and \
+            ops.native_gemm_ok(T, 2 * F, H, 1)
 
     def _unit_norm(self) -> torch.Tensor:
         u = getattr(self, "_ones", None)

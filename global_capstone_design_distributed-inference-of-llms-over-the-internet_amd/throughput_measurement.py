@@ -43,6 +43,14 @@ def measure_compute_throughput(executor, n_warmup: int = 2, n_steps: int = 10, b
     H = executor.cfg.hidden_size
     dev = executor.device
     sids = [f"__probe_{uuid.uuid4().hex[:8]}_{i}" for i in range(batch)]
+    # the probe shares the executor (scratch buffers, graphs, session table, stream) with the
+    # served steps of the RPC handler / device-channel threads: it runs under their lock
+    lock = getattr(executor, "exec_lock", None) or contextlib.nullcontext()
+    with lock:
+        return _measure_compute(executor, sids, batch, n_warmup, n_steps, rounds, H, dev)
+
+
+def _measure_compute(executor, sids, batch, n_warmup, n_steps, rounds, H, dev) -> float:
     try:
         if executor.is_first:
             x = torch.randint(0, executor.cfg.vocab_size, (batch,), device=dev)
@@ -85,6 +93,12 @@ def measure_forward_throughput(executor, n_tokens: int = 1024, n_steps: int = 3)
     else:
         x = torch.randn(n_tokens, H, device=dev).to(executor.dtype)
     sid = f"__probe_fwd_{uuid.uuid4().hex[:8]}"
+    lock = getattr(executor, "exec_lock", None) or contextlib.nullcontext()
+    with lock:
+        return _measure_forward(executor, sid, x, n_tokens, n_steps, dev)
+
+
+def _measure_forward(executor, sid, x, n_tokens, n_steps, dev) -> float:
     try:
         executor.forward([(sid, n_tokens)], x, reset=[True])
         if dev.type == "cuda":

@@ -109,3 +109,59 @@ def test_engine_gpu_two_ranks_match_one():
     # greedy over bf16 kernels: a 2-stage split runs the same per-layer kernels on the same rows
     agree = sum(one[k] == two[k] for k in one)
     assert agree >= len(one) - 1, (one, two)
+
+
+def _rccl_world1(port, q):
+    """RCCL first-run insurance on a one-GPU box: a world-1 Channel over RCCL builds its
+    data / ret communicators (``channel._nccl``), runs a collective on each, exercises the
+    preallocated slab rings, then tears down through ``abort()`` and ``close()``."""
+    try:
+        from src.parallel.channel import Channel, make_store
+
+        store = make_store("127.0.0.1", port, 1, True)
+        ch = Channel(store, "rccl1", 0, 1, "cuda:0", timeout_s=60, data_backend="nccl")
+        out = {"backend": ch.data_backend, "staged": ch.staged}
+        for name, pg in (("data", ch.data), ("ret", ch.ret)):
+            t = torch.arange(1024, device="cuda", dtype=torch.float32)
+            pg.allreduce([t]).wait()
+            torch.cuda.synchronize()
+            out[name] = float(t.sum())
+        out["ctrl"] = ch.all_gather_floats([1.5, 2.5])
+        ring = ch._rings[("data", "send")]
+        views = [ring.take((7, 64), torch.bfloat16)[1] for _ in range(40)]  # wraps around 32 slots
+        out["ring"] = [tuple(v.shape) for v in views[-2:]]
+        ch.abort()
+        out["aborted"] = ch.closed
+        ch2 = Channel(store, "rccl2", 0, 1, "cuda:0", timeout_s=60, data_backend="nccl")
+        t = torch.ones(16, device="cuda")
+        ch2.data.allreduce([t]).wait()
+        torch.cuda.synchronize()
+        ch2.close()
+        out["closed"] = ch2.closed
+        q.put(("ok", out))
+    except Exception as e:  # noqa: BLE001
+        q.put(("error", f"{type(e).__name__}: {e}"))
+
+
+def test_rccl_channel_world1_builds_collectives_and_tears_down():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_world1, args=(port, q))
+    p.start()
+    try:
+        status, out = q.get(timeout=100)
+    finally:
+        p.join(30)
+        if p.is_alive():
+            p.kill()
+    print("rccl world-1 channel:", status, out)
+    assert status == "ok", out
+    assert out["backend"] == "nccl" and not out["staged"]
+    assert out["data"] == out["ret"] == float(sum(range(1024)))
+    assert out["ctrl"] == [[1.5, 2.5]]
+    assert out["ring"] == [(7, 64), (7, 64)]
+    assert out["aborted"] and out["closed"]

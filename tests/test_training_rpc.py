@@ -111,6 +111,34 @@ def test_gpu_executor_deep_prompts():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n_tok", [12, 100])
+def test_gpu_executor_deep_prompts_nonunit_norms(n_tok):
+    """The fused-norm path packs qkv / gate_up with the RMSNorm weights folded in: the
+    row-major branch (deep prompts, 65..128-row steps) must not apply them twice."""
+    from src.runtime.executor import StageExecutor
+
+    cfg = resolve_model("small-llama")
+    L, H = cfg.num_hidden_layers, cfg.hidden_size
+    w = random_stage_weights(cfg, 1, L, has_embed=False, has_head=False, device="cuda", seed=6)
+    for i, lay in enumerate(w.layers):
+        gen = torch.Generator(device="cuda").manual_seed(50 + i)
+        lay.input_norm = (torch.rand(H, device="cuda", generator=gen) + 0.5).to(torch.bfloat16)
+        lay.post_norm = (torch.rand(H, device="cuda", generator=gen) + 0.5).to(torch.bfloat16)
+    ex = StageExecutor(cfg, w, "cuda", kv_cache_bytes=64 << 20, max_sessions=4, max_seq_len=256)
+    assert all(lay.folded for lay in w.layers)
+    g = torch.Generator().manual_seed(1)
+    h = torch.randn(n_tok, H, generator=g).to("cuda", torch.bfloat16)
+    p = (0.5 * torch.randn(L - 1, 4, H, generator=g)).to("cuda", torch.bfloat16)
+    ag = AutogradStage(cfg, w, "cuda")
+    out = ex.forward([("a", n_tok)], h, prompts=[p]).float()
+    ref = ag.forward(h[None], p[:, None])[0].float()
+    assert float((out - ref).norm() / ref.norm()) < 0.02
+    plain = ex.forward([("b", n_tok)], h).float()
+    ref_plain = ag.forward(h[None])[0].float()
+    assert float((plain - ref_plain).norm() / ref_plain.norm()) < 0.02
+
+
+@pytest.mark.gpu
 def test_autograd_stage_bf16_on_gpu_matches_fp32():
     import dataclasses
 

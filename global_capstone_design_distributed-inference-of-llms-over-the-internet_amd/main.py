@@ -116,6 +116,10 @@ def build_parser() -> argparse.ArgumentParser:
                    help="LB server: concurrent one-token steps of the compute-throughput probe (tokens/s)")
     p.add_argument("--num_sessions", type=int, default=1,
                    help="client: generate this many sessions concurrently (prompt repeated, distinct seeds)")
+    p.add_argument("--dump_tokens", type=str, default=None,
+                   help="client: write every session's generated token ids (JSON) here (harnesses, fault tests)")
+    p.add_argument("--max_replicas", type=int, default=0,
+                   help="client, device channel: pipelines to open over disjoint same-node routes (0 = all found)")
     return p
 
 
@@ -172,7 +176,9 @@ def _start_dht(args) -> DHT:
 
 # ================================================================================ client
 @torch.inference_mode()
-def run_rank0(args, device, cuts: List[int]):
+def run_rank0(args, device, cuts: List[int], on_token=None, results: Optional[list] = None):
+    """``on_token(request, token)`` / ``results`` (filled with every session's tokens) are
+    hooks for embedding the client (tests, fault-injection harnesses) on the device-channel path."""
     cfg = resolve_model(args.model)
     L = cfg.num_hidden_layers
     stage0_end = cuts[0]
@@ -197,7 +203,7 @@ def run_rank0(args, device, cuts: List[int]):
     if args.device_channel != "off":
         route = tx._get_route(sid)
         if args.device_channel == "on" or tx.device_channel_possible(route, device):
-            return _run_rank0_channel(args, device, ex, tok, tx, route, ids)
+            return _run_rank0_channel(args, device, ex, tok, tx, route, ids, on_token=on_token, results=results)
         logger.info("device channel not possible (a hop is on another machine or did not announce one): TCP path")
     if int(args.num_sessions) > 1:
         return _run_rank0_tcp_sessions(args, device, ex, tok, tx, ids)
@@ -297,39 +303,124 @@ def _run_rank0_tcp_sessions(args, device, ex, tok, tx, ids):
     return gen[sids[0]]
 
 
-def _run_rank0_channel(args, device, ex, tok, tx, route, ids):
-    """Same-node fast path of run_rank0: this process is the head of a device channel
-    (parallel/channel.py) through the route's servers, and generation runs on the
-    continuous-batching engine (parallel/engine.py); the TCP RPC only did discovery and the
-    channel handshake."""
+def _run_rank0_channel(args, device, ex, tok, tx, route, ids, on_token=None, results=None):
+    """Same-node fast path of run_rank0: this process heads a device channel
+    (parallel/channel.py) through the servers of every complete same-node route - one
+    pipeline replica per disjoint route - and generation runs on the continuous-batching
+    engine (parallel/engine.py) under the replica front end (parallel/router.py): sessions
+    are placed by throughput (measured tokens/s of each replica, EMA) and, when a pipeline
+    loses a stage, its dead servers are found over TCP (``rpc_echo``), a replacement route
+    is opened if the registry has one, and the unfinished sessions are re-prefilled
+    (prompt + generated tokens) on the surviving / rebuilt replicas - the fast-path form of
+    the reference client's exclude / rediscover / replay failover (src/rpc_transport.py:
+    587-712).  The TCP RPC only does discovery, liveness probes and the channel handshake."""
     from .parallel.engine import PipelineServingEngine, Request, request_seed
+    from .parallel.router import ReplicaFrontend
     from .runtime.sampler import SamplingParams
 
     n = max(1, int(args.num_sessions))
-    S = len(route) + 1
+    same_node = args.device_channel == "auto"
+    max_rep = int(getattr(args, "max_replicas", 0) or 0) or None
+    routes = tx.channel_routes(device, max_routes=max_rep, same_node=same_node) or [route]
+    S = len(routes[0]) + 1
     M = max(1, min(S + 1, n))
-    B = (n + M - 1) // M
-    ch = tx.open_device_channel(route, device, n_slots=M, batch=B, timeout=max(30.0, args.request_timeout * 2))
-    eng = PipelineServingEngine(ex, ch, n_slots=M, batch=B, name="client")
+    B = (n + M - 1) // M  # every replica can hold ALL sessions: a lone survivor takes them over
+    timeout = max(30.0, args.request_timeout * 2)
+    rep_routes = {}
+    counter = [0]
+
+    def open_replica(rt):
+        k = counter[0]
+        counter[0] += 1
+        ch = tx.open_device_channel(rt, device, n_slots=M, batch=B, timeout=timeout, timing=True)
+        eng = PipelineServingEngine(ex, ch, n_slots=M, batch=B, name=f"client-r{k}", timeout_s=timeout)
+        eng.timing = True
+        ch.timing = True
+        thr = min((float(h.info.get("throughput") or 0.0) for h in rt), default=0.0)
+        return eng, thr
+
+    engines, thrs = {}, []
+    for r, rt in enumerate(routes):
+        engines[r], t = open_replica(rt)
+        rep_routes[r] = rt
+        thrs.append(t)
+    known = all(t > 0 for t in thrs)
+
+    def recover(r):
+        """Replica r lost a stage: probe its servers, exclude the dead ones, open a replacement
+        route over servers no live replica uses (wait for one only if nothing else is left)."""
+        dead = [h for h in rep_routes[r] if not tx.hop_alive(h)]
+        for h in dead:
+            tx.failed_peers.setdefault(h.key, set()).add(h.peer_id)
+        logger.warning(f"replica {r} failed; dead servers: {[h.peer_id[:8] for h in dead] or 'none answered dead'}")
+        old = engines.get(r)
+        if old is not None and old.ch is not None:
+            old.ch.close()
+        live = [k for k in fe.alive_locals() if k != r]
+        busy = set().union(*[{h.peer_id for h in rep_routes[k]} for k in live]) if live else set()
+        new = tx.channel_routes(device, max_routes=1, exclude=busy, same_node=same_node,
+                                wait_s=0.0 if live else max(10.0, args.request_timeout))
+        if not new:
+            return None
+        eng, thr = open_replica(new[0])
+        r2 = fe.router.n  # the index add_replica will hand out
+        rep_routes[r2] = new[0]
+        engines[r2] = eng
+        logger.info(f"rebuilt a pipeline over {[h.peer_id[:8] for h in new[0]]}")
+        return eng, thr if thr > 0 else (max(fe.router.throughput) if fe.router.throughput else 1.0)
+
+    fe = ReplicaFrontend(len(engines), locals=engines, throughputs=thrs if known else None, timeout_s=timeout,
+                         recover=recover)
+    progress = {"n": 0, "t": time.perf_counter()}
+
+    def _on_token(req, tok_id):
+        progress["n"] += 1
+        now = time.perf_counter()
+        if now - progress["t"] >= 1.0:
+            progress["t"] = now
+            logger.info(f"progress: {progress['n']} tokens generated")
+        if on_token is not None:
+            on_token(req, tok_id)
+
+    fe.on_token = _on_token
     eos = getattr(tok, "eos_token_id", None)
     rp = args.repetition_penalty if args.repetition_penalty is not None else 1.5
     sp = SamplingParams(args.temperature, args.top_p, args.top_k, rp)
     t0 = time.perf_counter()
-    reqs = [eng.submit(Request(ids.tolist(), max_new_tokens=args.max_new_tokens, params=sp, eos_token_id=eos,
-                               seed=request_seed(args.seed, f"s{i}"), rid=f"s{i}")) for i in range(n)]
+    reqs = [fe.submit(Request(ids.tolist(), max_new_tokens=args.max_new_tokens, params=sp, eos_token_id=eos,
+                              seed=request_seed(args.seed, f"s{i}"), rid=f"s{i}")) for i in range(n)]
     try:
         with torch.inference_mode():
-            eng.run_until_idle()
+            fe.run(stop=False)
+        t2 = time.perf_counter()
+        for r, eng in fe.alive_locals().items():
+            try:
+                _log_stage_stats(r, eng.gather_stage_stats(), rep_routes.get(r, []))
+            except Exception as e:  # noqa: BLE001 - stats are diagnostics
+                logger.warning(f"replica {r}: stage stats unavailable ({e})")
     finally:
-        eng.stop()
-        ch.close()
-    t2 = time.perf_counter()
+        for r, eng in fe.alive_locals().items():
+            eng.stop()
+        for eng in engines.values():
+            if eng.ch is not None:
+                eng.ch.close()
     gen = reqs[0].generated
+    if results is not None:
+        results.extend(r.generated for r in reqs)
+    if getattr(args, "dump_tokens", None):
+        import json
+
+        with open(args.dump_tokens, "w") as f:
+            json.dump({r.rid: {"tokens": r.generated, "finish": r.finish_reason} for r in reqs}, f)
     text = tok.decode(gen, skip_special_tokens=True)
     print(f"\n{'=' * 80}\nPROMPT: {args.prompt}\nGENERATED: {text}\n{'=' * 80}\n", flush=True)
     ttft = (reqs[0].t_first or t2) - t0
     total = sum(len(r.generated) for r in reqs)
-    logger.info(f"device channel: {S} stages, {n} session(s), {M} slot(s) x {B}")
+    logger.info(f"device channel: {S} stages x {len(routes)} replica(s), {n} session(s), {M} slot(s) x {B}; "
+                f"tokens per replica {fe.replica_tokens}")
+    if fe.failures:
+        logger.info(f"failover: {len(fe.failures)} replica failure(s) recovered "
+                    f"({'; '.join(f'replica {r}: {w[:80]}' for r, w in fe.failures)})")
     # decode rate counts tokens after each session's first one over the time after the first
     # session's first token (as the TCP path does); end-to-end counts everything from t0
     logger.info(f"Decode completed in {t2 - t0 - ttft:.3f}s ({(total - n) / max(t2 - t0 - ttft, 1e-9):.2f} tokens/s "
@@ -338,6 +429,19 @@ def _run_rank0_channel(args, device, ex, tok, tx, route, ids):
     logger.info(f"TTFT (Time to First Token): {ttft:.3f}s")
     tx.shutdown()
     return gen
+
+
+def _log_stage_stats(replica: int, rows, route) -> None:
+    """Per-stage ms of a device-channel pipeline (the reference client's per-hop times,
+    src/rpc_transport.py:98-103, 824-839): compute per micro-batch step, how long the stage
+    waited for its input, bytes it sent downstream."""
+    names = ["stage0 (client)"] + [f"{h.key} {h.peer_id[:8]}" for h in route]
+    for row in rows:
+        k = int(row["stage"])
+        name = names[k] if k < len(names) else f"stage{k}"
+        logger.info(f"replica {replica} {name}: blocks {int(row['blocks'])}, compute {row['compute_ms']:.3f} ms/step "
+                    f"over {int(row['steps'])} steps, input wait {row['recv_wait_ms']:.3f} ms/step, "
+                    f"sent {row['bytes_sent'] / 2**20:.1f} MiB")
 
 
 # ================================================================================ servers

@@ -42,6 +42,7 @@ Here the same roles run as a chain of stage ranks, one process per GPU:
 """
 from __future__ import annotations
 
+import collections
 import dataclasses
 import logging
 import os
@@ -59,7 +60,7 @@ from .channel import Channel, ChannelError, wait_event
 
 logger = logging.getLogger(__name__)
 
-KIND_STEP, KIND_STOP = 0, 1
+KIND_STEP, KIND_STOP, KIND_STATS = 0, 1, 2
 F_RESET, F_SAMPLE = 1, 2
 HDR = 8          # kind, slot, n_seq, T, n_close, n_admit, round, reserved
 SEQ_REC = 5      # handle, n_tok, start, flags, seed
@@ -299,7 +300,7 @@ class PipelineServingEngine:
         self.name = name
         self.max_handles = int(max_handles or executor.sessions.max_sessions)
         self.timing = timing
-        self._events: List = []
+        self._events = collections.deque(maxlen=8192)  # (start, end) HIP events of timed steps
         self.stopped = False
         self.failed: Optional[str] = None
         self.rounds = 0
@@ -383,6 +384,8 @@ class PipelineServingEngine:
         chunk length) pairs; the first admission of a step always gets at least one chunk."""
         out: List[Tuple[_Live, int]] = []
         while self.queue and len(self.slots[m]) < self.B and self.free_handles:
+            if self.ex.sessions.free_rows() - len(out) <= 0:
+                break  # the head's executor is shared by several replica engines: no row left
             req = self.queue[0]
             res = self._reserve(req)
             if self.reserved_tokens + res > self.capacity_tokens and self.live:
@@ -603,6 +606,11 @@ class PipelineServingEngine:
             if not self.is_tail:
                 self.ch.send_msg(self.rank + 1, hdr)
             return False
+        if kind == KIND_STATS:
+            if not self.is_tail:
+                self.ch.send_msg(self.rank + 1, hdr)
+            self.ch.all_gather_floats(self._stats_row())
+            return True
         m, n_seq, T, n_close = int(hdr[1]), int(hdr[2]), int(hdr[3]), int(hdr[4])
         if not self.is_tail:
             self.ch.send_msg(self.rank + 1, hdr)  # the successor plans while we compute
@@ -697,8 +705,43 @@ class PipelineServingEngine:
             self.ch.abort()
         if self.is_head:
             pend = [lv.req for m in range(self.M) for lv in self.slots[m] if not lv.req.done] + list(self.queue)
+            with self.ex.exec_lock:  # the head's rows / pages go back to the (shared) executor
+                for m in range(self.M):
+                    for lv in self.slots[m]:
+                        self.ex.sessions.close(self._key(lv.handle))
+                    self.slots[m] = []
+                self.live.clear()
+                self.queue = []
             raise PipelineFailure(why, pend)
         raise PipelineFailure(why)
+
+    def _stats_row(self) -> List[float]:
+        st = self.ch.stats(reset=True) if self.ch is not None else {"recv_wait_ms": 0.0, "bytes_sent": 0}
+        n = len(self._events)
+        ms = self.stage_ms() if self.dev.type == "cuda" else None
+        return [float(ms or 0.0), float(n), float(st["recv_wait_ms"]), float(st["bytes_sent"]),
+                float(self.ex.end - self.ex.start)]
+
+    def gather_stage_stats(self) -> List[dict]:
+        """Head: per-stage timing of the steps since the last gather, every rank's row gathered
+        over the ctrl group (a STATS header walks the chain first): mean compute ms per
+        micro-batch step (HIP events), timed steps, mean ms the stage's stream waited for its
+        payload, hop bytes sent, blocks.  The pipeline analogue of the reference client's
+        per-hop ``last_decode_stage_times`` (src/rpc_transport.py:98-103, 824-839)."""
+        if not self.is_head:
+            raise RuntimeError("gather_stage_stats() is a head operation")
+        if self.ch is None:
+            rows = [self._stats_row()]
+        else:
+            hdr = np.zeros(HDR, dtype=np.int64)
+            hdr[0] = KIND_STATS
+            try:
+                self.ch.send_msg(1, hdr)
+                rows = self.ch.all_gather_floats(self._stats_row())
+            except ChannelError as e:
+                self._fail(str(e))
+        keys = ("compute_ms", "steps", "recv_wait_ms", "bytes_sent", "blocks")
+        return [dict(zip(keys, r), stage=k) for k, r in enumerate(rows)]
 
     def stage_ms(self) -> Optional[float]:
         if not self._events:

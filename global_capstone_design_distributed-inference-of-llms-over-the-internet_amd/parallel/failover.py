@@ -107,6 +107,14 @@ class ReplicaRouter:
             plans.append(ReplayPlan(sid, live[k], list(self.history[sid])))
         return plans
 
+    def add_replica(self, throughput: float = 1.0) -> int:
+        """A new (e.g. rebuilt) replica joins; returns its index."""
+        self.n += 1
+        self.throughput.append(float(throughput))
+        self.alive.append(True)
+        self.last_beat.append(time.monotonic())
+        return self.n - 1
+
     def close(self, session_id: str) -> None:
         self.placement.pop(session_id, None)
         self.history.pop(session_id, None)

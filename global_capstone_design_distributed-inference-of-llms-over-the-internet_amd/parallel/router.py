@@ -32,7 +32,7 @@ from __future__ import annotations
 import logging
 import threading
 import time
-from typing import Dict, List, Optional, Sequence, Tuple
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -152,24 +152,47 @@ def serve_replica_head(engine: PipelineServingEngine, link: HostLink, timeout_s:
 
 # ------------------------------------------------------------------ front end (global rank 0)
 class ReplicaFrontend:
-    def __init__(self, n_replicas: int, local: Optional[PipelineServingEngine], links: Dict[int, HostLink],
-                 throughputs: Optional[Sequence[float]] = None, timeout_s: float = 120.0):
+    """Routes sessions over replica pipelines and fails them over.
+
+    ``locals``: replica index -> a pipeline head engine driven by THIS thread (the CLI client
+    heads every same-node replica itself; bench / multi-process runs head replica 0 here);
+    ``links``: replica index -> host link to a remote replica head (``serve_replica_head``).
+    ``recover(r)`` (optional) is called when replica ``r`` fails, before its sessions are
+    re-placed: it may rebuild a pipeline (new route, excluding dead servers) and return
+    ``(engine, throughput)``, which joins as a new replica."""
+
+    def __init__(self, n_replicas: int, local: Optional[PipelineServingEngine] = None,
+                 links: Optional[Dict[int, HostLink]] = None, throughputs: Optional[Sequence[float]] = None,
+                 timeout_s: float = 120.0, *, locals: Optional[Dict[int, PipelineServingEngine]] = None,
+                 recover: Optional[Callable[[int], Optional[Tuple[PipelineServingEngine, float]]]] = None):
         self.n = int(n_replicas)
         self.router = ReplicaRouter(self.n, throughputs, timeout_s)
-        self.local = local
-        self.links = links
+        self.locals: Dict[int, PipelineServingEngine] = dict(locals or {})
+        if local is not None:
+            self.locals[0] = local
+        self.links = dict(links or {})
+        self.recover = recover
         self.timeout_s = timeout_s
         self.lock = threading.RLock()
         self.requests: Dict[int, Request] = {}
         self.pending: Dict[int, List[int]] = {r: [] for r in range(self.n)}
         self.failures: List[Tuple[int, str]] = []
         self._next = 0
-        self._local_map: Dict[str, int] = {}
         self._threads: List[threading.Thread] = []
         self.replica_tokens = [0] * self.n
-        if local is not None:
-            local.on_token = self._local_token
-            local.on_finish = self._local_finish
+        self._rate_mark: Dict[int, Tuple[float, int]] = {}
+        self._measured = [throughputs is not None] * self.n
+        self.on_token: Optional[Callable[[Request, int], None]] = None
+        for r, eng in self.locals.items():
+            self._attach(r, eng)
+
+    @property
+    def local(self) -> Optional[PipelineServingEngine]:
+        return self.locals.get(0)
+
+    def _attach(self, r: int, eng: PipelineServingEngine) -> None:
+        eng.on_token = lambda req, t, r=r: self._token(r, int(req.rid), t)
+        eng.on_finish = lambda req, r=r: self._finish(r, int(req.rid), req.finish_reason or "done")
 
     # ---------------------------------------------------------------- API
     def submit(self, req: Request) -> Request:
@@ -186,28 +209,34 @@ class ReplicaFrontend:
         with self.lock:
             return all(r.done for r in self.requests.values())
 
-    def run(self, poll_s: float = 0.002) -> List[Request]:
+    def alive_locals(self) -> Dict[int, PipelineServingEngine]:
+        return {r: e for r, e in self.locals.items() if self.router.alive[r]}
+
+    def run(self, poll_s: float = 0.002, stop: bool = True) -> List[Request]:
         for r, link in self.links.items():
             t = threading.Thread(target=self._remote_loop, args=(r, link), daemon=True, name=f"router-{r}")
             t.start()
             self._threads.append(t)
         while not self.all_done():
-            if self.local is not None and self.router.alive[0]:
-                self._feed_local()
+            busy = False
+            for r, eng in list(self.alive_locals().items()):
+                self._feed_local(r, eng)
+                if eng.idle:
+                    continue
+                busy = True
                 try:
-                    if self.local.idle:
-                        time.sleep(poll_s)
-                    else:
-                        self.local.run_rounds(1)
+                    eng.run_rounds(1)
                 except PipelineFailure as e:
-                    self._fail(0, f"local pipeline: {e}")
-            else:
+                    self._fail(r, f"local pipeline: {e}")
+            self._update_rates()
+            if not busy:
                 if not any(self.router.alive):
                     raise RuntimeError("every replica failed")
                 time.sleep(poll_s)
-        if self.local is not None and self.router.alive[0]:
-            self.local.drain()
-            self.local.stop()
+        for eng in self.alive_locals().values():
+            eng.drain()
+            if stop:
+                eng.stop()
         for t in self._threads:
             t.join(self.timeout_s)
         return [self.requests[k] for k in sorted(self.requests)]
@@ -223,6 +252,8 @@ class ReplicaFrontend:
             req.generated.append(int(tok))
             self.router.record(str(rid), int(tok))
             self.replica_tokens[r] += 1
+            if self.on_token is not None:
+                self.on_token(req, int(tok))
 
     def _finish(self, r: int, rid: int, reason: str) -> None:
         with self.lock:
@@ -232,26 +263,40 @@ class ReplicaFrontend:
             req.done, req.finish_reason, req.t_done = True, reason, time.perf_counter()
             self.router.close(str(rid))  # finished sessions no longer count as replica load
 
-    def _local_token(self, req: Request, tok: int) -> None:
-        self._token(0, int(req.rid), tok)
-
-    def _local_finish(self, req: Request) -> None:
-        self._finish(0, int(req.rid), req.finish_reason or "done")
+    def _update_rates(self, period_s: float = 0.5) -> None:
+        """Throughput EMA of the locally driven replicas from their delivered tokens/s (remote
+        heads report theirs): placement weights follow the measured rates."""
+        now = time.perf_counter()
+        for r in self.alive_locals():
+            t0, n0 = self._rate_mark.get(r, (now, self.replica_tokens[r]))
+            if r not in self._rate_mark:
+                self._rate_mark[r] = (t0, n0)
+                continue
+            if now - t0 < period_s:
+                continue
+            rate = (self.replica_tokens[r] - n0) / (now - t0)
+            self._rate_mark[r] = (now, self.replica_tokens[r])
+            if rate > 0:
+                with self.lock:
+                    old = self.router.throughput[r]
+                    self.router.throughput[r] = rate if not self._measured[r] else 0.8 * old + 0.2 * rate
+                    self._measured[r] = True
+                    self.router.heartbeat(r)
 
     def _take(self, r: int) -> List[Tuple[int, Request]]:
         with self.lock:
-            rids, self.pending[r] = self.pending[r], []
+            rids, self.pending[r] = self.pending.get(r, []), []
             return [(rid, self.requests[rid]) for rid in rids if not self.requests[rid].done]
 
-    def _feed_local(self) -> None:
-        for rid, m in self._take(0):
+    def _feed_local(self, r: int, eng: PipelineServingEngine) -> None:
+        for rid, m in self._take(r):
             try:
-                self.local.submit(Request(list(m.prompt), max_new_tokens=m.max_new_tokens, params=m.params,
-                                          eos_token_id=m.eos_token_id, stop_on_repeat=m.stop_on_repeat, seed=m.seed,
-                                          rid=str(rid), generated=list(m.generated)))
+                eng.submit(Request(list(m.prompt), max_new_tokens=m.max_new_tokens, params=m.params,
+                                   eos_token_id=m.eos_token_id, stop_on_repeat=m.stop_on_repeat, seed=m.seed,
+                                   rid=str(rid), generated=list(m.generated)))
             except ValueError as e:  # cannot fit this pipeline: finish it instead of killing the front end
-                logger.error(f"session {rid} rejected by the local pipeline: {e}")
-                self._finish(0, rid, "max_length")
+                logger.error(f"session {rid} rejected by replica {r}: {e}")
+                self._finish(r, rid, "max_length")
 
     def _fail(self, r: int, why: str) -> None:
         with self.lock:
@@ -259,6 +304,21 @@ class ReplicaFrontend:
                 return
             logger.error(f"replica {r} failed: {why}; re-placing its sessions")
             self.failures.append((r, why))
+            if self.recover is not None:
+                rep = None
+                try:
+                    rep = self.recover(r)
+                except Exception as e:  # noqa: BLE001 - a failed rebuild leaves the survivors
+                    logger.error(f"replica {r}: rebuilding a pipeline failed: {e}")
+                if rep is not None:
+                    eng, thr = rep
+                    r2 = self.router.add_replica(thr)
+                    self.pending[r2] = []
+                    self.replica_tokens.append(0)
+                    self._measured.append(False)
+                    self.locals[r2] = eng
+                    self._attach(r2, eng)
+                    logger.info(f"replica {r2} joined (rebuilt after replica {r} failed)")
             # every unfinished session placed on r (delivered or still pending) moves to a
             # survivor, which re-prefills prompt + generated tokens (the master copies)
             plans = self.router.fail(r)

@@ -209,6 +209,8 @@ class StageConnectionHandler:
             eng = PipelineServingEngine(ex, ch, n_slots=int(md.get("n_slots", 1)), batch=int(md.get("batch", 64)),
                                         name=name)
             eng.idle_timeout_s = float(md.get("idle_timeout", 3600.0))
+            eng.timing = bool(md.get("timing", False))  # per-stage ms for the client's STATS gathers
+            ch.timing = eng.timing
             with torch.inference_mode():
                 eng.serve()
             logger.info(f"device channel {name}: stopped after {eng.steps_run} steps")

@@ -402,8 +402,84 @@ class RpcTransport:
         return torch.device(device).type == "cuda" and bool(route) and route[-1].final and \
             all(h.info.get("channel_host") == me for h in route)
 
+    def channel_routes(self, device, max_routes: Optional[int] = None, exclude: Set[str] = frozenset(),
+                       same_node: bool = True, wait_s: float = 10.0) -> List[List[Hop]]:
+        """Disjoint complete routes for device channels: the node's pipeline replicas.
+
+        Every server hosts at most one route (a server's stage executor serves any number of
+        channels, but two replicas on one GPU would just share it).  With ``same_node`` only
+        servers that announced a device channel on this machine qualify.  Stage routing takes
+        one server per ``mini_petals:stage{k}`` key, newest record first; module routing
+        covers [start_block, total_blocks) greedily (largest end block, then throughput), as
+        ``_module_route`` does.  Waits up to ``wait_s`` for the FIRST route to appear."""
+        from .parallel.channel import host_id
+
+        me = host_id()
+        used = set(exclude) | set().union(*self.failed_peers.values()) if self.failed_peers else set(exclude)
+
+        def ok(e) -> bool:
+            return str(e.get("peer_id")) not in used and (not same_node or e.get("channel_host") == me)
+
+        def one() -> Optional[List[Hop]]:
+            hops: List[Hop] = []
+            if self.routing == "module":
+                cur = int(self.start_block)
+                while cur < int(self.total_blocks):
+                    cands = [e for e in self._candidates("", cur) if ok(e)]
+                    if not cands:
+                        return None
+                    cands.sort(key=lambda e: (int(e["end_block"]), float(e.get("throughput") or 0.0)), reverse=True)
+                    e = cands[0]
+                    end = int(e["end_block"])
+                    final = end >= int(self.total_blocks)
+                    if final and not bool(e.get("final_stage", False)):
+                        return None
+                    hops.append(Hop(f"petals:module:{self.model_name}:block_{cur}", str(e["peer_id"]),
+                                    e.get("p2p_maddrs") or [], cur, end, final, e))
+                    cur = end
+                return hops
+            for i, key in enumerate(self.stage_keys):
+                cands = [e for e in self._candidates(key) if ok(e)]
+                if not cands:
+                    return None
+                cands.sort(key=lambda e: (-float(e.get("timestamp", 0.0)), str(e.get("peer_id"))))
+                e = cands[0]
+                hops.append(Hop(key, str(e["peer_id"]), e.get("p2p_maddrs") or [], int(e.get("start_block", i)),
+                                int(e.get("end_block", i + 1)), i == len(self.stage_keys) - 1, e))
+            return hops
+
+        routes: List[List[Hop]] = []
+        t0 = time.monotonic()
+        while max_routes is None or len(routes) < max_routes:
+            r = one()
+            if r is None:
+                if routes or time.monotonic() - t0 > wait_s:
+                    break
+                time.sleep(0.25)
+                continue
+            routes.append(r)
+            used |= {h.peer_id for h in r}
+        return routes
+
+    def hop_alive(self, hop: Hop, timeout: float = 2.0) -> bool:
+        """Does the hop's server still answer (``rpc_echo`` over TCP)?  Failure detection for
+        device-channel routes: a channel error names no culprit, the TCP control plane does."""
+        async def ping():
+            for addr in hop.maddrs:
+                try:
+                    await self.client.call(addr, "StageConnectionHandler.rpc_echo", Message({"ping": True}), timeout)
+                    return True
+                except Exception:  # noqa: BLE001 - any failure = not alive on this address
+                    self.client.drop(addr)
+            return False
+
+        try:
+            return bool(self._run(ping()))
+        except Exception:  # noqa: BLE001
+            return False
+
     def open_device_channel(self, route: List[Hop], device, *, n_slots: int = 1, batch: int = 64,
-                            timeout: float = 60.0, idle_timeout: float = 3600.0):
+                            timeout: float = 60.0, idle_timeout: float = 3600.0, timing: bool = False):
         """Rendezvous a ``parallel.channel.Channel`` with every hop of ``route``: this client
         is rank 0 (head), hop i is rank i + 1, the final hop the tail.  The TCP RPC carries
         only this handshake; afterwards hidden states move GPU -> GPU (RCCL over xGMI) and the
@@ -425,7 +501,7 @@ class RpcTransport:
             for i, hop in enumerate(route):
                 md = {"store_host": "127.0.0.1", "store_port": port, "prefix": prefix, "rank": i + 1, "world": world,
                       "timeout": timeout, "idle_timeout": idle_timeout, "data_backend": data, "n_slots": n_slots,
-                      "batch": batch, "host_id": host_id()}
+                      "batch": batch, "host_id": host_id(), "timing": bool(timing)}
                 r = await self._call_hop(hop, "rpc_channel_open", [], md)
                 if not r.metadata.get("ok"):
                     raise ConnectionError(f"{hop}: device channel refused: {r.metadata.get('error')}")

@@ -70,6 +70,10 @@ class SessionManager:
             self.sessions[sid] = s
             return s
 
+    def free_rows(self) -> int:
+        """Session rows still available (several engines may share one table: the head's)."""
+        return len(self._free_rows)
+
     def get(self, sid: str) -> Optional[SessionState]:
         return self.sessions.get(sid)
 

@@ -156,14 +156,22 @@ def main(argv=None):
         from torch.distributed import distributed_c10d as c10d
 
         from src.parallel.channel import HostLink
-        from src.parallel.pipeline import assign_sessions
+        from src.parallel.failover import ReplicaRouter
         from src.parallel.router import gather_replica_throughput
 
         link = HostLink(c10d._get_default_store(), "bench/all", rank, world, timeout_s=600.0)
         thr = gather_replica_throughput(link, ex, lane // TP, stage, R, batch=min(B, 16))
-        # M slots of B sessions per pipeline: a faster replica's overflow goes to the others
-        placed = assign_sessions(M * B * R, thr, capacity=M * B)
-        counts = [placed.count(r) for r in range(R)]
+        # the replica front end's online placement (ReplicaRouter.place_one: lowest
+        # throughput-normalised load), capped at a pipeline's M slots x B sessions
+        router = ReplicaRouter(R, thr)
+        counts = [0] * R
+        for i in range(M * B * R):
+            r = router.place_one(f"s{i}", [])
+            if counts[r] >= M * B:  # full: the next-best replica with room takes it
+                r = min((k for k in range(R) if counts[k] < M * B),
+                        key=lambda k: ((counts[k] + 1) / max(thr[k], 1e-9), k))
+                router.placement[f"s{i}"] = r
+            counts[r] += 1
         n_sessions = counts[lane // TP]
         link.close()
         if rank == 0:

@@ -401,6 +401,72 @@ def attention_mfma(q, k_cache, v_cache, block_tables, q_seq, q_ctx, qblocks, nh,
     return out
 
 
+FA_WAVES = int(os.environ.get("MPAMD_FA_WAVES", "4"))  # waves per prefill workgroup (32 query rows each)
+
+
+def fa_blocks(ntoks, nrep: int, waves: int = None):
+    """Workgroup blocks of the FA2 prefill kernel (csrc/attention_fa.hip): int32 [2, NB] =
+    (first flat token, count), each <= 32 x waves / nrep consecutive tokens of ONE sequence."""
+    import numpy as np
+
+    waves = int(waves or FA_WAVES)
+    tb = max(1, (32 * waves) // max(int(nrep), 1))
+    n = np.asarray(ntoks, dtype=np.int64)
+    off = np.concatenate([[0], np.cumsum(n)[:-1]]) if n.size else n
+    nb = (n + tb - 1) // tb
+    seq_of_block = np.repeat(np.arange(n.size), nb)
+    k = np.arange(int(nb.sum())) - np.repeat(np.concatenate([[0], np.cumsum(nb)[:-1]]) if nb.size else nb, nb)
+    tok0 = off[seq_of_block] + k * tb
+    cnt = np.minimum(tb, n[seq_of_block] - k * tb)
+    return np.stack([tok0, cnt]).astype(np.int32)
+
+
+def fa_plan(ntoks, nh: int, nkv: int, n_cu: int = 256):
+    """(blocks, waves) for a prefill step on the FA2 kernel: 8-wave workgroups (256 query rows,
+    half the K/V traffic per row) unless their grid would not give every CU a second workgroup
+    (a single 2K GQA prompt: 4 waves measured 74.7 vs 91.7 us, profiles/r3_fa2/attn.jsonl)."""
+    nrep = max(1, nh // nkv)
+    fb8 = fa_blocks(ntoks, nrep, 8)
+    if FA_WAVES in (4, 8) and os.environ.get("MPAMD_FA_WAVES"):
+        return (fb8 if FA_WAVES == 8 else fa_blocks(ntoks, nrep, 4)), FA_WAVES
+    if fb8.shape[1] * nkv > n_cu:
+        return fb8, 8
+    return fa_blocks(ntoks, nrep, 4), 4
+
+
+def fa_ok(nh: int, nkv: int, D: int, page_size: int) -> bool:
+    """Shapes the FA2 prefill kernel covers (else the 16x16 grouped kernel runs)."""
+    return D == 128 and nh % nkv == 0 and (nh // nkv) in (1, 2, 4, 8) and page_size % 64 == 0
+
+
+def attention_fa(q, k_cache, v_cache, block_tables, q_seq, q_ctx, fablocks, nh, nkv, scale, out=None,
+                 workspace=None, max_ctx=None, waves=None, num_parts=None):
+    """Causal prefill attention, FA2 form on 32x32x16 MFMA with the transposed LDS reads of V
+    (csrc/attention_fa.hip).  Same semantics as ``paged_attention``; row-major output only.
+    ``fablocks`` from ``fa_blocks`` (device int32 [2, NB]).  The context is split over parts
+    only when the grid would leave CUs idle."""
+    if not _native(q):
+        return paged_attention(q, k_cache, v_cache, block_tables, q_seq, q_ctx, nh, nkv, scale, out=out)
+    T = q.shape[0]
+    D = k_cache.shape[-1]
+    waves = int(waves or FA_WAVES)
+    if max_ctx is None:
+        max_ctx = int(q_ctx.max().item()) if T else 1
+    if num_parts is None:
+        nblk = fablocks.shape[1] * (nh // (nh // nkv))
+        want = max(1, math.ceil(512 / max(1, nblk)))
+        num_parts = max(1, min(want, math.ceil(max_ctx / 256)))
+    part_size = 64 * math.ceil(math.ceil(max(max_ctx, 1) / num_parts) / 64)
+    num_parts = math.ceil(max(max_ctx, 1) / part_size)
+    if out is None:
+        out = torch.empty(T, nh * D, dtype=q.dtype, device=q.device)
+    if workspace is None or (num_parts > 1 and workspace.numel() < T * nh * num_parts * (D + 2)):
+        workspace = attention_workspace(T, nh, D, num_parts, q.device)
+    torch.ops.mpamd.attention_fa(q, k_cache, v_cache, block_tables, q_seq, q_ctx, fablocks, out, workspace, nh, nkv,
+                                 float(scale), int(part_size), int(num_parts), waves)
+    return out
+
+
 def attention_mfma_rope(qkv, k_cache, v_cache, block_tables, q_seq, q_ctx, qblocks, positions, cos, sin, slots, nh,
                         nkv, scale, out=None, workspace=None, part_size=None, num_parts=None, max_ctx=None,
                         packed=False):

@@ -37,6 +37,10 @@ int mp_attention_mfma(const void* q, int64_t q_stride, const void* kc, const voi
                       float scale, int packed_mt, const int64_t* rope_pos, const float* cos_t, const float* sin_t,
                       const int64_t* slots, const int32_t* sb_first, const int32_t* sb_n, int NSB,
                       hipStream_t stream);
+int mp_attention_fa(const void* q, int64_t q_stride, const void* kc, const void* vc, const int32_t* bt, int bt_stride,
+                    const int32_t* q_seq, const int32_t* q_ctx, const int32_t* fb_tok0, const int32_t* fb_ntok, int NBF,
+                    void* out, float* workspace, int T, int nh, int nkv, int D, int page_size, int PS, int NP,
+                    float scale, int nw, hipStream_t stream);
 int mp_quant_act_fp8(const void* ap, void* a8, float* scale, float* part, int M, int K, hipStream_t stream);
 int mp_gemm_fp8(const void* a8, const float* as, const void* wq, const float* ws, void* y, int64_t ys, const void* res,
                 int64_t rs, int M, int N, int K, int epilogue, int out_packed, int kind, float* part,
@@ -309,6 +313,44 @@ void attention_mfma(const at::Tensor& q, const at::Tensor& k_cache, const at::Te
                     const c10::optional<at::Tensor>& superblocks) {
   attention_mfma_impl(q, k_cache, v_cache, block_tables, q_seq, q_ctx, qblocks, out, workspace, nh, nkv, scale,
                       part_size, num_parts, packed, nullptr, nullptr, nullptr, nullptr, superblocks);
+}
+
+// Causal prefill attention, 32x32x16 MFMA FA2 form (attention_fa.hip): row-major output.
+void attention_fa(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
+                  const at::Tensor& block_tables, const at::Tensor& q_seq, const at::Tensor& q_ctx,
+                  const at::Tensor& fablocks, at::Tensor& out, at::Tensor& workspace, int64_t nh, int64_t nkv,
+                  double scale, int64_t part_size, int64_t num_parts, int64_t waves) {
+  check_bf16_cuda(q, "q");
+  check_rows(q, "q");
+  check_bf16_cuda(out, "out");
+  check_bf16_cuda(k_cache, "k_cache");
+  check_bf16_cuda(v_cache, "v_cache");
+  MP_CHECK(out.is_contiguous(), "out contiguous");
+  MP_CHECK(k_cache.dim() == 4 && k_cache.sizes() == v_cache.sizes(), "cache [pages, nkv, page, D]");
+  const int D = k_cache.size(3);
+  const int T = q.size(0);
+  MP_CHECK(D == 128, "attention_fa: head_dim 128");
+  MP_CHECK(q.size(1) >= nh * D, "q width");
+  MP_CHECK(out.numel() == (int64_t)T * nh * D, "out numel");
+  MP_CHECK(k_cache.size(1) == nkv && k_cache.is_contiguous() && v_cache.is_contiguous(), "cache");
+  MP_CHECK(block_tables.scalar_type() == at::kInt && block_tables.dim() == 2 && block_tables.stride(1) == 1,
+           "block_tables int32 [S, max_pages]");
+  MP_CHECK(q_seq.scalar_type() == at::kInt && q_seq.numel() == T, "q_seq");
+  MP_CHECK(q_ctx.scalar_type() == at::kInt && q_ctx.numel() == T, "q_ctx");
+  MP_CHECK(workspace.scalar_type() == at::kFloat, "workspace fp32");
+  if (num_parts > 1) MP_CHECK(workspace.numel() >= (int64_t)T * nh * num_parts * (D + 2), "workspace too small");
+  MP_CHECK(fablocks.is_cuda() && fablocks.scalar_type() == at::kInt && fablocks.dim() == 2 && fablocks.size(0) == 2 &&
+               fablocks.is_contiguous(),
+           "fablocks int32 [2, NB] (first token, token count), ops.fa_blocks");
+  MP_CHECK(waves == 4 || waves == 8, "waves 4 or 8");
+  const int NB = fablocks.size(1);
+  check_launch(mp_attention_fa(q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
+                               block_tables.data_ptr<int32_t>(), block_tables.stride(0), q_seq.data_ptr<int32_t>(),
+                               q_ctx.data_ptr<int32_t>(), fablocks.data_ptr<int32_t>(),
+                               fablocks.data_ptr<int32_t>() + NB, NB, out.data_ptr(), workspace.data_ptr<float>(), T,
+                               nh, nkv, D, k_cache.size(2), part_size, num_parts, (float)scale, (int)waves,
+                               cur_stream()),
+               "attention_fa");
 }
 
 // GQA decode with RoPE + KV write fused (attention_mfma.hip ROPE path): one token per query block.
@@ -643,6 +685,10 @@ TORCH_LIBRARY(mpamd, m) {
       "Tensor qblocks, Tensor(a!) out, Tensor(b!) workspace, int nh, int nkv, float scale, int part_size, "
       "int num_parts, int packed, Tensor? superblocks=None) -> ()");
   m.def(
+      "attention_fa(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor q_seq, Tensor q_ctx, "
+      "Tensor fablocks, Tensor(a!) out, Tensor(b!) workspace, int nh, int nkv, float scale, int part_size, "
+      "int num_parts, int waves) -> ()");
+  m.def(
       "attention_mfma_rope(Tensor qkv, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor block_tables, Tensor q_seq, "
       "Tensor q_ctx, Tensor qblocks, Tensor positions, Tensor cos, Tensor sin, Tensor slots, Tensor(c!) out, "
       "Tensor(d!) workspace, int nh, int nkv, float scale, int part_size, int num_parts, int packed) -> ()");
@@ -677,6 +723,7 @@ TORCH_LIBRARY_IMPL(mpamd, CUDA, m) {
   m.impl("paged_attention", &paged_attention);
   m.impl("paged_attention_rope", &paged_attention_rope);
   m.impl("attention_mfma", &attention_mfma);
+  m.impl("attention_fa", &attention_fa);
   m.impl("attention_mfma_rope", &attention_mfma_rope);
   m.impl("embedding", &embedding);
   m.impl("swiglu", &swiglu);

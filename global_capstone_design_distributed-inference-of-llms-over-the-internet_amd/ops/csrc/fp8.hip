@@ -17,6 +17,7 @@
 //     (gemm.hip): 8 waves interleave k-groups, ping-pong weight registers, LDS combine,
 //     fused epilogues (scales, SwiGLU on 16-row-interleaved gate/up, residual).
 #include "common.h"
+#include <type_traits>
 #include <stdlib.h>
 
 namespace mp {
@@ -578,8 +579,8 @@ __global__ __launch_bounds__(256) void gemm_fp8_rwk_kernel(const uint8_t* __rest
   }
 }
 
-template <int EPI>
-__global__ __launch_bounds__(256) void fp8_splitk_reduce_kernel(const float* __restrict__ part, int S, int M, int N,
+template <int EPI, int S>
+__global__ __launch_bounds__(256) void fp8_splitk_reduce_kernel(const float* __restrict__ part, int M, int N,
                                                                 const float* __restrict__ ascale,
                                                                 const float* __restrict__ wscale,
                                                                 bf16_t* __restrict__ y, int64_t ys,
@@ -587,17 +588,25 @@ __global__ __launch_bounds__(256) void fp8_splitk_reduce_kernel(const float* __r
   const int row = blockIdx.y;
   const int col = (blockIdx.x * 256 + threadIdx.x) * 8;
   if (col >= N) return;
-  f32x4 a0 = (f32x4)(0.f), a1 = (f32x4)(0.f);
-  for (int s = 0; s < S; ++s) {
-    const float* pp = part + ((int64_t)s * M + row) * N + col;
-    a0 += *reinterpret_cast<const f32x4*>(pp);
-    a1 += *reinterpret_cast<const f32x4*>(pp + 4);
-  }
+  // all slab / scale / residual loads in flight before the first add (S <= 8 by the launcher)
   const float as = ascale[row];
   const f32x4 w0 = *reinterpret_cast<const f32x4*>(wscale + col), w1 = *reinterpret_cast<const f32x4*>(wscale + col + 4);
-  u16x8 o;
   u16x8 rv = (u16x8)(0);
   if constexpr (EPI == 2) rv = *reinterpret_cast<const u16x8*>(res + (int64_t)row * rs + col);
+  f32x4 p0[S], p1[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    const float* pp = part + ((int64_t)s * M + row) * N + col;
+    p0[s] = *reinterpret_cast<const f32x4*>(pp);
+    p1[s] = *reinterpret_cast<const f32x4*>(pp + 4);
+  }
+  f32x4 a0 = (f32x4)(0.f), a1 = (f32x4)(0.f);
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    a0 += p0[s];
+    a1 += p1[s];
+  }
+  u16x8 o;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     float v = (j < 4 ? a0[j] : a1[j - 4]) * as * (j < 4 ? w0[j] : w1[j - 4]);
@@ -632,12 +641,24 @@ static int launch_gemm_fp8_rwk(const void* a8, const float* as, const void* wq, 
     go(gemm_fp8_rwk_kernel<MT, 2>);
   }
   const dim3 g2(N / 2048, M);
-  if (epi == 2)
-    hipLaunchKernelGGL(fp8_splitk_reduce_kernel<2>, g2, dim3(256), 0, stream, part, S, M, N, as, ws, (bf16_t*)y, ys,
-                       (const bf16_t*)res, rs);
-  else
-    hipLaunchKernelGGL(fp8_splitk_reduce_kernel<0>, g2, dim3(256), 0, stream, part, S, M, N, as, ws, (bf16_t*)y, ys,
-                       (const bf16_t*)res, rs);
+  auto reduce = [&](auto epi_c) {
+    constexpr int E = decltype(epi_c)::value;
+#define MP_F8R(S_)                                                                                              \
+  hipLaunchKernelGGL((fp8_splitk_reduce_kernel<E, S_>), g2, dim3(256), 0, stream, part, M, N, as, ws, (bf16_t*)y, \
+                     ys, (const bf16_t*)res, rs)
+    switch (S) {
+      case 2: MP_F8R(2); break;
+      case 3: MP_F8R(3); break;
+      case 4: MP_F8R(4); break;
+      case 5: MP_F8R(5); break;
+      case 6: MP_F8R(6); break;
+      case 7: MP_F8R(7); break;
+      default: MP_F8R(8); break;
+    }
+#undef MP_F8R
+  };
+  if (epi == 2) reduce(std::integral_constant<int, 2>{});
+  else reduce(std::integral_constant<int, 0>{});
   return 0;
 }
 

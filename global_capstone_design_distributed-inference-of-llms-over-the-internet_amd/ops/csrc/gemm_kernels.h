@@ -1329,8 +1329,8 @@ __global__ __launch_bounds__(256) void gemm_rwk_kernel(const bf16_t* __restrict_
 // Sum the S fp32 slabs (fixed order: deterministic) + epilogue.  One thread per 8 consecutive
 // columns of a row; a workgroup covers 2048 columns of one row (EPI 3: its row's sum of squares
 // is reduced in the workgroup and added to one shard with a single atomic).
-template <int EPI>
-__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ part, int S, int M, int N,
+template <int EPI, int S>
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ part, int M, int N,
                                                             bf16_t* __restrict__ y, int64_t ys,
                                                             const bf16_t* __restrict__ res, int64_t rs,
                                                             const EpiArgs ep) {
@@ -1353,18 +1353,28 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
     }
   }
   if (col < N) {
-    f32x4 a0 = (f32x4)(0.f), a1 = (f32x4)(0.f);
+    // every slab load (and the residual) is issued before the first add: one memory round
+    // trip instead of S dependent ones (the slab loop used to run with a runtime trip count)
+    u16x8 rv = (u16x8)(0);
+    if constexpr (EPI != 0) rv = *reinterpret_cast<const u16x8*>(res + (int64_t)row * rs + col);
+    f32x4 p0[S], p1[S];
+#pragma unroll
     for (int s = 0; s < S; ++s) {
       const float* pp = part + ((int64_t)s * M + row) * N + col;
-      a0 += *reinterpret_cast<const f32x4*>(pp);
-      a1 += *reinterpret_cast<const f32x4*>(pp + 4);
+      p0[s] = *reinterpret_cast<const f32x4*>(pp);
+      p1[s] = *reinterpret_cast<const f32x4*>(pp + 4);
+    }
+    f32x4 a0 = (f32x4)(0.f), a1 = (f32x4)(0.f);
+#pragma unroll
+    for (int s = 0; s < S; ++s) {  // fixed slab order: deterministic
+      a0 += p0[s];
+      a1 += p1[s];
     }
     u16x8 o;
     if constexpr (EPI == 0) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = f2bf((j < 4 ? a0[j] : a1[j - 4]) * sc);
     } else {
-      const u16x8 rv = *reinterpret_cast<const u16x8*>(res + (int64_t)row * rs + col);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         o[j] = f2bf(round_bf(j < 4 ? a0[j] : a1[j - 4]) + bf2f(rv[j]));
@@ -1384,6 +1394,32 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
       atomicAdd(ep.ss_out + ((blockIdx.y * gridDim.x + blockIdx.x) % SS_NSH) * 64 + row,
                 red[0] + red[1] + red[2] + red[3]);
   }
+}
+
+// The split count is a template parameter of the reduce (all S slab loads issued back to back).
+template <int EPI>
+static void launch_splitk_reduce_e(int S, dim3 g2, hipStream_t stream, const float* part, int M, int N, void* y,
+                                   int64_t ys, const void* res, int64_t rs, const EpiArgs& ep) {
+#define MP_SKR(S_)                                                                                        \
+  hipLaunchKernelGGL((splitk_reduce_kernel<EPI, S_>), g2, dim3(256), 0, stream, part, M, N, (bf16_t*)y, ys, \
+                     (const bf16_t*)res, rs, ep)
+  switch (S) {
+    case 2: MP_SKR(2); break;
+    case 3: MP_SKR(3); break;
+    case 4: MP_SKR(4); break;
+    case 5: MP_SKR(5); break;
+    case 6: MP_SKR(6); break;
+    case 7: MP_SKR(7); break;
+    default: MP_SKR(8); break;
+  }
+#undef MP_SKR
+}
+
+static inline void launch_splitk_reduce(int S, int epi, dim3 g2, hipStream_t stream, const float* part, int M, int N,
+                                        void* y, int64_t ys, const void* res, int64_t rs, const EpiArgs& ep) {
+  if (epi == 3) launch_splitk_reduce_e<3>(S, g2, stream, part, M, N, y, ys, res, rs, ep);
+  else if (epi == 2) launch_splitk_reduce_e<2>(S, g2, stream, part, M, N, y, ys, res, rs, ep);
+  else launch_splitk_reduce_e<0>(S, g2, stream, part, M, N, y, ys, res, rs, ep);
 }
 
 // Column-group width NT and split count S with C x S <= #CUs (prefer NT = 4, then 2, 8, 1;
@@ -1440,9 +1476,7 @@ static int launch_gemm_rwk(const void* x, const void* w, void* y, int64_t ys, co
       break;
   }
   const dim3 g2(N / 2048, M);
-  if (epi == 3) hipLaunchKernelGGL(splitk_reduce_kernel<3>, g2, dim3(256), 0, stream, part, S, M, N, (bf16_t*)y, ys, (const bf16_t*)res, rs, ep);
-  else if (epi == 2) hipLaunchKernelGGL(splitk_reduce_kernel<2>, g2, dim3(256), 0, stream, part, S, M, N, (bf16_t*)y, ys, (const bf16_t*)res, rs, ep);
-  else hipLaunchKernelGGL(splitk_reduce_kernel<0>, g2, dim3(256), 0, stream, part, S, M, N, (bf16_t*)y, ys, (const bf16_t*)res, rs, ep);
+  launch_splitk_reduce(S, epi, g2, stream, part, M, N, y, ys, res, rs, ep);
   return 0;
 }
 

@@ -63,6 +63,8 @@ class Plan:
     h32: np.ndarray                     # [2*T + S] q_seq, q_ctx, last_rows (pinned host view)
     qblocks: Optional[torch.Tensor] = None  # [2, NB] MFMA-attention query blocks (prefill steps)
     superblocks: Optional[torch.Tensor] = None  # [2, NSB] runs of <= 4 blocks (grouped prefill kernel)
+    fablocks: Optional[torch.Tensor] = None  # [2, NBF] FA2 prefill workgroup blocks (csrc/attention_fa.hip)
+    fa_waves: int = 4                   # waves per FA2 workgroup (ops.fa_plan)
     _dev: Optional[Tuple[torch.Tensor, torch.Tensor]] = None
     _upload: Optional[object] = None    # callable making the device copies
 
@@ -130,7 +132,7 @@ class StageExecutor:
                  page_size: int = 64, max_sessions: int = 256, max_seq_len: Optional[int] = None,
                  kv_cache_bytes: Optional[int] = None, kv_fraction: float = 0.9, use_graphs: Optional[bool] = None,
                  graph_max_batch: int = 256, max_tokens_per_step: int = 8192, offload: bool = False,
-                 keep_layers_on_gpu: int = 0, tp=None):
+                 keep_layers_on_gpu: int = 0, tp=None, warmup: Optional[bool] = None):
         """``tp``: a ``parallel.tensor_parallel.TPGroup`` when ``weights`` is a tensor-parallel
         shard (``cfg`` is then the shard config); partial sums are all-reduced after the
         o and down projections."""
@@ -191,6 +193,14 @@ class StageExecutor:
         # (csrc/attention_mfma.hip attn_mfma_grp_kernel); MPAMD_ATTN_GROUPED=0 = one block each
         self._attn_grouped = os.environ.get("MPAMD_ATTN_GROUPED", "1") != "0"
         self._cur_sb = None
+        # prefill steps with a row-major attention output: the FA2 kernel on 32x32x16 MFMA with
+        # transposed LDS reads of V (csrc/attention_fa.hip); MPAMD_ATTN_FA=0 keeps the 16x16 one
+        self._attn_fa = self._attn_mfma_prefill and os.environ.get("MPAMD_ATTN_FA", "1") != "0" and \
+            ops.fa_ok(cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim, page_size)
+        self._cur_fb = None
+        self._cur_fw = 4
+        self._n_cu = torch.cuda.get_device_properties(self.device).multi_processor_count \
+            if self.device.type == "cuda" else 256
         # decode steps on the flash-decoding kernel fold RoPE + the KV page write into it
         self._fuse_rope = os.environ.get("MPAMD_FUSE_ROPE", "1") != "0"
         # shortest split-K context slice (ops.attention_partition): longer on the MFMA GQA kernel
@@ -250,6 +260,11 @@ class StageExecutor:
         self._streamer, self._n_stream = None, self.n_layers
         if offload and self.device.type == "cuda":
             self._setup_offload(keep_layers_on_gpu)
+        if warmup is None:
+            warmup = self.device.type == "cuda" and os.environ.get("MPAMD_WARMUP", "1") != "0"
+        # (not under TP: a shape that fails on one rank would desynchronise the all-reduces)
+        if warmup and self.device.type == "cuda" and self.n_layers and self._tp is None and self._streamer is None:
+            self.warmup()
         logger.info(f"StageExecutor blocks [{self.start},{self.end}) embed={self.is_first} head={self.is_last} "
                     f"kv_pages={num_pages} x {page_size} tokens ({self.cache.nbytes / 2**30:.2f} GiB) "
                     f"graphs={self.use_graphs}")
@@ -301,13 +316,17 @@ class StageExecutor:
                 d32 = h32[: 2 * T + S].clone()
             return d64, d32
 
-        qb = sb = None
+        qb = sb = fb = None
+        fa_waves = 4
+        if self.device.type == "cuda" and not is_decode and self._attn_fa:
+            fbn, fa_waves = ops.fa_plan(ntoks, self.nh, self.nkv, self._n_cu)
+            fb = torch.from_numpy(fbn).to(self.device, non_blocking=True)
         if self.device.type == "cuda" and not is_decode and self._attn_mfma_prefill:
             qb = torch.from_numpy(ops.query_blocks(ntoks, self.nh // self.nkv)).to(self.device, non_blocking=True)
             if self._attn_grouped:
                 sb = torch.from_numpy(ops.query_superblocks(ntoks, self.nh // self.nkv)).to(self.device,
                                                                                               non_blocking=True)
-        return Plan(sess, ntoks, st, T, max_ctx, is_decode, n64, n32, qb, sb, _upload=upload)
+        return Plan(sess, ntoks, st, T, max_ctx, is_decode, n64, n32, qb, sb, fb, fa_waves, _upload=upload)
 
     def commit(self, plan: Plan) -> None:
         for s, n in zip(plan.sessions, plan.ntoks):
@@ -415,12 +434,15 @@ class StageExecutor:
             out = self._forward_gpt2(plan, x, prompt=prompt)
         else:
             self._cur_sb = plan.superblocks
+            self._cur_fb = plan.fablocks
+            self._cur_fw = plan.fa_waves
             try:
                 out = self._forward_llama(x, plan.positions, plan.slots, plan.q_seq, plan.q_ctx, plan.last_rows,
                                           plan.T, plan.max_ctx, None, qblocks=plan.qblocks, prompt=prompt,
                                           decode=plan.is_decode)
             finally:
                 self._cur_sb = None
+                self._cur_fb = None
         if ev is not None:
             ev[1].record()
             ev[1].synchronize()
@@ -450,6 +472,10 @@ class StageExecutor:
             return ops.attention_mfma(qkv, kc, vc, table, q_seq, q_ctx, self.decode_qblocks(T), self.nh, self.nkv,
                                       self.scale, out=out, workspace=ws, part_size=ps2, num_parts=np2,
                                       packed=packed)
+        fb = getattr(self, "_cur_fb", None)
+        if qblocks is not None and fb is not None and not packed:
+            return ops.attention_fa(qkv, kc, vc, table, q_seq, q_ctx, fb, self.nh, self.nkv, self.scale, out=out,
+                                    workspace=ws, max_ctx=max_ctx, waves=getattr(self, "_cur_fw", 4))
         if qblocks is not None:
             return ops.attention_mfma(qkv, kc, vc, table, q_seq, q_ctx, qblocks, self.nh, self.nkv, self.scale,
                                       out=out, workspace=ws, max_ctx=max_ctx, packed=packed,
@@ -634,6 +660,31 @@ class StageExecutor:
             return logits[:, :V]
         fn = ops.rmsnorm(hout, w.final_norm, eps, out=e("fn", (S, H)), rows=last_rows)
         return ops.linear(fn, w.lm_head, out=e("logits", (S, V)))
+
+    def warmup(self, sizes: Optional[Sequence[int]] = None) -> None:
+        """Run throwaway prefill steps at start-up so the first real request does not pay the
+        first-call costs of its shapes (hipBLASLt algorithm selection for the row-major GEMMs,
+        first launches of the prefill kernels): a cold 64 x 128-token prefill round took 4x
+        the warm one.  One single-sequence prefill per size (default: the step
+        capacity, 2048 and 512 tokens); the probe session is closed afterwards."""
+        cap = min(self.max_tokens, self.max_seq_len - 1)
+        sizes = sorted({int(n) for n in (sizes or (cap, 2048, 512)) if 128 < int(n) <= cap}, reverse=True)
+        if not sizes:
+            return
+        sid = "__warmup__"
+        with self.exec_lock, torch.inference_mode():
+            for n in sizes:
+                if self.is_first:
+                    x = torch.randint(0, self.cfg.vocab_size, (n,), device=self.device)
+                else:
+                    x = (0.1 * torch.randn(n, self.cfg.hidden_size, device=self.device)).to(self.dtype)
+                try:
+                    self.forward([(sid, n)], x, reset=[True])
+                except Exception as e:  # noqa: BLE001 - e.g. no KV room for n tokens: warm what fits
+                    logger.info(f"warmup of a {n}-token step skipped: {e}")
+                finally:
+                    self.sessions.close(sid)
+            torch.cuda.synchronize(self.device)
 
     def _folded_native(self, T: int) -> bool:
         """Would ``ops.linear`` run BOTH norm-consuming projections (qkv, gate/up) of a T-row

@@ -619,6 +619,45 @@ def test_attention_mfma_grouped_prefill(nh, nkv, D, ntoks, prefix, parts):
     torch.testing.assert_close(ops.unpack_act(outp, T, nh * D).float(), o_ref.float(), atol=2e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("nh,nkv", [(32, 32), (32, 8), (64, 8), (16, 8), (8, 4)])
+@pytest.mark.parametrize("ntoks,prefix", [([70, 9, 1, 33, 130], [0, 0, 0, 0, 0]), ([300, 17], [64, 5]),
+                                          ([1000], [0]), ([48, 64], [1, 200]), ([129, 256], [0, 63])])
+@pytest.mark.parametrize("waves,parts", [(4, None), (8, None), (4, 3)])
+def test_attention_fa_prefill(nh, nkv, ntoks, prefix, waves, parts):
+    """FA2 prefill kernel (32x32x16 MFMA, transposed LDS reads of V) vs the fp32 reference:
+    ragged prompts, chunked prefill over an existing prefix (ctx = prefix + i + 1), 4- and
+    8-wave workgroups, context split over parts.  Cache slots past every context hold NaN:
+    they must never reach the output."""
+    D = 128
+    ctxs = [p + n for p, n in zip(prefix, ntoks)]
+    q, kc, vc, bt, _, _ = _attn_case(nh, nkv, D, ctxs)
+    ps = kc.shape[2]
+    for i, c in enumerate(ctxs):  # poison the unused tail of every sequence's last page
+        pg = int(bt[i, (c - 1) // ps])
+        kc[pg, :, (c - 1) % ps + 1:] = float("nan")
+        vc[pg, :, (c - 1) % ps + 1:] = float("nan")
+    q_seq = torch.cat([torch.full((n,), i, dtype=torch.int32) for i, n in enumerate(ntoks)]).to(DEV)
+    q_ctx = torch.cat([torch.arange(p + 1, p + n + 1, dtype=torch.int32) for p, n in zip(prefix, ntoks)]).to(DEV)
+    T = q_seq.numel()
+    q = bf(torch.randn(T, (nh + 2 * nkv) * D, device=DEV))
+    fb = torch.from_numpy(ops.fa_blocks(ntoks, nh // nkv, waves)).to(DEV)
+    assert int(fb[1].sum()) == T
+    scale = 1 / math.sqrt(D)
+    out = ops.attention_fa(q, kc, vc, bt, q_seq, q_ctx, fb, nh, nkv, scale, waves=waves, num_parts=parts)
+    kr, vr = kc.clone(), vc.clone()
+    kr[kr.isnan()] = 0
+    vr[vr.isnan()] = 0
+    o_ref = ref.paged_attention(q.float(), kr.float(), vr.float(), bt, q_seq, q_ctx, nh, nkv, scale)
+    assert torch.isfinite(out.float()).all()
+    torch.testing.assert_close(out.float(), o_ref.float(), atol=2e-2, rtol=2e-2)
+
+
+def test_fa_blocks():
+    assert ops.fa_blocks([5, 1, 300], 1, 4).tolist() == [[0, 5, 6, 134, 262], [5, 1, 128, 128, 44]]
+    assert ops.fa_blocks([40], 4, 4).tolist() == [[0, 32], [32, 8]]
+    assert ops.fa_blocks([40], 8, 8).tolist() == [[0, 32], [32, 8]]
+
+
 def test_query_superblocks():
     assert ops.query_superblocks([5, 1, 70], 1).tolist() == [[0, 1, 2], [1, 1, 5]]
     assert ops.query_superblocks([5, 1, 70], 1, group=4).tolist() == [[0, 1, 2, 6], [1, 1, 4, 1]]

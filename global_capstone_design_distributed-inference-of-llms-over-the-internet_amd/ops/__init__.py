@@ -719,6 +719,9 @@ def linear(x, w, out=None, epilogue=0, residual=None, policy=None, wp=None, a_ro
         raise RuntimeError(f"packed activations need the native decode GEMM (M={M}, N={N}, K={K})")
     if w is None:
         raise RuntimeError(f"no row-major weight for the hipBLASLt path (M={M}, N={N}, K={K})")
+    if epilogue == 0 and out is not None and out.is_contiguous() and out.dtype == x.dtype and \
+            out.shape == (M, N) and x.dim() == 2:
+        return torch.mm(x, w.t(), out=out)  # hipBLASLt straight into the caller's buffer (no copy)
     y = torch.nn.functional.linear(x, w)  # hipBLASLt
     if epilogue == 1:
         return swiglu(y, out=out)

@@ -270,9 +270,10 @@ def unpack_act(ap, M, K):
 
 
 def norm_stats_buffer(device, n: int = 1) -> torch.Tensor:
-    """Zeroed fixed-point row statistics for the fused-norm decode path: int64 [n, 32, 64]
-    (32 atomic shards x 64 rows of exact sums of round(x^2 * 2^20), csrc/gemm.hip EpiArgs)."""
-    return torch.zeros(n, ref.SS_SHARDS, 64, dtype=torch.int64, device=device)
+    """Zeroed fixed-point row statistics for the fused-norm decode path: int64 [n, 32, 128]
+    (32 atomic shards x 128 rows of exact sums of round(x^2 * 2^20), csrc/gemm.hip EpiArgs):
+    decode steps of up to 128 rows."""
+    return torch.zeros(n, ref.SS_SHARDS, ref.SS_ROWS, dtype=torch.int64, device=device)
 
 
 def rmsnorm(x, w, eps, out=None, residual=None, mode=0, rows=None, packed=False, ss=None, a8=None, a8_scale=None):
@@ -638,6 +639,8 @@ def wide_gemm_ok(M: int, N: int, K: int, epilogue: int = 0, out_packed: bool = F
     """65..128 decode rows: the balanced ring kernel covers (packed A; epilogue 0 or packed SwiGLU,
     the widths it is built for)."""
     key = (M, N, K, int(epilogue), bool(out_packed))
+    if epilogue == 3 and os.environ.get("MPAMD_WIDE_SPLITK", "1") == "0":
+        return False  # the fused-norm producer only exists as the split-K ring + reduce form
     if key not in _RW_OK:
         _RW_OK[key] = bool(native_available() and
                            torch.ops.mpamd.gemm_rw_ok(int(M), int(N), int(K), int(epilogue), int(bool(out_packed))))

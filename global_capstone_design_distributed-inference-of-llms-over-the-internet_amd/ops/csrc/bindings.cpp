@@ -86,11 +86,11 @@ inline void check_rows(const at::Tensor& t, const char* name) {
 
 inline int64_t packed_numel(int64_t M, int64_t K) { return ((M + 15) / 16) * 16 * K; }
 
-// fused-norm row statistics: int64 [32 shards][64 rows] fixed-point sums (gemm.hip EpiArgs)
+// fused-norm row statistics: int64 [32 shards][128 rows] fixed-point sums (gemm.hip EpiArgs)
 inline void* opt_ss(const c10::optional<at::Tensor>& t, const char* name) {
   if (!t.has_value()) return nullptr;
   MP_CHECK(t->is_cuda() && t->scalar_type() == at::kLong && t->is_contiguous() && t->numel() >= mp_gemm_ss_elems(),
-           std::string(name) + ": int64 cuda contiguous [32, 64] (ops.norm_stats_buffer)");
+           std::string(name) + ": int64 cuda contiguous [32, 128] (ops.norm_stats_buffer)");
   return t->data_ptr();
 }
 
@@ -109,7 +109,7 @@ void rmsnorm(const at::Tensor& x, at::Tensor& residual, const at::Tensor& w, at:
   }
   MP_CHECK(mode >= 0 && mode <= 3, "mode");
   void* ssp = opt_ss(ss, "ss");
-  MP_CHECK(mode != 3 || (ssp != nullptr && x.size(0) <= 64), "mode 3 needs ss and <= 64 rows");
+  MP_CHECK(mode != 3 || (ssp != nullptr && x.size(0) <= 128), "mode 3 needs ss and <= 128 rows");
   if (mode != 0) {
     check_bf16_cuda(residual, "residual");
     check_rows(residual, "residual");

@@ -27,7 +27,7 @@ __global__ __launch_bounds__(256) void pack_weight_kernel(const bf16_t* __restri
 
 }  // namespace mp
 
-extern "C" int mp_gemm_ss_elems() { return mp::SS_NSH * 64; }
+extern "C" int mp_gemm_ss_elems() { return mp::SS_NSH * mp::SS_ROWS; }
 
 // byte offset / size of the split-K partial-slab region inside the GEMM workspace (shared with
 // the fp8 split-K kernel, fp8.hip)

@@ -69,12 +69,14 @@ __device__ __forceinline__ u16x8 load_a_rows(const bf16_t* p, int lane, bool row
 // same-address atomics serialise at the memory side, 256 adders on one row cost ~20 us);
 // consumers sum the shards of every row once per workgroup into LDS.
 constexpr int SS_NSH = 32;
+constexpr int SS_ROWS = 128;        // rows per shard: decode steps of up to 128 sessions
+constexpr int SS_PG = 4;            // shard groups a RowScale reduction uses at most (512 / SS_ROWS)
 constexpr float SS_FX = 1048576.f;  // 2^20
 typedef unsigned long long u64;
 
 struct EpiArgs {
   bf16_t* ap;          // EPI 3: packed copy of the output rows (mt_out row tiles)
-  u64* ss_out;         // EPI 3: [SS_NSH][64] fixed-point sums of squares (atomics)
+  u64* ss_out;         // EPI 3: [SS_NSH][SS_ROWS] fixed-point sums of squares (atomics)
   u64* ss_zero;        // cleared by block 0 at kernel start: the other norm buffer
   const u64* ss_in;    // non-null: scale accumulator row r by rsqrt(sum_r / K + eps)
   float inv_k;
@@ -109,40 +111,44 @@ __device__ __forceinline__ u64 fx_sq(float f) { return (u64)__float2ull_rn(f * f
 
 __device__ __forceinline__ void clear_other(const EpiArgs& ep) {
   if (ep.ss_zero != nullptr && blockIdx.x == 0) {
-    for (int i = threadIdx.x; i < SS_NSH * 64; i += blockDim.x) ep.ss_zero[i] = 0ull;
+    for (int i = threadIdx.x; i < SS_NSH * SS_ROWS; i += blockDim.x) ep.ss_zero[i] = 0ull;
   }
 }
 
 // Consumer side (EPI 0 / 1 only; compiled out of the producer epilogues), in two halves around
-// the main loop (512-thread workgroups): each thread loads SS_NSH/8 shard words right AFTER the
-// kernel's first weight loads and folds them into one 64-bit partial (in-order vmcnt: waiting
-// for them costs nothing beyond the first weight chunk the loop waits for anyway, and only 2
-// VGPRs stay live through the loop); the partials are reduced through LDS in the epilogue,
-// after the main loop's last barrier.
+// the main loop: thread t owns row t % SS_ROWS and shard group t / SS_ROWS (G = NW * 64 /
+// SS_ROWS groups), loads its SS_NSH / G shard words right AFTER the kernel's first weight loads
+// and folds them into one 64-bit partial (in-order vmcnt: waiting for them costs nothing beyond
+// the first weight chunk the loop waits for anyway, and only 2 VGPRs stay live through the
+// loop); the G partials of a row are reduced through LDS in the epilogue, after the main loop's
+// last barrier.  Rows past the step's M read zeroed shards: their scale is never used.
 template <bool ON, int NW = 8>
 struct RowScale {
+  static constexpr int G = NW * 64 / SS_ROWS;
+  static_assert(G >= 1 && G <= SS_PG && SS_NSH % G == 0, "shard groups");
   u64 v = 0;
   __device__ __forceinline__ void load(const EpiArgs& ep, const void* any_valid) {
     if constexpr (ON) {
       const u64* src = ep.ss_in != nullptr ? ep.ss_in : reinterpret_cast<const u64*>(any_valid);
       const int tid = threadIdx.x;
+      const int row = tid % SS_ROWS, grp = tid / SS_ROWS;
       u64 t = 0;
 #pragma unroll
-      for (int j = 0; j < SS_NSH / NW; ++j) t += src[ep.ss_in != nullptr ? ((tid >> 6) + NW * j) * 64 + (tid & 63) : 0];
+      for (int j = 0; j < SS_NSH / G; ++j) t += src[ep.ss_in != nullptr ? (grp + G * j) * SS_ROWS + row : 0];
       v = t;
     }
   }
   // every thread of the workgroup calls this (two barriers inside when ss_in is set)
-  __device__ __forceinline__ void finish(const EpiArgs& ep, u64 (*part)[64], float* rs) {
+  __device__ __forceinline__ void finish(const EpiArgs& ep, u64 (*part)[SS_ROWS], float* rs) {
     if constexpr (ON) {
       if (ep.ss_in == nullptr) return;
       const int tid = threadIdx.x;
-      part[tid >> 6][tid & 63] = v;
+      part[tid / SS_ROWS][tid % SS_ROWS] = v;
       __syncthreads();
-      if (tid < 64) {
+      if (tid < SS_ROWS) {
         u64 s = 0;
 #pragma unroll
-        for (int w = 0; w < NW; ++w) s += part[w][tid];
+        for (int w = 0; w < G; ++w) s += part[w][tid];
         rs[tid] = rsqrtf((float)s * (1.f / SS_FX) * ep.inv_k + ep.eps);
       }
       __syncthreads();
@@ -175,7 +181,7 @@ __device__ __forceinline__ void epi3_store(const EpiArgs& ep, bf16_t* __restrict
   ep.ap[apk_off(row, col, ep.mt_out)] = o;
   if (ep.ss_out == nullptr) return;  // (benchmark ablation only: the executor always passes ss_out)
   const u64 t = sum16(fx_sq(bf2f(o)));
-  if (c == 0) atomicAdd(ep.ss_out + (blockIdx.x % SS_NSH) * 64 + row, t);
+  if (c == 0) atomicAdd(ep.ss_out + (blockIdx.x % SS_NSH) * SS_ROWS + row, t);
 }
 
 __device__ __forceinline__ f32x4 mfma16(const u16x8& a, const u16x8& b, const f32x4& c) {
@@ -192,8 +198,8 @@ __global__ __launch_bounds__(512) void gemm_packed_kernel(const bf16_t* __restri
                                                           int64_t res_stride, int M, int N, int K,
                                                           const int* __restrict__ gate, const EpiArgs ep) {
   clear_other(ep);
-  __shared__ u64 rs_part[8][64];
-  __shared__ float rs_lds[64];
+  __shared__ u64 rs_part[SS_PG][SS_ROWS];
+  __shared__ float rs_lds[SS_ROWS];
   RowScale<EPI < 2> rsc;
   // MoE expert gate (ops/moe.py): a device-side count of tokens routed to this expert; 0 ->
   // the whole grid exits before streaming any weight (output left as is, combine weight 0).
@@ -463,8 +469,8 @@ __global__ __launch_bounds__(512) void gemm_lds_kernel(const bf16_t* __restrict_
                                                        const bf16_t* __restrict__ res, int64_t rs, int M, int N,
                                                        int K, const EpiArgs ep) {
   clear_other(ep);
-  __shared__ u64 rs_part[8][64];
-  __shared__ float rs_lds[64];
+  __shared__ u64 rs_part[SS_PG][SS_ROWS];
+  __shared__ float rs_lds[SS_ROWS];
   RowScale<EPI < 2> rsc;
   constexpr int KS = 8 / CH;
   constexpr int NSL = (CH * MT * NT + 7) / 8;  // epilogue quads per wave
@@ -625,8 +631,8 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(const bf16_t* __restrict__
                                                       int64_t rs, int M, int N, int K, int* __restrict__ cnt,
                                                       f32x4* __restrict__ slab, int remap, const EpiArgs ep) {
   clear_other(ep);
-  __shared__ u64 rs_part[8][64];
-  __shared__ float rs_lds[64];
+  __shared__ u64 rs_part[SS_PG][SS_ROWS];
+  __shared__ float rs_lds[SS_ROWS];
   RowScale<EPI < 2> rsc;
   constexpr int Q = MT * NT;  // accumulator quads (f32x4) per lane
   __shared__ __attribute__((aligned(16))) f32x4 red[8 * Q * 64 + 16];
@@ -939,7 +945,7 @@ constexpr int rw_depth2() {
 template <int MT, int NT, int EPI, bool OPK, bool F8 = false>
 __device__ __forceinline__ void rw_body(const bf16_t* __restrict__ x, const bf16_t* __restrict__ wp,
                                         bf16_t* __restrict__ y, int64_t ys, const bf16_t* __restrict__ res, int64_t rs,
-                                        int M, int K, int tile0, const EpiArgs& ep, f32x4* red, u64 (*rs_part)[64],
+                                        int M, int K, int tile0, const EpiArgs& ep, f32x4* red, u64 (*rs_part)[SS_ROWS],
                                         float* rs_lds) {
   constexpr int R = rw_depth2<MT, NT, F8>();
   constexpr int Q = MT * NT;
@@ -1053,8 +1059,8 @@ __global__ __launch_bounds__(256) void gemm_rw_kernel(const bf16_t* __restrict__
                                                       const bf16_t* __restrict__ res, int64_t rs, int M, int K,
                                                       int n_big, const EpiArgs ep) {
   clear_other(ep);
-  __shared__ u64 rs_part[8][64];
-  __shared__ float rs_lds[64];
+  __shared__ u64 rs_part[SS_PG][SS_ROWS];
+  __shared__ float rs_lds[SS_ROWS];
   __shared__ __attribute__((aligned(16))) f32x4 red[RW_WAVES * (MT * NTB < RW_QC ? MT * NTB : RW_QC) * 64];
   const int b = blockIdx.x;
   if (b < n_big) {
@@ -1261,8 +1267,8 @@ __global__ __launch_bounds__(256) void gemm_rwk_kernel(const bf16_t* __restrict_
       for (int t = 0; t < NT; ++t) acc[mt][t] *= wsc[t];
   }
   if constexpr (INL >= 0) {
-    __shared__ u64 rs_part[RW_WAVES][64];
-    __shared__ float rs_lds[64];
+    __shared__ u64 rs_part[SS_PG][SS_ROWS];
+    __shared__ float rs_lds[SS_ROWS];
     __shared__ int s_last;
     RowScale<INL < 2, RW_WAVES> rsc;
     rsc.load(ep, wp);
@@ -1343,7 +1349,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   if constexpr (EPI == 0) {  // fused-norm consumer (qkv): row scale rsqrt(sum of squares / K + eps)
     if (ep.ss_in != nullptr) {
       if (threadIdx.x < 64) {
-        u64 t = threadIdx.x < SS_NSH ? ep.ss_in[threadIdx.x * 64 + row] : 0ull;
+        u64 t = threadIdx.x < SS_NSH ? ep.ss_in[threadIdx.x * SS_ROWS + row] : 0ull;
 #pragma unroll
         for (int o2 = 32; o2 > 0; o2 >>= 1) t += __shfl_xor(t, o2, 64);
         if (threadIdx.x == 0) s_rs = rsqrtf((float)t * (1.f / SS_FX) * ep.inv_k + ep.eps);
@@ -1391,7 +1397,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sq;
     __syncthreads();
     if (threadIdx.x == 0)
-      atomicAdd(ep.ss_out + ((blockIdx.y * gridDim.x + blockIdx.x) % SS_NSH) * 64 + row,
+      atomicAdd(ep.ss_out + ((blockIdx.y * gridDim.x + blockIdx.x) % SS_NSH) * SS_ROWS + row,
                 red[0] + red[1] + red[2] + red[3]);
   }
 }

@@ -33,6 +33,9 @@ extern "C" int mp_gemm_bf16_wide(const void* x, const void* w, void* y, int64_t 
 extern "C" int mp_gemm_rw_ok(int M, int N, int K, int epilogue, int out_packed) {
   using namespace mp;
   if (M <= 64 || M > 128 || K % (32 * GU_MAX) || N % 16) return 0;
+  // the fused-norm producer (residual + packed copy + row statistics) at 65..128 rows runs as
+  // the split-K ring + its reduce launch (the reduce applies the epilogue): o / down widths
+  if (epilogue == 3) return !out_packed && N % 2048 == 0;
   const EpiArgs ep{};
   const int flags = 1 | (out_packed ? 2 : 0) | 128;
   int rc;

@@ -37,7 +37,7 @@ def unpack_act(ap, M, K):
     return x[:M]
 
 
-SS_SHARDS, SS_FX = 32, float(1 << 20)
+SS_SHARDS, SS_ROWS, SS_FX = 32, 128, float(1 << 20)
 
 
 def fx_sumsq(x):
@@ -49,8 +49,8 @@ def rmsnorm(x, w, eps, out=None, residual=None, mode=0, rows=None, ss=None):
     dt = x.dtype
     if mode == 3:  # fused-norm stage entry: residual = x, y = raw x, ss = fixed-point sum(x^2) per row
         residual.copy_(x)
-        ss.view(SS_SHARDS, 64).zero_()
-        ss.view(SS_SHARDS, 64)[0, : x.shape[0]] = fx_sumsq(x)
+        ss.view(SS_SHARDS, SS_ROWS).zero_()
+        ss.view(SS_SHARDS, SS_ROWS)[0, : x.shape[0]] = fx_sumsq(x)
         if out is not None:
             out[: x.shape[0]].copy_(x)
             return out
@@ -204,14 +204,14 @@ def linear(x, w, out=None, epilogue=0, residual=None, ss_in=None, inv_k=0.0, eps
         ss_zero.zero_()
     y = torch.nn.functional.linear(x, w) if x.dtype == w.dtype else torch.nn.functional.linear(x.to(w.dtype), w)
     if ss_in is not None:
-        tot = ss_in.view(SS_SHARDS, 64).sum(0)[: y.shape[0]].double() / SS_FX
+        tot = ss_in.view(SS_SHARDS, SS_ROWS).sum(0)[: y.shape[0]].double() / SS_FX
         y = y.float() * torch.rsqrt(tot.float() * inv_k + eps)[:, None]
     y = y.to(x.dtype)
     if epilogue == 3:
         o = add(y, residual)
         residual.copy_(o)
         pack_act(o, out=ap_out)
-        ss_out.view(SS_SHARDS, 64)[0, : o.shape[0]] += fx_sumsq(o)
+        ss_out.view(SS_SHARDS, SS_ROWS)[0, : o.shape[0]] += fx_sumsq(o)
         return residual
     if epilogue == 1:
         y = swiglu(y)

@@ -554,7 +554,8 @@ class StageExecutor:
                 ops.quant_rows_fp8(act, out=a8, scale=asc)
                 ops.linear_fp8(a8, asc, L.down_q, L.down_s, T, out=mlp)
                 self._ar(mlp)
-        elif prompt is None and self._fused and T <= 64 and (self._w8 or self._packed_ok(T)):
+        elif prompt is None and self._fused and (T <= 64 and (self._w8 or self._packed_ok(T)) or
+                                                  (not self._w8 and self._fused_wide_ok(T))):
             # fused-norm decode path: 5 launches per layer (qkv, attention, o, gate/up, down).
             # The residual stream r lives row-major in ``res`` and packed in ``xr``; o / down add
             # their product into it in their epilogue and accumulate sum(r^2) per row, and qkv /
@@ -797,6 +798,17 @@ class StageExecutor:
         self._streamer = LayerStreamer(host, self.device) if host else None
         self.use_graphs = False  # the slot ring is re-filled every step; graphs would pin one layer set
         logger.info(f"CPU offload: {n_stream} layers streamed from pinned host memory, {keep} resident")
+
+    def _fused_wide_ok(self, M: int) -> bool:
+        """Fused-norm decode path at 65..128 rows (bf16): the wide kernels cover every
+        projection with its fused epilogue - qkv and gate/up consume the row statistics
+        (balanced ring or split-K ring + reduce), o and down produce them (split-K ring, the
+        reduce launch applies the residual / packed copy / statistics epilogue)."""
+        if not 64 < M <= 128 or self.device.type != "cuda" or not self._packed_ok(M):
+            return False
+        cfg = self.cfg
+        H, F = cfg.hidden_size, cfg.intermediate_size
+        return ops.wide_gemm_ok(M, H, cfg.q_dim, 3) and ops.wide_gemm_ok(M, H, F, 3)
 
     def _head_packed_ok(self, M: int) -> bool:
         return self.device.type == "cuda" and ops.gemm_policy() != "hipblaslt" and 0 < M <= 64 and \

@@ -115,6 +115,92 @@ def test_producer_epilogue_residual_pack_and_sumsq(kern, M):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("M", [65, 96, 128])
+def test_wide_rows_consumer_and_producer(M):
+    """65..128 rows (decode steps of 65..128 sessions): the consumers (qkv: split-K ring +
+    reduce with the row scale; gate/up: balanced ring with the row scale and packed SwiGLU) and
+    the producer (split-K ring + the reduce launch's residual / packed copy / statistics)."""
+    dev = "cuda"
+    g = torch.Generator(device=dev).manual_seed(500 + M)
+    K, N = 2048, 2048
+    assert ops.wide_gemm_ok(M, N, K, 3)
+    x = (torch.randn(M, K, device=dev, generator=g) * 0.7).to(torch.bfloat16)
+    gw = (torch.rand(K, device=dev, generator=g) + 0.5).to(torch.bfloat16)
+    ss = ops.norm_stats_buffer(dev)[0] + 3
+    res = torch.empty_like(x)
+    xp = torch.zeros(ops.packed_numel(M, K), dtype=torch.bfloat16, device=dev)
+    ops.rmsnorm(x, gw, EPS, out=xp, residual=res, mode=3, packed=True, ss=ss)
+    assert torch.equal(ss.sum(0)[:M].cpu(), ref.fx_sumsq(x.cpu()))
+    w = (torch.randn(N, K, device=dev, generator=g) * 0.03).to(torch.bfloat16)
+    wp = ops.pack_weight((w.float() * gw.float()[None, :]).to(torch.bfloat16).contiguous())
+    y = ops.linear(xp, None, wp=wp, a_rows=M, ss_in=ss, eps=EPS)
+    wgu = (torch.randn(2 * N, K, device=dev, generator=g) * 0.03).to(torch.bfloat16)
+    wgup = ops.pack_weight((wgu.float() * gw.float()[None, :]).to(torch.bfloat16).contiguous())
+    act = torch.zeros(ops.packed_numel(M, N), dtype=torch.bfloat16, device=dev)
+    ops.linear(xp, None, out=act, epilogue=1, wp=wgup, a_rows=M, out_packed=True, ss_in=ss, eps=EPS)
+    xn = _rms_ref(x, gw).float()
+    torch.testing.assert_close(y.float(), xn @ w.float().t(), atol=3e-2, rtol=3e-2)
+    exp = ref.swiglu((xn @ wgu.float().t()).to(torch.bfloat16)).float()
+    # K = 2048: bf16 rounding of gate and up before the product (one element in 1e5 lands at 0.031)
+    torch.testing.assert_close(ref.unpack_act(act, M, N).float(), exp, atol=5e-2, rtol=3e-2)
+    # producer
+    a = (torch.randn(M, K, device=dev, generator=g) * 0.5).to(torch.bfloat16)
+    wo = (torch.randn(N, K, device=dev, generator=g) * 0.03).to(torch.bfloat16)
+    r = torch.randn(M, N, device=dev, generator=g).to(torch.bfloat16)
+    r0 = r.clone()
+    ap = torch.zeros(ops.packed_numel(M, N), dtype=torch.bfloat16, device=dev)
+    sso, ssz = ops.norm_stats_buffer(dev)[0], ops.norm_stats_buffer(dev)[0] + 7
+    ops.linear(ops.pack_act(a), None, out=r, epilogue=3, residual=r, wp=ops.pack_weight(wo), a_rows=M,
+               ap_out=ap, ss_out=sso, ss_zero=ssz)
+    exp = (r0.float() + (a.float() @ wo.float().t()).to(torch.bfloat16).float()).to(torch.bfloat16)
+    torch.testing.assert_close(r.float(), exp.float(), atol=2e-2, rtol=2e-2)
+    assert torch.equal(ref.unpack_act(ap, M, N), r)
+    assert torch.equal(sso.sum(0)[:M].cpu(), ref.fx_sumsq(r.cpu()))
+    assert int(ssz.abs().sum()) == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("graphs", [False, True])
+def test_fused_executor_wide_batch_matches_unfused(graphs, monkeypatch):
+    """A 100-session decode step takes the fused-norm path (wide kernels) and matches the
+    unfused packed path step by step."""
+    import dataclasses
+
+    from src.models.config import resolve_model
+    from src.models.weights import random_stage_weights
+    from src.runtime.executor import StageExecutor
+
+    cfg = dataclasses.replace(resolve_model("small-llama"), hidden_size=2048, intermediate_size=4096,
+                              num_attention_heads=16, num_key_value_heads=16, num_hidden_layers=2,
+                              name="wide-test")
+    n = 100
+
+    def build(fused):
+        monkeypatch.setenv("MPAMD_FUSED_NORM", "1" if fused else "0")
+        w = random_stage_weights(cfg, 0, 2, has_embed=True, has_head=True, device="cuda", seed=5)
+        for i, lay in enumerate(w.layers):
+            gen = torch.Generator(device="cuda").manual_seed(70 + i)
+            lay.input_norm = (torch.rand(cfg.hidden_size, device="cuda", generator=gen) + 0.5).to(torch.bfloat16)
+            lay.post_norm = (torch.rand(cfg.hidden_size, device="cuda", generator=gen) + 0.5).to(torch.bfloat16)
+        return StageExecutor(cfg, w, "cuda", kv_cache_bytes=512 << 20, max_sessions=128, max_seq_len=64,
+                             use_graphs=graphs)
+
+    fx, ux = build(True), build(False)
+    assert fx._fused and fx._fused_wide_ok(n)
+    gen = torch.Generator().manual_seed(9)
+    lens = [int(x) for x in torch.randint(3, 12, (n,), generator=gen)]
+    seqs = [(f"s{i}", L) for i, L in enumerate(lens)]
+    ids = torch.randint(0, cfg.vocab_size, (sum(lens),), generator=gen).cuda()
+    lf = fx.forward(seqs, ids, reset=[True] * n)
+    lu = ux.forward(seqs, ids, reset=[True] * n)
+    for _ in range(3):
+        tok = torch.argmax(lu.float(), -1)
+        lf = fx.forward([(s, 1) for s, _ in seqs], tok)
+        lu = ux.forward([(s, 1) for s, _ in seqs], tok)
+        torch.testing.assert_close(lf.float(), lu.float(), atol=0.08, rtol=0.05)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("graphs", [False, True])
 def test_fused_executor_matches_unfused_and_oracle(graphs, monkeypatch):
     from src.models.config import resolve_model

@@ -24,6 +24,9 @@ LIB_NAME = "_mpamd_kernels.so"
 LIB_PATH = os.path.join(HERE, LIB_NAME)
 ARCH = os.environ.get("MPAMD_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+# ablation builds: extra device-compile flags (e.g. "-DMP_RW_WAVES=8") go to their own object
+# directory and library name (``--out``), never over the default library
+EXTRA = os.environ.get("MPAMD_HIPCC_EXTRA", "").split()
 
 
 def _torch_paths():
@@ -55,11 +58,16 @@ def _run(cmd):
     return r.stdout
 
 
-def build(force: bool = False, jobs: int = 0, verbose: bool = False) -> str:
+def build(force: bool = False, jobs: int = 0, verbose: bool = False, out: str = None) -> str:
     """Compile (if stale) and return the path of the kernel library."""
     hips, binding = _sources()
     headers = [os.path.join(CSRC, f) for f in sorted(os.listdir(CSRC)) if f.endswith(".h")]
-    tag = _digest(hips + [binding] + headers, extra=ARCH + HIPCC)
+    xtag = " ".join(EXTRA)
+    if xtag and not out:
+        raise SystemExit("MPAMD_HIPCC_EXTRA builds need --out (the default library stays the default build)")
+    LIB_PATH = os.path.abspath(out) if out else globals()["LIB_PATH"]
+    BUILD = globals()["BUILD"] + ("_" + hashlib.sha256(xtag.encode()).hexdigest()[:8] if xtag else "")
+    tag = _digest(hips + [binding] + headers, extra=ARCH + HIPCC + xtag)
     stamp = os.path.join(BUILD, "stamp")
     if not force and os.path.exists(LIB_PATH) and os.path.exists(stamp):
         with open(stamp) as f:
@@ -67,10 +75,10 @@ def build(force: bool = False, jobs: int = 0, verbose: bool = False) -> str:
                 return LIB_PATH
     os.makedirs(BUILD, exist_ok=True)
     inc, libdir = _torch_paths()
-    common = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-I" + CSRC]
+    common = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-I" + CSRC] + EXTRA
     objs = []
     cmds = []
-    hdr_tag = _digest(headers, extra=ARCH + HIPCC)
+    hdr_tag = _digest(headers, extra=ARCH + HIPCC + xtag)
 
     def stale(src, obj):
         # per-object stamp: the source + every csrc header (a kernel edit rebuilds one object)
@@ -121,8 +129,9 @@ def main(argv=None):
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", "--jobs", type=int, default=0)
     ap.add_argument("-v", "--verbose", action="store_true")
+    ap.add_argument("--out", default=None, help="library path of an ablation build (MPAMD_HIPCC_EXTRA)")
     a = ap.parse_args(argv)
-    path = build(force=a.force, jobs=a.jobs, verbose=a.verbose)
+    path = build(force=a.force, jobs=a.jobs, verbose=a.verbose, out=a.out)
     print(path)
 
 

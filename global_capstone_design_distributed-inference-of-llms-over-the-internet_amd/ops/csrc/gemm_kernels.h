@@ -65,7 +65,7 @@ __device__ __forceinline__ u16x8 load_a_rows(const bf16_t* p, int lane, bool row
 // round(x^2 * 2^20) as a 64-bit integer, so the sum is exact and independent of the order in
 // which the 16-lane groups / workgroups / atomics add up (bitwise reproducible, and equal to
 // what the stage-entry kernel computes for the same rows: a model split over stages gives
-// the same bits as one stage).  Producers add into NSH shards [NSH][64] (shard = block % NSH:
+// the same bits as one stage).  Producers add into NSH shards [NSH][SS_ROWS] (shard = block % NSH:
 // same-address atomics serialise at the memory side, 256 adders on one row cost ~20 us);
 // consumers sum the shards of every row once per workgroup into LDS.
 constexpr int SS_NSH = 32;
@@ -133,8 +133,10 @@ struct RowScale {
       const int tid = threadIdx.x;
       const int row = tid % SS_ROWS, grp = tid / SS_ROWS;
       u64 t = 0;
+      if (row < 16 * ep.mt_out) {  // rows past the step's row tiles: never scaled, not loaded
 #pragma unroll
-      for (int j = 0; j < SS_NSH / G; ++j) t += src[ep.ss_in != nullptr ? (grp + G * j) * SS_ROWS + row : 0];
+        for (int j = 0; j < SS_NSH / G; ++j) t += src[ep.ss_in != nullptr ? (grp + G * j) * SS_ROWS + row : 0];
+      }
       v = t;
     }
   }
@@ -926,8 +928,11 @@ static int launch_gemm_sk(const void* x, void* y, int64_t ys, const void* w, con
 // order (in-order vmcnt never drains the ring; loads past the end are clamped to a valid slice
 // and their MFMAs skipped), then the 4 partial tiles are summed through LDS and the shared
 // epilogues run (row scale, SwiGLU, residual, the fused-norm producer).
-constexpr int RW_WAVES = 4;
-constexpr int RW_QC = 32;  // quads per LDS combine pass (4 waves x 32 x 1 KiB = 128 KiB)
+#ifndef MP_RW_WAVES
+#define MP_RW_WAVES 4
+#endif
+constexpr int RW_WAVES = MP_RW_WAVES;  // waves per ring workgroup (an ablation build sets 8)
+constexpr int RW_QC = 128 / RW_WAVES;  // quads per LDS combine pass (waves x RW_QC x 1 KiB = 128 KiB)
 
 // Ring slots: a power of two (K / 32 / 4 waves is a multiple of it at K = 4096, 11008: no
 // clamped tail turn); 4 (MT + NT) VGPRs each (one wave per SIMD: the accumulators go to AGPRs).
@@ -1054,7 +1059,7 @@ __device__ __forceinline__ void rw_body(const bf16_t* __restrict__ x, const bf16
 }
 
 template <int MT, int NTB, int NTS, int EPI, bool OPK, bool F8 = false>
-__global__ __launch_bounds__(256) void gemm_rw_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ wp,
+__global__ __launch_bounds__(RW_WAVES * 64) void gemm_rw_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ wp,
                                                       bf16_t* __restrict__ y, int64_t ys,
                                                       const bf16_t* __restrict__ res, int64_t rs, int M, int K,
                                                       int n_big, const EpiArgs ep) {
@@ -1085,13 +1090,13 @@ static int launch_gemm_rw_cfg(const void* x, const void* w, void* y, int64_t ys,
       if (dry) return 0;
       if (epi == 1) {
         if constexpr (NTB % 2 == 0 && NTS % 2 == 0)
-          hipLaunchKernelGGL((gemm_rw_kernel<MT, NTB, NTS, 1, true, true>), dim3(G), dim3(256), 0, stream,
+          hipLaunchKernelGGL((gemm_rw_kernel<MT, NTB, NTS, 1, true, true>), dim3(G), dim3(RW_WAVES * 64), 0, stream,
                              (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, ys, (const bf16_t*)res, rs, M, K, n_big, ep);
       } else if (epi == 3) {
-        hipLaunchKernelGGL((gemm_rw_kernel<MT, NTB, NTS, 3, false, true>), dim3(G), dim3(256), 0, stream,
+        hipLaunchKernelGGL((gemm_rw_kernel<MT, NTB, NTS, 3, false, true>), dim3(G), dim3(RW_WAVES * 64), 0, stream,
                            (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, ys, (const bf16_t*)res, rs, M, K, n_big, ep);
       } else {
-        hipLaunchKernelGGL((gemm_rw_kernel<MT, NTB, NTS, 0, false, true>), dim3(G), dim3(256), 0, stream,
+        hipLaunchKernelGGL((gemm_rw_kernel<MT, NTB, NTS, 0, false, true>), dim3(G), dim3(RW_WAVES * 64), 0, stream,
                            (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, ys, (const bf16_t*)res, rs, M, K, n_big, ep);
       }
       return 0;
@@ -1106,10 +1111,10 @@ static int launch_gemm_rw_cfg(const void* x, const void* w, void* y, int64_t ys,
       if (dry) return 0;
       if (epi == 1) {
         if constexpr (NTB % 2 == 0 && NTS % 2 == 0)
-          hipLaunchKernelGGL((gemm_rw_kernel<MT, NTB, NTS, 1, true>), dim3(G), dim3(256), 0, stream, (const bf16_t*)x,
+          hipLaunchKernelGGL((gemm_rw_kernel<MT, NTB, NTS, 1, true>), dim3(G), dim3(RW_WAVES * 64), 0, stream, (const bf16_t*)x,
                              (const bf16_t*)w, (bf16_t*)y, ys, (const bf16_t*)res, rs, M, K, n_big, ep);
       } else {
-        hipLaunchKernelGGL((gemm_rw_kernel<MT, NTB, NTS, 0, false>), dim3(G), dim3(256), 0, stream, (const bf16_t*)x,
+        hipLaunchKernelGGL((gemm_rw_kernel<MT, NTB, NTS, 0, false>), dim3(G), dim3(RW_WAVES * 64), 0, stream, (const bf16_t*)x,
                            (const bf16_t*)w, (bf16_t*)y, ys, (const bf16_t*)res, rs, M, K, n_big, ep);
       }
       return 0;
@@ -1118,7 +1123,7 @@ static int launch_gemm_rw_cfg(const void* x, const void* w, void* y, int64_t ys,
   if (epi == 1 && (NTB % 2 || NTS % 2)) return 1;
   if (dry) return 0;
 #define MP_RW(EPI_, OPK_)                                                                                          \
-  hipLaunchKernelGGL((gemm_rw_kernel<MT, NTB, NTS, EPI_, OPK_>), dim3(G), dim3(256), 0, stream, (const bf16_t*)x, \
+  hipLaunchKernelGGL((gemm_rw_kernel<MT, NTB, NTS, EPI_, OPK_>), dim3(G), dim3(RW_WAVES * 64), 0, stream, (const bf16_t*)x, \
                      (const bf16_t*)w, (bf16_t*)y, ys, (const bf16_t*)res, rs, M, K, n_big, ep)
   if (epi == 1) {
     if constexpr (NTB % 2 == 0 && NTS % 2 == 0) {
@@ -1196,7 +1201,7 @@ constexpr int64_t RWK_SLAB_BYTES = (int64_t)16 << 20;  // S x M x N fp32 partial
 // deterministic) and runs epilogue INL (0 with the optional row scale, 2, 3) itself - the
 // stream-K kernel's hand-off protocol (guide: splitk-seam, publish-large).
 template <int MT, int NT, bool F8 = false, int INL = -1>
-__global__ __launch_bounds__(256) void gemm_rwk_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ wp,
+__global__ __launch_bounds__(RW_WAVES * 64) void gemm_rwk_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ wp,
                                                        float* __restrict__ part, int M, int N, int K, int S,
                                                        const EpiArgs ep, bf16_t* __restrict__ y, int64_t ys,
                                                        const bf16_t* __restrict__ res, int64_t rs,
@@ -1458,7 +1463,7 @@ static int launch_gemm_rwk(const void* x, const void* w, void* y, int64_t ys, co
       (int64_t)tiles * MT * S * 1024 <= RWK_SLAB_BYTES) {
     if constexpr (MT <= 4) {
 #define MP_RWKI(NT_, E_)                                                                                       \
-  hipLaunchKernelGGL((gemm_rwk_kernel<MT, NT_, F8, E_>), g1, dim3(256), 0, stream, (const bf16_t*)x,            \
+  hipLaunchKernelGGL((gemm_rwk_kernel<MT, NT_, F8, E_>), g1, dim3(RW_WAVES * 64), 0, stream, (const bf16_t*)x,            \
                      (const bf16_t*)w, part, M, N, K, S, ep, (bf16_t*)y, ys, (const bf16_t*)res, rs, tick)
 #define MP_RWKI_E(NT_) \
   { if (epi == 3) MP_RWKI(NT_, 3); else if (epi == 2) MP_RWKI(NT_, 2); else MP_RWKI(NT_, 0); }
@@ -1473,12 +1478,12 @@ static int launch_gemm_rwk(const void* x, const void* w, void* y, int64_t ys, co
     }
   }
   switch (nt) {
-    case 1: hipLaunchKernelGGL((gemm_rwk_kernel<MT, 1, F8>), g1, dim3(256), 0, stream, (const bf16_t*)x, (const bf16_t*)w, part, M, N, K, S, ep, nullptr, 0, nullptr, 0, nullptr); break;
-    case 2: hipLaunchKernelGGL((gemm_rwk_kernel<MT, 2, F8>), g1, dim3(256), 0, stream, (const bf16_t*)x, (const bf16_t*)w, part, M, N, K, S, ep, nullptr, 0, nullptr, 0, nullptr); break;
-    case 4: hipLaunchKernelGGL((gemm_rwk_kernel<MT, 4, F8>), g1, dim3(256), 0, stream, (const bf16_t*)x, (const bf16_t*)w, part, M, N, K, S, ep, nullptr, 0, nullptr, 0, nullptr); break;
+    case 1: hipLaunchKernelGGL((gemm_rwk_kernel<MT, 1, F8>), g1, dim3(RW_WAVES * 64), 0, stream, (const bf16_t*)x, (const bf16_t*)w, part, M, N, K, S, ep, nullptr, 0, nullptr, 0, nullptr); break;
+    case 2: hipLaunchKernelGGL((gemm_rwk_kernel<MT, 2, F8>), g1, dim3(RW_WAVES * 64), 0, stream, (const bf16_t*)x, (const bf16_t*)w, part, M, N, K, S, ep, nullptr, 0, nullptr, 0, nullptr); break;
+    case 4: hipLaunchKernelGGL((gemm_rwk_kernel<MT, 4, F8>), g1, dim3(RW_WAVES * 64), 0, stream, (const bf16_t*)x, (const bf16_t*)w, part, M, N, K, S, ep, nullptr, 0, nullptr, 0, nullptr); break;
     default:
       if constexpr (4 * MT * 8 <= 192)
-        hipLaunchKernelGGL((gemm_rwk_kernel<MT, 8, F8>), g1, dim3(256), 0, stream, (const bf16_t*)x, (const bf16_t*)w, part, M, N, K, S, ep, nullptr, 0, nullptr, 0, nullptr);
+        hipLaunchKernelGGL((gemm_rwk_kernel<MT, 8, F8>), g1, dim3(RW_WAVES * 64), 0, stream, (const bf16_t*)x, (const bf16_t*)w, part, M, N, K, S, ep, nullptr, 0, nullptr, 0, nullptr);
       break;
   }
   const dim3 g2(N / 2048, M);

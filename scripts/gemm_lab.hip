@@ -7,7 +7,8 @@
 //
 // -DLAB_NO_A replaces every A-fragment load by a register value (ablation: what the weight stream
 // alone sustains in the same kernel structure); -DLAB_A_L1 serves every A load from one 4 KiB
-// L1-resident window; -DLAB_A_NT makes the A loads non-temporal.  Results: profiles/r1_gemm_lab.md.
+// L1-resident window; -DLAB_A_LDS from a 4 KiB LDS window; -DLAB_A_NT makes the A loads
+// non-temporal; -DMP_RW_WAVES=8 builds the ring kernels with 8 waves per workgroup.  Results: profiles/r1_gemm_lab.md.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -19,6 +20,10 @@
 #define MP_LOAD_A_FRAG(p) ((mp::u16x8)((unsigned short)(0x3c00u + (threadIdx.x & 7))))
 #elif defined(LAB_A_NT)  // non-temporal A loads
 #define MP_LOAD_A_FRAG(p) __builtin_nontemporal_load(reinterpret_cast<const mp::u16x8*>(p))
+#elif defined(LAB_A_LDS)  // every A load reads a 4 KiB LDS window (ablation: A at LDS cost)
+typedef unsigned short lab_u16x8 __attribute__((ext_vector_type(8)));
+__shared__ lab_u16x8 lab_lds[256];
+#define MP_LOAD_A_FRAG(p) (lab_lds[((uintptr_t)(p) >> 4) & 255])
 #elif defined(LAB_A_L1)  // every A load hits the same 4 KiB (L1-resident): prices the L2->CU path
 #define MP_LOAD_A_FRAG(p) (*reinterpret_cast<const mp::u16x8*>((const char*)x + (((uintptr_t)(p) - (uintptr_t)x) & 4095)))
 #endif

@@ -83,6 +83,40 @@ def gemm_policy() -> str:
     return _GEMM_POLICY
 
 
+# Library (hipBLASLt / rocBLAS) solutions for the row-major GEMMs - prefill and decode steps above
+# 128 rows - picked per shape by PyTorch TunableOp on MI355X (scripts/tune_gemms.py; the file's
+# validator lines pin the ROCm / hipBLASLt build it was measured on, other builds ignore it).
+# Loaded read-only: tuning stays off, shapes not in the file keep the library heuristic.
+TUNED_GEMMS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned", "gemm_gfx950.csv")
+_TUNED_STATE = {"loaded": None}
+
+
+def use_tuned_gemms(path: Optional[str] = None) -> bool:
+    """Turn on TunableOp with the shipped solution table (once per process); False if off
+    (``MPAMD_TUNED_GEMMS=0``), no GPU, or the table does not load."""
+    if _TUNED_STATE["loaded"] is not None:
+        return _TUNED_STATE["loaded"]
+    ok = False
+    path = path or TUNED_GEMMS
+    if os.environ.get("MPAMD_TUNED_GEMMS", "1") != "0" and torch.cuda.is_available() and os.path.exists(path):
+        import tempfile
+
+        from torch.cuda import tunable
+
+        try:
+            tunable.tuning_enable(False)
+            # results are never written back into the package: any output goes to a scratch file
+            tunable.set_filename(os.path.join(tempfile.gettempdir(), f"mpamd_tunableop_{os.getpid()}.csv"))
+            tunable.enable(True)
+            ok = bool(tunable.read_file(path))
+            if not ok:
+                tunable.enable(False)
+        except Exception:  # noqa: BLE001 - a TunableOp-less build: keep the heuristic
+            ok = False
+    _TUNED_STATE["loaded"] = ok
+    return ok
+
+
 # Decode GEMM kernel choice (gemm.hip): the one-group-per-workgroup kernel or the stream-K
 # kernel.  "auto" = per (M bucket, N, K, epilogue) choice measured by ``autotune_gemm`` (the
 # executor tunes its own shapes at start-up; untuned shapes use the first kernel); "on" /

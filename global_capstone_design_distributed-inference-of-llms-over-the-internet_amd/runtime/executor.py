@@ -238,6 +238,7 @@ class StageExecutor:
                 weights.pack_for_decode(fold_norms=self._fused)
                 if self._fused and not all(getattr(L, "folded", False) for L in weights.layers):
                     self._fused = False  # packed before (e.g. a shared weights object): norm kernels
+                ops.use_tuned_gemms()  # library GEMM solutions for the row-major shapes
                 ops.gemm_workspace(self.device)  # allocated before any hipGraph capture
                 ops.attention_counters(self.device)
                 if os.environ.get("MPAMD_GEMM_AUTOTUNE", "1") != "0":

@@ -811,3 +811,17 @@ def test_executor_wide_decode_batch_packed_path_matches_hipblaslt():
         finally:
             ops.set_gemm_policy("auto")
     torch.testing.assert_close(outs[0], outs[1], atol=0.08, rtol=0.05)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K", [(256, 12288, 4096), (256, 4096, 11008), (2048, 22016, 4096)])
+def test_tuned_library_gemm_table_loads_and_matches_fp32(M, N, K):
+    """The shipped TunableOp table (ops/tuned/gemm_gfx950.csv) loads on this ROCm build and
+    the solutions it picks for the row-major shapes compute x @ w^T (fp32 reference)."""
+    assert ops.use_tuned_gemms()
+    g = torch.Generator(device=DEV).manual_seed(M + N)
+    x = (torch.randn(M, K, device=DEV, generator=g) * 0.5).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV, generator=g) * 0.02).to(torch.bfloat16)
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    y = ops.linear(x, w, out=out, policy="hipblaslt")
+    torch.testing.assert_close(y.float(), x.float() @ w.float().t(), atol=2e-2, rtol=2e-2)

@@ -105,7 +105,7 @@ def main(argv=None):
     if world % (R * TP):
         raise SystemExit(f"--replicas {R} x --tp {TP} does not divide {world} GPUs")
     S = world // (R * TP)
-    tpg = make_tp_groups(world, S, TP)
+    tpg = make_tp_groups(world, S, TP, device=device)
     stage = rank % S
     lane = rank // S                      # pipeline index: replica * TP + tensor-parallel shard
     M = a.micro or (S + 1 if S > 1 else 1)  # one slot of slack for the token-return hop

@@ -19,26 +19,35 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 SRC = os.path.join(HERE, "runtime.cpp")
 SUFFIX = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
 LIB = os.path.join(HERE, "_mpamd_runtime" + SUFFIX)
+# direct RCCL communicators (rccl.cpp; dlopens torch's librccl at run time, links no ROCm library)
+RCCL_SRC = os.path.join(HERE, "rccl.cpp")
+RCCL_LIB = os.path.join(HERE, "_mpamd_rccl" + SUFFIX)
+
+
+def _build_one(src: str, lib: str, force: bool, libs=()) -> str:
+    import pybind11
+
+    with open(src, "rb") as f:
+        tag = hashlib.sha256(f.read()).hexdigest()
+    stamp = lib + ".stamp"
+    if not force and os.path.exists(lib) and os.path.exists(stamp) and open(stamp).read().strip() == tag:
+        return lib
+    inc = [pybind11.get_include(), sysconfig.get_paths()["include"]]
+    cmd = ["g++", "-O3", "-shared", "-fPIC", "-std=c++17", "-fvisibility=hidden"] + [f"-I{p}" for p in inc] + [
+        src, "-o", lib + ".tmp"] + list(libs)
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode:
+        raise RuntimeError(f"native build of {os.path.basename(src)} failed:\n" + r.stdout)
+    os.replace(lib + ".tmp", lib)
+    with open(stamp, "w") as f:
+        f.write(tag)
+    return lib
 
 
 def build(force: bool = False) -> str:
-    import pybind11
-
-    with open(SRC, "rb") as f:
-        tag = hashlib.sha256(f.read()).hexdigest()
-    stamp = LIB + ".stamp"
-    if not force and os.path.exists(LIB) and os.path.exists(stamp) and open(stamp).read().strip() == tag:
-        return LIB
-    inc = [pybind11.get_include(), sysconfig.get_paths()["include"]]
-    cmd = ["g++", "-O3", "-shared", "-fPIC", "-std=c++17", "-fvisibility=hidden"] + [f"-I{p}" for p in inc] + [
-        SRC, "-o", LIB + ".tmp"]
-    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
-    if r.returncode:
-        raise RuntimeError("native runtime build failed:\n" + r.stdout)
-    os.replace(LIB + ".tmp", LIB)
-    with open(stamp, "w") as f:
-        f.write(tag)
-    return LIB
+    """Build the host runtime and the direct-RCCL module; returns the runtime's path."""
+    _build_one(RCCL_SRC, RCCL_LIB, force, libs=("-ldl",))
+    return _build_one(SRC, LIB, force)
 
 
 _mod = None

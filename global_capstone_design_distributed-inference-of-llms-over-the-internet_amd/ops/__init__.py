@@ -26,6 +26,10 @@ _LOCK = threading.Lock()
 _LOADED: Optional[bool] = None
 _LOAD_ERROR: Optional[str] = None
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_mpamd_kernels.so")
+# an ablation build (``MPAMD_HIPCC_EXTRA=... python -m src.ops.build --out PATH``) is loaded as is
+_LIB_OVERRIDE = os.environ.get("MPAMD_KERNEL_LIB")
+if _LIB_OVERRIDE:
+    LIB_PATH = os.path.abspath(_LIB_OVERRIDE)
 
 
 def load_library(build_if_missing: bool = True) -> bool:
@@ -35,7 +39,7 @@ def load_library(build_if_missing: bool = True) -> bool:
         if _LOADED is not None:
             return _LOADED
         try:
-            if build_if_missing:
+            if build_if_missing and not _LIB_OVERRIDE:
                 try:
                     from .build import build
 

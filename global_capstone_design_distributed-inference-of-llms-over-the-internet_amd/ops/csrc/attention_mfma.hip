@@ -31,6 +31,9 @@
 // ctx - 1, and its v chunk overwrites that token's column of the wave's LDS V tile.  The cache
 // loads stay exactly as without ROPE.  Wave 0 of the first block of the kv head whose slice
 // holds the token writes k / v to the page slot (slots[t] < 0: nothing written).
+// (K/V loads keep the default cache policy here: non-temporal loads, a win for the MHA decode
+// kernel in attention.hip, measured 12-14 % SLOWER on this kernel at 64 / 256 sessions, cold
+// caches - profiles/r3_i/attn_nt.jsonl vs attn_def.jsonl.)
 #include "common.h"
 
 namespace mp {

@@ -1214,7 +1214,18 @@ __global__ __launch_bounds__(RW_WAVES * 64) void gemm_rwk_kernel(const bf16_t* _
   constexpr int QC = Q < RW_QC ? Q : RW_QC;
   __shared__ __attribute__((aligned(16))) f32x4 red[RW_WAVES * QC * 64];
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int c = blockIdx.x / S, sp = blockIdx.x - c * S;
+  int c, sp;
+  if (INL >= 0 && (gridDim.x % (8 * S)) == 0) {
+    // in-launch combine: the S splits of a column group share blockIdx % 8, i.e. one XCD under
+    // round-robin dispatch, so the slab hand-off stays inside one L2 (MI355X_MICROARCH
+    // handoff-payload: same-XCD 1.7x cross-XCD).  Placement only - never correctness.
+    const int x = blockIdx.x & 7, j = blockIdx.x >> 3;
+    c = x * (gridDim.x / (8 * S)) + j / S;
+    sp = j % S;
+  } else {
+    c = blockIdx.x / S;
+    sp = blockIdx.x - c * S;
+  }
   const int tile0 = c * NT;
   const int nks = K >> 5;
   const int ks0 = (int)((int64_t)sp * nks / S), ks1 = (int)((int64_t)(sp + 1) * nks / S);

@@ -23,6 +23,7 @@ replicas stay the default for throughput and TP is for fitting / per-token laten
 from __future__ import annotations
 
 import dataclasses
+import os
 from typing import Optional
 
 import torch
@@ -89,34 +90,69 @@ def shard_stage_weights(sw: StageWeights, rank: int, tp: int) -> StageWeights:
 
 
 class TPGroup:
-    """The all-reduce a sharded stage issues after its row-parallel GEMMs."""
+    """The all-reduce a sharded stage issues after its row-parallel GEMMs.
 
-    def __init__(self, group: Optional["dist.ProcessGroup"] = None):
+    With ``comm`` (a direct ``parallel.rccl.RcclComm`` over the group's GPUs) the all-reduce is
+    enqueued on the current stream, so the executor captures it inside its decode hipGraphs
+    (``capturable``); otherwise it is torch's all-reduce on ``group`` (gloo on CPU, or RCCL
+    through ProcessGroupNCCL, which a graph cannot replay).  ``force``: treat a one-rank group
+    as a TP group (issue the collectives anyway) - the 1-GPU test of the captured RCCL path."""
+
+    def __init__(self, group: Optional["dist.ProcessGroup"] = None, comm=None, force: bool = False):
         self.group = group
-        self.size = dist.get_world_size(group) if dist.is_initialized() else 1
-        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.comm = comm
+        if comm is not None:
+            self.size, self.rank = comm.world, comm.rank
+        else:
+            self.size = dist.get_world_size(group) if dist.is_initialized() else 1
+            self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.force = bool(force)
+
+    @property
+    def active(self) -> bool:
+        return self.size > 1 or self.force
+
+    @property
+    def capturable(self) -> bool:
+        return self.comm is not None
 
     def all_reduce(self, t: torch.Tensor) -> torch.Tensor:
-        if self.size > 1:
+        if self.comm is not None and t.is_cuda:
+            self.comm.all_reduce(t)
+        elif self.size > 1:
             dist.all_reduce(t, group=self.group)
         return t
 
+    def close(self) -> None:
+        if self.comm is not None:
+            self.comm.close()
 
-def make_tp_groups(world: int, stages: int, tp: int) -> Optional[TPGroup]:
+
+def make_tp_groups(world: int, stages: int, tp: int, device=None) -> Optional[TPGroup]:
     """TP groups for a (replica x tp-lane x stage) rank layout: rank = lane * stages + stage,
     lane = replica * tp + t.  Each lane is a full pipeline (its own send/recv chain, fed the
     identical hidden states); the ranks holding the same stage in the tp lanes of one replica
-    form a TP group.  Every rank must call this (groups are created in the same order)."""
+    form a TP group.  Every rank must call this (groups are created in the same order).
+
+    On GPU (``device`` a cuda device) each group also gets a direct RCCL communicator
+    (``MPAMD_TP_RCCL=0``: torch's all-reduce only), so TP decode steps run as hipGraphs."""
     if tp <= 1 or not dist.is_initialized():
         return None
     lanes = world // stages
     if world % stages or lanes % tp:
         raise ValueError(f"world {world} does not factor into stages={stages} x tp={tp} x replicas")
-    rank, mine = dist.get_rank(), None
+    rank, mine, mine_ranks = dist.get_rank(), None, None
     for lane0 in range(0, lanes, tp):
         for st in range(stages):
             ranks = [(lane0 + j) * stages + st for j in range(tp)]
             g = dist.new_group(ranks)
             if rank in ranks:
-                mine = g
-    return TPGroup(mine)
+                mine, mine_ranks = g, ranks
+    comm = None
+    if device is not None and torch.device(device).type == "cuda" and os.environ.get("MPAMD_TP_RCCL", "1") != "0":
+        from . import rccl
+        from torch.distributed import distributed_c10d as c10d
+
+        store = c10d._get_default_store()
+        comm = rccl.RcclComm(store, "tp/" + "_".join(map(str, mine_ranks)), mine_ranks.index(rank), tp, device)
+    return TPGroup(mine, comm=comm)

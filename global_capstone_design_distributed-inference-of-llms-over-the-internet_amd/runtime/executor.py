@@ -142,7 +142,7 @@ class StageExecutor:
             # also reads the router and per-expert row-major weights.  Mixtral-8x7B (93 GB bf16)
             # fits one MI355X resident, so offload is rejected rather than half-supported.
             raise ValueError("CPU offload is not supported for MoE (Mixtral) models: serve them resident")
-        self._tp = tp if (tp is not None and tp.size > 1) else None
+        self._tp = tp if (tp is not None and getattr(tp, "active", tp.size > 1)) else None
         self.cfg = cfg
         self.w = weights
         self.device = torch.device(device)
@@ -173,8 +173,11 @@ class StageExecutor:
         self.use_graphs = (self.device.type == "cuda") if use_graphs is None else bool(use_graphs)
         self.use_graphs = self.use_graphs and self.device.type == "cuda" and cfg.model_type != "gpt2" and \
             os.environ.get("MPAMD_GRAPHS", "1") != "0"
-        if self._tp is not None and os.environ.get("MPAMD_TP_GRAPHS", "0") != "1":
-            self.use_graphs = False  # RCCL all-reduce capture is opt-in until validated on a multi-GPU node
+        if self._tp is not None and not getattr(self._tp, "capturable", False) and \
+                os.environ.get("MPAMD_TP_GRAPHS", "0") != "1":
+            # torch's all-reduce (gloo, or ProcessGroupNCCL's private stream) is not replayable:
+            # graphs under TP need the direct RCCL communicator (parallel/rccl.py)
+            self.use_graphs = False
         self.graph_max_batch = graph_max_batch
         self._graphs: Dict[Tuple[int, int, int], "_DecodeGraph"] = {}
         self._graph_pool = None

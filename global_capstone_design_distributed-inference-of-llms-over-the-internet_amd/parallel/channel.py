@@ -25,7 +25,12 @@ successor BEFORE computing, so the next stage plans its step (session table, pag
 reservations, metadata H2D) while the payload is still being produced.
 
 ``MPAMD_CHANNEL_DATA=gloo`` stages GPU payloads through host memory over gloo (several
-ranks sharing one GPU, where RCCL refuses duplicate devices).
+ranks sharing one GPU, where RCCL refuses duplicate devices).  ``MPAMD_CHANNEL_DATA=rccl`` carries
+``data`` / ``ret`` on the direct communicators of ``parallel/rccl.py`` instead of
+ProcessGroupNCCL: one two-rank communicator per neighbouring stage pair and one tail -> head,
+all initialised when the channel is built (ProcessGroupNCCL creates its per-peer
+communicator lazily, at the first send of a serving step), each driven from a dedicated HIP
+stream of this rank ordered against the compute stream by events.
 """
 from __future__ import annotations
 
@@ -112,6 +117,26 @@ class _Pending:
                 w.wait(_td(timeout_s))
 
 
+class _EventWork:
+    """Completion of an operation enqueued on a side stream, with the ProcessGroup ``Work``
+    surface the slab ring and the pending-send queue use: ``wait()`` orders the CURRENT stream
+    after it (no host block); ``wait(timeout)`` blocks the host with a deadline (flush)."""
+
+    def __init__(self, ev):
+        self.ev = ev
+
+    def wait(self, timeout=None):
+        if timeout is None:
+            torch.cuda.current_stream().wait_event(self.ev)
+        else:
+            wait_event(self.ev, timeout.total_seconds() if hasattr(timeout, "total_seconds") else float(timeout),
+                       "RCCL send")
+        return True
+
+    def is_completed(self) -> bool:
+        return self.ev.query()
+
+
 class _SlabRing:
     """Preallocated device byte slabs reused round-robin for RCCL payloads (no per-hop
     ``clone`` / ``empty``: the caching allocator and its cross-stream bookkeeping stay off the
@@ -156,7 +181,13 @@ class Channel:
         self.data_backend = data_backend
         self.staged = data_backend == "gloo" and self.device.type == "cuda"
         self.ctrl = _gloo(store, prefix + "/ctrl", self.rank, self.world, timeout_s)
-        if data_backend == "nccl":
+        self._rc = {}
+        if data_backend == "rccl":
+            if self.device.type != "cuda":
+                raise ValueError("the rccl data backend needs a GPU device")
+            self.data = self.ret = None
+            self._init_rccl(store, prefix, timeout_s)
+        elif data_backend == "nccl":
             self.data = _nccl(store, prefix + "/data", self.rank, self.world, timeout_s, self.device)
             self.ret = _nccl(store, prefix + "/ret", self.rank, self.world, timeout_s, self.device)
         else:
@@ -174,8 +205,27 @@ class Channel:
         self._wait_events: List[Tuple[object, object]] = []
         self._wait_host_s: List[float] = []
         self._rings = {}
-        if data_backend == "nccl" and self.device.type == "cuda":
+        if data_backend in ("nccl", "rccl") and self.device.type == "cuda":
             self._rings = {(w, d): _SlabRing(self.device, ring_slots) for w in ("data", "ret") for d in ("send", "recv")}
+
+    def _init_rccl(self, store, prefix: str, timeout_s: float) -> None:
+        """Two-rank communicators: (k, k+1) for the hidden-state hop, (tail, head) for token
+        return.  Every rank initialises its pairs in increasing k (a blocking init pairs with the
+        neighbour's FIRST init), then the head / tail the return pair."""
+        from .rccl import RcclComm
+
+        r, P = self.rank, self.world
+        if P < 2:
+            return
+        if r > 0:    # (r-1, r): this rank receives, as rank 1 of the pair
+            self._rc[("data", "recv")] = (RcclComm(store, f"{prefix}/rdata/{r - 1}", 1, 2, self.device, timeout_s), 0)
+        if r < P - 1:  # (r, r+1): this rank sends, as rank 0
+            self._rc[("data", "send")] = (RcclComm(store, f"{prefix}/rdata/{r}", 0, 2, self.device, timeout_s), 1)
+        if r == P - 1:
+            self._rc[("ret", "send")] = (RcclComm(store, f"{prefix}/rret", 0, 2, self.device, timeout_s), 1)
+        elif r == 0:
+            self._rc[("ret", "recv")] = (RcclComm(store, f"{prefix}/rret", 1, 2, self.device, timeout_s), 0)
+        self._rstreams = {k: torch.cuda.Stream(self.device) for k in self._rc}
 
     # ------------------------------------------------------------------ host control messages
     def send_msg(self, dst: int, arr: np.ndarray) -> None:
@@ -220,6 +270,8 @@ class Channel:
     def send(self, dst: int, t: torch.Tensor, which: str = "data") -> None:
         """Send ``t`` (a private copy is taken, so the caller may overwrite ``t`` right away -
         e.g. a hipGraph output buffer - while the send is in flight)."""
+        if self._rc:
+            return self._rccl_send(dst, t, which)
         pg = self._pg(which)
         try:
             ring = self._rings.get((which, "send"))
@@ -244,6 +296,8 @@ class Channel:
         """Post a receive; returns ``(tensor, waiter)``.  ``waiter()`` makes the tensor usable
         on the current stream: on RCCL it is a stream dependency (no host block), on gloo a
         blocking wait bounded by the timeout."""
+        if self._rc:
+            return self._rccl_recv(src, shape, dtype, which)
         pg = self._pg(which)
         t = self.timeout_s if timeout_s is None else timeout_s
         try:
@@ -287,6 +341,68 @@ class Channel:
         except RuntimeError as e:
             raise ChannelError(f"{which} recv from {src} failed: {e}") from e
 
+    def _rccl_pair(self, which: str, direction: str, other: int):
+        key = (which, direction)
+        if key not in self._rc:
+            raise ChannelError(f"rank {self.rank} has no {which} {direction} pair (peer {other})")
+        comm, peer = self._rc[key]
+        expect = {("data", "send"): self.rank + 1, ("data", "recv"): self.rank - 1, ("ret", "send"): 0,
+                  ("ret", "recv"): self.world - 1}[key]
+        if other != expect:
+            raise ChannelError(f"{which} {direction}: rank {self.rank} talks to {expect}, not {other}")
+        return comm, peer, self._rstreams[key]
+
+    def _rccl_send(self, dst: int, t: torch.Tensor, which: str) -> None:
+        comm, peer, st = self._rccl_pair(which, "send", dst)
+        ring = self._rings[(which, "send")]
+        try:
+            k, buf = ring.take(tuple(t.shape), t.dtype)   # stream-waits the slab's previous send
+            buf.copy_(t.detach())                        # compute stream: the caller may reuse t
+            ready = torch.cuda.Event()
+            ready.record()
+            st.wait_event(ready)
+            comm.send(buf, peer, stream=st)
+            done = torch.cuda.Event()
+            done.record(st)
+        except RuntimeError as e:
+            raise ChannelError(f"{which} send to {dst} failed: {e}") from e
+        work = _EventWork(done)
+        self.bytes_sent += buf.numel() * buf.element_size()
+        self.sends += 1
+        ring.done(k, work)
+        self._sends.add(work, buf)
+        self._sends.reap()
+
+    def _rccl_recv(self, src: int, shape, dtype, which: str):
+        comm, peer, st = self._rccl_pair(which, "recv", src)
+        ring = self._rings[(which, "recv")]
+        try:
+            k, buf = ring.take(tuple(shape), dtype)
+            free = torch.cuda.Event()  # the slab's previous readers are on the compute stream
+            free.record()
+            st.wait_event(free)
+            comm.recv(buf, peer, stream=st)
+            done = torch.cuda.Event()
+            done.record(st)
+        except RuntimeError as e:
+            raise ChannelError(f"{which} recv from {src} failed: {e}") from e
+        work = _EventWork(done)
+        ring.done(k, work)
+
+        def waiter():
+            e0 = None
+            if self.timing:
+                e0 = torch.cuda.Event(enable_timing=True)
+                e0.record()
+            work.wait()
+            if e0 is not None:
+                e1 = torch.cuda.Event(enable_timing=True)
+                e1.record()
+                self._wait_events.append((e0, e1))
+            return buf
+
+        return buf, waiter
+
     def stats(self, reset: bool = True) -> dict:
         """Hop statistics since the last reset: backend, payload bytes / sends, and the mean
         ms this rank's stream (device) or host (gloo) waited for an incoming payload."""
@@ -313,7 +429,14 @@ class Channel:
         if self.closed:
             return
         self.closed = True
+        for comm, _ in self._rc.values():
+            try:
+                comm.abort()
+            except Exception:  # noqa: BLE001 - best effort during failure handling
+                pass
         for pg in (self.data, self.ret):
+            if pg is None:
+                continue
             for name in ("abort", "_abort", "shutdown"):
                 fn = getattr(pg, name, None)
                 if fn is not None:
@@ -333,6 +456,11 @@ class Channel:
         except RuntimeError:
             pass
         self.closed = True
+        for comm, _ in self._rc.values():
+            try:
+                comm.close()
+            except Exception:  # noqa: BLE001
+                pass
         for pg in (self.data, self.ret):
             fn = getattr(pg, "shutdown", None)
             if fn is not None:

@@ -440,6 +440,28 @@ __global__ __launch_bounds__(NW * 64) void paged_attn1_kernel(
     for (int u = 0; u < U; ++u) pgn[u] = bt[min(b0 + u * TPI + tg, end - 1) >> page_log2];
   }
 
+  auto issue = [&](int b, const int* pg, u16x8* kd, u16x8* vd) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int tc = min(b + u * TPI + tg, end - 1);
+      const int64_t off = (int64_t)pg[u] * page_stride + head_off + (int64_t)(tc & (page_size - 1)) * D;
+      kd[u] = MP_KV_LOAD(reinterpret_cast<const u16x8*>(kc + off));
+      vd[u] = MP_KV_LOAD(reinterpret_cast<const u16x8*>(vc + off));
+    }
+  };
+  auto page_ids = [&](int b, int* pg) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) pg[u] = bt[min(b + u * TPI + tg, end - 1) >> page_log2];
+  };
+  // first iteration's K / V (PIPE) issued here, ahead of the query / RoPE loads: the cache
+  // stream's round trip overlaps the rotary-table round trip instead of following it
+  u16x8 kv[U], vv[U];
+  int pgm[U];
+  if constexpr (PIPE) {
+    page_ids(start + w * TPW + NW * TPW, pgm);
+    issue(start + w * TPW, pgn, kv, vv);
+  }
+
   float qf[NREP][8];
   u16x8 kn = (u16x8)(0), vn = (u16x8)(0);
   int tnew = -1;
@@ -499,19 +521,6 @@ __global__ __launch_bounds__(NW * 64) void paged_attn1_kernel(
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[r][j] = 0.f;
   }
-  auto issue = [&](int b, const int* pg, u16x8* kd, u16x8* vd) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int tc = min(b + u * TPI + tg, end - 1);
-      const int64_t off = (int64_t)pg[u] * page_stride + head_off + (int64_t)(tc & (page_size - 1)) * D;
-      kd[u] = MP_KV_LOAD(reinterpret_cast<const u16x8*>(kc + off));
-      vd[u] = MP_KV_LOAD(reinterpret_cast<const u16x8*>(vc + off));
-    }
-  };
-  auto page_ids = [&](int b, int* pg) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) pg[u] = bt[min(b + u * TPI + tg, end - 1) >> page_log2];
-  };
   auto compute = [&](int base, u16x8 (&kv)[U], u16x8 (&vv)[U]) {
     if constexpr (ROPE) {
 #pragma unroll
@@ -550,13 +559,10 @@ __global__ __launch_bounds__(NW * 64) void paged_attn1_kernel(
       }
 
   };
-  u16x8 kv[U], vv[U];
   if constexpr (PIPE) {
     // software-pipelined: iteration i+1's K / V (and i+2's page ids) are in flight while
-    // iteration i computes, so the stream never stops between iterations
-    int pgm[U];
-    page_ids(start + w * TPW + NW * TPW, pgm);
-    issue(start + w * TPW, pgn, kv, vv);
+    // iteration i computes, so the stream never stops between iterations (the first
+    // iteration's loads were issued ahead of the query / RoPE prologue)
     for (int base = start + w * TPW; base < end; base += NW * TPW) {
       const int nb = base + NW * TPW;
       u16x8 kx[U], vx[U];

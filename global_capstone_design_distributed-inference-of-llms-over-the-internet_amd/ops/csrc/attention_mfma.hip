@@ -90,12 +90,47 @@ __global__ __launch_bounds__(256, 2) void attn_mfma_kernel(
   for (int i = 0; i < ntok; ++i) blk_ctx = max(blk_ctx, q_ctx[tok0 + i]);
   const int start = p * PS, end = min(start + PS, blk_ctx);
 
+  constexpr int NV = (32 * D * 2) / 1024;  // 16-B V chunks per lane per step
+  auto load_k = [&](int bs, int64_t pg, u16x8 (&kr)[2][KD]) {
+    const bf16_t* kpage = kc + pg * page_stride + head_off + (int64_t)(bs & (page_size - 1)) * D;
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+      for (int kd = 0; kd < KD; ++kd)
+        kr[sub][kd] = *reinterpret_cast<const u16x8*>(kpage + (int64_t)(sub * 16 + c) * D + kd * 32 + qd * 8);
+  };
+  auto load_v = [&](int bs, int64_t pg, u16x8 (&vr)[NV]) {
+    const bf16_t* vpage = vc + pg * page_stride + head_off + (int64_t)(bs & (page_size - 1)) * D;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int ci = i * 64 + lane;
+      vr[i] = *reinterpret_cast<const u16x8*>(vpage + (int64_t)(ci % 32) * D + (ci / 32) * 8);
+    }
+  };
+  // K in ping-pong register buffers one step ahead (no register copies: a copy of in-flight
+  // loads would force a vmcnt(0) early); a step's V is issued at its top, ahead of the next
+  // step's K and the page id two steps ahead, so waiting for it leaves those in flight
+  u16x8 ka[2][KD], kb[2][KD], vr[NV];
+  int64_t pg_cur = 0, pg_next = 0;
+  const int b_first = start + w * 32;
+  // The first step's page ids, then (below) the query / RoPE loads, then this step's K AND V:
+  // the page-table round trip and the K / V stream overlap the query and rotary-table loads
+  // instead of following the whole RoPE prologue (decode blocks have one or two steps per wave:
+  // these dependent round trips, not the bytes, set the kernel time).
+  if (b_first < end) pg_cur = bt[b_first >> page_log2];
+  if (b_first + 128 < end) pg_next = bt[(b_first + 128) >> page_log2];
+
   u16x8 qf[KD];
 #pragma unroll
   for (int kd = 0; kd < KD; ++kd) {
     if (row_ok) qf[kd] = *reinterpret_cast<const u16x8*>(q + (int64_t)(tok0 + my_t) * q_stride + (int64_t)my_h * D +
                                                          kd * 32 + qd * 8);
     else qf[kd] = (u16x8)(0);
+  }
+
+  if (b_first < end) {
+    load_k(b_first, pg_cur, ka);
+    load_v(b_first, pg_cur, vr);
   }
 
   int tnew = -1;
@@ -166,23 +201,6 @@ __global__ __launch_bounds__(256, 2) void attn_mfma_kernel(
   // step exposes one memory round trip (its V) instead of three dependent ones (page id -> K -> V).
   // At decode sizes every wave has one or two steps: the chain, not the bytes, set the time
   // (Llama-3-70B, 64 sessions: 16.9 us per layer for 37 MB of K/V).
-  constexpr int NV = (32 * D * 2) / 1024;  // 16-B V chunks per lane per step
-  auto load_k = [&](int bs, int64_t pg, u16x8 (&kr)[2][KD]) {
-    const bf16_t* kpage = kc + pg * page_stride + head_off + (int64_t)(bs & (page_size - 1)) * D;
-#pragma unroll
-    for (int sub = 0; sub < 2; ++sub)
-#pragma unroll
-      for (int kd = 0; kd < KD; ++kd)
-        kr[sub][kd] = *reinterpret_cast<const u16x8*>(kpage + (int64_t)(sub * 16 + c) * D + kd * 32 + qd * 8);
-  };
-  auto load_v = [&](int bs, int64_t pg, u16x8 (&vr)[NV]) {
-    const bf16_t* vpage = vc + pg * page_stride + head_off + (int64_t)(bs & (page_size - 1)) * D;
-#pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      const int ci = i * 64 + lane;
-      vr[i] = *reinterpret_cast<const u16x8*>(vpage + (int64_t)(ci % 32) * D + (ci / 32) * 8);
-    }
-  };
   // one 32-token step over K / V fragments already in registers
   auto step = [&](int b0, const u16x8 (&kr)[2][KD], const u16x8 (&vr)[NV]) {
     // ---- S^T = K . Q^T for tokens b0 .. b0+31 (two 16-token subtiles) ----
@@ -265,22 +283,9 @@ __global__ __launch_bounds__(256, 2) void attn_mfma_kernel(
       o[dt] = mfma_bf16(pa, vfrag, o[dt]);
     }
   };
-  // K in ping-pong register buffers one step ahead (no register copies: a copy of in-flight
-  // loads would force a vmcnt(0) early); a step's V is issued at its top, ahead of the next
-  // step's K and the page id two steps ahead, so waiting for it leaves those in flight
-  u16x8 ka[2][KD], kb[2][KD], vr[NV];
-  int64_t pg_cur = 0, pg_next = 0;
-  const int b_first = start + w * 32;
-  {
-    // both page ids first: in-order vmcnt would otherwise make the first use of pg_next wait for
-    // the first step's K as well
-    if (b_first < end) pg_cur = bt[b_first >> page_log2];
-    if (b_first + 128 < end) pg_next = bt[(b_first + 128) >> page_log2];
-    if (b_first < end) load_k(b_first, pg_cur, ka);
-  }
   for (int b0 = b_first; b0 < end; b0 += 256) {
     const bool more1 = b0 + 128 < end;
-    load_v(b0, pg_cur, vr);
+    if (b0 != b_first) load_v(b0, pg_cur, vr);
     int64_t pg2 = 0;
     if (more1) {
       load_k(b0 + 128, pg_next, kb);

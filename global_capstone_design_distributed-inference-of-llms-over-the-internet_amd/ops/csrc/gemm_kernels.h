@@ -1348,18 +1348,27 @@ __global__ __launch_bounds__(RW_WAVES * 64) void gemm_rwk_kernel(const bf16_t* _
   }
 }
 
-// Sum the S fp32 slabs (fixed order: deterministic) + epilogue.  One thread per 8 consecutive
-// columns of a row; a workgroup covers 2048 columns of one row (EPI 3: its row's sum of squares
-// is reduced in the workgroup and added to one shard with a single atomic).
+// Sum the S fp32 slabs (fixed order: deterministic) + epilogue.  One thread per CPT consecutive
+// columns of a row; a workgroup covers 256 CPT columns of one row (EPI 3: its row's sum of squares
+// is reduced in the workgroup and added to one shard with a single atomic).  The kernel is one
+// memory round trip deep (latency-bound at decode sizes), so CPT = 4 (default) puts twice as many
+// workgroups - and loads in flight - on the chip as CPT = 8: 256 instead of 128 workgroups for a
+// 64 x 4096 output (``-DMP_SKR_CPT=8``: the round-2 geometry).
+#ifndef MP_SKR_CPT
+#define MP_SKR_CPT 4
+#endif
+constexpr int SKR_CPT = MP_SKR_CPT;
 template <int EPI, int S>
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ part, int M, int N,
                                                             bf16_t* __restrict__ y, int64_t ys,
                                                             const bf16_t* __restrict__ res, int64_t rs,
                                                             const EpiArgs ep) {
+  constexpr int CPT = SKR_CPT, NQ = CPT / 4;
+  typedef __attribute__((ext_vector_type(CPT))) unsigned short uvec;
   __shared__ u64 red[4];
   __shared__ float s_rs;
   const int row = blockIdx.y;
-  const int col = (blockIdx.x * 256 + threadIdx.x) * 8;
+  const int col = (blockIdx.x * 256 + threadIdx.x) * CPT;
   u64 sq = 0;
   float sc = 1.f;
   if constexpr (EPI == 0) {  // fused-norm consumer (qkv): row scale rsqrt(sum of squares / K + eps)
@@ -1376,35 +1385,37 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   }
   if (col < N) {
     // every slab load (and the residual) is issued before the first add: one memory round
-    // trip instead of S dependent ones (the slab loop used to run with a runtime trip count)
-    u16x8 rv = (u16x8)(0);
-    if constexpr (EPI != 0) rv = *reinterpret_cast<const u16x8*>(res + (int64_t)row * rs + col);
-    f32x4 p0[S], p1[S];
+    // trip instead of S dependent ones
+    uvec rv = (uvec)(0);
+    if constexpr (EPI != 0) rv = *reinterpret_cast<const uvec*>(res + (int64_t)row * rs + col);
+    f32x4 pq[S][NQ];
 #pragma unroll
     for (int s = 0; s < S; ++s) {
       const float* pp = part + ((int64_t)s * M + row) * N + col;
-      p0[s] = *reinterpret_cast<const f32x4*>(pp);
-      p1[s] = *reinterpret_cast<const f32x4*>(pp + 4);
+#pragma unroll
+      for (int h = 0; h < NQ; ++h) pq[s][h] = *reinterpret_cast<const f32x4*>(pp + 4 * h);
     }
-    f32x4 a0 = (f32x4)(0.f), a1 = (f32x4)(0.f);
+    f32x4 acc[NQ];
 #pragma unroll
-    for (int s = 0; s < S; ++s) {  // fixed slab order: deterministic
-      a0 += p0[s];
-      a1 += p1[s];
-    }
-    u16x8 o;
-    if constexpr (EPI == 0) {
+    for (int h = 0; h < NQ; ++h) acc[h] = (f32x4)(0.f);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = f2bf((j < 4 ? a0[j] : a1[j - 4]) * sc);
-    } else {
+    for (int s = 0; s < S; ++s)  // fixed slab order: deterministic
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        o[j] = f2bf(round_bf(j < 4 ? a0[j] : a1[j - 4]) + bf2f(rv[j]));
+      for (int h = 0; h < NQ; ++h) acc[h] += pq[s][h];
+    uvec o;
+#pragma unroll
+    for (int j = 0; j < CPT; ++j) {
+      const float a = acc[j / 4][j & 3];
+      if constexpr (EPI == 0) {
+        o[j] = f2bf(a * sc);
+      } else {
+        o[j] = f2bf(round_bf(a) + bf2f(rv[j]));
         if constexpr (EPI == 3) sq += fx_sq(bf2f(o[j]));
       }
     }
-    *reinterpret_cast<u16x8*>(y + (int64_t)row * ys + col) = o;
-    if constexpr (EPI == 3) *reinterpret_cast<u16x8*>(ep.ap + apk_off(row, col, ep.mt_out)) = o;
+    *reinterpret_cast<uvec*>(y + (int64_t)row * ys + col) = o;
+    // (packed layout: 8 consecutive columns of a row are contiguous, so CPT in {4, 8} stays one store)
+    if constexpr (EPI == 3) *reinterpret_cast<uvec*>(ep.ap + apk_off(row, col, ep.mt_out)) = o;
   }
   if constexpr (EPI == 3) {
     if (ep.ss_out == nullptr) return;
@@ -1497,7 +1508,7 @@ static int launch_gemm_rwk(const void* x, const void* w, void* y, int64_t ys, co
         hipLaunchKernelGGL((gemm_rwk_kernel<MT, 8, F8>), g1, dim3(RW_WAVES * 64), 0, stream, (const bf16_t*)x, (const bf16_t*)w, part, M, N, K, S, ep, nullptr, 0, nullptr, 0, nullptr);
       break;
   }
-  const dim3 g2(N / 2048, M);
+  const dim3 g2(N / (256 * SKR_CPT), M);
   launch_splitk_reduce(S, epi, g2, stream, part, M, N, y, ys, res, rs, ep);
   return 0;
 }

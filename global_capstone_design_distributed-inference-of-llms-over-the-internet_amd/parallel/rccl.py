@@ -13,10 +13,12 @@ protects the buffers.  ``abort`` releases a stream blocked on a dead peer.
 """
 from __future__ import annotations
 
+import atexit
 import datetime
 import importlib.util
 import os
 import threading
+import weakref
 from typing import Optional
 
 import torch
@@ -24,6 +26,20 @@ import torch
 _LOCK = threading.Lock()
 _MOD = None
 VERSION: Optional[int] = None
+
+# live communicators, destroyed at interpreter exit while the HIP runtime is still up (a destructor
+# running during teardown would call into RCCL after it)
+_LIVE: "weakref.WeakSet[RcclComm]" = weakref.WeakSet()
+
+
+@atexit.register
+def _close_all() -> None:
+    for c in list(_LIVE):
+        try:
+            c.close()
+        except Exception:  # noqa: BLE001 - best effort at exit
+            pass
+
 
 _DTYPES = {torch.uint8: "UINT8", torch.int32: "INT32", torch.int64: "INT64", torch.float16: "FLOAT16",
            torch.float32: "FLOAT32", torch.bfloat16: "BFLOAT16"}
@@ -64,7 +80,11 @@ class RcclComm:
         mod = module()
         self.rank, self.world = int(rank), int(world)
         self.device = torch.device(device)
-        key = f"{prefix}/rccl_uid"
+        # a generation per (prefix, rank): every rank counts its own communicators under this
+        # prefix, so a communicator re-created under the same prefix (a rebuilt channel) never
+        # reads the unique id of its predecessor
+        gen = int(store.add(f"{prefix}/rccl_gen/{self.rank}", 1))
+        key = f"{prefix}/rccl_uid/{gen}"
         if self.rank == 0:
             uid = mod.unique_id()
             store.set(key, uid)
@@ -74,6 +94,7 @@ class RcclComm:
         torch.cuda.set_device(self.device)
         self._c = mod.Comm(self.world, self.rank, bytes(uid))
         self._mod = mod
+        _LIVE.add(self)
 
     def _dt(self, t: torch.Tensor) -> int:
         if not t.is_contiguous():

@@ -89,6 +89,10 @@ class StageConnectionHandler:
         self._default = SamplingParams(0.8, 0.9, 0, 1.5)  # reference handler defaults (:71-73, :164)
         self._pending: List[_Req] = []
         self._draining = False
+        # sessions seen recently (sid -> last arrival): the collection window only waits while
+        # some of them have not sent this step's request yet - a lone session (the reference
+        # client's mode) never pays it
+        self._recent: Dict[str, float] = {}
         self._worker = concurrent.futures.ThreadPoolExecutor(1, thread_name_prefix="stage-gpu")
         self._sampler = BatchSampler(self.device) if final_stage else None
         self.alloc_timeout = alloc_timeout
@@ -384,6 +388,7 @@ class StageConnectionHandler:
         req = self._parse(msg)
         req.priority = self.prioritizer.prioritize(int(req.x.shape[0]), bool(req.reset))
         req.fut = asyncio.get_running_loop().create_future()
+        self._recent[req.sid] = req.t0
         self._pending.append(req)
         self.stats["requests"] += 1
         if not self._draining:
@@ -396,7 +401,7 @@ class StageConnectionHandler:
         loop = asyncio.get_running_loop()
         try:
             while self._pending:
-                if self.batch_window > 0:
+                if self.batch_window > 0 and self._expect_more():
                     await asyncio.sleep(self.batch_window)
                 batch, rest, seen, ntok = [], [], set(), 0
                 # priority order (decode steps first), arrival order within a priority
@@ -432,6 +437,15 @@ class StageConnectionHandler:
                         r.fut.set_result(o)
         finally:
             self._draining = False
+
+    def _expect_more(self, horizon_s: float = 1.0) -> bool:
+        """Are sessions active within ``horizon_s`` missing from the pending queue?  Only then can
+        the collection window merge more requests into this step."""
+        now = time.perf_counter()
+        if len(self._recent) > 4 * len(self._pending) + 64:  # prune sessions gone quiet
+            self._recent = {k: t for k, t in self._recent.items() if now - t < horizon_s}
+        pending = {r.sid for r in self._pending}
+        return any(now - t < horizon_s and sid not in pending for sid, t in self._recent.items())
 
     async def _run_with_alloc_wait(self, loop, batch: List[_Req]):
         """Run a batch; when the KV cache is full, evict expired sessions and wait (up to

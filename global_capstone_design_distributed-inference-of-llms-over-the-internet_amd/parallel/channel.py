@@ -373,6 +373,26 @@ class Channel:
         self._sends.add(work, buf)
         self._sends.reap()
 
+    def send_on_stream(self, dst: int, t: torch.Tensor, which: str = "data") -> None:
+        """Direct-RCCL send of ``t`` on the CURRENT stream, no private copy: recorded into a
+        hipGraph when called during a capture (the engine's graph hop).  Stream order is what
+        keeps ``t`` alive and unmodified until the send has read it; every send of this pair must
+        then go this way (one stream per communicator keeps the op order the receiver sees)."""
+        if not self._rc:
+            raise ChannelError("send_on_stream needs the rccl data backend")
+        comm, peer, _ = self._rccl_pair(which, "send", dst)
+        try:
+            comm.send(t, peer)
+        except RuntimeError as e:
+            raise ChannelError(f"{which} send to {dst} failed: {e}") from e
+        if not torch.cuda.is_current_stream_capturing():
+            self.count_send(t.numel() * t.element_size())
+
+    def count_send(self, nbytes: int) -> None:
+        """Hop statistics for a send that ran inside a graph replay."""
+        self.bytes_sent += int(nbytes)
+        self.sends += 1
+
     def _rccl_recv(self, src: int, shape, dtype, which: str):
         comm, peer, st = self._rccl_pair(which, "recv", src)
         ring = self._rings[(which, "recv")]

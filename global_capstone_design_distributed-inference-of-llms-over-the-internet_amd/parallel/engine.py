@@ -332,14 +332,25 @@ class PipelineServingEngine:
         """All-gather (free KV tokens, max sessions, page size) over the channel: the head
         admits only what EVERY stage can hold (stages with more blocks hold fewer tokens)."""
         ex = self.ex
+        want_hop = (self.ch is not None and getattr(self.ch, "data_backend", "") == "rccl" and
+                    os.environ.get("MPAMD_GRAPH_HOP", "0") == "1")
         mine = [float(ex.sessions.cache_tokens_left()), float(ex.sessions.max_sessions), float(ex.cache.page_size),
-                float(ex.max_seq_len)]
+                float(ex.max_seq_len), float(want_hop), float(bool(ex.use_graphs)), float(ex.graph_max_batch)]
         allv = self.ch.all_gather_floats(mine) if self.ch is not None else [mine]
         self.stage_capacity = allv
         cap = int(min(v[0] for v in allv))
         self.max_handles = min(self.max_handles, int(min(v[1] for v in allv)))
         self.page = int(max(v[2] for v in allv))
         self.max_len = int(min(v[3] for v in allv))
+        # graph hop (opt-in, MPAMD_GRAPH_HOP=1 on the direct-RCCL data plane): every stage's
+        # decode graph ends with its hidden-state send, recorded into the graph on the compute
+        # stream; a receiver must then know the row count of every hop from the header alone,
+        # so all stages need identical graph settings (else no stage uses it)
+        self.graph_hop = (self.S > 1 and all(v[4] == 1.0 for v in allv) and all(v[5] == 1.0 for v in allv) and
+                          len({v[6] for v in allv}) == 1)
+        if self.graph_hop and not self.is_tail:
+            nxt = self.rank + 1
+            ex.set_graph_hook(lambda out: self.ch.send_on_stream(nxt, out))
         if self.is_head:
             self.capacity_tokens = cap
             self.free_handles = list(range(self.max_handles - 1, -1, -1))
@@ -540,11 +551,28 @@ class PipelineServingEngine:
             if self.S == 1:
                 step.tok_dev = self._sample_tail(hdr, out)
             else:
-                self.ch.send(1, out)
+                self._hop_send(1, out)
                 _, step.waiter = self.ch.recv(self.S - 1, (len(rows),), torch.long, which="ret")
         self.booking[m] = prev
         self.inflight[m] = step
         self.steps_run += 1
+
+    # ------------------------------------------------------------------ hidden-state hop
+    def _hop_rows(self, T: int, is_decode: bool) -> int:
+        """Rows a hop of a T-token step carries: T, or with the graph hop the sender's batch
+        bucket when its step replays a graph (the send recorded in it moves the whole static
+        output)."""
+        if self.graph_hop:
+            return self.ex.graph_rows(T, is_decode) or T
+        return T
+
+    def _hop_send(self, dst: int, out: torch.Tensor) -> None:
+        if not self.graph_hop:
+            self.ch.send(dst, out)
+        elif self.ex.last_graphed:  # the send ran inside the replay
+            self.ch.count_send(self.ex.graph_rows(out.shape[0], True) * out.shape[1] * out.element_size())
+        else:  # eager steps: the same compute stream, so the communicator sees one op order
+            self.ch.send_on_stream(dst, out.contiguous())
 
     def _header(self, m: int, recs, closes: List[int], admitted: List[_Live]) -> np.ndarray:
         hdr = np.zeros(HDR + SEQ_REC * len(recs) + len(closes) + ADM_REC * len(admitted), dtype=np.int64)
@@ -620,14 +648,17 @@ class PipelineServingEngine:
             for c in closes:  # before the compute: a closed handle may be re-admitted in this very step
                 self.ex.sessions.close(self._key(int(c)))
             if n_seq:
-                _, waiter = self.ch.recv(self.rank - 1, (T, self.H), self.ex.dtype)
+                rows = self._hop_rows(T, bool((recs[:, 1] == 1).all()))
+                _, waiter = self.ch.recv(self.rank - 1, (rows, self.H), self.ex.dtype)
                 x = waiter()
+                if x is not None and rows != T:
+                    x = x[:T]
                 out = self._compute(recs.tolist(), x, m)
                 if self.is_tail:
                     tok = self._sample_tail(hdr, out)
                     self.ch.send(0, tok, which="ret")
                 else:
-                    self.ch.send(self.rank + 1, out)
+                    self._hop_send(self.rank + 1, out)
         self.steps_run += 1
         return True
 

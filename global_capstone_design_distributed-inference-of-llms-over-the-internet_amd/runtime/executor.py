@@ -183,6 +183,11 @@ class StageExecutor:
         self._graph_pool = None
         self._pinned = _Pinned(2 * max_tokens_per_step, 2 * max_tokens_per_step + max_sessions, self.device)
         self.last_step_ms: Optional[float] = None
+        # graph_hook(out): recorded at the END of every decode graph capture (the static output
+        # buffer), e.g. the stage hop's RCCL send (parallel/engine.py graph hop); last_graphed
+        # says whether the last step ran as a graph replay
+        self.graph_hook = None
+        self.last_graphed = False
         # MFMA flash attention for prefill steps (csrc/attention_mfma.hip); MPAMD_ATTN_MFMA=off disables
         self._attn_mfma_prefill = os.environ.get("MPAMD_ATTN_MFMA", "prefill") != "off" and \
             cfg.model_type != "gpt2" and cfg.head_dim in (64, 128)
@@ -432,8 +437,10 @@ class StageExecutor:
         if self.timing and self.device.type == "cuda":
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
+        self.last_graphed = False
         if prompt is None and self.use_graphs and plan.is_decode and plan.T <= self.graph_max_batch:
             out = self._run_graph(plan, x)
+            self.last_graphed = True
         elif self.cfg.model_type == "gpt2":
             out = self._forward_gpt2(plan, x, prompt=prompt)
         else:
@@ -899,6 +906,18 @@ class StageExecutor:
             self._graphs[key] = g
         return g.replay(plan, x)
 
+    def graph_rows(self, T: int, is_decode: bool) -> Optional[int]:
+        """Rows of the static output a step of ``T`` tokens would replay into (its batch bucket),
+        or None when the step runs eagerly (same rule as ``run``, no deep prompts)."""
+        if self.use_graphs and is_decode and T <= self.graph_max_batch:
+            return self._bucket(T)
+        return None
+
+    def set_graph_hook(self, fn) -> None:
+        """Record ``fn(out)`` at the end of every decode graph (captures made earlier are dropped)."""
+        self.graph_hook = fn
+        self.clear_graphs()
+
     def clear_graphs(self):
         self._graphs.clear()
 
@@ -948,6 +967,8 @@ class _DecodeGraph:
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph, pool=pool):
             self.out = ex._forward_llama(*args, decode=True)
+            if ex.graph_hook is not None:  # recorded only: the warm-up runs above never call it
+                ex.graph_hook(self.out)
 
     def replay(self, plan: Plan, x: torch.Tensor) -> torch.Tensor:
         b, B = plan.T, self.B

@@ -96,7 +96,24 @@ def _body(port, q):
         out["tp_graphs_on"] = outs[True][2] and outs[True][3] > 0
         out["tp_tokens_equal"] = outs[True][0] == outs[False][0]
         out["tp_logits_maxdiff"] = float((outs[True][1] - outs[False][1]).abs().max())
-        del ex, g
+        # a decode graph that ends with an RCCL send recorded by the executor's graph hook (the
+        # engine's graph hop): every replay moves the step's static output
+        w2 = random_stage_weights(cfg, 0, cfg.num_hidden_layers, has_embed=True, has_head=False, device="cuda",
+                                  seed=4)
+        ex2 = StageExecutor(cfg, w2, "cuda", kv_cache_bytes=64 << 20, max_sessions=8, max_seq_len=256)
+        sink = torch.zeros(16, cfg.hidden_size, dtype=torch.bfloat16, device="cuda")
+        ex2.set_graph_hook(lambda o: comm.send_recv(o, 0, sink[: o.shape[0]], 0))
+        ids = torch.arange(3 * 9, device="cuda") % cfg.vocab_size
+        ex2.forward([(f"g{i}", 9) for i in range(3)], ids)
+        hook_ok = []
+        for st in range(3):
+            hh = ex2.forward([(f"g{i}", 1) for i in range(3)], ids[st * 3:st * 3 + 3])
+            torch.cuda.synchronize()
+            hook_ok.append(bool(ex2.last_graphed) and bool(torch.equal(sink[:3], hh[:3])))
+        out["graph_hook"] = hook_ok
+        out["graph_rows"] = ex2.graph_rows(3, True)
+        _say("graph hook", hook_ok)
+        del ex, g, ex2
         import gc
 
         gc.collect()
@@ -141,3 +158,4 @@ def test_rccl_world1_capture_and_tp_graphs():
     # graph steps pad the batch to its bucket (the decode GEMMs may pick another row-tile form)
     assert out["tp_logits_maxdiff"] < 5e-2
     assert out["alive"] and out["aborted"]
+    assert out["graph_hook"] == [True, True, True] and out["graph_rows"] == 4

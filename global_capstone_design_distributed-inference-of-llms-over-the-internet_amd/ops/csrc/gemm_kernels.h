@@ -959,6 +959,21 @@ constexpr int rw_depth2() {
   }
 }
 
+// Start offset of the k walk per workgroup (MP_RW_ROT=1 ablation): every ring workgroup reads
+// the SAME activation block, in lock-step from k-slice 0 up; rotating each workgroup's walk by a
+// per-workgroup offset spreads the 256 concurrent A streams over the whole block (L2 channels)
+// instead of one moving 16 KB window.  A bijection on the slices: every slice is still summed
+// exactly once (the accumulation order per column group changes, deterministically).
+#ifndef MP_RW_ROT
+#define MP_RW_ROT 0
+#endif
+__device__ __forceinline__ int rw_rot(int k, int rot, int n) {
+  if constexpr (MP_RW_ROT == 0) return k;
+  const int r = k + rot;
+  return r >= n ? r - n : r;
+}
+__device__ __forceinline__ int rw_krot(int n) { return MP_RW_ROT ? (int)((blockIdx.x * 37u) % (unsigned)n) : 0; }
+
 template <int MT, int NT, int EPI, bool OPK, bool F8 = false>
 __device__ __forceinline__ void rw_body(const bf16_t* __restrict__ x, const bf16_t* __restrict__ wp,
                                         bf16_t* __restrict__ y, int64_t ys, const bf16_t* __restrict__ res, int64_t rs,
@@ -971,6 +986,7 @@ __device__ __forceinline__ void rw_body(const bf16_t* __restrict__ x, const bf16
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nks = K >> 5;
   const int cnt = (nks + RW_WAVES - 1) / RW_WAVES;  // ring steps of the busiest wave
+  const int krot = rw_krot(nks);
   // F8: the same fragment order at 1 byte per weight (offsets below count elements)
   using WT = std::conditional_t<F8, uint8_t, bf16_t>;
   using BT = std::conditional_t<F8, u32x2, u16x8>;
@@ -1003,7 +1019,7 @@ __device__ __forceinline__ void rw_body(const bf16_t* __restrict__ x, const bf16
   BT rb[R][NT];
 #define RW_LOAD(s, i)                                                                                        \
   {                                                                                                          \
-    const int k_ = min(wid + RW_WAVES * (i), nks - 1);                                                       \
+    const int k_ = rw_rot(min(wid + RW_WAVES * (i), nks - 1), krot, nks);                                  \
     _Pragma("unroll") for (int t = 0; t < NT; ++t) rb[s][t] =                                                \
         __builtin_nontemporal_load(reinterpret_cast<const BT*>(wb + (((int64_t)t * nks + k_) << 9)));       \
     _Pragma("unroll") for (int mt = 0; mt < MT; ++mt) ra[s][mt] =                                            \
@@ -1242,6 +1258,7 @@ __global__ __launch_bounds__(RW_WAVES * 64) void gemm_rwk_kernel(const bf16_t* _
   const int nks = K >> 5;
   const int ks0 = (int)((int64_t)sp * nks / S), ks1 = (int)((int64_t)(sp + 1) * nks / S);
   const int cnt = (ks1 - ks0 + RW_WAVES - 1) / RW_WAVES;
+  const int krot = rw_krot(ks1 - ks0);
   const WT* wb = reinterpret_cast<const WT*>(wp) + ((int64_t)tile0 * nks) * 512 + lane * 8;
   const bf16_t* xl = x + lane * 8;
   float wsc[NT];
@@ -1258,7 +1275,7 @@ __global__ __launch_bounds__(RW_WAVES * 64) void gemm_rwk_kernel(const bf16_t* _
   BT rb[R][NT];
 #define RWK_LOAD(s, i)                                                                                       \
   {                                                                                                          \
-    const int k_ = min(ks0 + wid + RW_WAVES * (i), ks1 - 1);                                                 \
+    const int k_ = ks0 + rw_rot(min(wid + RW_WAVES * (i), ks1 - ks0 - 1), krot, ks1 - ks0);                \
     _Pragma("unroll") for (int t = 0; t < NT; ++t) rb[s][t] =                                                \
         __builtin_nontemporal_load(reinterpret_cast<const BT*>(wb + (((int64_t)t * nks + k_) << 9)));       \
     _Pragma("unroll") for (int mt = 0; mt < MT; ++mt) ra[s][mt] =                                            \

@@ -191,6 +191,23 @@ __device__ __forceinline__ f32x4 mfma16(const u16x8& a, const u16x8& b, const f3
                                                   0, 0, 0);
 }
 
+// Start offset of the k walk per workgroup (MP_RW_ROT, default on): every decode GEMM workgroup reads
+// the SAME activation block, in lock-step from k-slice 0 up; rotating each workgroup's walk by a
+// per-workgroup offset spreads the 256 concurrent A streams over the whole block (L2 channels)
+// instead of one moving 16 KB window.  A bijection on the slices: every slice is still summed
+// exactly once (the accumulation order per column group changes, deterministically).
+// Measured (profiles/r3_r): 64 sessions 4.352 / 4.339 -> 4.327 / 4.325 ms, Llama-3-70B fp8 17.82 ->
+// 17.40 ms, alternating runs on one box.  -DMP_RW_ROT=0 builds the lock-step walk.
+#ifndef MP_RW_ROT
+#define MP_RW_ROT 1
+#endif
+__device__ __forceinline__ int rw_rot(int k, int rot, int n) {
+  if constexpr (MP_RW_ROT == 0) return k;
+  const int r = k + rot;
+  return r >= n ? r - n : r;
+}
+__device__ __forceinline__ int rw_krot(int n) { return MP_RW_ROT ? (int)((blockIdx.x * 37u) % (unsigned)n) : 0; }
+
 constexpr int GU_MAX = 4;  // k-slices (of 32) per wave group (x 16 B per lane per column tile)
 
 template <int MT, int NT, int EPI, bool APK, bool OPK>
@@ -257,13 +274,14 @@ __global__ __launch_bounds__(512) void gemm_packed_kernel(const bf16_t* __restri
   // A fragments of group g issued BEFORE the prefetch of group g+8: vmcnt retires loads in
   // issue order, so waiting for A leaves the weight prefetch in flight across the MFMAs.
   u16x8 b0[NT][GU], b1[NT][GU], a[MT][GU];
+  const int grot = rw_krot(ngroups);
 #define MP_LOAD_B(dst, grp)                                                                                   \
   _Pragma("unroll") for (int t = 0; t < NT; ++t) _Pragma("unroll") for (int u = 0; u < GU; ++u) dst[t][u] =    \
-      __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(wbase[t] + (int64_t)((grp) * GU + u) * 512));
+      __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(wbase[t] + (int64_t)(rw_rot(grp, grot, ngroups) * GU + u) * 512));
 #define MP_LOAD_A(grp)                                                                                        \
   _Pragma("unroll") for (int mt = 0; mt < MT; ++mt) _Pragma("unroll") for (int u = 0; u < GU; ++u) a[mt][u] =  \
-      (APK ? load_a_rows(xrow[mt] + (int64_t)((grp) * GU + u) * MT * 512, lane, mt * 16 + (lane & 15) < M)     \
-           : MP_LOAD_A_FRAG(xrow[mt] + (int64_t)((grp) * GU * 32 + 32 * u)));
+      (APK ? load_a_rows(xrow[mt] + (int64_t)(rw_rot(grp, grot, ngroups) * GU + u) * MT * 512, lane, mt * 16 + (lane & 15) < M) \
+           : MP_LOAD_A_FRAG(xrow[mt] + (int64_t)(rw_rot(grp, grot, ngroups) * GU * 32 + 32 * u)));
 #define MP_MMA(bb)                                                                                            \
   _Pragma("unroll") for (int mt = 0; mt < MT; ++mt) _Pragma("unroll") for (int u = 0; u < GU; ++u)            \
       _Pragma("unroll") for (int t = 0; t < NT; ++t) acc[mt][t] = mfma16(a[mt][u], bb[t][u], acc[mt][t]);
@@ -513,7 +531,8 @@ __global__ __launch_bounds__(512) void gemm_lds_kernel(const bf16_t* __restrict_
     for (int t = 0; t < NT; ++t) acc[mt][t] = (f32x4)(0.f);
 
   u16x8 st[FH], b0[NT][GU], b1[NT][GU], a[MT][GU];
-#define MP_GRP(it) min((it) * KS + ksp, ngroups - 1)
+  const int grot = rw_krot(ngroups);
+#define MP_GRP(it) rw_rot(min((it) * KS + ksp, ngroups - 1), grot, ngroups)
 #define MP_LDA(it)                                                                                            \
   _Pragma("unroll") for (int f = 0; f < FH; ++f) st[f] =                                                     \
       *reinterpret_cast<const u16x8*>(xl + ((int64_t)MP_GRP(it) * F + ch * FH + f) * 512);
@@ -958,21 +977,6 @@ constexpr int rw_depth2() {
     return rw_depth<MT, NT>();
   }
 }
-
-// Start offset of the k walk per workgroup (MP_RW_ROT=1 ablation): every ring workgroup reads
-// the SAME activation block, in lock-step from k-slice 0 up; rotating each workgroup's walk by a
-// per-workgroup offset spreads the 256 concurrent A streams over the whole block (L2 channels)
-// instead of one moving 16 KB window.  A bijection on the slices: every slice is still summed
-// exactly once (the accumulation order per column group changes, deterministically).
-#ifndef MP_RW_ROT
-#define MP_RW_ROT 0
-#endif
-__device__ __forceinline__ int rw_rot(int k, int rot, int n) {
-  if constexpr (MP_RW_ROT == 0) return k;
-  const int r = k + rot;
-  return r >= n ? r - n : r;
-}
-__device__ __forceinline__ int rw_krot(int n) { return MP_RW_ROT ? (int)((blockIdx.x * 37u) % (unsigned)n) : 0; }
 
 template <int MT, int NT, int EPI, bool OPK, bool F8 = false>
 __device__ __forceinline__ void rw_body(const bf16_t* __restrict__ x, const bf16_t* __restrict__ wp,

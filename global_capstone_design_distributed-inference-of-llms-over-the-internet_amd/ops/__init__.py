@@ -135,13 +135,24 @@ _SK_CHOICE = {}  # (m_bucket, N, K, epilogue) -> kernel name (see _KERNEL_FLAGS)
 _KERNEL_FLAGS = {"pk": 0, "sk": 4, "lds22": 16, "lds24": 16 | 32, "lds42": 16 | 96, "rw": 128, "rwk": 256,
                  "rwki": 256 | 512}
 _LDS_CFG = {"lds22": (2, 2), "lds24": (2, 4), "lds42": (4, 2)}
+# "<kernel>+r": the same kernel with every workgroup's k walk rotated (csrc/gemm_kernels.h
+# rw_krot, flags bit 10) - kept by the autotuners per shape only where it measures faster
+ROT_FLAG = 1024
+
+
+def _base(name: str) -> str:
+    return name[:-2] if name.endswith("+r") else name
+
+
+def _kflags(name: str) -> int:
+    return _KERNEL_FLAGS[_base(name)] | (ROT_FLAG if name.endswith("+r") else 0)
 
 
 def set_gemm_sk(mode: str) -> None:
     """"auto" (autotuned table), "on" / "off" (stream-K wherever it applies / never), or a kernel
     name from ``_KERNEL_FLAGS`` to force it wherever it applies."""
     global _GEMM_SK
-    assert mode in ("auto", "on", "off") or mode in _KERNEL_FLAGS
+    assert mode in ("auto", "on", "off") or _base(mode) in _KERNEL_FLAGS
     _GEMM_SK = mode
 
 
@@ -183,6 +194,7 @@ def _lds_covered(name: str, M: int, N: int, K: int, epilogue: int) -> bool:
 
 
 def _covered(name: str, M: int, N: int, K: int, epilogue: int) -> bool:
+    name = _base(name)
     if name == "pk":
         return True
     if name == "sk":
@@ -278,7 +290,26 @@ def autotune_gemm(shapes, device, ms=(4, 16, 32, 48, 64), iters: int = 24, round
                         t[mode] = min(t[mode], e0.elapsed_time(e1) / iters)
                 best = min(t, key=t.get)
                 # keep the one-group kernel unless another wins by > 3 % (timing noise guard)
-                _SK_CHOICE[(_m_bucket(M), N, K, int(epi))] = best if t[best] < 0.97 * t["pk"] else "pk"
+                best = best if t[best] < 0.97 * t["pk"] else "pk"
+                # then the same kernel with the rotated k walk, kept if it wins by > 1 %
+                tr = {best: float("inf"), best + "+r": float("inf")}
+                for _ in range(rounds):
+                    for mode in tr:
+                        _GEMM_SK = mode
+                        for i in range(2):
+                            linear(xp, None, out=out, epilogue=epi, residual=res, wp=wps[i % copies], a_rows=M,
+                                   out_packed=epi == 1, **extra)
+                        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                        e0.record()
+                        for i in range(iters):
+                            linear(xp, None, out=out, epilogue=epi, residual=res, wp=wps[i % copies], a_rows=M,
+                                   out_packed=epi == 1, **extra)
+                        e1.record()
+                        e1.synchronize()
+                        tr[mode] = min(tr[mode], e0.elapsed_time(e1) / iters)
+                if tr[best + "+r"] < 0.99 * tr[best]:
+                    best = best + "+r"
+                _SK_CHOICE[(_m_bucket(M), N, K, int(epi))] = best
     finally:
         _GEMM_SK = saved
         del pool
@@ -749,8 +780,8 @@ def linear(x, w, out=None, epilogue=0, residual=None, policy=None, wp=None, a_ro
                              and os.environ.get("MPAMD_WIDE_SPLITK", "1") != "0") else "rw"
         else:
             kern = _kernel_for(M, N, K, epilogue)
-        flags = 1 | (2 if out_packed else 0) | _KERNEL_FLAGS[kern]
-        ws = gemm_workspace(x.device) if kern in ("sk", "rwk", "rwki") else None
+        flags = 1 | (2 if out_packed else 0) | _kflags(kern)
+        ws = gemm_workspace(x.device) if _base(kern) in ("sk", "rwk", "rwki") else None
         torch.ops.mpamd.gemm(x, wp, out, residual, int(epilogue), M, flags, ws, gate, ap_out, ss_out, ss_zero, ss_in,
                              1.0 / K, float(eps))
         return out
@@ -942,7 +973,9 @@ _W8_MODE = os.environ.get("MPAMD_W8_KERNEL", "auto")
 def _w8_kernel(M: int, N: int, K: int, epilogue: int) -> str:
     rwk_ok = epilogue != 1 and N % 2048 == 0
     mode = _W8_MODE if _W8_MODE != "auto" else _W8_CHOICE.get((_m_bucket(M), N, K, int(epilogue)), "rw")
-    return mode if (mode in ("rwk", "rwki") and rwk_ok) else "rw"
+    if _base(mode) in ("rwk", "rwki") and rwk_ok:
+        return mode
+    return "rw+r" if mode.endswith("+r") else "rw"
 
 
 def linear_w8(x, w8, w_scale, a_rows: int, out=None, epilogue: int = 0, residual=None, out_packed: bool = False,
@@ -961,9 +994,9 @@ def linear_w8(x, w8, w_scale, a_rows: int, out=None, epilogue: int = 0, residual
         out = (torch.empty(packed_numel(M, ncols), dtype=x.dtype, device=x.device) if out_packed
                else torch.empty(M, ncols, dtype=x.dtype, device=x.device))
     kern = _w8_kernel(M, N, K, epilogue)
-    flags = 1 | (2 if out_packed else 0) | _W8_KERNELS[kern]
+    flags = 1 | (2 if out_packed else 0) | _W8_KERNELS[_base(kern)] | (ROT_FLAG if kern.endswith("+r") else 0)
     torch.ops.mpamd.gemm_w8(x, w8, w_scale, out, residual, int(epilogue), M, flags,
-                            gemm_workspace(x.device) if kern in ("rwk", "rwki") else None, ap_out, ss_out, ss_zero, ss_in,
+                            gemm_workspace(x.device) if _base(kern) in ("rwk", "rwki") else None, ap_out, ss_out, ss_zero, ss_in,
                             1.0 / K, float(eps))
     return out
 
@@ -983,10 +1016,9 @@ def autotune_w8(shapes, device, ms=(4, 16, 32, 48, 64), iters: int = 12, rounds:
             todo = [M for M in ms if (_m_bucket(M), N, K, int(epi)) not in _W8_CHOICE]
             if not todo:
                 continue
-            if epi == 1 or N % 2048:
-                for M in todo:
-                    _W8_CHOICE[(_m_bucket(M), N, K, int(epi))] = "rw"
-                continue
+            # the ring form only (SwiGLU / narrow N) or all three, each also with the rotated k walk
+            names = ["rw"] if (epi == 1 or N % 2048) else list(_W8_KERNELS)
+            names = names + [n + "+r" for n in names]
             copies = max(1, min(8, (1 << 30) // (N * K)))
             wqs = [torch.randint(0, 0x77, (N // 16, K // 32, 64, 8), dtype=torch.uint8, device=device)
                    for _ in range(copies)]
@@ -998,21 +1030,28 @@ def autotune_w8(shapes, device, ms=(4, 16, 32, 48, 64), iters: int = 12, rounds:
                 if epi == 3:
                     extra = dict(ap_out=torch.zeros(packed_numel(M, N), dtype=torch.bfloat16, device=device),
                                  ss_out=norm_stats_buffer(device)[0], ss_zero=norm_stats_buffer(device)[0])
-                out = res if epi == 3 else torch.empty(M, N, dtype=torch.bfloat16, device=device)
-                t = {k: float("inf") for k in _W8_KERNELS}
+                ncols = N // 2 if epi == 1 else N
+                out = res if epi == 3 else (
+                    torch.empty(packed_numel(M, ncols), dtype=torch.bfloat16, device=device) if epi == 1
+                    else torch.empty(M, N, dtype=torch.bfloat16, device=device))
+                t = {k: float("inf") for k in names}
                 for _ in range(rounds):
-                    for name in _W8_KERNELS:
+                    for name in names:
                         _W8_MODE = name
                         for i in range(2):
-                            linear_w8(xp, wqs[i % copies], wsc, M, out=out, epilogue=epi, residual=res, **extra)
+                            linear_w8(xp, wqs[i % copies], wsc, M, out=out, epilogue=epi, residual=res,
+                                      out_packed=epi == 1, **extra)
                         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                         e0.record()
                         for i in range(iters):
-                            linear_w8(xp, wqs[i % copies], wsc, M, out=out, epilogue=epi, residual=res, **extra)
+                            linear_w8(xp, wqs[i % copies], wsc, M, out=out, epilogue=epi, residual=res,
+                                      out_packed=epi == 1, **extra)
                         e1.record()
                         e1.synchronize()
                         t[name] = min(t[name], e0.elapsed_time(e1) / iters)
-                _W8_CHOICE[(_m_bucket(M), N, K, int(epi))] = min(t, key=t.get)
+                best = min(t, key=t.get)
+                plain = _base(best)  # the rotated walk only where it wins by > 1 %
+                _W8_CHOICE[(_m_bucket(M), N, K, int(epi))] = best if t[best] < 0.99 * t[plain] else plain
             del wqs
     finally:
         _W8_MODE = saved

@@ -48,7 +48,8 @@ extern "C" int64_t mp_gemm_workspace_bytes() {
 //        used by one stream at a time); bit 3 = force the one-group-per-workgroup kernel;
 //        bit 4 = shared-A (LDS-staged activation) kernel when the shape allows it;
 //        bit 7 = balanced ring kernel; bit 8 = split-K ring kernel + reduce launch (epilogue
-//        0 / 2 / 3, needs ws); bits 8 + 9 = split-K ring kernel with the in-launch combine.
+//        0 / 2 / 3, needs ws); bits 8 + 9 = split-K ring kernel with the in-launch combine;
+//        bit 10 = rotated k walk per workgroup (EpiArgs::rot).
 //        epilogue 3 / ss_in: the fused-norm decode path (EpiArgs above; ap / ss_out / ss_zero /
 //        ss_in may be null when unused).
 extern "C" int mp_gemm_bf16(const void* x, int64_t x_stride, const void* w, void* y, int64_t y_stride,
@@ -58,7 +59,8 @@ extern "C" int mp_gemm_bf16(const void* x, int64_t x_stride, const void* w, void
   using namespace mp;
   if (M == 0) return 0;
   if (epilogue == 3 && (ap == nullptr || res == nullptr)) return -5;
-  const EpiArgs ep{(bf16_t*)ap, (u64*)ss_out, (u64*)ss_zero, (const u64*)ss_in, inv_k, eps, (M + 15) / 16};
+  EpiArgs ep{(bf16_t*)ap, (u64*)ss_out, (u64*)ss_zero, (const u64*)ss_in, inv_k, eps, (M + 15) / 16};
+  ep.rot = (flags >> 10) & 1;
   if (M > 128 || K % (32 * GU_MAX) || N % 16 || ((flags & 1) == 0 && x_stride % 8)) return -1;
   int rc;
   if (M > 64) {  // 65..128 rows: gemm_wide.hip (split-K ring / balanced ring, packed A, no gate)

@@ -83,6 +83,7 @@ struct EpiArgs {
   float eps;
   int mt_out;
   const float* wsc;    // fp8 weights (W8A16 kernels): per-output-column dequantization scales
+  int rot = 0;         // rotate each workgroup's k walk (rw_krot; flags bit 10, chosen per shape)
 };
 
 // fp8 (OCP e4m3) weight fragment -> bf16 MFMA B operand (exact: every e4m3 value is a bf16
@@ -196,8 +197,10 @@ __device__ __forceinline__ f32x4 mfma16(const u16x8& a, const u16x8& b, const f3
 // per-workgroup offset spreads the 256 concurrent A streams over the whole block (L2 channels)
 // instead of one moving 16 KB window.  A bijection on the slices: every slice is still summed
 // exactly once (the accumulation order per column group changes, deterministically).
-// Measured (profiles/r3_r): 64 sessions 4.352 / 4.339 -> 4.327 / 4.325 ms, Llama-3-70B fp8 17.82 ->
-// 17.40 ms, alternating runs on one box.  -DMP_RW_ROT=0 builds the lock-step walk.
+// Per launch (EpiArgs::rot, flags bit 10) and chosen per shape by the start-up autotuners: it
+// helped the Llama-2-7B and 70B fp8 shapes (profiles/r3_r, r3_s: 64 sessions 4.36 -> 4.32 ms, 70B
+// 17.8 -> 17.3-17.4) and cost 2.4 % on Llama-3-8B's (r3_t), whose lock-step readers share L2 lines
+// that a spread-out walk lets the weight stream evict.  -DMP_RW_ROT=0 compiles it out.
 #ifndef MP_RW_ROT
 #define MP_RW_ROT 1
 #endif
@@ -206,7 +209,9 @@ __device__ __forceinline__ int rw_rot(int k, int rot, int n) {
   const int r = k + rot;
   return r >= n ? r - n : r;
 }
-__device__ __forceinline__ int rw_krot(int n) { return MP_RW_ROT ? (int)((blockIdx.x * 37u) % (unsigned)n) : 0; }
+__device__ __forceinline__ int rw_krot(int n, int on) {
+  return (MP_RW_ROT && on) ? (int)((blockIdx.x * 37u) % (unsigned)n) : 0;
+}
 
 constexpr int GU_MAX = 4;  // k-slices (of 32) per wave group (x 16 B per lane per column tile)
 
@@ -274,7 +279,7 @@ __global__ __launch_bounds__(512) void gemm_packed_kernel(const bf16_t* __restri
   // A fragments of group g issued BEFORE the prefetch of group g+8: vmcnt retires loads in
   // issue order, so waiting for A leaves the weight prefetch in flight across the MFMAs.
   u16x8 b0[NT][GU], b1[NT][GU], a[MT][GU];
-  const int grot = rw_krot(ngroups);
+  const int grot = rw_krot(ngroups, ep.rot);
 #define MP_LOAD_B(dst, grp)                                                                                   \
   _Pragma("unroll") for (int t = 0; t < NT; ++t) _Pragma("unroll") for (int u = 0; u < GU; ++u) dst[t][u] =    \
       __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(wbase[t] + (int64_t)(rw_rot(grp, grot, ngroups) * GU + u) * 512));
@@ -531,7 +536,7 @@ __global__ __launch_bounds__(512) void gemm_lds_kernel(const bf16_t* __restrict_
     for (int t = 0; t < NT; ++t) acc[mt][t] = (f32x4)(0.f);
 
   u16x8 st[FH], b0[NT][GU], b1[NT][GU], a[MT][GU];
-  const int grot = rw_krot(ngroups);
+  const int grot = rw_krot(ngroups, ep.rot);
 #define MP_GRP(it) rw_rot(min((it) * KS + ksp, ngroups - 1), grot, ngroups)
 #define MP_LDA(it)                                                                                            \
   _Pragma("unroll") for (int f = 0; f < FH; ++f) st[f] =                                                     \
@@ -957,8 +962,15 @@ constexpr int RW_QC = 128 / RW_WAVES;  // quads per LDS combine pass (waves x RW
 // clamped tail turn); 4 (MT + NT) VGPRs each (one wave per SIMD: the accumulators go to AGPRs).
 // Measured at M = 64 (lab, us): qkv depth 2 / 4 / 6 = 21.2 / 21.7 / 22.7, gate/up 35.1 / 35.3 /
 // 35.4, o 14.3 / 13.7 / 14.1: two slots of 4 waves already cover the latency where tiles are wide.
+// MP_RW_DEEP1: 8 slots for the narrowest forms (one row tile, one column tile: the batch-1 o
+// projection, 256 workgroups of 128 KB of weights each), whose 4 waves x 4 slots keep only
+// ~32 KB per CU in flight.
+#ifndef MP_RW_DEEP1
+#define MP_RW_DEEP1 0
+#endif
 template <int MT, int NT>
 constexpr int rw_depth() {
+  if (MP_RW_DEEP1 && MT + NT <= 2) return 8;
   return 190 / (4 * (MT + NT)) >= 8 ? 4 : 2;
 }
 // fp8 weights: a slot is 4 MT + 2 NT VGPRs.  The 8-column split-K forms of the 70B shapes
@@ -990,7 +1002,7 @@ __device__ __forceinline__ void rw_body(const bf16_t* __restrict__ x, const bf16
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nks = K >> 5;
   const int cnt = (nks + RW_WAVES - 1) / RW_WAVES;  // ring steps of the busiest wave
-  const int krot = rw_krot(nks);
+  const int krot = rw_krot(nks, ep.rot);
   // F8: the same fragment order at 1 byte per weight (offsets below count elements)
   using WT = std::conditional_t<F8, uint8_t, bf16_t>;
   using BT = std::conditional_t<F8, u32x2, u16x8>;
@@ -1262,7 +1274,7 @@ __global__ __launch_bounds__(RW_WAVES * 64) void gemm_rwk_kernel(const bf16_t* _
   const int nks = K >> 5;
   const int ks0 = (int)((int64_t)sp * nks / S), ks1 = (int)((int64_t)(sp + 1) * nks / S);
   const int cnt = (ks1 - ks0 + RW_WAVES - 1) / RW_WAVES;
-  const int krot = rw_krot(ks1 - ks0);
+  const int krot = rw_krot(ks1 - ks0, ep.rot);
   const WT* wb = reinterpret_cast<const WT*>(wp) + ((int64_t)tile0 * nks) * 512 + lane * 8;
   const bf16_t* xl = x + lane * 8;
   float wsc[NT];

@@ -17,6 +17,7 @@ extern "C" int mp_gemm_w8(const void* x, const void* wq, const float* wsc, void*
   if (epilogue == 3 && (ap == nullptr || res == nullptr)) return -5;
   EpiArgs ep{(bf16_t*)ap, (u64*)ss_out, (u64*)ss_zero, (const u64*)ss_in, inv_k, eps, (M + 15) / 16};
   ep.wsc = wsc;
+  ep.rot = (flags >> 10) & 1;
   int rc = 1;
   if ((flags & 256) && !(flags & 2) && ws != nullptr) {
     switch ((M + 15) / 16) {

@@ -234,7 +234,8 @@ def test_gemm_stream_k(M, N, K, sk):
     assert int(ops.gemm_workspace(DEV)[:4 * 4096].view(torch.int32).abs().sum()) == 0  # counters re-zeroed
 
 
-@pytest.mark.parametrize("kern", ["lds22", "lds24", "lds42", "rw", "rwk", "rwki"])
+@pytest.mark.parametrize("kern", ["lds22", "lds24", "lds42", "rw", "rwk", "rwki", "pk+r", "lds24+r", "rw+r", "rwk+r",
+                                  "rwki+r"])
 @pytest.mark.parametrize("M", [1, 16, 20, 40, 64])
 @pytest.mark.parametrize("N,K,epi", [(4096, 4096, 0), (12288, 4096, 2), (4096, 11008, 0), (22016, 4096, 1),
                                      (32000, 4096, 0), (1024, 1024, 1)])
@@ -268,9 +269,10 @@ def test_gemm_shared_a(kern, M, N, K, epi):
     elif epi == 2:
         yr = yr + r.float()
     torch.testing.assert_close(y1.float(), yr, atol=4e-2, rtol=3e-2)
-    if M == 64 and N in (22016, 32000) and kern not in ("rwk", "rwki"):
+    base = ops._base(kern)
+    if M == 64 and N in (22016, 32000) and base not in ("rwk", "rwki", "pk"):
         assert applies  # the kernel itself ran (not the fallback)
-    if kern in ("rwk", "rwki") and N % 2048 == 0 and epi != 1:
+    if base in ("rwk", "rwki") and N % 2048 == 0 and epi != 1:
         assert applies
 
 
@@ -434,7 +436,7 @@ def test_fp8_gemm_kernel_matches_reference(kern, M, N, K, epi):
         ops.set_fp8_kernel("auto")
 
 
-@pytest.mark.parametrize("kern", ["rw", "rwk", "rwki"])
+@pytest.mark.parametrize("kern", ["rw", "rwk", "rwki", "rw+r", "rwk+r"])
 @pytest.mark.parametrize("M", [1, 30, 64])
 @pytest.mark.parametrize("N,K,epi", [(1024, 1024, 0), (10240, 8192, 0), (8192, 8192, 3), (8192, 28672, 3),
                                      (2048, 4096, 1), (57344, 512, 1), (4096, 1024, 0)])
@@ -716,7 +718,7 @@ def test_autotune_weight_larger_than_pool(monkeypatch):
     key = (64, N, K, 0)
     ops._SK_CHOICE.pop(key, None)
     table = ops.autotune_gemm([(N, K, 0)], DEV, ms=(64,), iters=2, rounds=1)
-    assert ops._SK_CHOICE.get(key) in (set(ops._KERNEL_FLAGS) | {"pk"}), table
+    assert ops._base(ops._SK_CHOICE.get(key)) in (set(ops._KERNEL_FLAGS) | {"pk"}), table
     ops._SK_CHOICE.pop(key, None)
 
 

@@ -962,11 +962,11 @@ constexpr int RW_QC = 128 / RW_WAVES;  // quads per LDS combine pass (waves x RW
 // clamped tail turn); 4 (MT + NT) VGPRs each (one wave per SIMD: the accumulators go to AGPRs).
 // Measured at M = 64 (lab, us): qkv depth 2 / 4 / 6 = 21.2 / 21.7 / 22.7, gate/up 35.1 / 35.3 /
 // 35.4, o 14.3 / 13.7 / 14.1: two slots of 4 waves already cover the latency where tiles are wide.
-// MP_RW_DEEP1: 8 slots for the narrowest forms (one row tile, one column tile: the batch-1 o
-// projection, 256 workgroups of 128 KB of weights each), whose 4 waves x 4 slots keep only
-// ~32 KB per CU in flight.
+// MP_RW_DEEP1 (default on): 8 slots for the narrowest forms (one row tile, one column tile: the
+// batch-1 o projection, 256 workgroups of 128 KB of weights each), whose 4 waves x 4 slots keep
+// only ~32 KB per CU in flight (batch 1: 2.809 -> 2.789 ms, profiles/r3_u).
 #ifndef MP_RW_DEEP1
-#define MP_RW_DEEP1 0
+#define MP_RW_DEEP1 1
 #endif
 template <int MT, int NT>
 constexpr int rw_depth() {

@@ -140,6 +140,10 @@ _LDS_CFG = {"lds22": (2, 2), "lds24": (2, 4), "lds42": (4, 2)}
 ROT_FLAG = 1024
 
 
+# 65..128-row steps (not autotuned): rotated k walk (MPAMD_WIDE_ROT=1) or the lock-step one
+_WIDE_ROT = os.environ.get("MPAMD_WIDE_ROT", "0") == "1"
+
+
 def _base(name: str) -> str:
     return name[:-2] if name.endswith("+r") else name
 
@@ -778,6 +782,8 @@ def linear(x, w, out=None, epilogue=0, residual=None, policy=None, wp=None, a_ro
         elif M > 64:  # 65..128 rows: split-K ring where it applies (o, down), else the ring kernel
             kern = "rwk" if (not out_packed and _covered("rwk", M, N, K, epilogue)
                              and os.environ.get("MPAMD_WIDE_SPLITK", "1") != "0") else "rw"
+            if _WIDE_ROT:
+                kern += "+r"
         else:
             kern = _kernel_for(M, N, K, epilogue)
         flags = 1 | (2 if out_packed else 0) | _kflags(kern)

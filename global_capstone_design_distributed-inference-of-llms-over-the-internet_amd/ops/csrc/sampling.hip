@@ -22,6 +22,7 @@
 // updated in place by the same kernel (``update`` flag), so the serving loop needs no extra
 // device ops per token.
 #include "common.h"
+#include <stdlib.h>
 
 namespace mp {
 
@@ -32,6 +33,7 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
   return x ^ (x >> 31);
 }
 
+typedef unsigned long long u64;
 constexpr int SB = 1024;   // threads per block
 constexpr int CAND = 1024;  // top-k candidate capacity of the fast path
 
@@ -85,7 +87,8 @@ __global__ __launch_bounds__(SB) void sample_kernel(const bf16_t* __restrict__ l
                                                     int32_t* __restrict__ recent, int recent_stride,
                                                     int32_t* __restrict__ recent_len,
                                                     const int64_t* __restrict__ seeds, float* __restrict__ ws,
-                                                    int64_t* __restrict__ out, int use_lds, int update) {
+                                                    int64_t* __restrict__ out, int use_lds, int update,
+                                                    int only_unset) {
   __shared__ float red[SB / 64 + 1];
   __shared__ unsigned hist[256];
   __shared__ float mass[256];
@@ -93,6 +96,7 @@ __global__ __launch_bounds__(SB) void sample_kernel(const bf16_t* __restrict__ l
   __shared__ int s_i[2];
   extern __shared__ __attribute__((aligned(16))) float s_row[];
   const int row = blockIdx.x, tid = threadIdx.x;
+  if (only_unset && out[row] >= 0) return;  // the split sampler already drew this row
   const bf16_t* lrow = logits + (int64_t)row * stride;
   // the working row lives in LDS when it fits (V <= 38K: every pass is an LDS sweep),
   // otherwise in the global workspace (L2-resident)
@@ -471,6 +475,371 @@ __global__ __launch_bounds__(SB) void sample_kernel(const bf16_t* __restrict__ l
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Split sampler: the rows' top-k path over CH-element chunks of the vocabulary, one 256-thread
+// workgroup per (chunk, row) - a 128K vocabulary does not fit one workgroup's LDS, and a single
+// 1024-thread workgroup per row left the 1K-64K-wide sweeps, ~40 barriers and one memory round
+// trip per row on ~R CUs (Llama-3 vocab: 128 us per 64-row step).  Same semantics as the fast
+// top-k path above: the union of the chunks' exact top-k sets holds the row's top-k set, the
+// merge orders it by (value desc, index asc) - the single workgroup's tie order - and the
+// probabilities are full-softmax ones from the chunk maxima / normalisers.  Rows the split
+// cannot take (k <= 0, k > SPLIT_KMAX, more than SPLIT_CAND candidates at a chunk's k-th
+// value) are left at -1 for sample_kernel(only_unset = 1).
+constexpr int SPLIT_CH = 8192;     // chunk width (fp32 in LDS: 32 KiB)
+constexpr int SPLIT_NT = 256;      // threads per chunk workgroup
+constexpr int SPLIT_KMAX = 64;     // largest top-k the split path takes
+constexpr int SPLIT_CAND = 512;    // candidates per chunk before the exact rank
+constexpr int SPLIT_MAXC = 64;     // chunks per row (one merge lane each): V <= 512K
+// per (row, chunk) record in the workspace: [0] max of the penalised logits, [1] sum exp((x - max)
+// / T), [2] raw max (greedy), [3] raw argmax, [4] candidate count (-1: degenerate), then
+// SPLIT_KMAX (key, index) pairs sorted by (value desc, index asc)
+constexpr int SPLIT_REC = 8 + 2 * SPLIT_KMAX;
+
+template <int CTRL>
+__device__ __forceinline__ u64 dpp_u64(u64 v) {
+  const int lo = __builtin_amdgcn_mov_dpp((int)(unsigned)v, CTRL, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(unsigned)(v >> 32), CTRL, 0xF, 0xF, true);
+  return ((u64)(unsigned)hi << 32) | (unsigned)lo;
+}
+__device__ __forceinline__ u64 max_u64(u64 a, u64 b) { return a > b ? a : b; }
+
+__device__ __forceinline__ float okey_inv(unsigned k) {
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+
+__global__ __launch_bounds__(SPLIT_NT) void sample_split_chunk_kernel(
+    const bf16_t* __restrict__ logits, int64_t stride, int V, const float* __restrict__ temps,
+    const int32_t* __restrict__ top_ks, const float* __restrict__ rep_pens, const int32_t* __restrict__ recent,
+    int recent_stride, const int32_t* __restrict__ recent_len, float* __restrict__ ws) {
+  __shared__ float x[SPLIT_CH];
+  __shared__ float red[SPLIT_NT / 64 + 1];
+  __shared__ unsigned hist[256];
+  __shared__ unsigned c_key[SPLIT_CAND];
+  __shared__ int c_idx[SPLIT_CAND];
+  __shared__ int s_cnt, s_sel, s_kk;
+  __shared__ float s_rmax[SPLIT_NT / 64];
+  __shared__ int s_ridx[SPLIT_NT / 64];
+  const int c = blockIdx.x, row = blockIdx.y, tid = threadIdx.x, C = gridDim.x;
+  const int lo = c * SPLIT_CH, n = min(SPLIT_CH, V - lo);
+  float* rec = ws + ((int64_t)row * C + c) * SPLIT_REC;
+  const bf16_t* lrow = logits + (int64_t)row * stride + lo;
+  // raw copy + raw max / first argmax (greedy rows take the argmax of the raw logits): 16-B loads,
+  // all of a thread's (SPLIT_CH / SPLIT_NT / 8 = 4) issued before the first use
+  float rmx = -INFINITY;
+  int rmi = 0x7fffffff;
+  if ((n & 7) == 0 && (stride & 7) == 0) {
+    constexpr int NV = SPLIT_CH / SPLIT_NT / 8;
+    u16x8 v[NV];
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+      const int i0 = (u * SPLIT_NT + tid) * 8;
+      v[u] = i0 < n ? *reinterpret_cast<const u16x8*>(lrow + i0) : (u16x8)(0);
+    }
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+      const int i0 = (u * SPLIT_NT + tid) * 8;
+      if (i0 < n) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float f = bf2f(v[u][j]);
+          x[i0 + j] = f;
+          if (f > rmx) { rmx = f; rmi = lo + i0 + j; }
+        }
+      }
+    }
+  } else {
+    for (int i = tid; i < n; i += SPLIT_NT) {
+      const float f = bf2f(lrow[i]);
+      x[i] = f;
+      if (f > rmx) { rmx = f; rmi = lo + i; }
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(rmx, o, 64);
+    const int oi = __shfl_xor(rmi, o, 64);
+    if (ov > rmx || (ov == rmx && oi < rmi)) { rmx = ov; rmi = oi; }
+  }
+  if ((tid & 63) == 0) { s_rmax[tid >> 6] = rmx; s_ridx[tid >> 6] = rmi; }
+  __syncthreads();
+  const float temp = temps[row];
+  const int k = top_ks[row];
+  if (tid == 0) {
+    float b = s_rmax[0];
+    int ix = s_ridx[0];
+    for (int w = 1; w < SPLIT_NT / 64; ++w)
+      if (s_rmax[w] > b || (s_rmax[w] == b && s_ridx[w] < ix)) { b = s_rmax[w]; ix = s_ridx[w]; }
+    rec[2] = b;
+    rec[3] = __int_as_float(ix);
+    if (temp <= 0.f || k <= 0 || k > SPLIT_KMAX || k >= V) rec[4] = __int_as_float(-1);
+  }
+  if (temp <= 0.f || k <= 0 || k > SPLIT_KMAX || k >= V) return;  // greedy / not a split row
+
+  // repetition penalty (reference src/rpc_handler.py:345-374) on the ids of this chunk
+  const float rp = rep_pens[row];
+  const int nrec = min((int)recent_len[row], recent_stride);
+  const int32_t* hrow = recent + (int64_t)row * recent_stride;
+  if (rp != 1.f && nrec > 0) {
+    if (tid < nrec) {
+      const int tok = hrow[tid];
+      bool first = true;
+      int count = 0;
+      for (int j = 0; j < nrec; ++j) {
+        const int h = hrow[j];
+        if (h == tok) {
+          ++count;
+          if (j < tid) first = false;
+        }
+      }
+      if (first && tok >= lo && tok < lo + n) {
+        const float pen = powf(rp, (float)count);
+        const float v = x[tok - lo];
+        x[tok - lo] = v > 0.f ? v / pen : v * pen;
+      }
+    }
+    __syncthreads();
+    if (tid == 0 && nrec >= 3) {
+      const int a = hrow[nrec - 1];
+      if (hrow[nrec - 2] == a && hrow[nrec - 3] == a && a >= lo && a < lo + n) {
+        const float pen = rp * rp * rp;
+        const float v = x[a - lo];
+        x[a - lo] = v > 0.f ? v / pen : v * pen;
+      }
+    }
+    __syncthreads();
+  }
+  // chunk max and normaliser; per-thread key maxima
+  const float inv_t = 1.f / fmaxf(temp, 1e-5f);
+  float lm = -INFINITY;
+  unsigned tmax = 0u;
+  for (int i = tid; i < n; i += SPLIT_NT) {
+    lm = fmaxf(lm, x[i]);
+    tmax = max(tmax, okey(x[i]));
+  }
+  const float m = block_max(lm, red);
+  float ls = 0.f;
+  for (int i = tid; i < n; i += SPLIT_NT) ls += __expf((x[i] - m) * inv_t);
+  const float zs = block_sum(ls, red);
+  // tau = the kk-th largest of the per-thread key maxima (<= the chunk's kk-th largest value),
+  // by 8-bit radix rounds: wave 0 finds the bin holding it from the top
+  const int kc = min(k, n);
+  const int nmax = min(SPLIT_NT, n);  // threads that saw at least one element
+  unsigned prefix = 0u, msk = 0u;
+  int kk = min(kc, nmax);
+  for (int shift = 24; shift >= 0; shift -= 8) {
+    for (int i = tid; i < 256; i += SPLIT_NT) hist[i] = 0u;
+    __syncthreads();
+    if (tid < nmax && (tmax & msk) == prefix) atomicAdd(&hist[(tmax >> shift) & 255u], 1u);
+    __syncthreads();
+    if (tid < 64) {
+      const int l = tid;
+      const unsigned h0 = hist[4 * l], h1 = hist[4 * l + 1], h2 = hist[4 * l + 2], h3 = hist[4 * l + 3];
+      const int own = (int)(h0 + h1 + h2 + h3);
+      int incl = own;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int nb = __shfl_down(incl, o, 64);
+        if (l + o < 64) incl += nb;
+      }
+      const unsigned long long hit = __ballot(incl >= kk);
+      const int cl = hit ? 63 - __builtin_clzll(hit) : 0;
+      if (l == cl) {
+        int cum = incl - own;
+        int sel = 4 * l;
+        const unsigned hb[4] = {h3, h2, h1, h0};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (cum + (int)hb[j] >= kk) { sel = 4 * l + 3 - j; break; }
+          cum += hb[j];
+        }
+        s_sel = sel;
+        s_kk = kk - cum;
+      }
+    }
+    __syncthreads();
+    prefix |= (unsigned)s_sel << shift;
+    msk |= 255u << shift;
+    kk = s_kk;
+    __syncthreads();
+  }
+  const unsigned tau = prefix;
+  if (tid == 0) s_cnt = 0;
+  __syncthreads();
+  for (int i = tid; i < n; i += SPLIT_NT) {
+    const unsigned key = okey(x[i]);
+    if (key >= tau) {
+      const int pos = atomicAdd(&s_cnt, 1);
+      if (pos < SPLIT_CAND) {
+        c_key[pos] = key;
+        c_idx[pos] = lo + i;
+      }
+    }
+  }
+  __syncthreads();
+  const int cnt = s_cnt;
+  if (tid == 0) {
+    rec[0] = m;
+    rec[1] = zs;
+    rec[4] = __int_as_float(cnt > SPLIT_CAND ? -1 : min(cnt, kc));
+  }
+  if (cnt > SPLIT_CAND) return;  // degenerate chunk: the row goes to the single-workgroup kernel
+  for (int t = tid; t < cnt; t += SPLIT_NT) {  // exact rank by (value desc, index asc)
+    const unsigned kt = c_key[t];
+    const int it = c_idx[t];
+    int rank = 0;
+    for (int j = 0; j < cnt; ++j) {
+      const unsigned kj = c_key[j];
+      rank += (kj > kt) || (kj == kt && c_idx[j] < it);
+    }
+    if (rank < kc) {
+      rec[8 + 2 * rank] = __uint_as_float(kt);
+      rec[9 + 2 * rank] = __int_as_float(it);
+    }
+  }
+}
+
+// One 64-lane wave per row: lane l walks chunk l's sorted top-k list; k rounds of a wave-wide
+// (key desc, index asc) argmax merge them into the row's sorted top-k; then the full-softmax
+// probabilities, top-p (keep the sorted prefix with cumulative <= p, always the first), one
+// inverse-CDF draw with the row's seeded uniform - the fast path's arithmetic.
+__global__ __launch_bounds__(64) void sample_split_merge_kernel(
+    int V, int C, const float* __restrict__ temps, const float* __restrict__ top_ps, const int32_t* __restrict__ top_ks,
+    int32_t* __restrict__ recent, int recent_stride, int32_t* __restrict__ recent_len,
+    const int64_t* __restrict__ seeds, const float* __restrict__ ws, int64_t* __restrict__ out, int update) {
+  __shared__ unsigned s_key[SPLIT_KMAX];
+  __shared__ int s_idx[SPLIT_KMAX];
+  __shared__ unsigned l_key[SPLIT_MAXC][SPLIT_KMAX];  // the chunks' sorted lists, staged once
+  __shared__ int l_idx[SPLIT_MAXC][SPLIT_KMAX];
+  const int row = blockIdx.x, l = threadIdx.x;
+  const float* base = ws + (int64_t)row * C * SPLIT_REC;
+  const float temp = temps[row];
+  const int k = top_ks[row];
+  if (temp <= 0.f) {  // greedy: first maximum of the raw logits over the chunks
+    if (l == 0) {
+      float b = -INFINITY;
+      int ix = 0x7fffffff;
+      for (int c = 0; c < C; ++c) {
+        const float v = base[c * SPLIT_REC + 2];
+        const int i = __float_as_int(base[c * SPLIT_REC + 3]);
+        if (v > b || (v == b && i < ix)) { b = v; ix = i; }
+      }
+      const int pick = ix == 0x7fffffff ? 0 : ix;
+      out[row] = pick;
+      if (update) push_history(recent + (int64_t)row * recent_stride, recent_len + row, recent_stride, pick);
+    }
+    return;
+  }
+  // any chunk unable to take the row (or k outside the split range): leave it to sample_kernel
+  bool bad = k <= 0 || k > SPLIT_KMAX || k >= V;
+  int mycnt = 0;
+  float mc = -INFINITY, zc = 0.f;
+  if (l < C) {
+    const float* r = base + l * SPLIT_REC;
+    mycnt = __float_as_int(r[4]);
+    mc = r[0];
+    zc = r[1];
+    if (mycnt < 0) bad = true;
+  }
+  if (__ballot(bad)) {
+    if (l == 0) out[row] = -1;
+    return;
+  }
+  // global max and normaliser
+  float M = mc;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) M = fmaxf(M, __shfl_xor(M, o, 64));
+  const float inv_t = 1.f / fmaxf(temp, 1e-5f);
+  float zp = l < C ? zc * __expf((mc - M) * inv_t) : 0.f;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) zp += __shfl_xor(zp, o, 64);
+  const float inv_s = 1.f / zp;
+  // stage every list in LDS (all loads in flight together: one memory round trip, not one per
+  // merge step), then a k-way merge of the lists
+  // (slots past a list's count hold stale words that the merge never reads)
+  for (int c0 = 0; c0 < C; c0 += 8) {
+    unsigned kv[8];
+    int iv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (c0 + u < C) {
+        kv[u] = __float_as_uint(base[(c0 + u) * SPLIT_REC + 8 + 2 * l]);
+        iv[u] = __float_as_int(base[(c0 + u) * SPLIT_REC + 9 + 2 * l]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (c0 + u < C) {
+        l_key[c0 + u][l] = kv[u];
+        l_idx[c0 + u][l] = iv[u];
+      }
+    }
+  }
+  __syncthreads();
+  // each lane's head as one 64-bit composite, larger = earlier in (value desc, index asc) order:
+  // (key << 32) | ~index (0: no head - every real key is > 0); the lists are merged by a
+  // DPP max over the 16 lanes of a row (+ two shuffle rounds past 16 chunks)
+  int pos = 0;
+  int got = 0;
+  auto head = [&]() -> u64 {
+    return (l < C && pos < mycnt) ? (((u64)l_key[l][pos] << 32) | (u64)(~(unsigned)l_idx[l][pos])) : 0ull;
+  };
+  u64 h = head();
+  for (int j = 0; j < k; ++j) {
+    u64 b = h;
+    b = max_u64(b, dpp_u64<0xB1>(b));   // quad_perm [1,0,3,2]
+    b = max_u64(b, dpp_u64<0x4E>(b));   // quad_perm [2,3,0,1]
+    b = max_u64(b, dpp_u64<0x141>(b));  // row_half_mirror
+    b = max_u64(b, dpp_u64<0x140>(b));  // row_mirror: the 16-lane row's max in every lane
+    if (C > 16) {
+      b = max_u64(b, (u64)__shfl_xor((unsigned long long)b, 16, 64));
+      b = max_u64(b, (u64)__shfl_xor((unsigned long long)b, 32, 64));
+    }
+    if (b == 0ull) break;  // every list exhausted (fewer than k ids in the row)
+    if (l == 0) {
+      s_key[j] = (unsigned)(b >> 32);
+      s_idx[j] = (int)~(unsigned)b;
+    }
+    if (h == b) {  // this lane's head was taken
+      ++pos;
+      h = head();
+    }
+    ++got;
+  }
+  // rows 1..3 of the wave (no lists when C <= 16) left the loop at once: lane 0's count is the row's
+  got = __shfl(got, 0, 64);
+  __syncthreads();
+  // probabilities of the sorted survivors (lane l holds ranks l and l + 64 - SPLIT_KMAX <= 64: one)
+  const float pv = l < got ? __expf((okey_inv(s_key[l]) - M) * inv_t) * inv_s : 0.f;
+  // exclusive prefix over the sorted order
+  float inc = pv;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const float nb = __shfl_up(inc, o, 64);
+    if (l >= o) inc += nb;
+  }
+  const float ex1 = inc - pv;
+  const float tp = top_ps[row];
+  const bool keep = l < got && (l == 0 || !(tp > 0.f && tp < 1.f) || ex1 + pv <= tp);
+  const float q = keep ? pv : 0.f;
+  float inc2 = q;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const float nb = __shfl_up(inc2, o, 64);
+    if (l >= o) inc2 += nb;
+  }
+  const float t2 = __shfl(inc2, 63, 64);
+  const float ex2 = inc2 - q;
+  const uint64_t rnd = splitmix64((uint64_t)seeds[row] * 0x9E3779B97F4A7C15ull + (uint64_t)row);
+  const float u01 = (float)((double)(rnd >> 11) * (1.0 / 9007199254740992.0));
+  const float uu = u01 * t2;
+  const unsigned long long hit = __ballot(q > 0.f && uu >= ex2 && uu < ex2 + q);
+  if (l == 0) {
+    const int pick = hit ? s_idx[__builtin_ctzll(hit)] : s_idx[0];  // rounding: the most likely id
+    out[row] = pick;
+    if (update) push_history(recent + (int64_t)row * recent_stride, recent_len + row, recent_stride, pick);
+  }
+}
+
 }  // namespace mp
 
 extern "C" int mp_sample(const void* logits, int64_t stride, int R, int V, const float* temps, const float* top_ps,
@@ -482,7 +851,25 @@ extern "C" int mp_sample(const void* logits, int64_t stride, int R, int V, const
   if (recent_stride > SB) return -1;
   const size_t lds = (size_t)V * sizeof(float);
   const int use_lds = lds <= 136 * 1024;  // + ~23 KB of histogram / candidate arrays
+  // split path for wide vocabularies (MPAMD_SAMPLE_SPLIT: 0 = never, else the smallest V that
+  // takes it; default 65536, i.e. the 128K Llama-3 vocabulary but not Llama-2's 32K)
+  static const int split_min = [] {
+    const char* v = getenv("MPAMD_SAMPLE_SPLIT");
+    return v ? atoi(v) : 65536;
+  }();
+  const int C = (V + SPLIT_CH - 1) / SPLIT_CH;
+  const bool split = split_min > 0 && V >= split_min && C <= SPLIT_MAXC && recent_stride <= SPLIT_NT &&
+                     (int64_t)R * V >= (int64_t)R * C * SPLIT_REC;  // the records fit the workspace
+  if (split) {
+    hipLaunchKernelGGL(sample_split_chunk_kernel, dim3(C, R), dim3(SPLIT_NT), 0, stream, (const bf16_t*)logits,
+                       stride, V, temps, top_ks, rep_pens, recent, recent_stride, recent_len, ws);
+    hipLaunchKernelGGL(sample_split_merge_kernel, dim3(R), dim3(64), 0, stream, V, C, temps, top_ps, top_ks, recent,
+                       recent_stride, recent_len, seeds, ws, out, update);
+    // rows the split could not take (out = -1) run the single-workgroup kernel; the others exit
+    // at once.  (Its global-workspace rows overlap the split records: only -1 rows use them.)
+  }
   hipLaunchKernelGGL(sample_kernel, dim3(R), dim3(SB), use_lds ? lds : 0, stream, (const bf16_t*)logits, stride, V,
-                     temps, top_ps, top_ks, rep_pens, recent, recent_stride, recent_len, seeds, ws, out, use_lds, update);
+                     temps, top_ps, top_ks, rep_pens, recent, recent_stride, recent_len, seeds, ws, out, use_lds, update,
+                     split ? 1 : 0);
   return (int)hipGetLastError();
 }

@@ -851,3 +851,58 @@ def test_linear_above_128_rows_matches_fp32(M, N, K, epi):
         yr = yr + r.float()
     assert y.shape == yr.shape
     torch.testing.assert_close(y.float(), yr, atol=4e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("k,tp", [(50, 0.92), (50, 1.0), (64, 0.5)])
+def test_sampler_split_wide_vocab_distribution(k, tp):
+    """V = 128256 (Llama-3): the split sampler (chunk top-k workgroups + a one-wave merge) samples
+    the reference's top-k / top-p filtered distribution."""
+    V, R = 128256, 2048
+    g = torch.Generator().manual_seed(5)
+    base = torch.randn(V, generator=g) * 1.5
+    base[:20] += 6
+    base[V - 7] += 7  # a head token in the last (partial) chunk
+    logits = bf(base.to(DEV).unsqueeze(0).repeat(R, 1))
+    kw = dict(top_ps=torch.full((R,), tp, device=DEV), top_ks=torch.full((R,), k, dtype=torch.int32, device=DEV),
+              rep_pens=torch.ones(R, device=DEV), recent=torch.zeros(R, 50, dtype=torch.int32, device=DEV),
+              recent_len=torch.zeros(R, dtype=torch.int32, device=DEV),
+              seeds=torch.arange(R, dtype=torch.long, device=DEV) * 7 + 3)
+    out = ops.sample(logits, torch.ones(R, device=DEV), **kw).cpu()
+    p = torch.softmax(logits[0].float().cpu(), -1)
+    tv, ti = torch.topk(p, k)
+    q = torch.zeros_like(p).scatter(0, ti, tv)
+    allowed = p >= tv[-1]
+    if 0 < tp < 1:
+        sp, si = torch.sort(q, descending=True)
+        keep = torch.cumsum(sp, 0) <= tp
+        keep[0] = True
+        q = torch.zeros_like(p).scatter(0, si, sp * keep)
+        allowed &= p >= sp[keep].min() * (1 - 1e-6)
+    f = q / q.sum()
+    freq = torch.bincount(out, minlength=V).float() / R
+    assert set(out.unique().tolist()) <= set(torch.nonzero(allowed).flatten().tolist())
+    assert (freq - f).abs().max().item() < 0.04
+
+
+def test_sampler_split_mixed_rows_and_history():
+    """Wide vocabulary, one launch with split rows (top-k), greedy rows (raw argmax, no penalty),
+    rows the split hands to the single-workgroup kernel (k = 0, k > 64), repetition penalty, and
+    the in-place history update on every row."""
+    V, R = 128256, 6
+    logits = torch.randn(R, V, device=DEV) * 0.5
+    logits[:, 100_000] = 30.0  # the head token, in chunk 12
+    logits[4, 5] = 29.0
+    logits = bf(logits)
+    temps = torch.tensor([1.0, 0.0, 1.0, 1.0, 1.0, 0.0], device=DEV)
+    top_ks = torch.tensor([50, 50, 0, 100, 50, 10], dtype=torch.int32, device=DEV)
+    rep = torch.tensor([1.0, 1.0, 1.0, 1.0, 1e4, 1e4], device=DEV)
+    recent = torch.zeros(R, 50, dtype=torch.int32, device=DEV)
+    recent[4, 0] = 100_000  # row 4: the head token is penalised away -> token 5 wins
+    recent[5, 0] = 100_000  # row 5 is greedy: raw argmax, the penalty does not apply
+    recent_len = torch.tensor([0, 0, 0, 0, 1, 1], dtype=torch.int32, device=DEV)
+    out = ops.sample(logits, temps, torch.full((R,), 0.9, device=DEV), top_ks, rep, recent, recent_len,
+                     torch.arange(R, device=DEV), update_history=True).cpu().tolist()
+    assert out == [100_000, 100_000, 100_000, 100_000, 5, 100_000]
+    assert recent_len.cpu().tolist() == [1, 1, 1, 1, 2, 2]
+    r = recent.cpu()
+    assert [int(r[i, 0]) for i in range(4)] == out[:4] and int(r[4, 1]) == 5 and int(r[5, 1]) == 100_000

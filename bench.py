@@ -142,6 +142,9 @@ def main(argv=None):
         if ops._FP8_CHOICE:
             print("fp8 gemm kernel choice:", {f"M{k[0]}:N{k[1]}xK{k[2]}e{k[3]}": v
                                               for k, v in sorted(ops._FP8_CHOICE.items())}, file=sys.stderr)
+        if ops._W8_CHOICE:
+            print("w8a16 gemm kernel choice:", {f"M{k[0]}:N{k[1]}xK{k[2]}e{k[3]}": v
+                                                for k, v in sorted(ops._W8_CHOICE.items())}, file=sys.stderr)
     ch = None
     if S > 1:  # this pipeline's device channel: ranks [lane*S, (lane+1)*S) over RCCL / xGMI
         from torch.distributed import distributed_c10d as c10d

@@ -19,6 +19,7 @@ advances every session by one token; value = generated tokens/s over the whole n
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import math
 import os
@@ -217,6 +218,13 @@ def main(argv=None):
     if ch is not None:
         ch.stats(reset=True)
         ch.timing = True
+    gc_runs = [0, 0, 0]  # collections per generation inside the timed window (host-side stalls)
+
+    def _gc_cb(phase, info):
+        if phase == "start":
+            gc_runs[info["generation"]] += 1
+
+    gc.callbacks.append(_gc_cb)
     t1 = time.perf_counter()
     eng.timing = True
     eng.run_rounds(a.steps)
@@ -224,6 +232,7 @@ def main(argv=None):
     pdist.barrier(device)
     sync()
     dt_local = time.perf_counter() - t1
+    gc.callbacks.remove(_gc_cb)
     eng.timing = False
     if ch is not None:
         ch.timing = False
@@ -281,6 +290,7 @@ def main(argv=None):
             },
             "per_stage_ms": [round(p[0], 3) for p in per_stage],
             "per_stage_blocks": [int(p[1]) for p in per_stage],
+            "gc_collections_timed": gc_runs,
             # the device channel of every pipeline: which backend carried the hops (RCCL over
             # xGMI on a multi-GPU node), payload bytes each rank sent during the timed steps,
             # and how long each rank's stream waited for its incoming payload per step

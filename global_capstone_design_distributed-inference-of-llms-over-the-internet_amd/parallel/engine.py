@@ -44,6 +44,7 @@ from __future__ import annotations
 
 import collections
 import dataclasses
+import gc
 import logging
 import os
 import time
@@ -663,10 +664,25 @@ class PipelineServingEngine:
         return True
 
     idle_timeout_s: Optional[float] = None  # None: the channel timeout
+    _heap_settled = False
 
     # ------------------------------------------------------------------ driving
+    def _settle_heap(self) -> None:
+        """Once per engine, before its first step: collect, then freeze every object alive now
+        (model, buffers, graphs, channel) into the interpreter's permanent generation.  The
+        serving loop allocates small objects every step; without this each full collection it
+        triggers (every few dozen steps) walks the whole setup heap and stalls the step loop
+        for milliseconds.  ``MPAMD_GC_FREEZE=0`` keeps the default collector."""
+        if self._heap_settled:
+            return
+        self._heap_settled = True
+        if os.environ.get("MPAMD_GC_FREEZE", "1") != "0":
+            gc.collect()
+            gc.freeze()
+
     def run_rounds(self, n: int) -> None:
         """n rounds x M slot-steps on every rank (lock-step unit of the benchmark)."""
+        self._settle_heap()
         try:
             for _ in range(n):
                 for m in range(self.M):
@@ -681,6 +697,7 @@ class PipelineServingEngine:
 
     def serve(self) -> None:
         """Non-head ranks: process steps until the head's STOP."""
+        self._settle_heap()
         try:
             while self._stage_step():
                 pass

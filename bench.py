@@ -14,6 +14,7 @@ its 32/N blocks per step (continuous-batching engine, parallel/engine.py).  A st
 advances every session by one token; value = generated tokens/s over the whole node.
 
     python bench.py                       # N=1 (defaults finish in ~1-2 minutes)
+    python bench.py --gpus N              # spawns the N ranks itself (no launcher needed)
     torchrun --nproc-per-node N bench.py --gpus N --steps K --warmup W
 """
 from __future__ import annotations
@@ -45,6 +46,17 @@ def baseline_value():
         return None
 
 
+def data_plane_name(ch, eng) -> str:
+    if ch is None:
+        return "none"
+    b = getattr(ch, "data_backend", "")
+    if b == "rccl":
+        return "rccl-graph-hop" if getattr(eng, "graph_hop", False) else "rccl-direct"
+    if b == "nccl":
+        return "pgnccl"
+    return "gloo" + ("(host-staged)" if getattr(ch, "staged", False) else "")
+
+
 def fp8_label(ex) -> str:
     """The precision path the executor actually runs for fp8 weights."""
     if getattr(ex, "_w8", False):
@@ -52,7 +64,70 @@ def fp8_label(ex) -> str:
     return "fp8-w8a8 (e4m3 weights and activations, bf16 KV)"
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n: int, argv) -> int:
+    """``--gpus N`` without a launcher (no WORLD_SIZE in the environment): start the N ranks as
+    child processes here - one per GPU, torchrun's environment contract (RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT) - forward rank 0's stdout (the one JSON
+    line) and return non-zero if any rank fails, after stopping the others.  Runs before this
+    process touches the GPU (no ``torch.cuda`` call here).  Reference launcher:
+    /root/reference/scripts/run_all.py:164-208 (one subprocess per stage, logs streamed)."""
+    import signal
+    import subprocess
+
+    port = _free_port()
+    base = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(n),
+                LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", ROLE_RANK="0")
+    base.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    procs = []
+    for r in range(n):
+        env = dict(base, RANK=str(r), LOCAL_RANK=str(r), ROLE_WORLD_SIZE=str(n))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
+                                      stdout=None if r == 0 else sys.stderr.fileno(), start_new_session=True))
+    rc = 0
+    try:
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+            if bad:
+                rc = bad[0][1] or 1
+                print(f"bench: rank {bad[0][0]} exited with {bad[0][1]}; stopping the other ranks", file=sys.stderr)
+                break
+            if all(c == 0 for c in codes):
+                return 0
+            time.sleep(0.2)
+    except KeyboardInterrupt:
+        rc = 130
+    for p in procs:  # only the process groups started above
+        if p.poll() is None:
+            try:
+                os.killpg(p.pid, signal.SIGTERM)
+            except ProcessLookupError:
+                pass
+    deadline = time.time() + 20
+    for p in procs:
+        try:
+            p.wait(timeout=max(0.1, deadline - time.time()))
+        except subprocess.TimeoutExpired:
+            os.killpg(p.pid, signal.SIGKILL)
+            p.wait()
+    return rc if rc > 0 else 1
+
+
 def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
+    pre = argparse.ArgumentParser(add_help=False)
+    pre.add_argument("--gpus", type=int, default=None)
+    known, _ = pre.parse_known_args(argv)
+    if known.gpus and known.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        raise SystemExit(spawn_ranks(known.gpus, argv))
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=None)
     ap.add_argument("--steps", type=int, default=32)
@@ -79,6 +154,11 @@ def main(argv=None):
                          "'even', or explicit cut points")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--device", default=None)
+    ap.add_argument("--channel-data", default=os.environ.get("MPAMD_CHANNEL_DATA", "auto"),
+                    choices=["auto", "nccl", "rccl", "gloo"],
+                    help="stage-hop data plane: ProcessGroupNCCL (nccl, the GPU default), the framework's own "
+                         "RCCL communicators (rccl; + MPAMD_GRAPH_HOP=1 records the hop inside the decode graph), "
+                         "or host-staged gloo")
     a = ap.parse_args(argv)
 
     from src import ops
@@ -150,8 +230,10 @@ def main(argv=None):
     if S > 1:  # this pipeline's device channel: ranks [lane*S, (lane+1)*S) over RCCL / xGMI
         from torch.distributed import distributed_c10d as c10d
 
-        ch = Channel(c10d._get_default_store(), f"bench/pipe{lane}", stage, S, device, timeout_s=600.0)
+        ch = Channel(c10d._get_default_store(), f"bench/pipe{lane}", stage, S, device, timeout_s=600.0,
+                     data_backend=None if a.channel_data == "auto" else a.channel_data)
     eng = PipelineServingEngine(ex, ch, n_slots=M, batch=B, max_step_tokens=B * a.prompt_len, name=f"p{lane}")
+    eng.freeze_heap = True  # a driver process: freeze the setup heap once before the first step
     n_sessions = M * B
     if R > 1:
         # replica placement from measured throughput: every rank times its stage's decode step,
@@ -238,6 +320,7 @@ def main(argv=None):
         ch.timing = False
     stage_ms = eng.stage_ms() or 0.0
     hop = ch.stats() if ch is not None else {"backend": "none", "bytes_sent": 0, "sends": 0, "recv_wait_ms": 0.0}
+    data_plane = data_plane_name(ch, eng)
     n_tokens = 0
     if stage == 0:
         eng.drain()
@@ -295,6 +378,11 @@ def main(argv=None):
             # xGMI on a multi-GPU node), payload bytes each rank sent during the timed steps,
             # and how long each rank's stream waited for its incoming payload per step
             "channel_backend": hop["backend"],
+            # which data plane carried the stage hops: pgnccl (ProcessGroupNCCL send/recv),
+            # rccl-direct (framework RCCL communicators on a side stream), rccl-graph-hop (the
+            # send recorded inside every decode hipGraph), gloo (host), none (one stage)
+            "data_plane": data_plane,
+            "graph_hop": bool(getattr(eng, "graph_hop", False)),
             "hop_bytes_sent_per_rank": [int(p[3]) for p in per_stage],
             "hop_sends_per_rank": [int(p[4]) for p in per_stage],
             "hop_recv_wait_ms_per_rank": [round(p[5], 4) for p in per_stage],

@@ -46,7 +46,7 @@ from .llama_partition import load_stage_model, resolve_dtype
 from .load_balancing import ServerState, choose_best_blocks, should_choose_other_blocks
 from .models.config import resolve_model
 from .models.tokenizer import load_tokenizer
-from .partition import parse_splits, stage_ranges
+from .partition import resolve_splits, stage_ranges
 from .rpc_handler import StageConnectionHandler
 from .rpc_transport import RpcTransport
 from .runtime.executor import StageExecutor
@@ -59,7 +59,10 @@ logger = logging.getLogger("src.main")
 def build_parser() -> argparse.ArgumentParser:
     p = argparse.ArgumentParser(description="MI355X-native Mini-Petals: pipeline-parallel LLM inference")
     p.add_argument("--model", required=True, help="local HF directory or preset (llama2-7b, llama3-8b, gpt2, ...)")
-    p.add_argument("--splits", required=True, help="comma-separated cut points, e.g. 10,20,30 (N cuts -> N+1 stages)")
+    p.add_argument("--splits", required=True,
+                   help="comma-separated cut points, e.g. 10,20,30 (N cuts -> N+1 stages), or auto:N = the "
+                        "cost-balanced cuts for N stages (partition.balanced_splits: the tail's lm_head + sampler "
+                        "count against its blocks); every process must pass the same value")
     p.add_argument("--dtype", default="fp16", choices=["fp16", "bf16", "fp32"])
     p.add_argument("--max_new_tokens", type=int, default=64)
     p.add_argument("--prompt", type=str, default="Hello, how are you?")
@@ -112,6 +115,10 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--device_channel", choices=["auto", "on", "off"], default="auto",
                    help="same-node fast path: hidden states GPU->GPU over RCCL (xGMI) instead of TCP. Servers "
                         "announce it; the client uses it when every hop runs on its machine (auto) or always (on)")
+    p.add_argument("--channel_data", choices=["nccl", "rccl"], default=None,
+                   help="device channel data plane on GPUs: nccl (ProcessGroupNCCL send/recv, default) or rccl "
+                        "(the framework's own RCCL communicators on a side stream; MPAMD_GRAPH_HOP=1 records the hop "
+                        "in the decode graphs). Default: MPAMD_CHANNEL_DATA or nccl")
     p.add_argument("--throughput_batch", type=int, default=16,
                    help="LB server: concurrent one-token steps of the compute-throughput probe (tokens/s)")
     p.add_argument("--num_sessions", type=int, default=1,
@@ -332,8 +339,10 @@ def _run_rank0_channel(args, device, ex, tok, tx, route, ids, on_token=None, res
     def open_replica(rt):
         k = counter[0]
         counter[0] += 1
-        ch = tx.open_device_channel(rt, device, n_slots=M, batch=B, timeout=timeout, timing=True)
+        ch = tx.open_device_channel(rt, device, n_slots=M, batch=B, timeout=timeout, timing=True,
+                                    data_backend=getattr(args, "channel_data", None))
         eng = PipelineServingEngine(ex, ch, n_slots=M, batch=B, name=f"client-r{k}", timeout_s=timeout)
+        eng.freeze_heap = True  # the client is a driver process: one heap freeze per process
         eng.timing = True
         ch.timing = True
         thr = min((float(h.info.get("throughput") or 0.0) for h in rt), default=0.0)
@@ -728,9 +737,14 @@ def main(argv=None):
     setup_logging(args.log_level)
     device = pick_device(args)
     cfg = resolve_model(args.model)
-    cuts = parse_splits(args.splits, cfg.num_hidden_layers)
+    try:
+        cuts = resolve_splits(args.splits, cfg)  # model defaults only: every process derives the same cuts
+    except ValueError as e:
+        raise SystemExit(f"--splits {args.splits}: {e}")
     if not cuts:
         raise SystemExit("--splits must contain at least one cut point")
+    if str(args.splits).startswith("auto"):
+        logger.info(f"--splits {args.splits} -> {','.join(map(str, cuts))}")
     if args.stage == 0:
         run_rank0(args, device, cuts)
     else:

@@ -49,7 +49,9 @@ extern "C" int64_t mp_gemm_workspace_bytes() {
 //        bit 4 = shared-A (LDS-staged activation) kernel when the shape allows it;
 //        bit 7 = balanced ring kernel; bit 8 = split-K ring kernel + reduce launch (epilogue
 //        0 / 2 / 3, needs ws); bits 8 + 9 = split-K ring kernel with the in-launch combine;
-//        bit 10 = rotated k walk per workgroup (EpiArgs::rot).
+//        bit 10 = rotated k walk per workgroup (EpiArgs::rot); bits 8 + 11 = split-K ring with
+//        the symmetric in-launch combine; bit 12 = row-split ring (epilogue 0 / 2 / 3, even row
+//        tiles), + bit 13 = its weights loaded with the default cache policy.
 //        epilogue 3 / ss_in: the fused-norm decode path (EpiArgs above; ap / ss_out / ss_zero /
 //        ss_in may be null when unused).
 extern "C" int mp_gemm_bf16(const void* x, int64_t x_stride, const void* w, void* y, int64_t y_stride,
@@ -67,9 +69,18 @@ extern "C" int mp_gemm_bf16(const void* x, int64_t x_stride, const void* w, void
     if (!(flags & 1) || gate != nullptr) return -1;
     return mp_gemm_bf16_wide(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, ws, ep, stream);
   }
+  if ((flags & 1) && (flags & 4096) && !(flags & 2) && gate == nullptr) {  // row-split ring
+    switch ((M + 15) / 16) {
+      case 2: rc = launch_gemm_rwr<2>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, ep, stream); break;
+      case 4: rc = launch_gemm_rwr<4>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, ep, stream); break;
+      default: rc = 1; break;
+    }
+    if (rc < 0) return rc;
+    if (rc == 0) return (int)hipGetLastError();
+  }
   if ((flags & 1) && (flags & 256) && !(flags & 2) && gate == nullptr && ws != nullptr) {  // split-K ring
 #define MP_RWK(MT_) \
-  rc = launch_gemm_rwk<MT_>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, ep, ws, stream, (flags & 512) != 0)
+  rc = launch_gemm_rwk<MT_>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, ep, ws, stream, rwk_comb(flags))
     switch ((M + 15) / 16) {  // the packed layout's row-tile count is part of its strides
       case 1: MP_RWK(1); break;
       case 2: MP_RWK(2); break;

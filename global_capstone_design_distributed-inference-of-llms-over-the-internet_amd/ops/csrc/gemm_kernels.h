@@ -990,11 +990,14 @@ constexpr int rw_depth2() {
   }
 }
 
-template <int MT, int NT, int EPI, bool OPK, bool F8 = false>
+// ``mt0`` / ``mta`` (row-split form, gemm_rwr_kernel): this workgroup computes the MT row tiles
+// starting at tile mt0 of an activation packed with mta row tiles (default: all rows, mta = MT).
+// NTW = false loads the weights with the default cache policy (a row-split pair re-reads them).
+template <int MT, int NT, int EPI, bool OPK, bool F8 = false, bool NTW = true>
 __device__ __forceinline__ void rw_body(const bf16_t* __restrict__ x, const bf16_t* __restrict__ wp,
                                         bf16_t* __restrict__ y, int64_t ys, const bf16_t* __restrict__ res, int64_t rs,
                                         int M, int K, int tile0, const EpiArgs& ep, f32x4* red, u64 (*rs_part)[SS_ROWS],
-                                        float* rs_lds) {
+                                        float* rs_lds, int mt0 = 0, int mta = MT) {
   constexpr int R = rw_depth2<MT, NT, F8>();
   constexpr int Q = MT * NT;
   constexpr int NQ = (Q + RW_WAVES - 1) / RW_WAVES;  // epilogue quads per wave
@@ -1022,7 +1025,8 @@ __device__ __forceinline__ void rw_body(const bf16_t* __restrict__ x, const bf16
       const int qd = min(wid + RW_WAVES * j, Q - 1), mt = qd / NT, t = qd % NT;
       const int col = (tile0 + t) * 16 + (lane & 15);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) rpre[j][r] = res[(int64_t)min(mt * 16 + (lane >> 4) * 4 + r, M - 1) * rs + col];
+      for (int r = 0; r < 4; ++r)
+        rpre[j][r] = res[(int64_t)min((mt0 + mt) * 16 + (lane >> 4) * 4 + r, M - 1) * rs + col];
     }
   }
 
@@ -1036,10 +1040,12 @@ __device__ __forceinline__ void rw_body(const bf16_t* __restrict__ x, const bf16
 #define RW_LOAD(s, i)                                                                                        \
   {                                                                                                          \
     const int k_ = rw_rot(min(wid + RW_WAVES * (i), nks - 1), krot, nks);                                  \
-    _Pragma("unroll") for (int t = 0; t < NT; ++t) rb[s][t] =                                                \
-        __builtin_nontemporal_load(reinterpret_cast<const BT*>(wb + (((int64_t)t * nks + k_) << 9)));       \
+    _Pragma("unroll") for (int t = 0; t < NT; ++t) {                                                         \
+      const BT* p_ = reinterpret_cast<const BT*>(wb + (((int64_t)t * nks + k_) << 9));                      \
+      rb[s][t] = NTW ? __builtin_nontemporal_load(p_) : *p_;                                                 \
+    }                                                                                                        \
     _Pragma("unroll") for (int mt = 0; mt < MT; ++mt) ra[s][mt] =                                            \
-        load_a_rows(xl + (((int64_t)k_ * MT + mt) << 9), lane, mt * 16 + (lane & 15) < M);                  \
+        load_a_rows(xl + (((int64_t)k_ * mta + mt0 + mt) << 9), lane, (mt0 + mt) * 16 + (lane & 15) < M);   \
   }
 #pragma unroll
   for (int s = 0; s < R; ++s) RW_LOAD(s, s)
@@ -1096,7 +1102,7 @@ __device__ __forceinline__ void rw_body(const bf16_t* __restrict__ x, const bf16
 #pragma unroll
         for (int w = 0; w < RW_WAVES; ++w) up += red[(w * QC + qd + 1 - p0) * 64 + lane];
       }
-      tile_epilogue<MT, EPI, OPK>(qd / NT, tile0 + qd % NT, v, up, y, ys, res, rs, M, lane, ep, rs_lds,
+      tile_epilogue<MT, EPI, OPK>(mt0 + qd / NT, tile0 + qd % NT, v, up, y, ys, res, rs, M, lane, ep, rs_lds,
                                   EPI == 3 ? &rpre[j] : nullptr);
     }
   }
@@ -1229,6 +1235,68 @@ static int launch_gemm_rw(const void* x, const void* w, void* y, int64_t ys, con
 }
 
 // ---------------------------------------------------------------------------------------
+// Row-split ring form ("rwr") for the narrowest projection (o: N = K = 4096).  A ring workgroup
+// that owns all M rows of NT column tiles takes in the whole M x K activation block for NT x 16
+// weight columns: at M = 64, NT = 1 that is 4x the weight bytes through the CU's load path
+// (profiles/r3_f).  Here a PAIR of workgroups shares NT = 2 column tiles and splits the rows
+// (MTH = MT / 2 row tiles each): per CU the activation bytes halve and the weight bytes double,
+// 512 KB instead of 643 KB of intake at M = 64, and no K split - so no partial slabs, no
+// combine, and the fused epilogues (residual-stream producer) run straight from the ring.  The
+// pair reads the same weight columns: blocks b and b + 8 (one XCD under round-robin dispatch,
+// dispatched together) so the second read is an L2 / Infinity Cache hit; NTW picks the weight
+// load policy (non-temporal or default).  Placement only - never correctness.
+template <int MTH, int NT, int EPI, bool NTW>
+__global__ __launch_bounds__(RW_WAVES * 64) void gemm_rwr_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ wp,
+                                                       bf16_t* __restrict__ y, int64_t ys,
+                                                       const bf16_t* __restrict__ res, int64_t rs, int M, int K,
+                                                       const EpiArgs ep) {
+  clear_other(ep);
+  __shared__ u64 rs_part[SS_PG][SS_ROWS];
+  __shared__ float rs_lds[SS_ROWS];
+  __shared__ __attribute__((aligned(16))) f32x4 red[RW_WAVES * (MTH * NT < RW_QC ? MTH * NT : RW_QC) * 64];
+  const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
+  const int half = j & 1, g = (j >> 1) * 8 + xcd;
+  rw_body<MTH, NT, EPI, false, false, NTW>(x, wp, y, ys, res, rs, M, K, g * NT, ep, red, rs_part, rs_lds, half * MTH,
+                                           2 * MTH);
+}
+
+// Grid = 2 x (tiles / NT) = #CUs (a multiple of 16); epilogues 0 / 2 / 3, MT even.  Returns 1
+// (caller falls back) when the shape does not split that way.
+template <int MT>
+static int launch_gemm_rwr(const void* x, const void* w, void* y, int64_t ys, const void* res, int64_t rs, int M,
+                           int N, int K, int epi, int flags, const EpiArgs& ep, hipStream_t stream) {
+  if constexpr (MT % 2 != 0) {
+    return 1;
+  } else {
+    constexpr int MTH = MT / 2;
+    const int tiles = N / 16, C0 = sk_num_cus();
+    if (epi == 1 || (flags & 2) || C0 % 16 || (2 * tiles) % C0) return 1;
+    const int nt = 2 * tiles / C0;
+    const bool ntw = !(flags & 8192);
+#define MP_RWR(NT_, EPI_)                                                                                          \
+  {                                                                                                                \
+    if (ntw)                                                                                                       \
+      hipLaunchKernelGGL((gemm_rwr_kernel<MTH, NT_, EPI_, true>), dim3(C0), dim3(RW_WAVES * 64), 0, stream,       \
+                         (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, ys, (const bf16_t*)res, rs, M, K, ep);    \
+    else                                                                                                           \
+      hipLaunchKernelGGL((gemm_rwr_kernel<MTH, NT_, EPI_, false>), dim3(C0), dim3(RW_WAVES * 64), 0, stream,      \
+                         (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, ys, (const bf16_t*)res, rs, M, K, ep);    \
+  }
+#define MP_RWR_E(NT_) \
+  { if (epi == 3) MP_RWR(NT_, 3) else if (epi == 2) MP_RWR(NT_, 2) else MP_RWR(NT_, 0) }
+    switch (nt) {
+      case 1: MP_RWR_E(1); break;
+      case 2: MP_RWR_E(2); break;
+      case 4: MP_RWR_E(4); break;
+      default: return 1;
+    }
+#undef MP_RWR_E
+#undef MP_RWR
+    return 0;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // Split-K ring form ("rwk") for the narrow projections (o, down: N = 4096 -> 256 column tiles,
 // one per CU): with every CU owning all of K, each CU streams ALL of the activation block
 // (M x K) for just 16 weight columns - at M = 64 that is 4x the weight bytes through the
@@ -1244,7 +1312,17 @@ constexpr int64_t RWK_SLAB_BYTES = (int64_t)16 << 20;  // S x M x N fp32 partial
 // column group, and the LAST of the S splits reads the S slabs back (sc1 loads, slab order:
 // deterministic) and runs epilogue INL (0 with the optional row scale, 2, 3) itself - the
 // stream-K kernel's hand-off protocol (guide: splitk-seam, publish-large).
-template <int MT, int NT, bool F8 = false, int INL = -1>
+//
+// COMB (INL >= 0 only) picks the combine: 1 = the last arriver of the S splits sums all S slabs
+// and runs the whole epilogue (arrival ticket); 2 = symmetric (reduce-scatter): quad qd belongs
+// to split qd % S, every split publishes only the quads the others own, keeps its own in LDS,
+// waits until all S splits of its column group have published (arrive counter + bounded sc1 poll;
+// the S splits are co-resident: the grid is at most one workgroup per CU) and finalises its own
+// quads - 1/S of the slab reads and of the epilogue per workgroup, no serial tail on one CU.
+// Both sum the S partials in split order (0..S-1) from zero: the reduce launch's order, so every
+// combine gives the same bits.  Residual quads of EPI 3 are prefetched before the main loop.
+constexpr int RWK_SPIN_LIMIT = 1 << 25;  // symmetric combine: bounded poll (~1 s), then flag an error
+template <int MT, int NT, bool F8 = false, int INL = -1, int COMB = 1>
 __global__ __launch_bounds__(RW_WAVES * 64) void gemm_rwk_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ wp,
                                                        float* __restrict__ part, int M, int N, int K, int S,
                                                        const EpiArgs ep, bf16_t* __restrict__ y, int64_t ys,
@@ -1256,6 +1334,7 @@ __global__ __launch_bounds__(RW_WAVES * 64) void gemm_rwk_kernel(const bf16_t* _
   using BT = std::conditional_t<F8, u32x2, u16x8>;
   constexpr int Q = MT * NT;
   constexpr int QC = Q < RW_QC ? Q : RW_QC;
+  constexpr int NQ = (Q + RW_WAVES - 1) / RW_WAVES;  // epilogue quads per wave (at most)
   __shared__ __attribute__((aligned(16))) f32x4 red[RW_WAVES * QC * 64];
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int c, sp;
@@ -1282,6 +1361,16 @@ __global__ __launch_bounds__(RW_WAVES * 64) void gemm_rwk_kernel(const bf16_t* _
 #pragma unroll
     for (int t = 0; t < NT; ++t) wsc[t] = ep.wsc[(tile0 + t) * 16 + (lane & 15)];
   }
+  // EPI 3 in-launch: the residual quads this wave may finalise (COMB 1: qd = wid + 4 j of the
+  // whole group; COMB 2: this split's own quads qd = S (wid + 4 j) + sp), in flight during the loop
+  u16x4 rpre[NQ];
+  if constexpr (INL == 3) {
+#pragma unroll
+    for (int j = 0; j < NQ; ++j) {
+      const int qd = COMB == 2 ? S * (wid + RW_WAVES * j) + sp : wid + RW_WAVES * j;
+      rpre[j] = res_quad<NT>(res, rs, min(qd, Q - 1), c, M, lane);
+    }
+  }
   f32x4 acc[MT][NT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
@@ -1289,7 +1378,7 @@ __global__ __launch_bounds__(RW_WAVES * 64) void gemm_rwk_kernel(const bf16_t* _
     for (int t = 0; t < NT; ++t) acc[mt][t] = (f32x4)(0.f);
   u16x8 ra[R][MT];
   BT rb[R][NT];
-#define RWK_LOAD(s, i)                                                                                       \
+#define RWK_LOAD(s, i)                                                                                     \
   {                                                                                                          \
     const int k_ = ks0 + rw_rot(min(wid + RW_WAVES * (i), ks1 - ks0 - 1), krot, ks1 - ks0);                \
     _Pragma("unroll") for (int t = 0; t < NT; ++t) rb[s][t] =                                                \
@@ -1335,6 +1424,8 @@ __global__ __launch_bounds__(RW_WAVES * 64) void gemm_rwk_kernel(const bf16_t* _
     rsc.load(ep, wp);
     const __amdgpu_buffer_rsrc_t rsrc =
         __builtin_amdgcn_make_buffer_rsrc(part, (short)0, (int)RWK_SLAB_BYTES, 0x00020000);
+    // COMB 2: this split's own quads (qd % S == sp) stay in LDS, slot qd / S
+    __shared__ __attribute__((aligned(16))) f32x4 own[COMB == 2 ? ((Q + 1) / 2) * 64 : 1];
 #pragma unroll
     for (int p0 = 0; p0 < Q; p0 += QC) {
       if (p0 > 0) __syncthreads();
@@ -1345,12 +1436,55 @@ __global__ __launch_bounds__(RW_WAVES * 64) void gemm_rwk_kernel(const bf16_t* _
         f32x4 v = red[(qd - p0) * 64 + lane];
 #pragma unroll
         for (int w = 1; w < RW_WAVES; ++w) v += red[(w * QC + qd - p0) * 64 + lane];
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rsrc,
-                                               (((c * S + sp) * Q + qd) * 64 + lane) * 16, 0, 16);
+        if (COMB == 2 && qd % S == sp)
+          own[(qd / S) * 64 + lane] = v;
+        else
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rsrc,
+                                                 (((c * S + sp) * Q + qd) * 64 + lane) * 16, 0, 16);
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 slab stores landed
     __syncthreads();
+    if constexpr (COMB == 2) {
+      // tick: [2 c] arrivals, [2 c + 1] departures; the last to depart re-zeroes both (every split
+      // has seen all S arrivals by then), so the zeroed workspace stays valid across launches
+      if (threadIdx.x == 0) {
+        __hip_atomic_fetch_add(tick + 2 * c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int spins = 0;
+        while (__hip_atomic_load(tick + 2 * c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < S) {
+          __builtin_amdgcn_s_sleep(1);
+          if (++spins > RWK_SPIN_LIMIT) {  // a partner never ran: flag it, never hang the GPU
+            __hip_atomic_store(tick - 1 + 2 * (SK_MAX_GROUPS / 8), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+        }
+        const int old = __hip_atomic_fetch_add(tick + 2 * c + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (old == S - 1) {
+          __hip_atomic_store(tick + 2 * c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(tick + 2 * c + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+      __syncthreads();
+      rsc.finish(ep, rs_part, rs_lds);
+#pragma unroll
+      for (int j = 0; j < NQ; ++j) {
+        const int jo = wid + RW_WAVES * j, qd = S * jo + sp;
+        if (qd >= Q) break;
+        f32x4 pv[8];
+#pragma unroll
+        for (int s2 = 0; s2 < 8; ++s2)
+          if (s2 < S && s2 != sp)
+            pv[s2] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                   rsrc, (((c * S + s2) * Q + qd) * 64 + lane) * 16, 0, 16));
+        f32x4 v = (f32x4)(0.f);
+#pragma unroll
+        for (int s2 = 0; s2 < 8; ++s2)
+          if (s2 < S) v += s2 == sp ? own[jo * 64 + lane] : pv[s2];
+        tile_epilogue<MT, INL, false>(qd / NT, tile0 + qd % NT, v, (f32x4)(0.f), y, ys, res, rs, M, lane, ep, rs_lds,
+                                      INL == 3 ? &rpre[j] : nullptr);
+      }
+      return;
+    }
     if (threadIdx.x == 0) {
       const int old = __hip_atomic_fetch_add(tick + c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       s_last = old == S - 1;
@@ -1360,13 +1494,16 @@ __global__ __launch_bounds__(RW_WAVES * 64) void gemm_rwk_kernel(const bf16_t* _
     if (!s_last) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keep the slab loads below the ticket
     rsc.finish(ep, rs_part, rs_lds);
-    for (int qd = wid; qd < Q; qd += RW_WAVES) {
+#pragma unroll
+    for (int j = 0; j < NQ; ++j) {
+      const int qd = wid + RW_WAVES * j;
+      if (qd >= Q) break;
       f32x4 v = (f32x4)(0.f);
       for (int s2 = 0; s2 < S; ++s2)
         v += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
                                            rsrc, (((c * S + s2) * Q + qd) * 64 + lane) * 16, 0, 16));
       tile_epilogue<MT, INL, false>(qd / NT, tile0 + qd % NT, v, (f32x4)(0.f), y, ys, res, rs, M, lane, ep, rs_lds,
-                                    nullptr);
+                                    INL == 3 ? &rpre[j] : nullptr);
     }
     return;
   }
@@ -1502,17 +1639,33 @@ static inline void launch_splitk_reduce(int S, int epi, dim3 g2, hipStream_t str
 
 // Column-group width NT and split count S with C x S <= #CUs (prefer NT = 4, then 2, 8, 1;
 // 2 <= S <= 8); returns 1 when no split applies (the caller falls back).
+// ``comb``: 0 = reduce launch, 1 = in-launch combine by the last arriver, 2 = symmetric in-launch
+// combine (gemm_rwk_kernel COMB).  Flags: 256 = split-K ring, + 512 -> comb 1, + 2048 -> comb 2.
+static inline int rwk_comb(int flags) { return (flags & 2048) ? 2 : ((flags & 512) ? 1 : 0); }
+
+// symmetric-combine counters [2 per column group] and the error word (last int of the region)
+static inline int* rwk_sym_counters(void* ws) { return (int*)ws + 3 * (SK_MAX_GROUPS / 4); }
+
 template <int MT, bool F8 = false>
 static int launch_gemm_rwk(const void* x, const void* w, void* y, int64_t ys, const void* res, int64_t rs, int M,
                            int N, int K, int epi, const EpiArgs& ep, void* ws, hipStream_t stream,
-                           bool inl = false) {
+                           int comb = 0) {
+  const bool inl = comb != 0;
   if (epi == 1 || ws == nullptr || N % 2048 != 0) return 1;
   const int tiles = N / 16, C0 = sk_num_cus(), nks = K / 32;
   int nt = 0, S = 0;
   // fp8 weights: the bf16 activation block costs 2M / (16 NT) x the weight bytes per CU - the
   // widest column group first (NT = 8: A and W bytes equal at M = 64)
   static constexpr int kOrderBf16[4] = {4, 2, 8, 1}, kOrderF8[4] = {8, 4, 2, 1};
-  for (int cand : (F8 ? kOrderF8 : kOrderBf16)) {
+  // MPAMD_RWK_NT (ablation): try this column-group width first
+  static const int nt_first = [] {
+    const char* v = getenv("MPAMD_RWK_NT");
+    return v ? atoi(v) : 0;
+  }();
+  int order[5] = {nt_first, 0, 0, 0, 0};
+  for (int i = 0; i < 4; ++i) order[i + 1] = (F8 ? kOrderF8 : kOrderBf16)[i];
+  for (int cand : order) {
+    if (cand <= 0) continue;
     if (tiles % cand) continue;
     const int C = tiles / cand, s = C0 / C;
     if (s >= 2 && s <= 8 && nks >= 4 * s) { nt = cand; S = s; break; }
@@ -1526,12 +1679,17 @@ static int launch_gemm_rwk(const void* x, const void* w, void* y, int64_t ys, co
                          (int64_t)SK_MAX_BLOCKS * 2 * SK_MAX_S * 64 * sizeof(float));
   const dim3 g1((tiles / nt) * S);
   int* tick = (int*)ws + SK_MAX_GROUPS / 2;  // rwk arrival tickets (the stream-K kernel uses the low half)
-  if (inl && MT <= 4 && nt >= 2 && tiles / nt <= SK_MAX_GROUPS / 2 &&
+  if (comb == 2) tick = rwk_sym_counters(ws);
+  if (inl && MT <= 4 && nt >= 2 && tiles / nt <= SK_MAX_GROUPS / 8 - 1 &&
       (int64_t)tiles * MT * S * 1024 <= RWK_SLAB_BYTES) {
     if constexpr (MT <= 4) {
 #define MP_RWKI(NT_, E_)                                                                                       \
-  hipLaunchKernelGGL((gemm_rwk_kernel<MT, NT_, F8, E_>), g1, dim3(RW_WAVES * 64), 0, stream, (const bf16_t*)x,            \
-                     (const bf16_t*)w, part, M, N, K, S, ep, (bf16_t*)y, ys, (const bf16_t*)res, rs, tick)
+  if (comb == 2)                                                                                               \
+    hipLaunchKernelGGL((gemm_rwk_kernel<MT, NT_, F8, E_, 2>), g1, dim3(RW_WAVES * 64), 0, stream, (const bf16_t*)x,       \
+                       (const bf16_t*)w, part, M, N, K, S, ep, (bf16_t*)y, ys, (const bf16_t*)res, rs, tick);  \
+  else                                                                                                         \
+    hipLaunchKernelGGL((gemm_rwk_kernel<MT, NT_, F8, E_, 1>), g1, dim3(RW_WAVES * 64), 0, stream, (const bf16_t*)x,       \
+                       (const bf16_t*)w, part, M, N, K, S, ep, (bf16_t*)y, ys, (const bf16_t*)res, rs, tick)
 #define MP_RWKI_E(NT_) \
   { if (epi == 3) MP_RWKI(NT_, 3); else if (epi == 2) MP_RWKI(NT_, 2); else MP_RWKI(NT_, 0); }
       switch (nt) {

@@ -21,10 +21,10 @@ extern "C" int mp_gemm_w8(const void* x, const void* wq, const float* wsc, void*
   int rc = 1;
   if ((flags & 256) && !(flags & 2) && ws != nullptr) {
     switch ((M + 15) / 16) {
-      case 1: rc = launch_gemm_rwk<1, true>(x, wq, y, y_stride, res, res_stride, M, N, K, epilogue, ep, ws, stream, (flags & 512) != 0); break;
-      case 2: rc = launch_gemm_rwk<2, true>(x, wq, y, y_stride, res, res_stride, M, N, K, epilogue, ep, ws, stream, (flags & 512) != 0); break;
-      case 3: rc = launch_gemm_rwk<3, true>(x, wq, y, y_stride, res, res_stride, M, N, K, epilogue, ep, ws, stream, (flags & 512) != 0); break;
-      default: rc = launch_gemm_rwk<4, true>(x, wq, y, y_stride, res, res_stride, M, N, K, epilogue, ep, ws, stream, (flags & 512) != 0); break;
+      case 1: rc = launch_gemm_rwk<1, true>(x, wq, y, y_stride, res, res_stride, M, N, K, epilogue, ep, ws, stream, rwk_comb(flags)); break;
+      case 2: rc = launch_gemm_rwk<2, true>(x, wq, y, y_stride, res, res_stride, M, N, K, epilogue, ep, ws, stream, rwk_comb(flags)); break;
+      case 3: rc = launch_gemm_rwk<3, true>(x, wq, y, y_stride, res, res_stride, M, N, K, epilogue, ep, ws, stream, rwk_comb(flags)); break;
+      default: rc = launch_gemm_rwk<4, true>(x, wq, y, y_stride, res, res_stride, M, N, K, epilogue, ep, ws, stream, rwk_comb(flags)); break;
     }
     if (rc < 0) return rc;
     if (rc == 0) return (int)hipGetLastError();

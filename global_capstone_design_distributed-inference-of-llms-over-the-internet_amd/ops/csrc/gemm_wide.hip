@@ -9,7 +9,7 @@ extern "C" int mp_gemm_bf16_wide(const void* x, const void* w, void* y, int64_t 
   int rc = 1;
   if ((flags & 256) && !(flags & 2) && ws != nullptr) {  // split-K ring
 #define MP_RWK(MT_) \
-  rc = launch_gemm_rwk<MT_>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, ep, ws, stream, (flags & 512) != 0)
+  rc = launch_gemm_rwk<MT_>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, ep, ws, stream, rwk_comb(flags))
     switch ((M + 15) / 16) {
       case 5: MP_RWK(5); break;
       case 6: MP_RWK(6); break;

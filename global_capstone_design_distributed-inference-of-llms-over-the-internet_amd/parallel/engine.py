@@ -22,9 +22,16 @@ Here the same roles run as a chain of stage ranks, one process per GPU:
   stage forwards to its successor before computing; the payload (hidden states) follows on
   RCCL.  Stage k therefore never waits on a host round trip of stage k-1's compute.
 * The tail samples with per-session parameters and a device-resident repetition history
-  (reference semantics, ``ops.sample``), seeded by (session seed, position): a session
-  produces the same tokens no matter which micro-batch, replica or batch mix it runs in -
-  which is what makes replica failover exact.
+  (reference semantics, ``ops.sample``), seeded by (session seed, position): the random draw
+  of a session never depends on which micro-batch, replica or batch mix it runs in.  The
+  LOGITS do, in their last bits, on the GPU: the decode GEMM form (and so its reduction order)
+  is chosen per row bucket, and a failed-over session's KV is rebuilt by a prefill (hipBLASLt
+  + FA2) where the original came from decode steps.  Exactness contract: on the CPU path
+  (fp32 reference ops) a re-placed session's tokens equal the uninterrupted run's
+  (``tests/test_channel_failover.py``); on the GPU the tokens generated before a failure are
+  identical and, after re-placement, the teacher-forced logits agree within bf16 tolerance
+  (``tests/test_failover_gpu.py``), so a sampled token can differ only where two candidates
+  are within that tolerance of each other.
 * Stop conditions are checked on the head from a pinned copy of each step's tokens one
   round later, so the decode loop never blocks the host on the device: the next step's
   inputs are gathered on the device from the previous step's sampled tokens.  A finished
@@ -129,6 +136,26 @@ def repeat_run(generated: Sequence[int]) -> int:
             break
         n += 1
     return n
+
+
+_HEAP_FROZEN = False
+
+
+def settle_heap() -> bool:
+    """Once per PROCESS, before a driver's first serving step: collect, then freeze every object
+    alive now (model, buffers, graphs, channels) into the interpreter's permanent generation.  The
+    serving loop allocates small objects every step; without this each full collection it triggers
+    (every few dozen steps) walks the whole setup heap and stalls the step loop for milliseconds.
+    Only drivers call it (engines with ``freeze_heap``): frozen objects are never collected, so a
+    server that builds an engine per client channel must not freeze each one's transient state.
+    ``MPAMD_GC_FREEZE=0`` keeps the default collector.  Returns True if this call froze the heap."""
+    global _HEAP_FROZEN
+    if _HEAP_FROZEN or os.environ.get("MPAMD_GC_FREEZE", "1") == "0":
+        return False
+    _HEAP_FROZEN = True
+    gc.collect()
+    gc.freeze()
+    return True
 
 
 def request_seed(seed: int, rid: str) -> int:
@@ -334,7 +361,7 @@ class PipelineServingEngine:
         admits only what EVERY stage can hold (stages with more blocks hold fewer tokens)."""
         ex = self.ex
         want_hop = (self.ch is not None and getattr(self.ch, "data_backend", "") == "rccl" and
-                    os.environ.get("MPAMD_GRAPH_HOP", "0") == "1")
+                    os.environ.get("MPAMD_GRAPH_HOP", "0") == "1" and ex.graph_hook_free(self))
         mine = [float(ex.sessions.cache_tokens_left()), float(ex.sessions.max_sessions), float(ex.cache.page_size),
                 float(ex.max_seq_len), float(want_hop), float(bool(ex.use_graphs)), float(ex.graph_max_batch)]
         allv = self.ch.all_gather_floats(mine) if self.ch is not None else [mine]
@@ -351,7 +378,7 @@ class PipelineServingEngine:
                           len({v[6] for v in allv}) == 1)
         if self.graph_hop and not self.is_tail:
             nxt = self.rank + 1
-            ex.set_graph_hook(lambda out: self.ch.send_on_stream(nxt, out))
+            ex.set_graph_hook(lambda out: self.ch.send_on_stream(nxt, out), owner=self)
         if self.is_head:
             self.capacity_tokens = cap
             self.free_handles = list(range(self.max_handles - 1, -1, -1))
@@ -570,7 +597,7 @@ class PipelineServingEngine:
     def _hop_send(self, dst: int, out: torch.Tensor) -> None:
         if not self.graph_hop:
             self.ch.send(dst, out)
-        elif self.ex.last_graphed:  # the send ran inside the replay
+        elif self.ex.last_hooked:  # the send ran inside the replay
             self.ch.count_send(self.ex.graph_rows(out.shape[0], True) * out.shape[1] * out.element_size())
         else:  # eager steps: the same compute stream, so the communicator sees one op order
             self.ch.send_on_stream(dst, out.contiguous())
@@ -606,7 +633,7 @@ class PipelineServingEngine:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
         with trace_range(f"pp.rank{self.rank}.slot{m}"):
-            out = ex.forward(seqs, x, reset=reset, starts=starts, max_length=self.max_len)
+            out = ex.forward(seqs, x, reset=reset, starts=starts, max_length=self.max_len, hook_owner=self)
         if e1 is not None:
             e1.record()
             self._events.append((e0, e1))
@@ -664,21 +691,21 @@ class PipelineServingEngine:
         return True
 
     idle_timeout_s: Optional[float] = None  # None: the channel timeout
-    _heap_settled = False
+    # driver processes (bench.py, the CLI client) set this: the first engine of the process freezes
+    # the setup heap (``settle_heap``); long-lived servers, which build an engine per client
+    # channel, leave the collector alone
+    freeze_heap: bool = False
 
     # ------------------------------------------------------------------ driving
     def _settle_heap(self) -> None:
-        """Once per engine, before its first step: collect, then freeze every object alive now
-        (model, buffers, graphs, channel) into the interpreter's permanent generation.  The
-        serving loop allocates small objects every step; without this each full collection it
-        triggers (every few dozen steps) walks the whole setup heap and stalls the step loop
-        for milliseconds.  ``MPAMD_GC_FREEZE=0`` keeps the default collector."""
-        if self._heap_settled:
-            return
-        self._heap_settled = True
-        if os.environ.get("MPAMD_GC_FREEZE", "1") != "0":
-            gc.collect()
-            gc.freeze()
+        if self.freeze_heap:
+            settle_heap()
+
+    def release(self) -> None:
+        """Give the executor back: remove this engine's graph hook and the graphs that recorded its
+        send (idempotent; stop / failure / end of ``serve`` call it, so a shared executor never
+        replays a send on a closed communicator)."""
+        self.ex.clear_graph_hook(self)
 
     def run_rounds(self, n: int) -> None:
         """n rounds x M slot-steps on every rank (lock-step unit of the benchmark)."""
@@ -690,6 +717,7 @@ class PipelineServingEngine:
                         self._head_step(m)
                     elif not self._stage_step():
                         self.stopped = True
+                        self.release()
                         return
                 self.rounds += 1
         except ChannelError as e:
@@ -704,6 +732,8 @@ class PipelineServingEngine:
             self.stopped = True
         except ChannelError as e:
             self._fail(str(e))
+        finally:
+            self.release()
 
     def run_until_idle(self, max_rounds: Optional[int] = None) -> List[Request]:
         """Head: run rounds until every submitted request has finished."""
@@ -745,10 +775,13 @@ class PipelineServingEngine:
             self.ch.flush(timeout_s=self.timeout_s)
         except (ChannelError, RuntimeError) as e:
             logger.warning(f"stop: {e}")
+        finally:
+            self.release()
 
     def _fail(self, why: str) -> None:
         self.failed = why
         logger.error(f"[{self.name} rank {self.rank}] pipeline failure: {why}")
+        self.release()
         if self.ch is not None:
             self.ch.abort()
         if self.is_head:

@@ -149,10 +149,19 @@ def make_tp_groups(world: int, stages: int, tp: int, device=None) -> Optional[TP
             if rank in ranks:
                 mine, mine_ranks = g, ranks
     comm = None
-    if device is not None and torch.device(device).type == "cuda" and os.environ.get("MPAMD_TP_RCCL", "1") != "0":
+    # the direct RCCL communicator (graph-capturable all-reduces) stays opt-in (MPAMD_TP_RCCL=1) until a
+    # tp2 run on two GPUs has matched the eager TP tokens; if its init fails (e.g. several TP ranks on
+    # one GPU) the group keeps torch's ProcessGroupNCCL and eager steps
+    if device is not None and torch.device(device).type == "cuda" and os.environ.get("MPAMD_TP_RCCL", "0") == "1":
         from . import rccl
         from torch.distributed import distributed_c10d as c10d
 
-        store = c10d._get_default_store()
-        comm = rccl.RcclComm(store, "tp/" + "_".join(map(str, mine_ranks)), mine_ranks.index(rank), tp, device)
+        try:
+            store = c10d._get_default_store()
+            comm = rccl.RcclComm(store, "tp/" + "_".join(map(str, mine_ranks)), mine_ranks.index(rank), tp, device)
+        except Exception as e:  # noqa: BLE001
+            import logging
+
+            logging.getLogger(__name__).warning(f"TP RCCL communicator unavailable ({e}): eager ProcessGroupNCCL")
+            comm = None
     return TPGroup(mine, comm=comm)

@@ -203,7 +203,7 @@ class StageConnectionHandler:
         from .parallel.engine import PipelineFailure, PipelineServingEngine
 
         ex = self.executor
-        ch = None
+        ch = eng = None
         name = str(md.get("prefix", "chan"))
         try:
             store = make_store(md["store_host"], int(md["store_port"]), int(md["world"]), False,
@@ -221,6 +221,8 @@ class StageConnectionHandler:
         except (PipelineFailure, RuntimeError) as e:
             logger.warning(f"device channel {name} failed: {e}")
         finally:
+            if eng is not None:
+                eng.release()  # no graph of this channel's hop survives it (TCP steps, probes, next channel)
             with ex.exec_lock:
                 for sid in [k for k in ex.sessions.sessions if k.startswith(name + ":")]:
                     ex.sessions.close(sid)

@@ -32,6 +32,7 @@ from __future__ import annotations
 
 import asyncio
 import logging
+import os
 import random
 import time
 from typing import Any, Dict, List, Optional, Sequence, Set, Tuple
@@ -479,12 +480,16 @@ class RpcTransport:
             return False
 
     def open_device_channel(self, route: List[Hop], device, *, n_slots: int = 1, batch: int = 64,
-                            timeout: float = 60.0, idle_timeout: float = 3600.0, timing: bool = False):
+                            timeout: float = 60.0, idle_timeout: float = 3600.0, timing: bool = False,
+                            data_backend: Optional[str] = None):
         """Rendezvous a ``parallel.channel.Channel`` with every hop of ``route``: this client
         is rank 0 (head), hop i is rank i + 1, the final hop the tail.  The TCP RPC carries
         only this handshake; afterwards hidden states move GPU -> GPU (RCCL over xGMI) and the
         tail returns token ids on the channel.  Payloads are staged through gloo when two
-        participants share a GPU (RCCL refuses duplicate devices) or on CPU."""
+        participants share a GPU (RCCL refuses duplicate devices) or on CPU.  ``data_backend``
+        (``--channel_data``) picks the GPU data plane: "nccl" (ProcessGroupNCCL, default) or "rccl"
+        (the framework's own communicators, ``parallel/rccl.py``; ``MPAMD_GRAPH_HOP=1`` then records
+        the hop inside the decode graphs); None reads ``MPAMD_CHANNEL_DATA``."""
         import uuid
 
         from .parallel.channel import Channel, free_port, host_id, make_store
@@ -492,7 +497,8 @@ class RpcTransport:
         world = len(route) + 1
         devs = [str(torch.device(device))] + [str(h.info.get("device", "")) for h in route]
         gpu = torch.device(device).type == "cuda"
-        data = "nccl" if gpu and len(set(devs)) == len(devs) else "gloo"
+        want = data_backend or os.environ.get("MPAMD_CHANNEL_DATA") or "nccl"
+        data = want if gpu and len(set(devs)) == len(devs) and want in ("nccl", "rccl") else "gloo"
         port = free_port("127.0.0.1")
         store = make_store("127.0.0.1", port, world, True, timeout_s=timeout)
         prefix = f"chan-{uuid.uuid4().hex[:12]}"

@@ -187,7 +187,8 @@ class StageExecutor:
         # buffer), e.g. the stage hop's RCCL send (parallel/engine.py graph hop); last_graphed
         # says whether the last step ran as a graph replay
         self.graph_hook = None
-        self.last_graphed = False
+        self._hook_owner = None
+        self.last_graphed = self.last_hooked = False
         # MFMA flash attention for prefill steps (csrc/attention_mfma.hip); MPAMD_ATTN_MFMA=off disables
         self._attn_mfma_prefill = os.environ.get("MPAMD_ATTN_MFMA", "prefill") != "off" and \
             cfg.model_type != "gpt2" and cfg.head_dim in (64, 128)
@@ -353,6 +354,7 @@ class StageExecutor:
         """
         T = sum(int(n) for _, n in seqs)
         prompts = plan_kw.pop("prompts", None)
+        hook_owner = plan_kw.pop("hook_owner", None)
         if prompts is not None and not any(p is not None for p in prompts):
             prompts = None
         if T > self.max_tokens:
@@ -360,7 +362,8 @@ class StageExecutor:
                 raise ValueError("deep prompts need the step to fit max_tokens_per_step")
             return self._forward_chunked(seqs, x, **plan_kw)
         plan = self.plan(seqs, **plan_kw)
-        out = self.run(plan, x, prompt=self._prompt_rows(seqs, prompts) if prompts is not None else None)
+        out = self.run(plan, x, prompt=self._prompt_rows(seqs, prompts) if prompts is not None else None,
+                       hook_owner=hook_owner)
         self.commit(plan)
         return out
 
@@ -426,7 +429,7 @@ class StageExecutor:
             return torch.stack(logits)
         return torch.cat(hidden)
 
-    def run(self, plan: Plan, x: torch.Tensor, prompt=None) -> torch.Tensor:
+    def run(self, plan: Plan, x: torch.Tensor, prompt=None, hook_owner=None) -> torch.Tensor:
         if plan.T == 0:
             H = self.cfg.hidden_size
             return torch.empty(0, self.cfg.vocab_size if self.is_last else H, dtype=self.dtype, device=self.device)
@@ -437,10 +440,11 @@ class StageExecutor:
         if self.timing and self.device.type == "cuda":
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
-        self.last_graphed = False
+        self.last_graphed = self.last_hooked = False
         if prompt is None and self.use_graphs and plan.is_decode and plan.T <= self.graph_max_batch:
-            out = self._run_graph(plan, x)
-            self.last_graphed = True
+            hooked = self.graph_hook is not None and hook_owner is not None and hook_owner is self._hook_owner
+            out = self._run_graph(plan, x, hooked)
+            self.last_graphed, self.last_hooked = True, hooked
         elif self.cfg.model_type == "gpt2":
             out = self._forward_gpt2(plan, x, prompt=prompt)
         else:
@@ -893,16 +897,16 @@ class StageExecutor:
         c = max(c, 256)
         return 1 << (c - 1).bit_length()
 
-    def _run_graph(self, plan: Plan, x: torch.Tensor) -> torch.Tensor:
+    def _run_graph(self, plan: Plan, x: torch.Tensor, hooked: bool = False) -> torch.Tensor:
         B = self._bucket(plan.T)
         ctxb = min(self._ctx_bucket(plan.max_ctx), self._ctx_bucket(self.max_seq_len))
         part = ops.attention_partition(B, self.nkv, ctxb, min_part=self._attn_min_part)
-        key = (B, part[0], part[1])
+        key = (B, part[0], part[1], hooked)
         g = self._graphs.get(key)
         if g is None:
             if self._graph_pool is None:
                 self._graph_pool = torch.cuda.graph_pool_handle()
-            g = _DecodeGraph(self, B, part, self._graph_pool)
+            g = _DecodeGraph(self, B, part, self._graph_pool, hook=self.graph_hook if hooked else None)
             self._graphs[key] = g
         return g.replay(plan, x)
 
@@ -913,10 +917,34 @@ class StageExecutor:
             return self._bucket(T)
         return None
 
-    def set_graph_hook(self, fn) -> None:
-        """Record ``fn(out)`` at the end of every decode graph (captures made earlier are dropped)."""
-        self.graph_hook = fn
-        self.clear_graphs()
+    def graph_hook_free(self, owner=None) -> bool:
+        """True when no other owner's graph hook is installed (``owner`` may hold it already)."""
+        return self.graph_hook is None or self._hook_owner is owner
+
+    def set_graph_hook(self, fn, owner=None) -> None:
+        """Record ``fn(out)`` at the end of the decode graphs captured for ``owner`` (the engine
+        whose stage hop it is).  Steps run with ``forward(..., hook_owner=owner)`` replay those
+        graphs; every other caller (a second engine on a shared executor, TCP requests, the
+        throughput probe) gets hook-free graphs of its own, so a recorded send can never be
+        replayed on someone else's behalf.  One owner at a time: a different owner raises."""
+        with self.exec_lock:
+            if fn is not None and not self.graph_hook_free(owner):
+                raise RuntimeError("this executor already records another engine's graph hop")
+            self._drop_hooked()
+            self.graph_hook = fn
+            self._hook_owner = owner if fn is not None else None
+
+    def clear_graph_hook(self, owner=None) -> None:
+        """Remove ``owner``'s hook and the graphs that recorded it (no-op for a non-owner)."""
+        with self.exec_lock:
+            if self.graph_hook is not None and self._hook_owner is owner:
+                self._drop_hooked()
+                self.graph_hook = None
+                self._hook_owner = None
+
+    def _drop_hooked(self) -> None:
+        for k in [k for k in self._graphs if k[-1]]:
+            del self._graphs[k]
 
     def clear_graphs(self):
         self._graphs.clear()
@@ -930,7 +958,7 @@ class _DecodeGraph:
     blob, padded for the bucket (padding rows: slot -1, context 0): round 1 issued six small
     copies / fills per step (profiles/r2_decode_step_*.txt)."""
 
-    def __init__(self, ex: StageExecutor, B: int, part: Tuple[int, int], pool):
+    def __init__(self, ex: StageExecutor, B: int, part: Tuple[int, int], pool, hook=None):
         self.ex, self.B, self.part = ex, B, part
         dev, H, dt = ex.device, ex.cfg.hidden_size, ex.dtype
         if ex.is_first:
@@ -967,8 +995,8 @@ class _DecodeGraph:
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph, pool=pool):
             self.out = ex._forward_llama(*args, decode=True)
-            if ex.graph_hook is not None:  # recorded only: the warm-up runs above never call it
-                ex.graph_hook(self.out)
+            if hook is not None:  # recorded only: the warm-up runs above never call it
+                hook(self.out)
 
     def replay(self, plan: Plan, x: torch.Tensor) -> torch.Tensor:
         b, B = plan.T, self.B

@@ -31,3 +31,30 @@ def test_bench_torchrun_gloo(nproc, extra, par, gb):
     assert rec["value"] > 0 and rec["higher_is_better"] is True and rec["scaling"] == "weak"
     assert rec["config"]["parallelism"] == par
     assert rec["config"]["global_batch"] == gb  # (stages + 1) slots x batch x replicas (TP lanes share)
+
+
+def test_bench_spawns_its_own_ranks():
+    """``python bench.py --gpus 2`` with no launcher: bench.py starts the two ranks itself, rank 0's
+    JSON line is forwarded (data plane reported), the command exits 0."""
+    cmd = [sys.executable, "bench.py", "--gpus", "2", "--steps", "3", "--warmup", "1", "--model", "tiny-llama",
+           "--device", "cpu", "--batch", "2", "--prompt-len", "8"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["OMP_NUM_THREADS"] = "1"
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert KEYS <= set(rec) and rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "pp2"
+    assert rec["data_plane"].startswith("gloo") and rec["graph_hop"] is False
+
+
+def test_bench_spawn_fails_loudly():
+    """A rank that dies makes the launcher exit non-zero (here: cut points for 4 stages on 2 ranks)."""
+    cmd = [sys.executable, "bench.py", "--gpus", "2", "--steps", "1", "--warmup", "0", "--model", "tiny-llama",
+           "--device", "cpu", "--batch", "1", "--prompt-len", "4", "--splits", "1,2,3"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["OMP_NUM_THREADS"] = "1"
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode != 0
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]

@@ -102,14 +102,22 @@ def _body(port, q):
                                   seed=4)
         ex2 = StageExecutor(cfg, w2, "cuda", kv_cache_bytes=64 << 20, max_sessions=8, max_seq_len=256)
         sink = torch.zeros(16, cfg.hidden_size, dtype=torch.bfloat16, device="cuda")
-        ex2.set_graph_hook(lambda o: comm.send_recv(o, 0, sink[: o.shape[0]], 0))
+        owner = object()
+        ex2.set_graph_hook(lambda o: comm.send_recv(o, 0, sink[: o.shape[0]], 0), owner=owner)
         ids = torch.arange(3 * 9, device="cuda") % cfg.vocab_size
         ex2.forward([(f"g{i}", 9) for i in range(3)], ids)
         hook_ok = []
         for st in range(3):
-            hh = ex2.forward([(f"g{i}", 1) for i in range(3)], ids[st * 3:st * 3 + 3])
+            hh = ex2.forward([(f"g{i}", 1) for i in range(3)], ids[st * 3:st * 3 + 3], hook_owner=owner)
             torch.cuda.synchronize()
-            hook_ok.append(bool(ex2.last_graphed) and bool(torch.equal(sink[:3], hh[:3])))
+            hook_ok.append(bool(ex2.last_hooked) and bool(torch.equal(sink[:3], hh[:3])))
+        # a caller that is not the hook's owner replays a hook-free graph: the sink keeps its bytes
+        sink.zero_()
+        hh = ex2.forward([(f"g{i}", 1) for i in range(3)], ids[:3])
+        torch.cuda.synchronize()
+        hook_ok.append(bool(ex2.last_graphed) and not ex2.last_hooked and float(sink.abs().sum()) == 0.0)
+        ex2.clear_graph_hook(owner)
+        hook_ok.append(ex2.graph_hook is None and not any(k[-1] for k in ex2._graphs))
         out["graph_hook"] = hook_ok
         out["graph_rows"] = ex2.graph_rows(3, True)
         _say("graph hook", hook_ok)
@@ -158,4 +166,4 @@ def test_rccl_world1_capture_and_tp_graphs():
     # graph steps pad the batch to its bucket (the decode GEMMs may pick another row-tile form)
     assert out["tp_logits_maxdiff"] < 5e-2
     assert out["alive"] and out["aborted"]
-    assert out["graph_hook"] == [True, True, True] and out["graph_rows"] == 4
+    assert out["graph_hook"] == [True] * 5 and out["graph_rows"] == 4

@@ -64,12 +64,121 @@ def fp8_label(ex) -> str:
     return "fp8-w8a8 (e4m3 weights and activations, bf16 KV)"
 
 
+def run_failover_drill(a, cfg, eng, ex, rank, world, S, R, M, B, device, load_s):
+    """BASELINE config 5 as a runnable drill: R replica pipelines of S stages; global rank 0 (replica
+    0's head) runs the replica front end (parallel/router.py ReplicaFrontend) with host links to the
+    other heads (serve_replica_head); stage rank K is SIGKILLed after running N micro-batch steps;
+    the front end marks its replica dead and re-places the unfinished sessions on the survivors
+    (re-prefill of prompt + generated tokens).  Reference FT loop: /root/reference/src/
+    rpc_transport.py:587-712, /root/reference/scripts/test_fault_tolerance.py:24-88,
+    /root/reference/scripts/kill_stage.py:16-67.  No collective runs after the kill (a dead rank
+    would hang it): every rank leaves with os._exit."""
+    import signal
+
+    from torch.distributed import distributed_c10d as c10d
+
+    from src.parallel.channel import HostLink
+    from src.parallel.engine import PipelineFailure, Request
+    from src.parallel.router import ReplicaFrontend, gather_replica_throughput, serve_replica_head
+    from src.runtime.sampler import SamplingParams
+
+    kill_rank, _, kill_steps = (a.kill or "-1@0").partition("@")
+    kill_rank, kill_steps = int(kill_rank), int(kill_steps or 8)
+    if a.kill and (not (0 < kill_rank < world) or kill_rank % S == 0):
+        raise SystemExit(f"--kill {a.kill}: pick a non-head stage rank (rank % {S} != 0)")
+    store = c10d._get_default_store()
+    lane, stage = rank // S, rank % S
+    link = HostLink(store, "bench/all", rank, world, timeout_s=600.0)
+    thr = gather_replica_throughput(link, ex, lane, stage, R, batch=min(B, 16))
+    link.close()
+    timeout = float(os.environ.get("MPAMD_DRILL_TIMEOUT", "60"))
+    code = 0
+    if rank == 0:
+        links = {r: HostLink(store, f"bench/link{r}", 0, 2, timeout_s=timeout) for r in range(1, R)}
+        fe = ReplicaFrontend(R, eng, links, throughputs=thr, timeout_s=timeout)
+        sp = SamplingParams(a.temperature, a.top_p, a.top_k, a.repetition_penalty)
+        gen = torch.Generator().manual_seed(1234)
+        n_total = R * M * B
+        reqs = []
+        stamps = []  # (time, rid) of every delivered token
+        for i in range(n_total):
+            prompt = torch.randint(0, cfg.vocab_size, (a.prompt_len,), generator=gen).tolist()
+            reqs.append(fe.submit(Request(prompt, max_new_tokens=a.steps, params=sp, stop_on_repeat=0,
+                                          seed=a.seed * 1000003 + i, rid=f"s{i}")))
+        fe.on_token = lambda req, t: stamps.append((time.perf_counter(), req.rid))
+        t0 = time.perf_counter()
+        fe.run()
+        t1 = time.perf_counter()
+        fails = list(fe.failures)
+        t_fail = fe.failure_times[0] if fails else None
+        moved = {reqs[k].rid for k in fe.replaced}
+        before = sum(1 for ts, _ in stamps if t_fail is None or ts < t_fail)
+        rec = [ts for ts, rid in stamps if t_fail is not None and ts >= t_fail and rid in moved]
+        t_rec = rec[0] if rec else None
+        after = sum(1 for ts, _ in stamps if t_rec is not None and ts >= t_rec)
+        done = sum(1 for r in reqs if r.done and len(r.generated) >= a.steps)
+        total_tokens = sum(len(r.generated) for r in reqs)
+        out = {
+            "metric": METRIC, "value": round(total_tokens / (t1 - t0), 2), "unit": "tokens/s", "n_gpus": world,
+            "steps": a.steps, "warmup": 0, "ms_per_step": None, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "bf16", "data": f"synthetic (random-init {cfg.name} weights, random prompt ids)",
+            "config": {"model": cfg.name, "global_batch": n_total, "seq_len": a.prompt_len,
+                       "parallelism": f"pp{S}xdp{R}", "micro_batches": M, "sessions_per_micro_batch": B,
+                       "engine": "ReplicaFrontend over PipelineServingEngine replicas (failover drill)"},
+            "failover": {
+                "killed_rank": kill_rank, "kill_after_steps": kill_steps,
+                "failed_replicas": [f[0] for f in fails], "failure_reasons": [f[1] for f in fails],
+                "sessions_total": n_total, "sessions_completed": done, "sessions_replaced": len(moved),
+                "tokens_per_s_before": round(before / (t_fail - t0), 2) if t_fail else None,
+                "tokens_per_s_after": round(after / max(t1 - t_rec, 1e-9), 2) if t_rec else None,
+                "recovery_s": round(t_rec - t_fail, 4) if (t_rec and t_fail) else None,
+                "drill_s": round(t1 - t0, 3),
+            },
+            "load_s": round(load_s, 1),
+        }
+        print(json.dumps(out), flush=True)
+        if a.dump_tokens:  # per session: tokens, and for re-placed ones how many preceded the failure
+            with open(a.dump_tokens, "w") as f:
+                json.dump({"tokens": {r.rid: list(r.generated) for r in reqs},
+                           "replaced": {reqs[k].rid: n for k, n in fe.replaced.items()},
+                           "at_failure": {reqs[k].rid: n for k, n in fe.at_failure.items()}}, f)
+        code = 0 if done == n_total else 3
+    elif stage == 0:
+        link = HostLink(store, f"bench/link{lane}", 1, 2, timeout_s=timeout)
+        serve_replica_head(eng, link, timeout_s=timeout)
+    elif rank == kill_rank:
+        try:
+            for _ in range(kill_steps):
+                if not eng._stage_step():
+                    break
+        finally:
+            os.kill(os.getpid(), signal.SIGKILL)
+    else:
+        try:
+            eng.serve()
+        except PipelineFailure:
+            pass  # a stage of the failed replica: its neighbour died
+    sys.stdout.flush()
+    sys.stderr.flush()
+    os._exit(code)
+
+
 def _free_port() -> int:
     import socket
 
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]
+
+
+def _drill_victim(argv):
+    """The rank a ``--kill RANK@STEPS`` drill kills on purpose (its SIGKILL is not a failure)."""
+    for i, v in enumerate(argv):
+        spec = v.split("=", 1)[1] if v.startswith("--kill=") else (argv[i + 1] if v == "--kill" and i + 1 < len(argv)
+                                                                  else None)
+        if spec:
+            return int(spec.partition("@")[0])
+    return None
 
 
 def spawn_ranks(n: int, argv) -> int:
@@ -92,9 +201,12 @@ def spawn_ranks(n: int, argv) -> int:
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
                                       stdout=None if r == 0 else sys.stderr.fileno(), start_new_session=True))
     rc = 0
+    victim = _drill_victim(argv)
     try:
         while True:
             codes = [p.poll() for p in procs]
+            if victim is not None and codes[victim] == -signal.SIGKILL:
+                codes[victim] = 0  # the drill's own kill
             bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
             if bad:
                 rc = bad[0][1] or 1
@@ -154,6 +266,14 @@ def main(argv=None):
                          "'even', or explicit cut points")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--device", default=None)
+    ap.add_argument("--kill", default=None, metavar="RANK@STEPS",
+                    help="replica failover drill (BASELINE config 5): SIGKILL this stage rank after it has run STEPS "
+                         "micro-batch steps; replica 0's head routes the sessions (ReplicaFrontend), re-places the "
+                         "failed replica's sessions on the survivors, and the JSON reports tokens/s before / after, "
+                         "recovery seconds and sessions completed.  Ranks are this launcher's own children")
+    ap.add_argument("--drill", action="store_true",
+                    help="run the failover drill's front end without killing anyone (the uninterrupted reference)")
+    ap.add_argument("--dump-tokens", default=None, help="drill: write every session's tokens (JSON) here")
     ap.add_argument("--channel-data", default=os.environ.get("MPAMD_CHANNEL_DATA", "auto"),
                     choices=["auto", "nccl", "rccl", "gloo"],
                     help="stage-hop data plane: ProcessGroupNCCL (nccl, the GPU default), the framework's own "
@@ -234,6 +354,11 @@ def main(argv=None):
                      data_backend=None if a.channel_data == "auto" else a.channel_data)
     eng = PipelineServingEngine(ex, ch, n_slots=M, batch=B, max_step_tokens=B * a.prompt_len, name=f"p{lane}")
     eng.freeze_heap = True  # a driver process: freeze the setup heap once before the first step
+    if a.kill or a.drill:
+        if R < 2 or TP != 1:
+            raise SystemExit("--kill needs --replicas >= 2 (and no --tp): a failover needs a survivor")
+        run_failover_drill(a, cfg, eng, ex, rank, world, S, R, M, B, device, time.time() - t0)
+        return
     n_sessions = M * B
     if R > 1:
         # replica placement from measured throughput: every rank times its stage's decode step,

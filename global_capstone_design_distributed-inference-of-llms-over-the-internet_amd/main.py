@@ -46,7 +46,7 @@ from .llama_partition import load_stage_model, resolve_dtype
 from .load_balancing import ServerState, choose_best_blocks, should_choose_other_blocks
 from .models.config import resolve_model
 from .models.tokenizer import load_tokenizer
-from .partition import resolve_splits, stage_ranges
+from .partition import parse_splits, resolve_splits, stage_ranges  # noqa: F401 (parse_splits: API)
 from .rpc_handler import StageConnectionHandler
 from .rpc_transport import RpcTransport
 from .runtime.executor import StageExecutor

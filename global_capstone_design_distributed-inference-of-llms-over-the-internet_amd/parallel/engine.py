@@ -27,11 +27,11 @@ Here the same roles run as a chain of stage ranks, one process per GPU:
   LOGITS do, in their last bits, on the GPU: the decode GEMM form (and so its reduction order)
   is chosen per row bucket, and a failed-over session's KV is rebuilt by a prefill (hipBLASLt
   + FA2) where the original came from decode steps.  Exactness contract: on the CPU path
-  (fp32 reference ops) a re-placed session's tokens equal the uninterrupted run's
-  (``tests/test_channel_failover.py``); on the GPU the tokens generated before a failure are
-  identical and, after re-placement, the teacher-forced logits agree within bf16 tolerance
-  (``tests/test_failover_gpu.py``), so a sampled token can differ only where two candidates
-  are within that tolerance of each other.
+  (fp32 reference ops) a re-placed session's logits agree to fp32 rounding and its tokens equal
+  the uninterrupted run's (``tests/test_channel_failover.py``, ``tests/test_failover_drill.py``);
+  on the GPU the tokens generated before a failure are identical and, after re-placement, the
+  teacher-forced logits agree within bf16 tolerance (``tests/test_failover_gpu.py``), so a
+  sampled token can differ only where two candidates are within that tolerance of each other.
 * Stop conditions are checked on the head from a pinned copy of each step's tokens one
   round later, so the decode loop never blocks the host on the device: the next step's
   inputs are gathered on the device from the previous step's sampled tokens.  A finished
@@ -311,7 +311,7 @@ class PipelineServingEngine:
     def __init__(self, executor: StageExecutor, channel: Optional[Channel], *, n_slots: Optional[int] = None,
                  batch: int = 64, max_step_tokens: Optional[int] = None, prefill_chunk: Optional[int] = None,
                  timeout_s: float = 120.0, max_handles: Optional[int] = None, timing: bool = False,
-                 name: str = "pipe"):
+                 name: str = "pipe", warmup: Optional[bool] = None):
         self.ex = executor
         self.ch = channel
         self.rank = channel.rank if channel is not None else 0
@@ -354,6 +354,12 @@ class PipelineServingEngine:
             self.reserved_tokens = 0
             self.tokens_generated = 0
         self._exchange_capacity()
+        if warmup is None:
+            warmup = self.dev.type == "cuda" and os.environ.get("MPAMD_WARMUP", "1") != "0"
+        if warmup:
+            # the first steps' real shapes (a batch-wide ragged prefill, the decode graph of the
+            # batch bucket, the sampler at batch rows): the first request pays no first-call costs
+            self.ex.warmup_serving(self.B, max(1, min(self.max_step_tokens // max(self.B, 1), 512)))
 
     # ------------------------------------------------------------------ setup
     def _exchange_capacity(self) -> None:

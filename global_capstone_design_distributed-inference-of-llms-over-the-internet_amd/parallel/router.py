@@ -177,6 +177,9 @@ class ReplicaFrontend:
         self.requests: Dict[int, Request] = {}
         self.pending: Dict[int, List[int]] = {r: [] for r in range(self.n)}
         self.failures: List[Tuple[int, str]] = []
+        self.failure_times: List[float] = []  # perf_counter() of each failure (drill reporting)
+        self.replaced: Dict[int, int] = {}    # re-placed session -> tokens it had at its failure
+        self.at_failure: Dict[int, int] = {}  # every session -> tokens it had at the first failure
         self._next = 0
         self._threads: List[threading.Thread] = []
         self.replica_tokens = [0] * self.n
@@ -304,6 +307,9 @@ class ReplicaFrontend:
                 return
             logger.error(f"replica {r} failed: {why}; re-placing its sessions")
             self.failures.append((r, why))
+            self.failure_times.append(time.perf_counter())
+            if not self.at_failure:
+                self.at_failure = {k: len(q.generated) for k, q in self.requests.items()}
             if self.recover is not None:
                 rep = None
                 try:
@@ -324,7 +330,9 @@ class ReplicaFrontend:
             plans = self.router.fail(r)
             self.pending[r] = []
             for plan in plans:
-                self.pending[plan.replica].append(int(plan.session_id))
+                rid = int(plan.session_id)
+                self.pending[plan.replica].append(rid)
+                self.replaced.setdefault(rid, len(self.requests[rid].generated))
 
     def _remote_loop(self, r: int, link: HostLink) -> None:
         try:

@@ -212,6 +212,7 @@ class StageConnectionHandler:
                          timeout_s=float(md.get("timeout", 60.0)), data_backend=md.get("data_backend"))
             eng = PipelineServingEngine(ex, ch, n_slots=int(md.get("n_slots", 1)), batch=int(md.get("batch", 64)),
                                         name=name)
+            logger.info(f"device channel {name}: open as rank {int(md['rank'])} of {int(md['world'])}")
             eng.idle_timeout_s = float(md.get("idle_timeout", 3600.0))
             eng.timing = bool(md.get("timing", False))  # per-stage ms for the client's STATS gathers
             ch.timing = eng.timing

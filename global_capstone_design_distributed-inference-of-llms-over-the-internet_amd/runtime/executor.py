@@ -702,6 +702,66 @@ class StageExecutor:
                     self.sessions.close(sid)
             torch.cuda.synchronize(self.device)
 
+    def warmup_serving(self, batch: int, prompt_len: int, decode_steps: int = 2) -> bool:
+        """Warm the shapes a serving engine's FIRST steps run, so the first request pays no
+        first-call costs: one ragged prefill of ``batch`` sequences x ``prompt_len`` tokens (the
+        library GEMM heuristics at batch x prompt rows, the FA2 prefill plan, the last-row lm_head
+        and sampler shapes), then ``decode_steps`` decode steps of the batch - the first one
+        captures the decode hipGraph of that batch bucket, which the real steps then replay (same
+        bucket, same attention partition).  The probe sessions are closed afterwards.  Once per
+        (batch, prompt_len) per executor; returns False when skipped (already warm, no room)."""
+        if self.device.type != "cuda" or not self.n_layers or batch < 1 or prompt_len < 1:
+            return False
+        key = (int(batch), int(prompt_len))
+        done = self.__dict__.setdefault("_served_warm", set())
+        if key in done:
+            return False
+        prompt_len = int(min(prompt_len, self.max_seq_len - decode_steps - 2))
+        if prompt_len < 1 or batch > self.sessions.max_sessions:
+            return False
+        sids = [f"__warm{i}__" for i in range(batch)]
+        H = self.cfg.hidden_size
+        gen = torch.Generator(device=self.device).manual_seed(1)
+        with self.exec_lock, torch.inference_mode():
+            try:
+                T = batch * prompt_len
+                if self.is_first:
+                    x = torch.randint(0, self.cfg.vocab_size, (T,), device=self.device, generator=gen)
+                else:
+                    x = (0.1 * torch.randn(T, H, device=self.device, generator=gen)).to(self.dtype)
+                out = self.forward([(s, prompt_len) for s in sids], x, reset=[True] * batch)
+                if self.is_last:
+                    self._warm_sampler(out)
+                for _ in range(decode_steps):
+                    if self.is_first:
+                        x = torch.randint(0, self.cfg.vocab_size, (batch,), device=self.device, generator=gen)
+                    else:
+                        x = (0.1 * torch.randn(batch, H, device=self.device, generator=gen)).to(self.dtype)
+                    out = self.forward([(s, 1) for s in sids], x)
+                    if self.is_last:
+                        self._warm_sampler(out)
+                done.add(key)
+            except Exception as e:  # noqa: BLE001 - e.g. no KV room: the first request warms itself
+                logger.info(f"serving warm-up ({batch} x {prompt_len}) skipped: {e}")
+                return False
+            finally:
+                for s in sids:
+                    self.sessions.close(s)
+            torch.cuda.synchronize(self.device)
+        return True
+
+    def _warm_sampler(self, logits: torch.Tensor) -> None:
+        """The sampling kernel at this row count, on scratch parameters (no session state)."""
+        n, dev = logits.shape[0], self.device
+        from .sampler import RECENT
+
+        ops.sample(logits, torch.ones(n, device=dev), torch.full((n,), 0.92, device=dev),
+                   torch.full((n,), 50, dtype=torch.int32, device=dev), torch.full((n,), 1.5, device=dev),
+                   torch.zeros(n, RECENT, dtype=torch.int32, device=dev), torch.zeros(n, dtype=torch.int32, device=dev),
+                   torch.arange(n, dtype=torch.int64, device=dev),
+                   workspace=torch.empty(max(n, 64) * logits.shape[1], dtype=torch.float32, device=dev),
+                   update_history=True)
+
     def _folded_native(self, T: int) -> bool:
         """Would ``ops.linear`` run BOTH norm-consuming projections (qkv, gate/up) of a T-row
         row-major step on the native GEMM (i.e. over the norm-folded packed weights)?  The

@@ -155,3 +155,56 @@ def test_cli_process_client_survives_sigkill(swarm, tmp_path):
     assert len(got) == 8 and all(v["finish"] in ("length", "eos", "repeat") for v in got.values()), got
     assert "recovered" in txt, txt[-3000:]
     assert got == ref
+
+
+@pytest.mark.timeout(300)
+def test_single_route_rebuilt_through_spare_server(tmp_path, caplog):
+    """One replica only (``--max_replicas 1``) and a spare tail server: the tail in use is SIGKILLed
+    mid-decode, so no surviving replica can take the sessions - ``recover()`` (main.py
+    ``_run_rank0_channel``) finds the dead server over TCP, opens a new channel through the
+    surviving stage-1 server and the spare, and the sessions are re-prefilled there; every
+    session completes with the uninterrupted run's tokens."""
+    procs = {}
+    p, pid, maddr = _start(0, tmp_path, 1)
+    procs[pid] = (p, 1, tmp_path / "s0.log")
+    for i in (1, 2):
+        p, pid, _ = _start(i, tmp_path, 2, maddr)
+        procs[pid] = (p, 2, tmp_path / f"s{i}.log")
+    try:
+        assert _wait_routes(maddr, n=1)
+        args = ARGS + " --max_replicas 1"
+        ref = []
+        M.run_rank0(client_args(MODEL, SPLITS, maddr, args), torch.device("cpu"), [1, 2], results=ref)
+        assert len(ref) == 8 and all(len(g) == 20 for g in ref)
+        caplog.clear()
+        killed = []
+        count = [0]
+        tails = [(pid, p, log) for pid, (p, st, log) in procs.items() if st == 2]
+        opens0 = {pid: log.read_text().count("open as rank") for pid, p, log in tails}
+
+        def on_token(req, tok):
+            count[0] += 1
+            if count[0] == 40 and not killed:
+                # the tail the CURRENT channel uses: the one that opened a channel since the reference run
+                now = {pid: log.read_text().count("open as rank") for pid, p, log in tails}
+                victim = next(t for t in tails if now[t[0]] > opens0[t[0]])
+                victim[1].send_signal(signal.SIGKILL)
+                victim[1].wait(10)
+                killed.append(victim[0])
+
+        out = []
+        with caplog.at_level("INFO", logger="src.main"):
+            M.run_rank0(client_args(MODEL, SPLITS, maddr, args), torch.device("cpu"), [1, 2], on_token=on_token,
+                        results=out)
+        assert killed, "the fault was never injected"
+        assert "rebuilt a pipeline" in caplog.text, caplog.text[-3000:]
+        assert "replica failure(s) recovered" in caplog.text
+        assert out == ref
+    finally:
+        for p, _, _ in procs.values():
+            if p.poll() is None:
+                p.terminate()
+                try:
+                    p.wait(10)
+                except subprocess.TimeoutExpired:
+                    p.kill()

@@ -50,7 +50,7 @@ def test_reference_fold_identity_cpu():
     assert int(ssz.abs().sum()) == 0
 
 
-KERNELS = ["pk", "sk", "lds22", "lds24", "lds42", "rw", "rwk", "rwki"]
+KERNELS = ["pk", "sk", "lds22", "lds24", "lds42", "rw", "rwk", "rwki", "rwks", "rwr"]
 
 
 @pytest.mark.gpu
@@ -89,7 +89,7 @@ def test_consumer_row_scale_matches_rmsnorm_then_gemm(kern, M):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("kern", KERNELS)
-@pytest.mark.parametrize("M", [1, 33, 64])
+@pytest.mark.parametrize("M", [1, 16, 33, 48, 64])
 def test_producer_epilogue_residual_pack_and_sumsq(kern, M):
     dev = "cuda"
     g = torch.Generator(device=dev).manual_seed(100 + M)

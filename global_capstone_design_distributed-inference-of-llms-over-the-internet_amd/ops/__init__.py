@@ -547,10 +547,14 @@ def attention_fa(q, k_cache, v_cache, block_tables, q_seq, q_ctx, fablocks, nh, 
 
 def attention_mfma_rope(qkv, k_cache, v_cache, block_tables, q_seq, q_ctx, qblocks, positions, cos, sin, slots, nh,
                         nkv, scale, out=None, workspace=None, part_size=None, num_parts=None, max_ctx=None,
-                        packed=False):
+                        packed=False, qkv_part=None):
     """GQA decode step on the MFMA kernel with RoPE of q / new k and the new token's page-slot
     write folded in (csrc/attention_mfma.hip ROPE path).  ``qblocks`` holds one token per block
-    (``decode_qblocks``); ``qkv`` is the unrotated fused projection and is not modified."""
+    (``decode_qblocks``); ``qkv`` is the unrotated fused projection and is not modified; with
+    ``qkv_part`` the kernel reads q / k / v from the qkv GEMM's partial slabs instead."""
+    if qkv_part is not None and not _native(qkv):
+        qkv = reduce_qkv_part(qkv_part, qkv.dtype)
+        qkv_part = None
     if not _native(qkv):
         q = qkv.clone()
         ref.rope_kv_write(q, positions, cos, sin, k_cache, v_cache, slots, nh, nkv)
@@ -570,7 +574,7 @@ def attention_mfma_rope(qkv, k_cache, v_cache, block_tables, q_seq, q_ctx, qbloc
         workspace = attention_workspace(T, nh, D, num_parts, qkv.device)
     torch.ops.mpamd.attention_mfma_rope(qkv, k_cache, v_cache, block_tables, q_seq, q_ctx, qblocks, positions, cos,
                                         sin, slots, out, workspace, nh, nkv, float(scale), int(part_size),
-                                        int(num_parts), int(bool(packed)))
+                                        int(num_parts), int(bool(packed)), *_qkv_part_args(qkv_part))
     return out
 
 
@@ -625,12 +629,39 @@ def paged_attention(q, k_cache, v_cache, block_tables, q_seq, q_ctx, nh, nkv, sc
     return out
 
 
+def _qkv_part_args(qkv_part):
+    """(part, splits, ss, inv_k, eps) op arguments of a ``qkv_part`` = (slabs [S, T, width],
+    row statistics or None, inv_k, eps) from ``linear_partials``; all-None when absent."""
+    if qkv_part is None:
+        return None, 0, None, 0.0, 0.0
+    part, ss, inv_k, eps = qkv_part
+    return part, int(part.shape[0]), ss, float(inv_k), float(eps)
+
+
+def reduce_qkv_part(qkv_part, dtype=torch.bfloat16):
+    """The bf16 qkv rows a ``qkv_part`` stands for (reference of the in-kernel fold)."""
+    part, ss, inv_k, eps = qkv_part
+    acc = torch.zeros_like(part[0])
+    for s in range(part.shape[0]):
+        acc = acc + part[s]
+    if ss is not None:
+        tot = ss.view(-1, 128).sum(0)[: part.shape[1]].double()
+        rs = torch.rsqrt((tot.float() * (1.0 / 1048576.0)) * inv_k + eps)
+        acc = acc * rs[:, None]
+    return acc.to(dtype)
+
+
 def paged_attention_rope(qkv, k_cache, v_cache, block_tables, q_seq, q_ctx, positions, cos, sin, slots, nh, nkv,
                          scale, out=None, workspace=None, part_size=None, num_parts=None, max_ctx=None,
-                         packed=False):
+                         packed=False, qkv_part=None):
     """Decode step (one query per sequence, q_ctx = position + 1): RoPE of q / new k, the new
     token's page-slot write and paged attention in ONE kernel (csrc/attention.hip ROPE path).
-    ``qkv`` is the unrotated fused projection and is not modified."""
+    ``qkv`` is the unrotated fused projection and is not modified; with ``qkv_part``
+    (``linear_partials`` slabs + row statistics) the kernel reads q / k / v from the slabs and
+    ``qkv`` is not read at all."""
+    if qkv_part is not None and not _native(qkv):
+        qkv = reduce_qkv_part(qkv_part, qkv.dtype)
+        qkv_part = None
     if not _native(qkv):
         q = qkv.clone()
         ref.rope_kv_write(q, positions, cos, sin, k_cache, v_cache, slots, nh, nkv)
@@ -650,7 +681,8 @@ def paged_attention_rope(qkv, k_cache, v_cache, block_tables, q_seq, q_ctx, posi
         workspace = attention_workspace(T, nh, D, num_parts, qkv.device)
     torch.ops.mpamd.paged_attention_rope(qkv, k_cache, v_cache, block_tables, q_seq, q_ctx, positions, cos, sin,
                                          slots, out, workspace, int(nh), int(nkv), float(scale), int(part_size),
-                                         int(num_parts), int(bool(packed)), _attn_cnt(qkv.device))
+                                         int(num_parts), int(bool(packed)), _attn_cnt(qkv.device),
+                                         *_qkv_part_args(qkv_part))
     return out
 
 
@@ -813,6 +845,108 @@ def linear(x, w, out=None, epilogue=0, residual=None, policy=None, wp=None, a_ro
         out.copy_(y)
         return out
     return y
+
+
+# ---------------------------------------------------------------------------------------
+# qkv projection as split-K partial slabs, summed by the decode attention kernel (the "fold"):
+# the split-K ring streams the weights without the reduce launch, and the attention kernel's q /
+# k / v loads add the S slabs, apply the fused-norm row scale and round to bf16 - the bits the
+# reduce launch would have stored (csrc/common.h qkv_part_load8).
+PART_FLAG = 16384
+_RWK_SPLIT = {}
+_QKV_FOLD = {}  # (m_bucket, N, K, fp8) -> True where partials + fold beat the chosen kernel
+
+
+def rwk_split(M: int, N: int, K: int, fp8: bool = False) -> int:
+    """Split count of the split-K ring form for this shape (0: not covered)."""
+    key = (int(M), int(N), int(K), bool(fp8))
+    if key not in _RWK_SPLIT:
+        _RWK_SPLIT[key] = int(torch.ops.mpamd.gemm_rwk_split(int(M), int(N), int(K), int(bool(fp8))))
+    return _RWK_SPLIT[key]
+
+
+def _slab_view(device, S: int, M: int, N: int) -> torch.Tensor:
+    ws = gemm_workspace(device)
+    off = int(torch.ops.mpamd.gemm_slab_offset())
+    return ws[off:off + S * M * N * 4].view(torch.float32).view(S, M, N)
+
+
+def linear_partials(x, M: int, wp=None, w8=None, w_scale=None, out=None, rot: bool = False):
+    """The decode GEMM of a PACKED activation as fp32 split-K partial slabs [S, M, N] (a view into
+    the GEMM workspace, valid until the next split-K GEMM on this device's stream): no epilogue,
+    no row scale.  ``wp`` (bf16 packed) or ``w8`` / ``w_scale`` (fp8 W8A16).  ``out`` is the
+    caller's would-be output (not written; the op needs a tensor of the output's shape)."""
+    f8 = w8 is not None
+    N = 16 * (w8.shape[0] if f8 else wp.shape[0])
+    K = 32 * (w8.shape[1] if f8 else wp.shape[1])
+    S = rwk_split(M, N, K, f8)
+    if S <= 0:
+        raise RuntimeError(f"no split-K ring form for M={M}, N={N}, K={K}")
+    if out is None:
+        out = torch.empty(M, N, dtype=x.dtype, device=x.device)
+    flags = 1 | 256 | PART_FLAG | (ROT_FLAG if rot else 0)
+    ws = gemm_workspace(x.device)
+    if f8:
+        torch.ops.mpamd.gemm_w8(x, w8, w_scale, out, None, 0, M, flags, ws, None, None, None, None, 1.0 / K, 0.0)
+    else:
+        torch.ops.mpamd.gemm(x, wp, out, None, 0, M, flags, ws, None, None, None, None, None, 1.0 / K, 0.0)
+    return _slab_view(x.device, S, M, N)
+
+
+def qkv_fold(M: int, N: int, K: int, fp8: bool = False) -> bool:
+    return bool(_QKV_FOLD.get((_m_bucket(M), N, K, bool(fp8)), False)) and rwk_split(M, N, K, fp8) > 0
+
+
+def autotune_qkv_fold(N: int, K: int, device, fp8: bool = False, ms=(16, 32, 48, 64), iters: int = 24,
+                      rounds: int = 3) -> dict:
+    """Per M bucket: the qkv GEMM as partial slabs (no reduce launch) vs the kernel the GEMM
+    autotuner chose for the full projection; the fold is kept where it wins by > 3 %.  Weights
+    rotated over ~1 GiB of copies, as in ``autotune_gemm``."""
+    global _W8_MODE
+    device = torch.device(device)
+    if device.type != "cuda" or os.environ.get("MPAMD_QKV_FOLD", "1") == "0":
+        return {}
+    copies = max(1, min(8, (1 << 30) // (N * K * (1 if fp8 else 2))))
+    if fp8:
+        ws = [torch.randint(0, 0x77, (N // 16, K // 32, 64, 8), dtype=torch.uint8, device=device)
+              for _ in range(copies)]
+        wsc = torch.full((N,), 1e-3, dtype=torch.float32, device=device)
+    else:
+        ws = [(torch.randn(N // 16, K // 32, 64, 8, device=device) * 0.02).to(torch.bfloat16) for _ in range(copies)]
+    for M in ms:
+        key = (_m_bucket(M), N, K, bool(fp8))
+        if key in _QKV_FOLD or rwk_split(M, N, K, fp8) <= 0:
+            continue
+        xp = pack_act(torch.randn(M, K, device=device).to(torch.bfloat16))
+        y = torch.empty(M, N, dtype=torch.bfloat16, device=device)
+
+        def full(i):
+            if fp8:
+                linear_w8(xp, ws[i % copies], wsc, M, out=y)
+            else:
+                linear(xp, None, out=y, wp=ws[i % copies], a_rows=M)
+
+        def part(i):
+            if fp8:
+                linear_partials(xp, M, w8=ws[i % copies], w_scale=wsc, out=y)
+            else:
+                linear_partials(xp, M, wp=ws[i % copies], out=y)
+
+        t = {"full": float("inf"), "part": float("inf")}
+        for _ in range(rounds):
+            for name, fn in (("full", full), ("part", part)):
+                for i in range(2):
+                    fn(i)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for i in range(iters):
+                    fn(i)
+                e1.record()
+                e1.synchronize()
+                t[name] = min(t[name], e0.elapsed_time(e1) / iters)
+        _QKV_FOLD[key] = t["part"] < 0.97 * t["full"]
+    del ws
+    return dict(_QKV_FOLD)
 
 
 # ---------------------------------------------------------------------------------------

@@ -69,6 +69,7 @@ struct RopeFuse {
   const int64_t* slots; // [T] cache slot of the new token (page * page_size + offset)
   bf16_t* kw;           // the k / v caches, written only at the new token's slot
   bf16_t* vw;
+  QkvPart qp;           // qp.part != nullptr: q / k / v from the qkv GEMM's split-K partials
 };
 
 // In-launch split-K combine (NP > 1 with a counter buffer): every context-slice workgroup of a
@@ -173,14 +174,19 @@ __global__ __launch_bounds__(256) void paged_attn_kernel(
     const int c0 = (sl * 8) & (HALF - 1);
     const bool lo = sl * 8 < HALF;
     const int po = lo ? HALF : -HALF;
+    const float qrs = rf.qp.part != nullptr ? qkv_part_scale(rf.qp, t) : 1.f;
+    auto ld8 = [&](int col) -> u16x8 {  // element col of this token's fused qkv row
+      return rf.qp.part != nullptr ? qkv_part_load8(rf.qp, t, col, qrs)
+                                   : *reinterpret_cast<const u16x8*>(row + col);
+    };
     const int64_t ps_ = rf.pos[t];
     const f32x4 ca = *reinterpret_cast<const f32x4*>(rf.cos_t + ps_ * HALF + c0);
     const f32x4 cb = *reinterpret_cast<const f32x4*>(rf.cos_t + ps_ * HALF + c0 + 4);
     const f32x4 sa = *reinterpret_cast<const f32x4*>(rf.sin_t + ps_ * HALF + c0);
     const f32x4 sb = *reinterpret_cast<const f32x4*>(rf.sin_t + ps_ * HALF + c0 + 4);
-    auto rot = [&](const bf16_t* hp) {
-      const u16x8 me = *reinterpret_cast<const u16x8*>(hp + sl * 8);
-      const u16x8 ot = *reinterpret_cast<const u16x8*>(hp + sl * 8 + po);
+    auto rot = [&](int hc) {  // hc: first column of the head in the qkv row
+      const u16x8 me = ld8(hc + sl * 8);
+      const u16x8 ot = ld8(hc + sl * 8 + po);
       u16x8 r;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -192,12 +198,12 @@ __global__ __launch_bounds__(256) void paged_attn_kernel(
     };
 #pragma unroll
     for (int r = 0; r < NREP; ++r) {
-      const u16x8 v = rot(row + (hbase + r) * D);
+      const u16x8 v = rot((hbase + r) * D);
 #pragma unroll
       for (int j = 0; j < 8; ++j) qf[r][j] = bf2f(v[j]) * scale_log2;
     }
-    kn = rot(row + (nh + g) * D);
-    vn = *reinterpret_cast<const u16x8*>(row + (nh + nkv + g) * D + sl * 8);
+    kn = rot((nh + g) * D);
+    vn = ld8((nh + nkv + g) * D + sl * 8);
     tnew = ctx - 1;
     const int64_t slot = rf.slots[t];
     if (tnew >= start && tnew < end && slot >= 0 && tid < LPT && hbase % (nh / nkv) == 0) {
@@ -471,14 +477,19 @@ __global__ __launch_bounds__(NW * 64) void paged_attn1_kernel(
     const int c0 = (sl * 8) & (HALF - 1);
     const bool lo = sl * 8 < HALF;
     const int po = lo ? HALF : -HALF;
+    const float qrs = rf.qp.part != nullptr ? qkv_part_scale(rf.qp, t) : 1.f;
+    auto ld8 = [&](int col) -> u16x8 {  // element col of this token's fused qkv row
+      return rf.qp.part != nullptr ? qkv_part_load8(rf.qp, t, col, qrs)
+                                   : *reinterpret_cast<const u16x8*>(row + col);
+    };
     const int64_t ps_ = rf.pos[t];
     const f32x4 ca = *reinterpret_cast<const f32x4*>(rf.cos_t + ps_ * HALF + c0);
     const f32x4 cb = *reinterpret_cast<const f32x4*>(rf.cos_t + ps_ * HALF + c0 + 4);
     const f32x4 sa = *reinterpret_cast<const f32x4*>(rf.sin_t + ps_ * HALF + c0);
     const f32x4 sb = *reinterpret_cast<const f32x4*>(rf.sin_t + ps_ * HALF + c0 + 4);
-    auto rot = [&](const bf16_t* hp) {
-      const u16x8 me = *reinterpret_cast<const u16x8*>(hp + sl * 8);
-      const u16x8 ot = *reinterpret_cast<const u16x8*>(hp + sl * 8 + po);
+    auto rot = [&](int hc) {  // hc: first column of the head in the qkv row
+      const u16x8 me = ld8(hc + sl * 8);
+      const u16x8 ot = ld8(hc + sl * 8 + po);
       u16x8 r;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -490,12 +501,12 @@ __global__ __launch_bounds__(NW * 64) void paged_attn1_kernel(
     };
 #pragma unroll
     for (int r = 0; r < NREP; ++r) {
-      const u16x8 v = rot(row + (hbase + r) * D);
+      const u16x8 v = rot((hbase + r) * D);
 #pragma unroll
       for (int j = 0; j < 8; ++j) qf[r][j] = bf2f(v[j]) * scale_log2;
     }
-    kn = rot(row + (nh + g) * D);
-    vn = *reinterpret_cast<const u16x8*>(row + (nh + nkv + g) * D + sl * 8);
+    kn = rot((nh + g) * D);
+    vn = ld8((nh + nkv + g) * D + sl * 8);
     tnew = ctx - 1;
     const int64_t slot = rf.slots[t];
     if (tnew >= start && tnew < end && slot >= 0 && tid < LPT && hbase % (nh / nkv) == 0) {
@@ -722,9 +733,16 @@ extern "C" int mp_paged_attention(const void* q, int64_t q_stride, const void* k
                                   void* out, float* workspace, int T, int nh, int nkv, int D, int page_size,
                                   int PS, int NP, float scale, int packed_mt, const int64_t* rope_pos,
                                   const float* cos_t, const float* sin_t, const int64_t* slots, int* counters,
-                                  int n_counters, hipStream_t stream) {
+                                  int n_counters, const void* qkv_part_v, hipStream_t stream) {
+  (void)hipGetLastError();  // an earlier non-mpamd HIP call's stale error is not this launch's
   using namespace mp;
-  const RopeFuse rf{rope_pos, cos_t, sin_t, slots, (bf16_t*)const_cast<void*>(kc), (bf16_t*)const_cast<void*>(vc)};
+  RopeFuse rf{rope_pos, cos_t, sin_t, slots, (bf16_t*)const_cast<void*>(kc), (bf16_t*)const_cast<void*>(vc),
+              QkvPart{nullptr, 0, 0, 0, nullptr, 0.f, 0.f}};
+  const QkvPart* qkv_part = static_cast<const QkvPart*>(qkv_part_v);  // layout mirrored by bindings.cpp
+  if (qkv_part != nullptr && qkv_part->part != nullptr) {
+    if (rope_pos == nullptr || qkv_part->S < 1) return -4;  // partials only on the fused RoPE decode path
+    rf.qp = *qkv_part;
+  }
   if (T == 0) return 0;
   if (nh % nkv != 0 || PS % 64 != 0 || PS > 2048 || NP < 1) return -1;
   int page_log2 = 0;

@@ -296,6 +296,7 @@ extern "C" int mp_attention_fa(const void* q, int64_t q_stride, const void* kc, 
                                int bt_stride, const int32_t* q_seq, const int32_t* q_ctx, const int32_t* fb_tok0,
                                const int32_t* fb_ntok, int NBF, void* out, float* workspace, int T, int nh, int nkv,
                                int D, int page_size, int PS, int NP, float scale, int nw, hipStream_t stream) {
+  (void)hipGetLastError();  // an earlier non-mpamd HIP call's stale error is not this launch's
   using namespace mp;
   if (NBF == 0 || T == 0) return 0;
   if (D != 128 || nh % nkv != 0 || PS % 64 != 0 || NP < 1 || page_size % 64 != 0) return -1;

@@ -45,6 +45,7 @@ struct RopeFuseM {
   const int64_t* slots;
   bf16_t* kw;
   bf16_t* vw;
+  QkvPart qp;  // qp.part != nullptr: q / k / v from the qkv GEMM's split-K partials (ROPE path)
 };
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_mf;
@@ -120,12 +121,24 @@ __global__ __launch_bounds__(256, 2) void attn_mfma_kernel(
   if (b_first < end) pg_cur = bt[b_first >> page_log2];
   if (b_first + 128 < end) pg_next = bt[(b_first + 128) >> page_log2];
 
+  // ROPE with qkv partials: this block's token row of the fused qkv, summed from the split-K slabs
+  // and row-scaled on the fly (common.h qkv_part_load8: the reduce launch's bits)
+  const bool from_part = ROPE && rf.qp.part != nullptr;
+  const float qrs = from_part ? qkv_part_scale(rf.qp, tok0) : 1.f;
+  auto ld8 = [&](int col) -> u16x8 {  // element col of the block's (first) token's qkv row
+    return from_part ? qkv_part_load8(rf.qp, tok0, col, qrs)
+                     : *reinterpret_cast<const u16x8*>(q + (int64_t)tok0 * q_stride + col);
+  };
   u16x8 qf[KD];
 #pragma unroll
   for (int kd = 0; kd < KD; ++kd) {
-    if (row_ok) qf[kd] = *reinterpret_cast<const u16x8*>(q + (int64_t)(tok0 + my_t) * q_stride + (int64_t)my_h * D +
-                                                         kd * 32 + qd * 8);
-    else qf[kd] = (u16x8)(0);
+    if (row_ok) {
+      qf[kd] = from_part ? ld8(my_h * D + kd * 32 + qd * 8)
+                         : *reinterpret_cast<const u16x8*>(q + (int64_t)(tok0 + my_t) * q_stride + (int64_t)my_h * D +
+                                                           kd * 32 + qd * 8);
+    } else {
+      qf[kd] = (u16x8)(0);
+    }
   }
 
   if (b_first < end) {
@@ -139,11 +152,10 @@ __global__ __launch_bounds__(256, 2) void attn_mfma_kernel(
   if constexpr (ROPE) {
     constexpr int HK = KD / 2, HALF = D / 2;
     const int64_t ps_ = rf.pos[tok0];
-    const bf16_t* row = q + (int64_t)tok0 * q_stride;
     u16x8 kr[KD];
 #pragma unroll
-    for (int kd = 0; kd < KD; ++kd) kr[kd] = *reinterpret_cast<const u16x8*>(row + (nh + g) * D + kd * 32 + qd * 8);
-    vn = *reinterpret_cast<const u16x8*>(row + (nh + nkv + g) * D + ((lane * 8) % D));
+    for (int kd = 0; kd < KD; ++kd) kr[kd] = ld8((nh + g) * D + kd * 32 + qd * 8);
+    vn = ld8((nh + nkv + g) * D + ((lane * 8) % D));
     f32x4 cs[HK][2], sn[HK][2];
 #pragma unroll
     for (int h = 0; h < HK; ++h) {
@@ -563,9 +575,16 @@ extern "C" int mp_attention_mfma(const void* q, int64_t q_stride, const void* kc
                                  int D, int page_size, int PS, int NP, float scale, int packed_mt,
                                  const int64_t* rope_pos, const float* cos_t, const float* sin_t,
                                  const int64_t* slots, const int32_t* sb_first, const int32_t* sb_n, int NSB,
-                                 hipStream_t stream) {
+                                 const void* qkv_part_v, hipStream_t stream) {
+  (void)hipGetLastError();  // an earlier non-mpamd HIP call's stale error is not this launch's
   using namespace mp;
-  const RopeFuseM rf{rope_pos, cos_t, sin_t, slots, (bf16_t*)const_cast<void*>(kc), (bf16_t*)const_cast<void*>(vc)};
+  RopeFuseM rf{rope_pos, cos_t, sin_t, slots, (bf16_t*)const_cast<void*>(kc), (bf16_t*)const_cast<void*>(vc),
+               QkvPart{nullptr, 0, 0, 0, nullptr, 0.f, 0.f}};
+  const QkvPart* qkv_part = static_cast<const QkvPart*>(qkv_part_v);  // layout mirrored by bindings.cpp
+  if (qkv_part != nullptr && qkv_part->part != nullptr) {
+    if (rope_pos == nullptr || qkv_part->S < 1) return -4;  // partials only on the fused RoPE decode path
+    rf.qp = *qkv_part;
+  }
   if (NB == 0 || T == 0) return 0;
   if (nh % nkv != 0 || PS % 128 != 0 || NP < 1 || page_size % 32 != 0) return -1;
   int page_log2 = 0;

@@ -22,7 +22,7 @@ int mp_paged_attention(const void* q, int64_t q_stride, const void* kc, const vo
                        int bt_stride, const int32_t* q_seq, const int32_t* q_ctx, void* out, float* workspace, int T,
                        int nh, int nkv, int D, int page_size, int PS, int NP, float scale, int packed_mt,
                        const int64_t* rope_pos, const float* cos_t, const float* sin_t, const int64_t* slots,
-                       int* counters, int n_counters, hipStream_t stream);
+                       int* counters, int n_counters, const void* qkv_part, hipStream_t stream);
 int mp_embedding(const int64_t* ids, const void* table, void* out, int T, int H, int64_t vocab, hipStream_t stream);
 int mp_swiglu(const void* gu, void* out, int64_t T, int F, hipStream_t stream);
 int mp_add(const void* a, const void* b, void* y, int64_t n, hipStream_t stream);
@@ -31,12 +31,14 @@ int mp_sample(const void* logits, int64_t stride, int R, int V, const float* tem
               const int32_t* top_ks, const float* rep_pens, int32_t* recent, int recent_stride, int32_t* recent_len,
               const int64_t* seeds, float* ws, int64_t* out, int update, hipStream_t stream);
 int64_t mp_gemm_workspace_bytes();
+int64_t mp_gemm_slab_offset();
+int mp_gemm_rwk_split(int M, int N, int K, int f8);
 int mp_attention_mfma(const void* q, int64_t q_stride, const void* kc, const void* vc, const int32_t* bt, int bt_stride,
                       const int32_t* q_seq, const int32_t* q_ctx, const int32_t* qb_tok0, const int32_t* qb_ntok, int NB,
                       void* out, float* workspace, int T, int nh, int nkv, int D, int page_size, int PS, int NP,
                       float scale, int packed_mt, const int64_t* rope_pos, const float* cos_t, const float* sin_t,
                       const int64_t* slots, const int32_t* sb_first, const int32_t* sb_n, int NSB,
-                      hipStream_t stream);
+                      const void* qkv_part, hipStream_t stream);
 int mp_attention_fa(const void* q, int64_t q_stride, const void* kc, const void* vc, const int32_t* bt, int bt_stride,
                     const int32_t* q_seq, const int32_t* q_ctx, const int32_t* fb_tok0, const int32_t* fb_ntok, int NBF,
                     void* out, float* workspace, int T, int nh, int nkv, int D, int page_size, int PS, int NP,
@@ -185,12 +187,40 @@ void kv_write(const at::Tensor& k, const at::Tensor& v, at::Tensor& k_cache, at:
                "kv_write");
 }
 
+// Host mirror of mp::QkvPart (common.h): the qkv projection as split-K partial slabs
+// [S][M][width] fp32 + the fused-norm row statistics, read by the decode attention kernels.
+struct QkvPartArgs {
+  const float* part;
+  int S;
+  int64_t slab;
+  int ldn;
+  const unsigned long long* ss;
+  float inv_k, eps;
+};
+
+static bool qkv_part_args(const c10::optional<at::Tensor>& part, int64_t splits, const c10::optional<at::Tensor>& ss,
+                          double inv_k, double eps, int64_t T, int64_t width, QkvPartArgs& a) {
+  if (!part.has_value()) return false;
+  MP_CHECK(part->is_cuda() && part->scalar_type() == at::kFloat && part->is_contiguous() && part->dim() == 3 &&
+               part->size(0) == splits && part->size(1) == T && part->size(2) == width,
+           "qkv_part: fp32 [S, T, qkv width] split-K slabs (ops.linear_partials)");
+  MP_CHECK(splits >= 1 && splits <= 8, "qkv_part splits");
+  const unsigned long long* ssp = nullptr;
+  if (ss.has_value()) {
+    MP_CHECK(ss->is_cuda() && ss->scalar_type() == at::kLong && ss->is_contiguous() && ss->numel() >= 32 * 128,
+             "part_ss: row statistics [32, 128] int64");
+    ssp = reinterpret_cast<const unsigned long long*>(ss->data_ptr<int64_t>());
+  }
+  a = QkvPartArgs{part->data_ptr<float>(), (int)splits, T * width, (int)width, ssp, (float)inv_k, (float)eps};
+  return true;
+}
+
 static void paged_attention_impl(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
                                  const at::Tensor& block_tables, const at::Tensor& q_seq, const at::Tensor& q_ctx,
                                  at::Tensor& out, at::Tensor& workspace, int64_t nh, int64_t nkv, double scale,
                                  int64_t part_size, int64_t num_parts, int64_t packed, const int64_t* rope_pos,
                                  const float* cos_t, const float* sin_t, const int64_t* slots,
-                                 const c10::optional<at::Tensor>& counters) {
+                                 const c10::optional<at::Tensor>& counters, const QkvPartArgs* qp = nullptr) {
   check_bf16_cuda(q, "q");
   check_rows(q, "q");
   check_bf16_cuda(out, "out");
@@ -223,7 +253,7 @@ static void paged_attention_impl(const at::Tensor& q, const at::Tensor& k_cache,
                                   q_ctx.data_ptr<int32_t>(), out.data_ptr(), workspace.data_ptr<float>(), T, nh, nkv,
                                   D, k_cache.size(2), part_size, num_parts, (float)scale,
                                   packed ? (int)((T + 15) / 16) : 0, rope_pos, cos_t, sin_t, slots, cp, ncnt,
-                                  cur_stream()),
+                                  qp, cur_stream()),
                "paged_attention");
 }
 
@@ -242,7 +272,8 @@ void paged_attention_rope(const at::Tensor& qkv, at::Tensor& k_cache, at::Tensor
                           const at::Tensor& positions, const at::Tensor& cos, const at::Tensor& sin,
                           const at::Tensor& slots, at::Tensor& out, at::Tensor& workspace, int64_t nh, int64_t nkv,
                           double scale, int64_t part_size, int64_t num_parts, int64_t packed,
-                          const c10::optional<at::Tensor>& counters) {
+                          const c10::optional<at::Tensor>& counters, const c10::optional<at::Tensor>& qkv_part,
+                          int64_t part_splits, const c10::optional<at::Tensor>& part_ss, double inv_k, double eps) {
   check_bf16_cuda(k_cache, "k_cache");
   check_bf16_cuda(v_cache, "v_cache");
   MP_CHECK(k_cache.dim() == 4 && k_cache.sizes() == v_cache.sizes(), "cache [pages, nkv, page, D]");
@@ -254,9 +285,11 @@ void paged_attention_rope(const at::Tensor& qkv, at::Tensor& k_cache, at::Tensor
                sin.is_contiguous() && cos.size(1) == D / 2 && sin.sizes() == cos.sizes(),
            "cos/sin tables fp32 [max_pos, D/2]");
   MP_CHECK(D % 16 == 0, "head dim");
+  QkvPartArgs qp;
+  const bool has_qp = qkv_part_args(qkv_part, part_splits, part_ss, inv_k, eps, T, qkv.size(1), qp);
   paged_attention_impl(qkv, k_cache, v_cache, block_tables, q_seq, q_ctx, out, workspace, nh, nkv, scale, part_size,
                        num_parts, packed, positions.data_ptr<int64_t>(), cos.data_ptr<float>(), sin.data_ptr<float>(),
-                       slots.data_ptr<int64_t>(), counters);
+                       slots.data_ptr<int64_t>(), counters, has_qp ? &qp : nullptr);
 }
 
 static void attention_mfma_impl(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
@@ -264,7 +297,8 @@ static void attention_mfma_impl(const at::Tensor& q, const at::Tensor& k_cache, 
                                 const at::Tensor& qblocks, at::Tensor& out, at::Tensor& workspace, int64_t nh,
                                 int64_t nkv, double scale, int64_t part_size, int64_t num_parts, int64_t packed,
                                 const int64_t* rope_pos, const float* cos_t, const float* sin_t,
-                                const int64_t* slots, const c10::optional<at::Tensor>& superblocks = c10::nullopt) {
+                                const int64_t* slots, const c10::optional<at::Tensor>& superblocks = c10::nullopt,
+                                const QkvPartArgs* qp = nullptr) {
   check_bf16_cuda(q, "q");
   check_rows(q, "q");
   check_bf16_cuda(out, "out");
@@ -302,7 +336,7 @@ static void attention_mfma_impl(const at::Tensor& q, const at::Tensor& k_cache, 
                                  qblocks.data_ptr<int32_t>() + NB, NB, out.data_ptr(), workspace.data_ptr<float>(), T,
                                  nh, nkv, D, k_cache.size(2), part_size, num_parts, (float)scale,
                                  packed ? (int)((T + 15) / 16) : 0, rope_pos, cos_t, sin_t, slots, sbp,
-                                 sbp != nullptr ? sbp + NSB : nullptr, NSB, cur_stream()),
+                                 sbp != nullptr ? sbp + NSB : nullptr, NSB, qp, cur_stream()),
                "attention_mfma");
 }
 
@@ -358,7 +392,9 @@ void attention_mfma_rope(const at::Tensor& qkv, at::Tensor& k_cache, at::Tensor&
                          const at::Tensor& block_tables, const at::Tensor& q_seq, const at::Tensor& q_ctx,
                          const at::Tensor& qblocks, const at::Tensor& positions, const at::Tensor& cos,
                          const at::Tensor& sin, const at::Tensor& slots, at::Tensor& out, at::Tensor& workspace,
-                         int64_t nh, int64_t nkv, double scale, int64_t part_size, int64_t num_parts, int64_t packed) {
+                         int64_t nh, int64_t nkv, double scale, int64_t part_size, int64_t num_parts, int64_t packed,
+                         const c10::optional<at::Tensor>& qkv_part, int64_t part_splits,
+                         const c10::optional<at::Tensor>& part_ss, double inv_k, double eps) {
   check_bf16_cuda(k_cache, "k_cache");
   check_bf16_cuda(v_cache, "v_cache");
   MP_CHECK(k_cache.dim() == 4 && k_cache.sizes() == v_cache.sizes(), "cache [pages, nkv, page, D]");
@@ -370,9 +406,11 @@ void attention_mfma_rope(const at::Tensor& qkv, at::Tensor& k_cache, at::Tensor&
                sin.is_contiguous() && cos.size(1) == D / 2 && sin.sizes() == cos.sizes(),
            "cos/sin tables fp32 [max_pos, D/2]");
   MP_CHECK(qblocks.size(1) == T, "fused RoPE needs one query token per block (decode)");
+  QkvPartArgs qp;
+  const bool has_qp = qkv_part_args(qkv_part, part_splits, part_ss, inv_k, eps, T, qkv.size(1), qp);
   attention_mfma_impl(qkv, k_cache, v_cache, block_tables, q_seq, q_ctx, qblocks, out, workspace, nh, nkv, scale,
                       part_size, num_parts, packed, positions.data_ptr<int64_t>(), cos.data_ptr<float>(),
-                      sin.data_ptr<float>(), slots.data_ptr<int64_t>());
+                      sin.data_ptr<float>(), slots.data_ptr<int64_t>(), c10::nullopt, has_qp ? &qp : nullptr);
 }
 
 void embedding(const at::Tensor& ids, const at::Tensor& table, at::Tensor& out) {
@@ -582,6 +620,10 @@ void gemm_w8(const at::Tensor& x, const at::Tensor& wq, const at::Tensor& wsc, a
 }
 
 int64_t gemm_workspace_bytes() { return mp_gemm_workspace_bytes(); }
+int64_t gemm_slab_offset() { return mp_gemm_slab_offset(); }
+int64_t gemm_rwk_split(int64_t M, int64_t N, int64_t K, int64_t f8) {
+  return mp_gemm_rwk_split((int)M, (int)N, (int)K, (int)f8);
+}
 void fp8_gemm_kernel(int64_t kind) { mp_fp8_set_kernel((int)kind); }
 bool gemm_rw_ok(int64_t M, int64_t N, int64_t K, int64_t epilogue, int64_t out_packed) {
   return mp_gemm_rw_ok((int)M, (int)N, (int)K, (int)epilogue, (int)out_packed) != 0;
@@ -663,6 +705,8 @@ void gemm_fp8(const at::Tensor& a8, const at::Tensor& as, const at::Tensor& wq, 
 
 TORCH_LIBRARY(mpamd, m) {
   m.def("gemm_workspace_bytes() -> int", &gemm_workspace_bytes);
+  m.def("gemm_slab_offset() -> int", &gemm_slab_offset);
+  m.def("gemm_rwk_split(int M, int N, int K, int f8) -> int", &gemm_rwk_split);
   m.def("fp8_gemm_kernel(int kind) -> ()", &fp8_gemm_kernel);
   m.def("gemm_rw_ok(int M, int N, int K, int epilogue, int out_packed) -> bool", &gemm_rw_ok);
   m.def(
@@ -679,7 +723,8 @@ TORCH_LIBRARY(mpamd, m) {
   m.def(
       "paged_attention_rope(Tensor qkv, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor block_tables, Tensor q_seq, "
       "Tensor q_ctx, Tensor positions, Tensor cos, Tensor sin, Tensor slots, Tensor(c!) out, Tensor(d!) workspace, "
-      "int nh, int nkv, float scale, int part_size, int num_parts, int packed, Tensor(e!)? counters=None) -> ()");
+      "int nh, int nkv, float scale, int part_size, int num_parts, int packed, Tensor(e!)? counters=None, "
+      "Tensor? qkv_part=None, int part_splits=0, Tensor? part_ss=None, float inv_k=0., float eps=0.) -> ()");
   m.def(
       "attention_mfma(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor q_seq, Tensor q_ctx, "
       "Tensor qblocks, Tensor(a!) out, Tensor(b!) workspace, int nh, int nkv, float scale, int part_size, "
@@ -691,7 +736,8 @@ TORCH_LIBRARY(mpamd, m) {
   m.def(
       "attention_mfma_rope(Tensor qkv, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor block_tables, Tensor q_seq, "
       "Tensor q_ctx, Tensor qblocks, Tensor positions, Tensor cos, Tensor sin, Tensor slots, Tensor(c!) out, "
-      "Tensor(d!) workspace, int nh, int nkv, float scale, int part_size, int num_parts, int packed) -> ()");
+      "Tensor(d!) workspace, int nh, int nkv, float scale, int part_size, int num_parts, int packed, "
+      "Tensor? qkv_part=None, int part_splits=0, Tensor? part_ss=None, float inv_k=0., float eps=0.) -> ()");
   m.def("embedding(Tensor ids, Tensor table, Tensor(a!) out) -> ()");
   m.def("swiglu(Tensor gu, Tensor(a!) out) -> ()");
   m.def("add(Tensor a, Tensor b, Tensor(a!) y) -> ()");

@@ -78,4 +78,45 @@ __device__ __forceinline__ int64_t apk_off(int row, int col, int MT) {
   return ((((int64_t)(col >> 5) * MT + (row >> 4)) * 64 + ((col >> 3) & 3) * 16 + (row & 15)) << 3) + (col & 7);
 }
 
+// The qkv projection left as split-K partial slabs (decode GEMM flags bit 14, mp_gemm_rwk_split):
+// part[s][row][col] fp32, s < S, plus the fused-norm row statistics (gemm_kernels.h EpiArgs::ss_in:
+// QP_SS_NSH shards of QP_SS_ROWS rows, fixed-point sums of squares).  The decode attention kernels
+// read q / k / v through qkv_part_load8, which is the split-K reduce launch's epilogue 0 inlined:
+// the S slabs summed in split order from zero, times rsqrt(ss / K + eps), rounded to bf16 - the
+// same bits the reduce launch would have stored, without its launch.
+constexpr int QP_SS_NSH = 32, QP_SS_ROWS = 128;
+constexpr float QP_SS_FX = 1048576.f;
+struct QkvPart {
+  const float* part;               // nullptr: read the bf16 qkv rows instead
+  int S;                           // split count
+  int64_t slab;                    // elements per slab (M x ldn)
+  int ldn;                         // row pitch (the qkv width)
+  const unsigned long long* ss;    // row statistics, or nullptr (no row scale)
+  float inv_k, eps;
+};
+
+__device__ __forceinline__ float qkv_part_scale(const QkvPart& qp, int row) {
+  if (qp.ss == nullptr) return 1.f;
+  unsigned long long t = 0;
+#pragma unroll
+  for (int j = 0; j < QP_SS_NSH; ++j) t += qp.ss[j * QP_SS_ROWS + row];
+  return rsqrtf((float)t * (1.f / QP_SS_FX) * qp.inv_k + qp.eps);
+}
+
+__device__ __forceinline__ u16x8 qkv_part_load8(const QkvPart& qp, int row, int col, float rs) {
+  f32x4 a = (f32x4)(0.f), b = (f32x4)(0.f);
+  for (int s = 0; s < qp.S; ++s) {  // fixed split order: the reduce launch's sum
+    const float* p = qp.part + s * qp.slab + (int64_t)row * qp.ldn + col;
+    a += *reinterpret_cast<const f32x4*>(p);
+    b += *reinterpret_cast<const f32x4*>(p + 4);
+  }
+  u16x8 r;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    r[j] = f2bf(a[j] * rs);
+    r[j + 4] = f2bf(b[j] * rs);
+  }
+  return r;
+}
+
 }  // namespace mp

@@ -719,6 +719,7 @@ extern "C" int mp_quant_rows_fp8(const void* x, int64_t xs, void* a8, float* sca
 extern "C" int mp_gemm_fp8(const void* a8, const float* as, const void* wq, const float* ws, void* y, int64_t ys,
                            const void* res, int64_t rs, int M, int N, int K, int epilogue, int out_packed, int kind,
                            float* part, int64_t part_bytes, hipStream_t stream) {
+  (void)hipGetLastError();  // an earlier non-mpamd HIP call's stale error is not this launch's
   using namespace mp;
   if (M == 0) return 0;
   if (M > 64 || K % (64 * F8_GU_MAX) || N % 16) return -1;

@@ -37,6 +37,18 @@ extern "C" int64_t mp_gemm_slab_offset() {
 }
 extern "C" int64_t mp_gemm_slab_bytes() { return mp::RWK_SLAB_BYTES; }
 
+// Split count S of the split-K ring form for this shape (0: not covered): with flags bit 14 the
+// GEMM leaves S fp32 partial slabs [S][M][N] at mp_gemm_slab_offset() of the workspace for a
+// consumer that sums them (fixed order s = 0..S-1 from zero: the reduce launch's bits).
+extern "C" int mp_gemm_rwk_split(int M, int N, int K, int f8) {
+  using namespace mp;
+  if (M < 1 || M > 128 || N % 2048 || K % 128) return 0;
+  int nt, S;
+  rwk_choose(N / 16, K / 32, sk_num_cus(), f8 != 0, nt, S);
+  if (nt == 0 || (int64_t)S * M * N * 4 > RWK_SLAB_BYTES) return 0;
+  return S;
+}
+
 extern "C" int64_t mp_gemm_workspace_bytes() {
   using namespace mp;
   return (int64_t)SK_MAX_GROUPS * sizeof(int) + SK_ZERO_BYTES +
@@ -58,6 +70,7 @@ extern "C" int mp_gemm_bf16(const void* x, int64_t x_stride, const void* w, void
                             const void* res, int64_t res_stride, int M, int N, int K, int epilogue, int flags,
                             void* ws, const int* gate, void* ap, void* ss_out, void* ss_zero, const void* ss_in,
                             float inv_k, float eps, hipStream_t stream) {
+  (void)hipGetLastError();  // an earlier non-mpamd HIP call's stale error is not this launch's
   using namespace mp;
   if (M == 0) return 0;
   if (epilogue == 3 && (ap == nullptr || res == nullptr)) return -5;
@@ -91,6 +104,7 @@ extern "C" int mp_gemm_bf16(const void* x, int64_t x_stride, const void* w, void
     if (rc < 0) return rc;
     if (rc == 0) return (int)hipGetLastError();
   }
+  if (flags & 16384) return -6;  // partials only: nothing else writes them
   if (gate != nullptr) flags &= ~(4 | 16 | 128);  // gated (MoE expert) GEMMs use the one-group kernel
   if ((flags & 1) && (flags & 128) && !(flags & 8)) {  // balanced ring kernel
     if (M <= 16) rc = launch_gemm_rw<1>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, ep, stream);

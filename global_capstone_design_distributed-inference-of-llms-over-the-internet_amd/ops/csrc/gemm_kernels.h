@@ -73,6 +73,8 @@ constexpr int SS_ROWS = 128;        // rows per shard: decode steps of up to 128
 constexpr int SS_PG = 4;            // shard groups a RowScale reduction uses at most (512 / SS_ROWS)
 constexpr float SS_FX = 1048576.f;  // 2^20
 typedef unsigned long long u64;
+static_assert(SS_NSH == QP_SS_NSH && SS_ROWS == QP_SS_ROWS && SS_FX == QP_SS_FX,
+              "row statistics layout shared with the attention kernels' qkv_part_load8");
 
 struct EpiArgs {
   bf16_t* ap;          // EPI 3: packed copy of the output rows (mt_out row tiles)
@@ -1639,9 +1641,32 @@ static inline void launch_splitk_reduce(int S, int epi, dim3 g2, hipStream_t str
 
 // Column-group width NT and split count S with C x S <= #CUs (prefer NT = 4, then 2, 8, 1;
 // 2 <= S <= 8); returns 1 when no split applies (the caller falls back).
+// Split-K ring geometry: column-group width NT and split count S (C x S <= #CUs, 2 <= S <= 8):
+// the width whose grid C x S fills the most CUs, ties to the earlier candidate (qkv, 768 tiles:
+// NT = 6, S = 2 fills 256 CUs where NT = 8, S = 2 leaves 64 idle).  fp8 weights: the bf16
+// activation block costs 2M / (16 NT) x the weight bytes per CU - the widest group first.
+// nt = 0 when no split applies.  MPAMD_RWK_NT (ablation) allows only that width.
+static inline void rwk_choose(int tiles, int nks, int C0, bool f8, int& nt, int& S) {
+  static constexpr int kOrderBf16[5] = {4, 2, 8, 6, 1}, kOrderF8[5] = {8, 4, 2, 6, 1};
+  static const int nt_only = [] {
+    const char* v = getenv("MPAMD_RWK_NT");
+    return v ? atoi(v) : 0;
+  }();
+  nt = S = 0;
+  int best_fill = 0;
+  for (int cand : (f8 ? kOrderF8 : kOrderBf16)) {
+    if ((nt_only && cand != nt_only) || tiles % cand) continue;
+    const int C = tiles / cand, s = C0 / C;
+    if (s >= 2 && s <= 8 && nks >= 4 * s && C * s > best_fill) { nt = cand; S = s; best_fill = C * s; }
+  }
+}
+
 // ``comb``: 0 = reduce launch, 1 = in-launch combine by the last arriver, 2 = symmetric in-launch
 // combine (gemm_rwk_kernel COMB).  Flags: 256 = split-K ring, + 512 -> comb 1, + 2048 -> comb 2.
-static inline int rwk_comb(int flags) { return (flags & 2048) ? 2 : ((flags & 512) ? 1 : 0); }
+static inline int rwk_comb(int flags) {
+  if (flags & 16384) return -1;  // bit 14: fp32 partial slabs only, no reduce launch
+  return (flags & 2048) ? 2 : ((flags & 512) ? 1 : 0);
+}
 
 // symmetric-combine counters [2 per column group] and the error word (last int of the region)
 static inline int* rwk_sym_counters(void* ws) { return (int*)ws + 3 * (SK_MAX_GROUPS / 4); }
@@ -1650,26 +1675,11 @@ template <int MT, bool F8 = false>
 static int launch_gemm_rwk(const void* x, const void* w, void* y, int64_t ys, const void* res, int64_t rs, int M,
                            int N, int K, int epi, const EpiArgs& ep, void* ws, hipStream_t stream,
                            int comb = 0) {
-  const bool inl = comb != 0;
+  const bool inl = comb > 0;
   if (epi == 1 || ws == nullptr || N % 2048 != 0) return 1;
   const int tiles = N / 16, C0 = sk_num_cus(), nks = K / 32;
   int nt = 0, S = 0;
-  // fp8 weights: the bf16 activation block costs 2M / (16 NT) x the weight bytes per CU - the
-  // widest column group first (NT = 8: A and W bytes equal at M = 64)
-  static constexpr int kOrderBf16[4] = {4, 2, 8, 1}, kOrderF8[4] = {8, 4, 2, 1};
-  // MPAMD_RWK_NT (ablation): try this column-group width first
-  static const int nt_first = [] {
-    const char* v = getenv("MPAMD_RWK_NT");
-    return v ? atoi(v) : 0;
-  }();
-  int order[5] = {nt_first, 0, 0, 0, 0};
-  for (int i = 0; i < 4; ++i) order[i + 1] = (F8 ? kOrderF8 : kOrderBf16)[i];
-  for (int cand : order) {
-    if (cand <= 0) continue;
-    if (tiles % cand) continue;
-    const int C = tiles / cand, s = C0 / C;
-    if (s >= 2 && s <= 8 && nks >= 4 * s) { nt = cand; S = s; break; }
-  }
+  rwk_choose(tiles, nks, C0, F8, nt, S);
   if (nt == 0) return 1;
   if ((int64_t)S * M * N * 4 > RWK_SLAB_BYTES) return 1;
   if constexpr (4 * MT * 8 > 192) {
@@ -1695,6 +1705,7 @@ static int launch_gemm_rwk(const void* x, const void* w, void* y, int64_t ys, co
       switch (nt) {
         case 2: MP_RWKI_E(2); break;
         case 4: MP_RWKI_E(4); break;
+        case 6: MP_RWKI_E(6); break;
         default: MP_RWKI_E(8); break;
       }
 #undef MP_RWKI_E
@@ -1706,11 +1717,16 @@ static int launch_gemm_rwk(const void* x, const void* w, void* y, int64_t ys, co
     case 1: hipLaunchKernelGGL((gemm_rwk_kernel<MT, 1, F8>), g1, dim3(RW_WAVES * 64), 0, stream, (const bf16_t*)x, (const bf16_t*)w, part, M, N, K, S, ep, nullptr, 0, nullptr, 0, nullptr); break;
     case 2: hipLaunchKernelGGL((gemm_rwk_kernel<MT, 2, F8>), g1, dim3(RW_WAVES * 64), 0, stream, (const bf16_t*)x, (const bf16_t*)w, part, M, N, K, S, ep, nullptr, 0, nullptr, 0, nullptr); break;
     case 4: hipLaunchKernelGGL((gemm_rwk_kernel<MT, 4, F8>), g1, dim3(RW_WAVES * 64), 0, stream, (const bf16_t*)x, (const bf16_t*)w, part, M, N, K, S, ep, nullptr, 0, nullptr, 0, nullptr); break;
+    case 6:
+      if constexpr (4 * MT * 6 <= 192)
+        hipLaunchKernelGGL((gemm_rwk_kernel<MT, 6, F8>), g1, dim3(RW_WAVES * 64), 0, stream, (const bf16_t*)x, (const bf16_t*)w, part, M, N, K, S, ep, nullptr, 0, nullptr, 0, nullptr);
+      break;
     default:
       if constexpr (4 * MT * 8 <= 192)
         hipLaunchKernelGGL((gemm_rwk_kernel<MT, 8, F8>), g1, dim3(RW_WAVES * 64), 0, stream, (const bf16_t*)x, (const bf16_t*)w, part, M, N, K, S, ep, nullptr, 0, nullptr, 0, nullptr);
       break;
   }
+  if (comb < 0) return 0;  // partials only: the consumer sums the S slabs itself (rwk_split)
   const dim3 g2(N / (256 * SKR_CPT), M);
   launch_splitk_reduce(S, epi, g2, stream, part, M, N, y, ys, res, rs, ep);
   return 0;

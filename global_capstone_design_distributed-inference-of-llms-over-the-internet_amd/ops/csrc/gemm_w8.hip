@@ -11,6 +11,7 @@ extern "C" int mp_gemm_w8(const void* x, const void* wq, const float* wsc, void*
                           const void* res, int64_t res_stride, int M, int N, int K, int epilogue, int flags, void* ws,
                           void* ap, void* ss_out, void* ss_zero, const void* ss_in, float inv_k, float eps,
                           hipStream_t stream) {
+  (void)hipGetLastError();  // an earlier non-mpamd HIP call's stale error is not this launch's
   using namespace mp;
   if (M == 0) return 0;
   if (M > 64 || K % (32 * GU_MAX) || N % 16 || wsc == nullptr) return -1;
@@ -29,6 +30,7 @@ extern "C" int mp_gemm_w8(const void* x, const void* wq, const float* wsc, void*
     if (rc < 0) return rc;
     if (rc == 0) return (int)hipGetLastError();
   }
+  if (flags & 16384) return -6;  // partials only: nothing else writes them
   const int fl = flags | 1;
   if (M <= 16) rc = launch_gemm_rw<1, true>(x, wq, y, y_stride, res, res_stride, M, N, K, epilogue, fl, ep, stream);
   else if (M <= 32) rc = launch_gemm_rw<2, true>(x, wq, y, y_stride, res, res_stride, M, N, K, epilogue, fl, ep, stream);

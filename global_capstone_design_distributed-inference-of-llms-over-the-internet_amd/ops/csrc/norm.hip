@@ -140,6 +140,7 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(
 extern "C" int mp_rmsnorm(const void* x, int64_t x_stride, void* res, int64_t res_stride, const void* w,
                           void* y, int64_t y_stride, const int32_t* rows, int nrows, int H, float eps,
                           int mode, int packed_mt, void* ss_out, void* a8, float* a8_scale, hipStream_t stream) {
+  (void)hipGetLastError();  // an earlier non-mpamd HIP call's stale error is not this launch's
   using namespace mp;
   if (H % 8 != 0 || H > 8 * 256 * 8) return -1;
   if (mode == 3 && (ss_out == nullptr || nrows > 128)) return -2;

@@ -846,6 +846,7 @@ extern "C" int mp_sample(const void* logits, int64_t stride, int R, int V, const
                          const int32_t* top_ks, const float* rep_pens, int32_t* recent, int recent_stride,
                          int32_t* recent_len, const int64_t* seeds, float* ws, int64_t* out, int update,
                          hipStream_t stream) {
+  (void)hipGetLastError();  // an earlier non-mpamd HIP call's stale error is not this launch's
   using namespace mp;
   if (R == 0) return 0;
   if (recent_stride > SB) return -1;

@@ -264,6 +264,9 @@ class StageExecutor:
                     if self._w8 and weights.layers:
                         ops.autotune_w8([(cfg.q_dim + 2 * cfg.kv_dim, H, 0), (H, cfg.q_dim, 3), (2 * F, H, 1),
                                          (H, F, 3)], self.device)
+                    if self._fused and weights.layers and self._fuse_rope:
+                        # qkv as split-K partials summed in the attention kernel, per row bucket
+                        ops.autotune_qkv_fold(cfg.q_dim + 2 * cfg.kv_dim, H, self.device, fp8=bool(self._w8))
                     elif weights.fp8 and weights.layers:
                         ops.autotune_fp8([(cfg.q_dim + 2 * cfg.kv_dim, H, 0), (H, cfg.q_dim, 0), (2 * F, H, 1),
                                           (H, F, 0)], self.device)
@@ -498,22 +501,35 @@ class StageExecutor:
         return ops.paged_attention(qkv, kc, vc, table, q_seq, q_ctx, self.nh, self.nkv, self.scale, out=out,
                                    workspace=ws, part_size=ps, num_parts=np_, packed=packed)
 
+    def _qkv_fold(self, T: int) -> bool:
+        """Decode steps of T rows: qkv as split-K partial slabs folded into the attention kernel's
+        loads (``ops.autotune_qkv_fold`` measured it faster than the chosen qkv GEMM)."""
+        if not (self._fuse_rope and self._fused and self.device.type == "cuda") or \
+                os.environ.get("MPAMD_QKV_FOLD", "1") == "0":
+            return False
+        cfg = self.cfg
+        return ops.qkv_fold(T, cfg.q_dim + 2 * cfg.kv_dim, cfg.hidden_size, bool(self._w8))
+
     def _rope_attend(self, qkv, positions, slots, kc, vc, q_seq, q_ctx, out, ws, ps, np_, packed, qblocks, max_ctx,
-                     decode):
+                     decode, qkv_part=None):
         """RoPE + KV write + attention.  Decode steps that run on the flash-decoding kernel do all
-        three in one launch (ops.paged_attention_rope); everything else keeps rope_kv_write."""
+        three in one launch (ops.paged_attention_rope); everything else keeps rope_kv_write.
+        ``qkv_part``: q / k / v as the qkv GEMM's split-K slabs (decode RoPE paths only)."""
         if decode and qblocks is None and self._fuse_rope and self._attn_mfma_gqa and self.device.type == "cuda":
             T = qkv.shape[0]
             ps2 = 128 * math.ceil(ps / 128)
             np2 = max(1, math.ceil(ps * np_ / ps2))
             return ops.attention_mfma_rope(qkv, kc, vc, self.sessions.table_dev, q_seq, q_ctx, self.decode_qblocks(T),
                                            positions, self.cos, self.sin, slots, self.nh, self.nkv, self.scale,
-                                           out=out, workspace=ws, part_size=ps2, num_parts=np2, packed=packed)
+                                           out=out, workspace=ws, part_size=ps2, num_parts=np2, packed=packed,
+                                           qkv_part=qkv_part)
         if decode and qblocks is None and self._fuse_rope and not (
                 self._attn_mfma_gqa and self.device.type == "cuda"):
             return ops.paged_attention_rope(qkv, kc, vc, self.sessions.table_dev, q_seq, q_ctx, positions, self.cos,
                                             self.sin, slots, self.nh, self.nkv, self.scale, out=out, workspace=ws,
-                                            part_size=ps, num_parts=np_, packed=packed)
+                                            part_size=ps, num_parts=np_, packed=packed, qkv_part=qkv_part)
+        if qkv_part is not None:
+            raise RuntimeError("qkv partial slabs need a fused RoPE decode attention path")
         ops.rope_kv_write(qkv, positions, self.cos, self.sin, kc, vc, slots, self.nh, self.nkv)
         return self._attend(qkv, kc, vc, q_seq, q_ctx, out, ws, ps, np_, packed, qblocks, max_ctx)
 
@@ -588,13 +604,24 @@ class StageExecutor:
             else:
                 def gemm(a, L, name, **kw):
                     return ops.linear(a, None, wp=getattr(L, name + "_p"), a_rows=T, **kw)
+            # decode steps whose qkv GEMM measured faster as split-K partial slabs: the attention
+            # kernel sums the slabs + applies the row scale on its q / k / v loads (no reduce launch)
+            fold = decode and qblocks is None and self._qkv_fold(T)
             for li, L in self._iter_layers(_PACKED_FIELDS):
                 if li == 0:
                     ops.rmsnorm(h, L.input_norm, eps, out=xr, residual=res, mode=3, packed=True, ss=ss_in)
-                gemm(xr, L, "qkv", out=qkv, ss_in=ss_in, eps=eps)
+                qp = None
+                if fold:
+                    if self._w8:
+                        part = ops.linear_partials(xr, T, w8=L.qkv_w8, w_scale=L.qkv_ws, out=qkv)
+                    else:
+                        part = ops.linear_partials(xr, T, wp=L.qkv_p, out=qkv)
+                    qp = (part, ss_in, 1.0 / H, eps)
+                else:
+                    gemm(xr, L, "qkv", out=qkv, ss_in=ss_in, eps=eps)
                 kc, vc = self.cache.layer(li)
                 self._rope_attend(qkv, positions, slots, kc, vc, q_seq, q_ctx, attn, ws, ps, np_, True, qblocks,
-                                  max_ctx, decode)
+                                  max_ctx, decode, qkv_part=qp)
                 gemm(attn, L, "o", out=res, epilogue=3, residual=res, ap_out=xr, ss_out=ss_post, ss_zero=ss_in)
                 gemm(xr, L, "gate_up", out=act, epilogue=1, out_packed=True, ss_in=ss_post, eps=eps)
                 gemm(act, L, "down", out=res, epilogue=3, residual=res, ap_out=xr, ss_out=ss_in, ss_zero=ss_post)
@@ -722,7 +749,9 @@ class StageExecutor:
         sids = [f"__warm{i}__" for i in range(batch)]
         H = self.cfg.hidden_size
         gen = torch.Generator(device=self.device).manual_seed(1)
-        with self.exec_lock, torch.inference_mode():
+        # no_grad, not inference_mode: the decode graph captured here keeps its static buffers,
+        # which later steps (inside or outside inference mode) update in place
+        with self.exec_lock, torch.no_grad():
             try:
                 T = batch * prompt_len
                 if self.is_first:

@@ -67,11 +67,13 @@ def main():
                     sb = torch.from_numpy(ops.query_superblocks(ntoks, nh // nkv)).to(dev)
                     fn = lambda: ops.attention_mfma(q, kc, vc, bt, q_seq, q_ctx, qb, nh, nkv, scale, out=out,  # noqa
                                                     max_ctx=L, superblocks=sb)
-                else:
-                    w = int(k[2:])
+                else:  # fa<waves>[:p<parts>] (parts: explicit context split; "auto": the library's rule)
+                    name, _, pp = k.partition(":")
+                    w = int(name[2:])
+                    nparts = int(pp[1:]) if pp.startswith("p") else None
                     fb = torch.from_numpy(ops.fa_blocks(ntoks, nh // nkv, w)).to(dev)
                     fn = lambda: ops.attention_fa(q, kc, vc, bt, q_seq, q_ctx, fb, nh, nkv, scale, out=out,  # noqa
-                                                  max_ctx=L, waves=w)
+                                                  max_ctx=L, waves=w, num_parts=nparts)
                 us = timeit(fn)
                 o = out.float().clone()
                 if ref_out is None:

@@ -56,13 +56,14 @@ int main(int argc, char** argv) {
     const char* name;
     int N, K, epi;
   };
-  const Shape shapes[] = {{"o", 4096, 4096, 3}, {"down", 4096, 11008, 3}, {"o_e0", 4096, 4096, 0}};
+  const Shape shapes[] = {{"o", 4096, 4096, 3}, {"down", 4096, 11008, 3}, {"o_e0", 4096, 4096, 0},
+                          {"qkv", 12288, 4096, 0}};
   std::vector<int> Ms = {32, 64};
   if (argc > 1) {
     Ms.clear();
     for (char* t = strtok(argv[1], ","); t; t = strtok(nullptr, ",")) Ms.push_back(atoi(t));
   }
-  const Kind kinds[] = {{"pk", 8},          {"pk+r", 8 | 1024},     {"rwk", 256},           {"rwk+r", 256 | 1024},
+  const Kind kinds[] = {{"pk", 8}, {"rw", 128}, {"rw+r", 128 | 1024}, {"rwkp", 256 | 16384},          {"pk+r", 8 | 1024},     {"rwk", 256},           {"rwk+r", 256 | 1024},
                         {"rwki", 256 | 512}, {"rwki+r", 256 | 512 | 1024}, {"rwks", 256 | 2048},
                         {"rwks+r", 256 | 2048 | 1024}, {"rwr", 4096}, {"rwr+r", 4096 | 1024},
                         {"rwrt", 4096 | 8192}, {"rwrt+r", 4096 | 8192 | 1024}};
@@ -71,11 +72,11 @@ int main(int argc, char** argv) {
   unsigned short *pool, *x, *res, *res0, *ap, *yref, *apref;
   CK(hipMalloc(&pool, pool_bytes));
   CK(hipMalloc(&x, (size_t)64 * 11008 * 2));
-  CK(hipMalloc(&res, (size_t)64 * 4096 * 2));
-  CK(hipMalloc(&res0, (size_t)64 * 4096 * 2));
-  CK(hipMalloc(&yref, (size_t)64 * 4096 * 2));
-  CK(hipMalloc(&ap, (size_t)64 * 4096 * 2));
-  CK(hipMalloc(&apref, (size_t)64 * 4096 * 2));
+  CK(hipMalloc(&res, (size_t)64 * 12288 * 2));
+  CK(hipMalloc(&res0, (size_t)64 * 12288 * 2));
+  CK(hipMalloc(&yref, (size_t)64 * 12288 * 2));
+  CK(hipMalloc(&ap, (size_t)64 * 12288 * 2));
+  CK(hipMalloc(&apref, (size_t)64 * 12288 * 2));
   const int ssn = mp_gemm_ss_elems();
   unsigned long long *ss, *ss2, *ssref;
   CK(hipMalloc(&ss, ssn * 8));
@@ -92,7 +93,7 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  std::vector<unsigned short> h0(64 * 4096), h1(64 * 4096);
+  std::vector<unsigned short> h0(64 * 12288), h1(64 * 12288);
   std::vector<unsigned long long> s0(ssn), s1(ssn);
   int bad = 0;
   for (const Shape& s : shapes) {
@@ -110,9 +111,9 @@ int main(int argc, char** argv) {
                               ws, nullptr, ap, ss, ss2, nullptr, 1.f / s.K, 1e-5f, 0);
         };
         // correctness: one call from the saved residual with zeroed statistics
-        CK(hipMemcpy(res, res0, (size_t)64 * 4096 * 2, hipMemcpyDeviceToDevice));
+        CK(hipMemcpy(res, res0, (size_t)64 * 12288 * 2, hipMemcpyDeviceToDevice));
         CK(hipMemset(ss, 0, ssn * 8));
-        CK(hipMemset(ap, 0, (size_t)64 * 4096 * 2));
+        CK(hipMemset(ap, 0, (size_t)64 * 12288 * 2));
         int rc = run(0);
         if (rc) {
           printf("%-6s M=%2d %-7s rc=%d\n", s.name, M, kd.name, rc);
@@ -121,8 +122,8 @@ int main(int argc, char** argv) {
         CK(hipDeviceSynchronize());
         int err = 0;
         CK(hipMemcpy(&err, (int*)ws + mp::SK_MAX_GROUPS - 1, 4, hipMemcpyDeviceToHost));
-        if (kk == 0 || kk == 2) {  // pk: tolerance reference; rwk: bitwise reference of the split-K forms
-          if (kk == 2) {
+        if (kk == 0 || kk == 5) {  // pk: tolerance reference; rwk: bitwise reference of the split-K forms
+          if (kk == 5) {
             CK(hipMemcpy(yref, res, ny * 2, hipMemcpyDeviceToDevice));
             CK(hipMemcpy(apref, ap, ny * 2, hipMemcpyDeviceToDevice));
             CK(hipMemcpy(ssref, ss, ssn * 8, hipMemcpyDeviceToDevice));
@@ -137,7 +138,7 @@ int main(int argc, char** argv) {
           if (!(d <= maxd)) maxd = d;
         }
         long long ndiff = -1;  // bitwise mismatches against rwk (split-K forms only)
-        if ((kd.flags & 256) && !(kd.flags & 1024) && kk >= 2) {  // rotated walks sum in another order
+        if ((kd.flags & 256) && !(kd.flags & 1024) && !(kd.flags & 16384) && kk >= 5) {  // rotated walks sum in another order
           std::vector<unsigned short> r0(ny), a0(ny), a1(ny);
           CK(hipMemcpy(r0.data(), yref, ny * 2, hipMemcpyDeviceToHost));
           CK(hipMemcpy(a0.data(), apref, ny * 2, hipMemcpyDeviceToHost));

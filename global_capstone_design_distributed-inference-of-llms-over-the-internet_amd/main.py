@@ -127,6 +127,11 @@ def build_parser() -> argparse.ArgumentParser:
                    help="client: write every session's generated token ids (JSON) here (harnesses, fault tests)")
     p.add_argument("--max_replicas", type=int, default=0,
                    help="client, device channel: pipelines to open over disjoint same-node routes (0 = all found)")
+    p.add_argument("--replay_cache", action="store_true",
+                   help="client, device channel: stage-local recovery - every non-tail stage keeps its output "
+                        "rows in HBM, so when ONE server of a pipeline dies only its spare is rebuilt (the stage "
+                        "before it replays its rows; every other stage keeps its KV) instead of re-prefilling "
+                        "every session on every stage")
     return p
 
 
@@ -336,12 +341,17 @@ def _run_rank0_channel(args, device, ex, tok, tx, route, ids, on_token=None, res
     rep_routes = {}
     counter = [0]
 
-    def open_replica(rt):
+    replay = bool(getattr(args, "replay_cache", False))
+
+    def open_replica(rt, old=None):
         k = counter[0]
         counter[0] += 1
         ch = tx.open_device_channel(rt, device, n_slots=M, batch=B, timeout=timeout, timing=True,
-                                    data_backend=getattr(args, "channel_data", None))
-        eng = PipelineServingEngine(ex, ch, n_slots=M, batch=B, name=f"client-r{k}", timeout_s=timeout)
+                                    data_backend=getattr(args, "channel_data", None), replay_cache=replay,
+                                    resume_prefix=old.ch.prefix if old is not None else None)
+        eng = PipelineServingEngine(ex, ch, n_slots=M, batch=B, name=f"client-r{k}", timeout_s=timeout,
+                                    replay_cache=replay,
+                                    resume={"prefix": old.name, "cache": old.replay} if old is not None else None)
         eng.freeze_heap = True  # the client is a driver process: one heap freeze per process
         eng.timing = True
         ch.timing = True
@@ -367,6 +377,27 @@ def _run_rank0_channel(args, device, ex, tok, tx, route, ids, on_token=None, res
             old.ch.close()
         live = [k for k in fe.alive_locals() if k != r]
         busy = set().union(*[{h.peer_id for h in rep_routes[k]} for k in live]) if live else set()
+        if replay and len(dead) == 1 and old is not None and old.failed_sessions:
+            # stage-local recovery: swap only the dead hop; the survivors adopt their sessions and
+            # the stage before the spare replays its cached rows into it
+            k = rep_routes[r].index(dead[0])
+            hop = tx.replacement_hop(dead[0], device, exclude=busy | {h.peer_id for h in rep_routes[r]},
+                                     same_node=same_node, wait_s=0.0 if live else max(10.0, args.request_timeout))
+            if hop is not None:
+                rt = rep_routes[r][:k] + [hop] + rep_routes[r][k + 1:]
+                try:
+                    eng, thr = open_replica(rt, old=old)
+                except (ConnectionError, OSError, RuntimeError) as e:
+                    logger.warning(f"stage-local rebuild through {hop.peer_id[:8]} failed ({e}); full rebuild")
+                else:
+                    eng.resume_target = k + 1
+                    eng.resume_from = old
+                    r2 = fe.router.n
+                    rep_routes[r2] = rt
+                    engines[r2] = eng
+                    logger.info(f"rebuilt a pipeline over {[h.peer_id[:8] for h in rt]} (stage {k + 1} replaced, "
+                                f"the other stages keep their KV)")
+                    return eng, thr if thr > 0 else (max(fe.router.throughput) if fe.router.throughput else 1.0)
         new = tx.channel_routes(device, max_routes=1, exclude=busy, same_node=same_node,
                                 wait_s=0.0 if live else max(10.0, args.request_timeout))
         if not new:
@@ -429,7 +460,8 @@ def _run_rank0_channel(args, device, ex, tok, tx, route, ids, on_token=None, res
                 f"tokens per replica {fe.replica_tokens}")
     if fe.failures:
         logger.info(f"failover: {len(fe.failures)} replica failure(s) recovered "
-                    f"({'; '.join(f'replica {r}: {w[:80]}' for r, w in fe.failures)})")
+                    f"({'; '.join(f'replica {r}: {w[:80]}' for r, w in fe.failures)}); "
+                    f"{len(fe.resumed)} session(s) resumed in place, {len(fe.replaced)} re-prefilled")
     # decode rate counts tokens after each session's first one over the time after the first
     # session's first token (as the TCP path does); end-to-end counts everything from t0
     logger.info(f"Decode completed in {t2 - t0 - ttft:.3f}s ({(total - n) / max(t2 - t0 - ttft, 1e-9):.2f} tokens/s "

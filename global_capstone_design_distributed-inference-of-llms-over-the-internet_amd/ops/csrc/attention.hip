@@ -72,6 +72,48 @@ struct RopeFuse {
   QkvPart qp;           // qp.part != nullptr: q / k / v from the qkv GEMM's split-K partials
 };
 
+// x * cos -/+ partner * sin for one 8-element chunk of a head (lo: the chunk is in the first
+// half, its partner in the second), rounded to bf16 - the fused RoPE of the decode kernels.
+__device__ __forceinline__ u16x8 rope8(u16x8 me, u16x8 ot, f32x4 ca, f32x4 cb, f32x4 sa, f32x4 sb, bool lo) {
+  u16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float c = j < 4 ? ca[j] : cb[j - 4], s = j < 4 ? sa[j] : sb[j - 4];
+    const float x = bf2f(me[j]), y = bf2f(ot[j]);
+    r[j] = lo ? f2bf(x * c - y * s) : f2bf(x * c + y * s);
+  }
+  return r;
+}
+
+// The folded qkv projection (rf.qp: split-K partial slabs): the workgroup's NREP rotated query
+// chunks, the rotated new key and the new value of token t, built once into LDS s[(NREP + 2) * D/8]
+// (item-major, 8 columns per entry).  Bit-identical to RoPE over the reduce launch's bf16 row.
+// Every thread of the workgroup must call it (ends in a barrier; qrs from qkv_part_scale).
+template <int D, int NREP>
+__device__ __forceinline__ void fold_qkv_lds(const RopeFuse& rf, int t, int hbase, int g, int nh, int nkv, float qrs,
+                                             u16x8* s) {
+  constexpr int LPT = D / 8, HALF = D / 2;
+  const int64_t ps_ = rf.pos[t];
+  for (int i = threadIdx.x; i < (NREP + 2) * LPT; i += blockDim.x) {
+    const int item = i / LPT, sl = i % LPT;
+    const int hc = item < NREP ? (hbase + item) * D : item == NREP ? (nh + g) * D : (nh + nkv + g) * D;
+    const u16x8 me = qkv_part_load8(rf.qp, t, hc + sl * 8, qrs);
+    if (item == NREP + 1) {
+      s[i] = me;  // the value: no rotation
+      continue;
+    }
+    const int c0 = (sl * 8) & (HALF - 1);
+    const bool lo = sl * 8 < HALF;
+    const u16x8 ot = qkv_part_load8(rf.qp, t, hc + sl * 8 + (lo ? HALF : -HALF), qrs);
+    const f32x4 ca = *reinterpret_cast<const f32x4*>(rf.cos_t + ps_ * HALF + c0);
+    const f32x4 cb = *reinterpret_cast<const f32x4*>(rf.cos_t + ps_ * HALF + c0 + 4);
+    const f32x4 sa = *reinterpret_cast<const f32x4*>(rf.sin_t + ps_ * HALF + c0);
+    const f32x4 sb = *reinterpret_cast<const f32x4*>(rf.sin_t + ps_ * HALF + c0 + 4);
+    s[i] = rope8(me, ot, ca, cb, sa, sb, lo);
+  }
+  __syncthreads();
+}
+
 // In-launch split-K combine (NP > 1 with a counter buffer): every context-slice workgroup of a
 // (query, head group) publishes its partials (plain stores, every wave drained, one agent-scope
 // release by lane 0 before the arrival ticket), and the LAST arriver (ticket NP - 1) acquires,
@@ -174,36 +216,39 @@ __global__ __launch_bounds__(256) void paged_attn_kernel(
     const int c0 = (sl * 8) & (HALF - 1);
     const bool lo = sl * 8 < HALF;
     const int po = lo ? HALF : -HALF;
-    const float qrs = rf.qp.part != nullptr ? qkv_part_scale(rf.qp, t) : 1.f;
-    auto ld8 = [&](int col) -> u16x8 {  // element col of this token's fused qkv row
-      return rf.qp.part != nullptr ? qkv_part_load8(rf.qp, t, col, qrs)
-                                   : *reinterpret_cast<const u16x8*>(row + col);
-    };
-    const int64_t ps_ = rf.pos[t];
-    const f32x4 ca = *reinterpret_cast<const f32x4*>(rf.cos_t + ps_ * HALF + c0);
-    const f32x4 cb = *reinterpret_cast<const f32x4*>(rf.cos_t + ps_ * HALF + c0 + 4);
-    const f32x4 sa = *reinterpret_cast<const f32x4*>(rf.sin_t + ps_ * HALF + c0);
-    const f32x4 sb = *reinterpret_cast<const f32x4*>(rf.sin_t + ps_ * HALF + c0 + 4);
-    auto rot = [&](int hc) {  // hc: first column of the head in the qkv row
-      const u16x8 me = ld8(hc + sl * 8);
-      const u16x8 ot = ld8(hc + sl * 8 + po);
-      u16x8 r;
+    if (rf.qp.part != nullptr) {
+      // the qkv split-K partials: this workgroup's q / k / v chunks built once into LDS (every slab
+      // element read once per workgroup, not once per token group of every wave)
+      __shared__ u16x8 s_fold[(NREP + 2) * LPT];
+      fold_qkv_lds<D, NREP>(rf, t, hbase, g, nh, nkv, qkv_part_scale(rf.qp, t), s_fold);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float c = j < 4 ? ca[j] : cb[j - 4], s = j < 4 ? sa[j] : sb[j - 4];
-        const float x = bf2f(me[j]), y = bf2f(ot[j]);
-        r[j] = lo ? f2bf(x * c - y * s) : f2bf(x * c + y * s);
+      for (int r = 0; r < NREP; ++r) {
+        const u16x8 v = s_fold[r * LPT + sl];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) qf[r][j] = bf2f(v[j]) * scale_log2;
       }
-      return r;
-    };
+      kn = s_fold[NREP * LPT + sl];
+      vn = s_fold[(NREP + 1) * LPT + sl];
+    } else {
+      const int64_t ps_ = rf.pos[t];
+      const f32x4 ca = *reinterpret_cast<const f32x4*>(rf.cos_t + ps_ * HALF + c0);
+      const f32x4 cb = *reinterpret_cast<const f32x4*>(rf.cos_t + ps_ * HALF + c0 + 4);
+      const f32x4 sa = *reinterpret_cast<const f32x4*>(rf.sin_t + ps_ * HALF + c0);
+      const f32x4 sb = *reinterpret_cast<const f32x4*>(rf.sin_t + ps_ * HALF + c0 + 4);
+      auto rot = [&](int hc) {  // hc: first column of the head in the qkv row
+        const u16x8 me = *reinterpret_cast<const u16x8*>(row + hc + sl * 8);
+        const u16x8 ot = *reinterpret_cast<const u16x8*>(row + hc + sl * 8 + po);
+        return rope8(me, ot, ca, cb, sa, sb, lo);
+      };
 #pragma unroll
-    for (int r = 0; r < NREP; ++r) {
-      const u16x8 v = rot((hbase + r) * D);
+      for (int r = 0; r < NREP; ++r) {
+        const u16x8 v = rot((hbase + r) * D);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) qf[r][j] = bf2f(v[j]) * scale_log2;
+        for (int j = 0; j < 8; ++j) qf[r][j] = bf2f(v[j]) * scale_log2;
+      }
+      kn = rot((nh + g) * D);
+      vn = *reinterpret_cast<const u16x8*>(row + (nh + nkv + g) * D + sl * 8);
     }
-    kn = rot((nh + g) * D);
-    vn = ld8((nh + nkv + g) * D + sl * 8);
     tnew = ctx - 1;
     const int64_t slot = rf.slots[t];
     if (tnew >= start && tnew < end && slot >= 0 && tid < LPT && hbase % (nh / nkv) == 0) {
@@ -477,36 +522,39 @@ __global__ __launch_bounds__(NW * 64) void paged_attn1_kernel(
     const int c0 = (sl * 8) & (HALF - 1);
     const bool lo = sl * 8 < HALF;
     const int po = lo ? HALF : -HALF;
-    const float qrs = rf.qp.part != nullptr ? qkv_part_scale(rf.qp, t) : 1.f;
-    auto ld8 = [&](int col) -> u16x8 {  // element col of this token's fused qkv row
-      return rf.qp.part != nullptr ? qkv_part_load8(rf.qp, t, col, qrs)
-                                   : *reinterpret_cast<const u16x8*>(row + col);
-    };
-    const int64_t ps_ = rf.pos[t];
-    const f32x4 ca = *reinterpret_cast<const f32x4*>(rf.cos_t + ps_ * HALF + c0);
-    const f32x4 cb = *reinterpret_cast<const f32x4*>(rf.cos_t + ps_ * HALF + c0 + 4);
-    const f32x4 sa = *reinterpret_cast<const f32x4*>(rf.sin_t + ps_ * HALF + c0);
-    const f32x4 sb = *reinterpret_cast<const f32x4*>(rf.sin_t + ps_ * HALF + c0 + 4);
-    auto rot = [&](int hc) {  // hc: first column of the head in the qkv row
-      const u16x8 me = ld8(hc + sl * 8);
-      const u16x8 ot = ld8(hc + sl * 8 + po);
-      u16x8 r;
+    if (rf.qp.part != nullptr) {
+      // the qkv split-K partials: this workgroup's q / k / v chunks built once into LDS (every slab
+      // element read once per workgroup, not once per token group of every wave)
+      __shared__ u16x8 s_fold[(NREP + 2) * LPT];
+      fold_qkv_lds<D, NREP>(rf, t, hbase, g, nh, nkv, qkv_part_scale(rf.qp, t), s_fold);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float c = j < 4 ? ca[j] : cb[j - 4], s = j < 4 ? sa[j] : sb[j - 4];
-        const float x = bf2f(me[j]), y = bf2f(ot[j]);
-        r[j] = lo ? f2bf(x * c - y * s) : f2bf(x * c + y * s);
+      for (int r = 0; r < NREP; ++r) {
+        const u16x8 v = s_fold[r * LPT + sl];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) qf[r][j] = bf2f(v[j]) * scale_log2;
       }
-      return r;
-    };
+      kn = s_fold[NREP * LPT + sl];
+      vn = s_fold[(NREP + 1) * LPT + sl];
+    } else {
+      const int64_t ps_ = rf.pos[t];
+      const f32x4 ca = *reinterpret_cast<const f32x4*>(rf.cos_t + ps_ * HALF + c0);
+      const f32x4 cb = *reinterpret_cast<const f32x4*>(rf.cos_t + ps_ * HALF + c0 + 4);
+      const f32x4 sa = *reinterpret_cast<const f32x4*>(rf.sin_t + ps_ * HALF + c0);
+      const f32x4 sb = *reinterpret_cast<const f32x4*>(rf.sin_t + ps_ * HALF + c0 + 4);
+      auto rot = [&](int hc) {  // hc: first column of the head in the qkv row
+        const u16x8 me = *reinterpret_cast<const u16x8*>(row + hc + sl * 8);
+        const u16x8 ot = *reinterpret_cast<const u16x8*>(row + hc + sl * 8 + po);
+        return rope8(me, ot, ca, cb, sa, sb, lo);
+      };
 #pragma unroll
-    for (int r = 0; r < NREP; ++r) {
-      const u16x8 v = rot((hbase + r) * D);
+      for (int r = 0; r < NREP; ++r) {
+        const u16x8 v = rot((hbase + r) * D);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) qf[r][j] = bf2f(v[j]) * scale_log2;
+        for (int j = 0; j < 8; ++j) qf[r][j] = bf2f(v[j]) * scale_log2;
+      }
+      kn = rot((nh + g) * D);
+      vn = *reinterpret_cast<const u16x8*>(row + (nh + nkv + g) * D + sl * 8);
     }
-    kn = rot((nh + g) * D);
-    vn = ld8((nh + nkv + g) * D + sl * 8);
     tnew = ctx - 1;
     const int64_t slot = rf.slots[t];
     if (tnew >= start && tnew < end && slot >= 0 && tid < LPT && hbase % (nh / nkv) == 0) {

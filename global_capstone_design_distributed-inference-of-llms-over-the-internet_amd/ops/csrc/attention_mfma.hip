@@ -121,19 +121,27 @@ __global__ __launch_bounds__(256, 2) void attn_mfma_kernel(
   if (b_first < end) pg_cur = bt[b_first >> page_log2];
   if (b_first + 128 < end) pg_next = bt[(b_first + 128) >> page_log2];
 
-  // ROPE with qkv partials: this block's token row of the fused qkv, summed from the split-K slabs
-  // and row-scaled on the fly (common.h qkv_part_load8: the reduce launch's bits)
+  // ROPE with qkv partials (decode blocks, one token): the block's HB query heads, its key and its
+  // value summed from the split-K slabs, row-scaled and rounded (common.h qkv_part_load8: the
+  // reduce launch's bits) ONCE per block into LDS - every slab element read once, not once per
+  // lane group of every wave; the RoPE below then reads them as it would the bf16 qkv row
+  constexpr int CK = D / 8;  // 8-column chunks per head
+  __shared__ u16x8 s_fold[(HB + 2) * CK];
   const bool from_part = ROPE && rf.qp.part != nullptr;
-  const float qrs = from_part ? qkv_part_scale(rf.qp, tok0) : 1.f;
-  auto ld8 = [&](int col) -> u16x8 {  // element col of the block's (first) token's qkv row
-    return from_part ? qkv_part_load8(rf.qp, tok0, col, qrs)
-                     : *reinterpret_cast<const u16x8*>(q + (int64_t)tok0 * q_stride + col);
-  };
+  if (from_part) {
+    const float qrs = qkv_part_scale(rf.qp, tok0);
+    for (int i = tid; i < (HB + 2) * CK; i += blockDim.x) {
+      const int item = i / CK, cc = (i % CK) * 8;
+      const int col = (item < HB ? (hbase + item) * D : item == HB ? (nh + g) * D : (nh + nkv + g) * D) + cc;
+      s_fold[i] = qkv_part_load8(rf.qp, tok0, col, qrs);
+    }
+    __syncthreads();
+  }
   u16x8 qf[KD];
 #pragma unroll
   for (int kd = 0; kd < KD; ++kd) {
     if (row_ok) {
-      qf[kd] = from_part ? ld8(my_h * D + kd * 32 + qd * 8)
+      qf[kd] = from_part ? s_fold[(my_h - hbase) * CK + kd * 4 + qd]
                          : *reinterpret_cast<const u16x8*>(q + (int64_t)(tok0 + my_t) * q_stride + (int64_t)my_h * D +
                                                            kd * 32 + qd * 8);
     } else {
@@ -153,9 +161,13 @@ __global__ __launch_bounds__(256, 2) void attn_mfma_kernel(
     constexpr int HK = KD / 2, HALF = D / 2;
     const int64_t ps_ = rf.pos[tok0];
     u16x8 kr[KD];
+    const bf16_t* qrow = q + (int64_t)tok0 * q_stride;
 #pragma unroll
-    for (int kd = 0; kd < KD; ++kd) kr[kd] = ld8((nh + g) * D + kd * 32 + qd * 8);
-    vn = ld8((nh + nkv + g) * D + ((lane * 8) % D));
+    for (int kd = 0; kd < KD; ++kd)
+      kr[kd] = from_part ? s_fold[HB * CK + kd * 4 + qd]
+                         : *reinterpret_cast<const u16x8*>(qrow + (nh + g) * D + kd * 32 + qd * 8);
+    vn = from_part ? s_fold[(HB + 1) * CK + ((lane * 8) % D) / 8]
+                   : *reinterpret_cast<const u16x8*>(qrow + (nh + nkv + g) * D + ((lane * 8) % D));
     f32x4 cs[HK][2], sn[HK][2];
 #pragma unroll
     for (int h = 0; h < HK; ++h) {

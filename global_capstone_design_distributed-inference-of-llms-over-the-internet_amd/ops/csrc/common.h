@@ -95,11 +95,14 @@ struct QkvPart {
   float inv_k, eps;
 };
 
+// Every lane of the wave must call it (a wave reduction): lane j < QP_SS_NSH loads shard j, the
+// integer sum is exact in any order.
 __device__ __forceinline__ float qkv_part_scale(const QkvPart& qp, int row) {
   if (qp.ss == nullptr) return 1.f;
-  unsigned long long t = 0;
+  const int lane = threadIdx.x & 63;
+  unsigned long long t = lane < QP_SS_NSH ? qp.ss[lane * QP_SS_ROWS + row] : 0ull;
 #pragma unroll
-  for (int j = 0; j < QP_SS_NSH; ++j) t += qp.ss[j * QP_SS_ROWS + row];
+  for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
   return rsqrtf((float)t * (1.f / QP_SS_FX) * qp.inv_k + qp.eps);
 }
 

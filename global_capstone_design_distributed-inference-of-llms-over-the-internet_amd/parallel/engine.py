@@ -68,7 +68,8 @@ from .channel import Channel, ChannelError, wait_event
 
 logger = logging.getLogger(__name__)
 
-KIND_STEP, KIND_STOP, KIND_STATS = 0, 1, 2
+KIND_STEP, KIND_STOP, KIND_STATS, KIND_REPLAY = 0, 1, 2, 3
+REPLAY_REC = 3   # new handle, replayed length L, handle in the failed channel
 F_RESET, F_SAMPLE = 1, 2
 HDR = 8          # kind, slot, n_seq, T, n_close, n_admit, round, reserved
 SEQ_REC = 5      # handle, n_tok, start, flags, seed
@@ -193,6 +194,24 @@ class TailSampler:
         self._cur_key: Optional[bytes] = None
         self._cur: Optional[dict] = None
 
+    def warm(self, rows: int) -> None:
+        """First-call costs of the serving path's sampler bookkeeping (admission scatter, history
+        gather / write-back, the staged seed copy, the sampling kernel at ``rows`` rows) paid at
+        start-up on scratch records for handles 0..rows-1, which every real admission overwrites."""
+        n = min(int(rows), self.temp.shape[0])
+        if n <= 0 or self.device.type != "cuda":
+            return
+        recs = np.zeros((n, ADM_REC), dtype=np.int64)
+        recs[:, 0] = np.arange(n)
+        recs[:, 1], recs[:, 2], recs[:, 3], recs[:, 4] = _f2i(1.0), _f2i(0.92), 50, _f2i(1.5)
+        self.admit(recs)
+        logits = torch.zeros(n, self.vocab, dtype=torch.bfloat16, device=self.device)
+        self.sample(logits, np.arange(n, dtype=np.int64), np.zeros(n, dtype=np.int64))
+        self._writeback()
+        self.hist_len.zero_()
+        self.hist.zero_()
+        torch.cuda.synchronize(self.device)
+
     def _writeback(self) -> None:
         if self._cur is not None:
             c = self._cur
@@ -279,6 +298,40 @@ class TailSampler:
                           workspace=ws, update_history=True)
 
 
+# ====================================================================== stage-local recovery
+class ReplayCache:
+    """A non-tail stage's OUTPUT hidden states per session and position, in HBM - the reference
+    client's per-hop input cache (src/rpc_transport.py:741,805; replayed to a replacement server
+    by ``_replay_past_inputs`` :670-712) kept where the data already is.  When the next stage dies
+    and a spare takes over its blocks, this stage replays the cached rows of every unfinished
+    session to the spare, which rebuilds its KV with one prefill; every other surviving stage keeps
+    its KV (adopted into the new channel) and does no work.  One ``index_copy_`` per step."""
+
+    def __init__(self, max_handles: int, max_len: int, hidden: int, dtype, device):
+        self.max_len = int(max_len)
+        self.buf = torch.zeros(int(max_handles) * self.max_len, hidden, dtype=dtype, device=device)
+
+    def store(self, recs, out: torch.Tensor) -> None:
+        """``recs``: the step's (handle, n_tokens, start, ...) records, ``out`` its [T, H] rows."""
+        idx, keep, off = [], [], 0
+        for r in recs:
+            h, n, st = int(r[0]), int(r[1]), int(r[2])
+            pos = np.arange(st, st + n)
+            ok = pos < self.max_len
+            idx.append(h * self.max_len + pos[ok])
+            keep.append(off + np.nonzero(ok)[0])
+            off += n
+        if not idx:
+            return
+        idx, keep = np.concatenate(idx), np.concatenate(keep)
+        dev = self.buf.device
+        src = out if len(keep) == out.shape[0] else out.index_select(0, torch.from_numpy(keep).to(dev))
+        self.buf.index_copy_(0, torch.from_numpy(idx.astype(np.int64)).to(dev), src)
+
+    def rows(self, handle: int, n: int) -> torch.Tensor:
+        return self.buf[int(handle) * self.max_len: int(handle) * self.max_len + int(n)]
+
+
 # ====================================================================== head-side state
 @dataclasses.dataclass
 class _Live:
@@ -311,7 +364,8 @@ class PipelineServingEngine:
     def __init__(self, executor: StageExecutor, channel: Optional[Channel], *, n_slots: Optional[int] = None,
                  batch: int = 64, max_step_tokens: Optional[int] = None, prefill_chunk: Optional[int] = None,
                  timeout_s: float = 120.0, max_handles: Optional[int] = None, timing: bool = False,
-                 name: str = "pipe", warmup: Optional[bool] = None):
+                 name: str = "pipe", warmup: Optional[bool] = None, replay_cache: bool = False,
+                 resume: Optional[dict] = None):
         self.ex = executor
         self.ch = channel
         self.rank = channel.rank if channel is not None else 0
@@ -354,12 +408,20 @@ class PipelineServingEngine:
             self.reserved_tokens = 0
             self.tokens_generated = 0
         self._exchange_capacity()
+        # stage-local recovery (opt-in): park KV on failure, keep a replay cache of the outputs
+        self.park_on_fail = bool(replay_cache)
+        self.replay = (ReplayCache(self.max_handles, self.max_len, self.H, executor.dtype, self.dev)
+                       if replay_cache and not self.is_tail else None)
+        self.resume = dict(resume or {})  # {"prefix": failed channel's engine name, "cache": its ReplayCache}
+        self.failed_sessions: Dict[str, Tuple[int, Request]] = {}  # head: rid -> (handle, request) at failure
         if warmup is None:
             warmup = self.dev.type == "cuda" and os.environ.get("MPAMD_WARMUP", "1") != "0"
         if warmup:
             # the first steps' real shapes (a batch-wide ragged prefill, the decode graph of the
             # batch bucket, the sampler at batch rows): the first request pays no first-call costs
             self.ex.warmup_serving(self.B, max(1, min(self.max_step_tokens // max(self.B, 1), 512)))
+            if self.is_tail:
+                self.sampler.warm(self.B)
 
     # ------------------------------------------------------------------ setup
     def _exchange_capacity(self) -> None:
@@ -640,6 +702,8 @@ class PipelineServingEngine:
             e0.record()
         with trace_range(f"pp.rank{self.rank}.slot{m}"):
             out = ex.forward(seqs, x, reset=reset, starts=starts, max_length=self.max_len, hook_owner=self)
+        if self.replay is not None:
+            self.replay.store(seq_recs, out)
         if e1 is not None:
             e1.record()
             self._events.append((e0, e1))
@@ -672,6 +736,12 @@ class PipelineServingEngine:
             if not self.is_tail:
                 self.ch.send_msg(self.rank + 1, hdr)
             self.ch.all_gather_floats(self._stats_row())
+            return True
+        if kind == KIND_REPLAY:
+            if not self.is_tail:
+                self.ch.send_msg(self.rank + 1, hdr)
+            self._replay_step(hdr)
+            self.steps_run += 1
             return True
         m, n_seq, T, n_close = int(hdr[1]), int(hdr[2]), int(hdr[3]), int(hdr[4])
         if not self.is_tail:
@@ -795,12 +865,138 @@ class PipelineServingEngine:
             with self.ex.exec_lock:  # the head's rows / pages go back to the (shared) executor
                 for m in range(self.M):
                     for lv in self.slots[m]:
-                        self.ex.sessions.close(self._key(lv.handle))
+                        if not lv.req.done:
+                            self.failed_sessions[lv.req.rid] = (lv.handle, lv.req)
+                        if not self.park_on_fail:
+                            self.ex.sessions.close(self._key(lv.handle))
                     self.slots[m] = []
                 self.live.clear()
                 self.queue = []
+            if self.park_on_fail:
+                self.park_sessions()
             raise PipelineFailure(why, pend)
+        if self.park_on_fail:
+            self.park_sessions()
         raise PipelineFailure(why)
+
+    # ------------------------------------------------------------------ stage-local recovery
+    def park_sessions(self) -> int:
+        """Keep this engine's KV past its channel's failure under ``park:<name>:<handle>`` keys (the
+        session TTL still evicts them) so a replacement channel can adopt them."""
+        pre, n = self.name + ":", 0
+        with self.ex.exec_lock:
+            for sid in [k for k in self.ex.sessions.sessions if k.startswith(pre)]:
+                self.ex.sessions.rename(sid, "park:" + sid)
+                n += 1
+        return n
+
+    def _adopt(self, handle: int, length: int, old_handle: int) -> Tuple[bool, bool]:
+        """Take over the failed channel's session ``old_handle`` as ``handle``: its KV (truncated to
+        ``length``: a step in flight at the failure may have reached some stages) and its replay
+        rows.  The failed engine's keys are ``<old>:<handle>`` (its thread may not have noticed
+        the failure yet) or, parked, ``park:<old>:<handle>``.  Returns (KV found, rows found)."""
+        old = self.resume.get("prefix")
+        if old is None:
+            return False, False
+        s = None
+        for key in (f"{old}:{int(old_handle)}", f"park:{old}:{int(old_handle)}"):
+            s = self.ex.sessions.rename(key, self._key(int(handle)))
+            if s is not None:
+                s.length = min(s.length, int(length))
+                break
+        cache = self.resume.get("cache")
+        rows = self.replay is not None and cache is not None and 0 < length <= cache.max_len
+        if rows:
+            self.replay.rows(handle, length).copy_(cache.rows(old_handle, length))
+        return s is not None, rows
+
+    def _replay_step(self, hdr: np.ndarray) -> None:
+        """REPLAY header: adopt the listed sessions; the stage before ``target`` sends its cached
+        output rows, the ``target`` (the replacement) prefills them (rebuilding its KV), everyone
+        else only adopts; the tail also admits the sessions' sampling state.  A survivor that lost
+        a session's KV (evicted) or the source's rows fails the channel loudly: the front end then
+        re-places the sessions by re-prefill."""
+        n, T, target, n_adm = int(hdr[2]), int(hdr[3]), int(hdr[4]), int(hdr[5])
+        recs = hdr[HDR:HDR + REPLAY_REC * n].reshape(n, REPLAY_REC)
+        adm = hdr[HDR + REPLAY_REC * n:HDR + REPLAY_REC * n + ADM_REC * n_adm].reshape(n_adm, ADM_REC)
+        with self.ex.exec_lock:
+            lost = 0
+            for h, L, oh in recs:
+                kv, rows = self._adopt(int(h), int(L), int(oh))
+                lost += int(self.rank != target and not kv) + int(self.rank == target - 1 and not rows)
+            if lost:
+                self._fail(f"replay: {lost} session state(s) missing on rank {self.rank}")
+            if self.rank == target - 1:
+                x = torch.cat([self.replay.rows(int(h), int(L)) for h, L, _ in recs])
+                self.ch.send(self.rank + 1, x)
+            elif self.rank == target:
+                _, waiter = self.ch.recv(self.rank - 1, (T, self.H), self.ex.dtype)
+                x = waiter()
+                out = self.ex.forward([(self._key(int(h)), int(L)) for h, L, _ in recs], x, reset=[True] * n,
+                                      max_length=self.max_len)
+                if self.replay is not None:
+                    self.replay.store([(int(h), int(L), 0) for h, L, _ in recs], out)
+            if self.is_tail and n_adm:
+                self.sampler.admit(adm)
+        logger.info(f"[{self.name} rank {self.rank}] replay: " +
+                    (f"rebuilt the KV of {n} session(s) from {T} replayed rows" if self.rank == target
+                     else f"adopted {n} session(s)"))
+
+    def resume_sessions(self, items: Sequence[Tuple[Request, int, int]], target: int) -> List[Request]:
+        """Head of the channel that replaced a failed one (same surviving servers, a spare in
+        position ``target``): continue ``items`` = (request, its handle in the failed channel, L =
+        tokens every stage had processed: prompt + all generated but the last) without
+        re-prefilling - the survivors adopt their KV, the stage before ``target`` replays its cached
+        outputs to the spare, and decoding resumes by feeding each session's last token at position
+        L.  Returns the requests resumed (the rest should be re-placed the usual way)."""
+        if not self.is_head or self.ch is None or not (0 < target < self.S):
+            return []
+        done: List[Tuple[_Live, int]] = []
+        with self.ex.exec_lock:
+            for req, oh, L in items:
+                if L <= 0 or not req.generated or not self.free_handles or L > self.max_len:
+                    continue
+                m = min(range(self.M), key=lambda k: len(self.slots[k]))
+                if len(self.slots[m]) >= self.B:
+                    continue
+                res = self._reserve(req)
+                if self.reserved_tokens + res > self.capacity_tokens:
+                    continue
+                h = self.free_handles.pop()
+                kv, rows = self._adopt(h, int(L), int(oh))
+                if not kv or (target == 1 and not rows):
+                    self.ex.sessions.close(self._key(h))
+                    self.free_handles.append(h)
+                    continue  # the head lost it: re-placed by re-prefill instead
+                lv = _Live(req, h, m, fed=int(L), pending=[int(req.generated[-1])], admitted=True)
+                self.reserved_tokens += res
+                self.slots[m].append(lv)
+                self.live[req.rid] = lv
+                req._repeat = repeat_run(req.generated)
+                done.append((lv, int(oh)))
+        if not done:
+            return []
+        recs = np.asarray([(lv.handle, lv.fed, oh) for lv, oh in done], dtype=np.int64)
+        hdr = np.zeros(HDR + REPLAY_REC * len(done) + ADM_REC * len(done), dtype=np.int64)
+        hdr[:HDR] = (KIND_REPLAY, 0, len(done), int(recs[:, 1].sum()), int(target), len(done), self.rounds, 0)
+        hdr[HDR:HDR + REPLAY_REC * len(done)] = recs.reshape(-1)
+        off = HDR + REPLAY_REC * len(done)
+        for lv, _ in done:
+            p = lv.req.params
+            hist = list(lv.req.generated)[-RECENT:]  # what the sampler held when the last token was drawn
+            hdr[off:off + 6] = (lv.handle, _f2i(p.temperature), _f2i(p.top_p), int(p.top_k),
+                                _f2i(p.repetition_penalty), len(hist))
+            hdr[off + 6:off + 6 + len(hist)] = hist
+            off += ADM_REC
+        try:
+            self.ch.send_msg(1, hdr)
+            if target == 1:
+                self.ch.send(1, torch.cat([self.replay.rows(lv.handle, lv.fed) for lv, _ in done]))
+        except ChannelError as e:
+            self._fail(str(e))
+        logger.info(f"[{self.name}] stage-local recovery: {len(done)} session(s) resumed, stage {target} "
+                    f"rebuilt from {sum(lv.fed for lv, _ in done)} replayed rows")
+        return [lv.req for lv, _ in done]
 
     def _stats_row(self) -> List[float]:
         st = self.ch.stats(reset=True) if self.ch is not None else {"recv_wait_ms": 0.0, "bytes_sent": 0}

@@ -180,6 +180,7 @@ class ReplicaFrontend:
         self.failure_times: List[float] = []  # perf_counter() of each failure (drill reporting)
         self.replaced: Dict[int, int] = {}    # re-placed session -> tokens it had at its failure
         self.at_failure: Dict[int, int] = {}  # every session -> tokens it had at the first failure
+        self.resumed: Dict[int, int] = {}     # session resumed in place (stage-local) -> tokens at failure
         self._next = 0
         self._threads: List[threading.Thread] = []
         self.replica_tokens = [0] * self.n
@@ -325,6 +326,7 @@ class ReplicaFrontend:
                     self.locals[r2] = eng
                     self._attach(r2, eng)
                     logger.info(f"replica {r2} joined (rebuilt after replica {r} failed)")
+                    self._resume(r, r2, eng)
             # every unfinished session placed on r (delivered or still pending) moves to a
             # survivor, which re-prefills prompt + generated tokens (the master copies)
             plans = self.router.fail(r)
@@ -333,6 +335,31 @@ class ReplicaFrontend:
                 rid = int(plan.session_id)
                 self.pending[plan.replica].append(rid)
                 self.replaced.setdefault(rid, len(self.requests[rid].generated))
+
+    def _resume(self, r: int, r2: int, eng: PipelineServingEngine) -> None:
+        """Stage-local recovery: a rebuilt replica that replaced only the dead stage of replica
+        ``r`` (``eng.resume_target`` = that stage's rank, ``eng.resume_from`` = r's failed head)
+        continues r's unfinished sessions from their KV (``PipelineServingEngine.resume_sessions``)
+        - no re-prefill; whatever it cannot resume is re-placed by ``router.fail`` as usual."""
+        target, old = int(getattr(eng, "resume_target", 0) or 0), getattr(eng, "resume_from", None)
+        if target <= 0 or old is None:
+            return
+        items = []
+        for rid_s, (oh, _) in old.failed_sessions.items():
+            rid = int(rid_s)
+            m = self.requests.get(rid)
+            if m is None or m.done or self.router.placement.get(str(rid)) != r or not m.generated:
+                continue
+            req = Request(list(m.prompt), max_new_tokens=m.max_new_tokens, params=m.params,
+                          eos_token_id=m.eos_token_id, stop_on_repeat=m.stop_on_repeat, seed=m.seed,
+                          rid=str(rid), generated=list(m.generated))
+            items.append((req, int(oh), len(m.prompt) + len(m.generated) - 1))
+        for req in eng.resume_sessions(items, target):
+            rid = int(req.rid)
+            self.router.placement[str(rid)] = r2
+            if rid in self.pending.get(r, []):
+                self.pending[r].remove(rid)
+            self.resumed[rid] = len(req.generated)
 
     def _remote_loop(self, r: int, link: HostLink) -> None:
         try:

@@ -34,6 +34,7 @@ import asyncio
 import concurrent.futures
 import dataclasses
 import logging
+import threading
 import time
 from typing import Dict, List, Optional
 
@@ -99,6 +100,10 @@ class StageConnectionHandler:
         self.prioritizer = prioritizer or TaskPrioritizer()
         self._client: Optional[RpcClient] = None  # for push forwarding (created on the server loop)
         self._steps: Dict[str, Dict[str, Message]] = {}  # session -> step_id -> reply (dedup, rpc_inference)
+        # device-channel engines by channel name: a channel that failed stays here (its sessions
+        # parked, its replay cache alive) until a replacement channel adopts it (stage-local recovery)
+        self._chan_engines: Dict[str, object] = {}
+        self._chan_lock = threading.Lock()
         self.stats = {"requests": 0, "batches": 0, "tokens": 0, "pushed": 0}
         self.timer = PhaseTimer()  # host wall time per phase (+ roctx ranges when MPAMD_TRACE=1)
 
@@ -210,9 +215,20 @@ class StageConnectionHandler:
                                timeout_s=float(md.get("timeout", 60.0)))
             ch = Channel(store, name, int(md["rank"]), int(md["world"]), ex.device,
                          timeout_s=float(md.get("timeout", 60.0)), data_backend=md.get("data_backend"))
+            resume = None
+            old = md.get("resume_prefix")
+            if old:
+                with self._chan_lock:
+                    prev = self._chan_engines.pop(str(old), None)
+                if prev is not None:
+                    prev.release()  # a failed channel's thread may still be blocked: free the executor's hook
+                resume = {"prefix": str(old), "cache": getattr(prev, "replay", None)}
             eng = PipelineServingEngine(ex, ch, n_slots=int(md.get("n_slots", 1)), batch=int(md.get("batch", 64)),
-                                        name=name)
-            logger.info(f"device channel {name}: open as rank {int(md['rank'])} of {int(md['world'])}")
+                                        name=name, replay_cache=bool(md.get("replay_cache", False)), resume=resume)
+            with self._chan_lock:
+                self._chan_engines[name] = eng
+            logger.info(f"device channel {name}: open as rank {int(md['rank'])} of {int(md['world'])}"
+                        + (f", resuming {old}" if old else ""))
             eng.idle_timeout_s = float(md.get("idle_timeout", 3600.0))
             eng.timing = bool(md.get("timing", False))  # per-stage ms for the client's STATS gathers
             ch.timing = eng.timing
@@ -224,7 +240,13 @@ class StageConnectionHandler:
         finally:
             if eng is not None:
                 eng.release()  # no graph of this channel's hop survives it (TCP steps, probes, next channel)
-            with ex.exec_lock:
+                with self._chan_lock:
+                    if eng.failed is None or not eng.park_on_fail:
+                        self._chan_engines.pop(name, None)
+                    dead = [k for k, e in self._chan_engines.items() if getattr(e, "failed", None) is not None]
+                    for k in dead[:-4]:  # keep the 4 newest failed channels nobody adopted
+                        self._chan_engines.pop(k)
+            with ex.exec_lock:  # (parked sessions - ``park:`` keys - wait for adoption or the session TTL)
                 for sid in [k for k in ex.sessions.sessions if k.startswith(name + ":")]:
                     ex.sessions.close(sid)
             if ch is not None:

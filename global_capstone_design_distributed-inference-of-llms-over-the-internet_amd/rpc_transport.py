@@ -462,6 +462,35 @@ class RpcTransport:
             used |= {h.peer_id for h in r}
         return routes
 
+    def replacement_hop(self, dead: Hop, device, exclude: Set[str] = frozenset(), same_node: bool = True,
+                        wait_s: float = 10.0) -> Optional[Hop]:
+        """A server that can take the place of ``dead`` in a device-channel route: the same stage
+        key (stage routing) or exactly the same block span [start, end) (module routing - a
+        different span would shift every later stage), not in ``exclude`` nor failed, on this
+        machine if ``same_node``; newest record first.  Stage-local recovery swaps only this hop
+        (``_run_rank0_channel``'s ``recover``).  Waits up to ``wait_s``; None if nothing qualifies."""
+        from .parallel.channel import host_id
+
+        me = host_id()
+        used = set(exclude) | set().union(*self.failed_peers.values()) if self.failed_peers else set(exclude)
+        used.add(dead.peer_id)
+        t0 = time.monotonic()
+        while True:
+            if self.routing == "module":
+                cands = [e for e in self._candidates("", dead.start) if int(e["end_block"]) == dead.end]
+            else:
+                cands = list(self._candidates(dead.key))
+            cands = [e for e in cands if str(e.get("peer_id")) not in used and
+                     (not same_node or e.get("channel_host") == me) and
+                     (not dead.final or bool(e.get("final_stage", dead.final)))]
+            if cands:
+                cands.sort(key=lambda e: (-float(e.get("timestamp", 0.0)), str(e.get("peer_id"))))
+                e = cands[0]
+                return Hop(dead.key, str(e["peer_id"]), e.get("p2p_maddrs") or [], dead.start, dead.end, dead.final, e)
+            if time.monotonic() - t0 > wait_s:
+                return None
+            time.sleep(0.25)
+
     def hop_alive(self, hop: Hop, timeout: float = 2.0) -> bool:
         """Does the hop's server still answer (``rpc_echo`` over TCP)?  Failure detection for
         device-channel routes: a channel error names no culprit, the TCP control plane does."""
@@ -481,7 +510,8 @@ class RpcTransport:
 
     def open_device_channel(self, route: List[Hop], device, *, n_slots: int = 1, batch: int = 64,
                             timeout: float = 60.0, idle_timeout: float = 3600.0, timing: bool = False,
-                            data_backend: Optional[str] = None):
+                            data_backend: Optional[str] = None, replay_cache: bool = False,
+                            resume_prefix: Optional[str] = None):
         """Rendezvous a ``parallel.channel.Channel`` with every hop of ``route``: this client
         is rank 0 (head), hop i is rank i + 1, the final hop the tail.  The TCP RPC carries
         only this handshake; afterwards hidden states move GPU -> GPU (RCCL over xGMI) and the
@@ -489,7 +519,10 @@ class RpcTransport:
         participants share a GPU (RCCL refuses duplicate devices) or on CPU.  ``data_backend``
         (``--channel_data``) picks the GPU data plane: "nccl" (ProcessGroupNCCL, default) or "rccl"
         (the framework's own communicators, ``parallel/rccl.py``; ``MPAMD_GRAPH_HOP=1`` then records
-        the hop inside the decode graphs); None reads ``MPAMD_CHANNEL_DATA``."""
+        the hop inside the decode graphs); None reads ``MPAMD_CHANNEL_DATA``.  ``replay_cache``
+        makes every non-tail server keep its output rows for stage-local recovery; ``resume_prefix``
+        (the failed channel's name) lets the servers of a replacement channel adopt that channel's
+        sessions (``PipelineServingEngine.resume_sessions``)."""
         import uuid
 
         from .parallel.channel import Channel, free_port, host_id, make_store
@@ -507,7 +540,8 @@ class RpcTransport:
             for i, hop in enumerate(route):
                 md = {"store_host": "127.0.0.1", "store_port": port, "prefix": prefix, "rank": i + 1, "world": world,
                       "timeout": timeout, "idle_timeout": idle_timeout, "data_backend": data, "n_slots": n_slots,
-                      "batch": batch, "host_id": host_id(), "timing": bool(timing)}
+                      "batch": batch, "host_id": host_id(), "timing": bool(timing),
+                      "replay_cache": bool(replay_cache), "resume_prefix": resume_prefix}
                 r = await self._call_hop(hop, "rpc_channel_open", [], md)
                 if not r.metadata.get("ok"):
                     raise ConnectionError(f"{hop}: device channel refused: {r.metadata.get('error')}")

@@ -100,6 +100,20 @@ class SessionManager:
             self._dirty = True
             self._free_rows.append(s.row)
 
+    def rename(self, src: str, dst: str) -> Optional[SessionState]:
+        """Move session ``src`` (row, pages, length) to the key ``dst`` - a stage adopting the
+        KV it held for a failed device channel into the channel that replaces it.  None if
+        ``src`` is unknown; an existing ``dst`` is closed first."""
+        with self.lock:
+            s = self.sessions.pop(src, None)
+            if s is None:
+                return None
+            self.close(dst)
+            s.sid = dst
+            s.last_used = time.monotonic()
+            self.sessions[dst] = s
+            return s
+
     def fork(self, src: str, dst: str, max_length: Optional[int] = None) -> SessionState:
         """``dst`` becomes a copy of ``src`` (its KV pages are copied on the device): the
         building block of beam search (upstream Petals reorders a session's hypotheses by

@@ -512,13 +512,25 @@ def fa_plan(ntoks, nh: int, nkv: int, n_cu: int = 256):
     return fa_blocks(ntoks, nrep, 4), 4
 
 
+FA_PAIR = os.environ.get("MPAMD_FA_PAIR", "auto")
+
+
+def fa_pair(nblocks: int, nh: int, nkv: int, num_parts: int, n_cu: int = 256) -> bool:
+    """Pair each long causal query block with its short mirror in one workgroup (csrc/attention_fa.hip
+    ``pair``) when the grid is at most 2 workgroups per CU: there the longest blocks, not the total
+    work, set the kernel time.  MPAMD_FA_PAIR=0/1 forces it."""
+    if FA_PAIR in ("0", "1"):
+        return FA_PAIR == "1" and num_parts == 1
+    return num_parts == 1 and nblocks >= 4 and nblocks * nkv <= 2 * n_cu
+
+
 def fa_ok(nh: int, nkv: int, D: int, page_size: int) -> bool:
     """Shapes the FA2 prefill kernel covers (else the 16x16 grouped kernel runs)."""
     return D == 128 and nh % nkv == 0 and (nh // nkv) in (1, 2, 4, 8) and page_size % 64 == 0
 
 
 def attention_fa(q, k_cache, v_cache, block_tables, q_seq, q_ctx, fablocks, nh, nkv, scale, out=None,
-                 workspace=None, max_ctx=None, waves=None, num_parts=None):
+                 workspace=None, max_ctx=None, waves=None, num_parts=None, pair=None):
     """Causal prefill attention, FA2 form on 32x32x16 MFMA with the transposed LDS reads of V
     (csrc/attention_fa.hip).  Same semantics as ``paged_attention``; row-major output only.
     ``fablocks`` from ``fa_blocks`` (device int32 [2, NB]).  The context is split over parts
@@ -540,8 +552,10 @@ def attention_fa(q, k_cache, v_cache, block_tables, q_seq, q_ctx, fablocks, nh, 
         out = torch.empty(T, nh * D, dtype=q.dtype, device=q.device)
     if workspace is None or (num_parts > 1 and workspace.numel() < T * nh * num_parts * (D + 2)):
         workspace = attention_workspace(T, nh, D, num_parts, q.device)
+    if pair is None:
+        pair = fa_pair(int(fablocks.shape[1]), nh, nkv, num_parts)
     torch.ops.mpamd.attention_fa(q, k_cache, v_cache, block_tables, q_seq, q_ctx, fablocks, out, workspace, nh, nkv,
-                                 float(scale), int(part_size), int(num_parts), waves)
+                                 float(scale), int(part_size), int(num_parts), waves, int(bool(pair) and num_parts == 1))
     return out
 
 
@@ -645,7 +659,7 @@ def reduce_qkv_part(qkv_part, dtype=torch.bfloat16):
     for s in range(part.shape[0]):
         acc = acc + part[s]
     if ss is not None:
-        tot = ss.view(-1, 128).sum(0)[: part.shape[1]].double()
+        tot = ss.view(-1, ref.SS_ROWS).sum(0)[: part.shape[1]].double()
         rs = torch.rsqrt((tot.float() * (1.0 / 1048576.0)) * inv_k + eps)
         acc = acc * rs[:, None]
     return acc.to(dtype)
@@ -745,8 +759,8 @@ _RW_OK = {}
 
 
 def wide_gemm_ok(M: int, N: int, K: int, epilogue: int = 0, out_packed: bool = False) -> bool:
-    """65..128 decode rows: the balanced ring kernel covers (packed A; epilogue 0 or packed SwiGLU,
-    the widths it is built for)."""
+    """65..256 decode rows: the balanced ring kernel covers (packed A; epilogue 0 or packed SwiGLU,
+    the widths it is built for; 129..256 rows at 12 / 16 row tiles)."""
     key = (M, N, K, int(epilogue), bool(out_packed))
     if epilogue == 3 and os.environ.get("MPAMD_WIDE_SPLITK", "1") == "0":
         return False  # the fused-norm producer only exists as the split-K ring + reduce form
@@ -759,7 +773,7 @@ def wide_gemm_ok(M: int, N: int, K: int, epilogue: int = 0, out_packed: bool = F
 def native_gemm_ok(M: int, N: int, K: int, epilogue: int = 0, out_packed: bool = False) -> bool:
     if not (K % 128 == 0 and N % (32 if epilogue == 1 else 16) == 0):
         return False
-    if 64 < M <= 128:
+    if 64 < M <= 256:
         return wide_gemm_ok(M, N, K, epilogue, out_packed)
     return 0 < M <= 64
 
@@ -815,7 +829,7 @@ def linear(x, w, out=None, epilogue=0, residual=None, policy=None, wp=None, a_ro
                    else torch.empty(M, ncols, dtype=x.dtype, device=x.device))
         if gate is not None:
             kern = "pk"
-        elif M > 64:  # 65..128 rows: split-K ring where it applies (o, down), else the ring kernel
+        elif M > 64:  # 65..256 rows: split-K ring where it applies (o, down), else the ring kernel
             kern = "rwk" if (not out_packed and _covered("rwk", M, N, K, epilogue)
                              and os.environ.get("MPAMD_WIDE_SPLITK", "1") != "0") else "rw"
             if _WIDE_ROT:

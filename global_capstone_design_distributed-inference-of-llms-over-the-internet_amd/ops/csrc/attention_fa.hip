@@ -67,7 +67,7 @@ __global__ __launch_bounds__(NW * 64) void attn_fa_kernel(
     const int32_t* __restrict__ block_tables, int bt_stride, const int32_t* __restrict__ q_seq,
     const int32_t* __restrict__ q_ctx, const int32_t* __restrict__ fb_tok0, const int32_t* __restrict__ fb_ntok,
     int NBF, bf16_t* __restrict__ out, int64_t out_stride, float* __restrict__ part_o, float* __restrict__ part_ml,
-    int nkv, int nh, int page_log2, int PS, int NP, float scale_log2) {
+    int nkv, int nh, int page_log2, int PS, int NP, float scale_log2, int pair) {
   constexpr int D = 128;
   constexpr int STEP = 64;
   constexpr int TILE = STEP * D * 2;            // bytes of one K or V tile (16 KiB)
@@ -80,20 +80,27 @@ __global__ __launch_bounds__(NW * 64) void attn_fa_kernel(
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   // XCD-aware order: the query blocks of one head sit on one XCD (its K / V stay in that L2),
   // longest causal context first inside a head
+  // pair (causal balance for small grids): workgroup j of a head runs query block NBF-1-j, then
+  // block j - every workgroup streams the same total context (a long block + its short mirror),
+  // instead of the longest blocks setting the kernel time on a grid of ~2 workgroups per CU
   const int G = gridDim.x, NHG = nh / HB;
+  const int NBP = pair ? (NBF + 1) / 2 : NBF;  // workgroups per head
   int lin = blockIdx.x;
   if ((G & 7) == 0) lin = (lin & 7) * (G >> 3) + (lin >> 3);
-  const int hg = lin / NBF;
-  const int bx = NBF - 1 - (lin - hg * NBF);
+  const int hg = lin / NBP;
+  const int jb = lin - hg * NBP;
   const int p = blockIdx.y;
   const int hbase = hg * HB;
   const int g = hbase / (nh / nkv);
+  const int npass = pair && (NBF - 1 - jb) != jb ? 2 : 1;
+  (void)NHG;
+  for (int pass = 0; pass < npass; ++pass) {
+  const int bx = pair ? (pass == 0 ? NBF - 1 - jb : jb) : NBF - 1 - jb;
   const int tok0 = fb_tok0[bx], ntok = fb_ntok[bx];
   const int32_t* bt = block_tables + (int64_t)q_seq[tok0] * bt_stride;
   const int page_size = 1 << page_log2;
   const int64_t page_stride = (int64_t)nkv * page_size * D;
   const int64_t head_off = (int64_t)g * page_size * D;
-  (void)NHG;
 
   // contexts are non-decreasing along a sequence's tokens: the last token's is the largest
   const int grp_ctx = q_ctx[tok0 + ntok - 1];
@@ -251,7 +258,7 @@ __global__ __launch_bounds__(NW * 64) void attn_fa_kernel(
   // ---- epilogue: lane owns row r; O^T accumulator register j of d-tile dt holds
   //      d = 32 dt + 8 (j >> 2) + 4 hh + (j & 3) ----
   l += __shfl_xor(l, 32, 64);
-  if (!row_ok) return;
+  if (!row_ok) continue;  // (every step above ended in a barrier: the LDS tiles are free)
   const int tok = tok0 + my_t;
   if (NP == 1) {
     const float inv = l > 0.f ? 1.f / l : 0.f;
@@ -282,6 +289,7 @@ __global__ __launch_bounds__(NW * 64) void attn_fa_kernel(
       part_ml[hp * 2 + 1] = l;
     }
   }
+  }  // pass
 }
 
 __global__ void paged_attn_reduce_kernel(const float* __restrict__ part_o, const float* __restrict__ part_ml,
@@ -295,7 +303,8 @@ __global__ void paged_attn_reduce_kernel(const float* __restrict__ part_o, const
 extern "C" int mp_attention_fa(const void* q, int64_t q_stride, const void* kc, const void* vc, const int32_t* bt,
                                int bt_stride, const int32_t* q_seq, const int32_t* q_ctx, const int32_t* fb_tok0,
                                const int32_t* fb_ntok, int NBF, void* out, float* workspace, int T, int nh, int nkv,
-                               int D, int page_size, int PS, int NP, float scale, int nw, hipStream_t stream) {
+                               int D, int page_size, int PS, int NP, float scale, int nw, int pair,
+                               hipStream_t stream) {
   (void)hipGetLastError();  // an earlier non-mpamd HIP call's stale error is not this launch's
   using namespace mp;
   if (NBF == 0 || T == 0) return 0;
@@ -304,14 +313,16 @@ extern "C" int mp_attention_fa(const void* q, int64_t q_stride, const void* kc, 
   while ((1 << page_log2) < page_size) ++page_log2;
   if ((1 << page_log2) != page_size) return -2;
   const int hb = nh / nkv;
+  pair = pair ? 1 : 0;
+  const int nbp = pair ? (NBF + 1) / 2 : NBF;
   const float scale_log2 = scale * 1.4426950408889634f;
   float* ws_o = workspace;
   float* ws_ml = workspace + (int64_t)T * nh * NP * D;
 #define MP_FA(HB_, NW_)                                                                                         \
-  hipLaunchKernelGGL((attn_fa_kernel<HB_, NW_>), dim3(NBF * (nh / HB_), NP), dim3(NW_ * 64), 0, stream,           \
+  hipLaunchKernelGGL((attn_fa_kernel<HB_, NW_>), dim3(nbp * (nh / HB_), NP), dim3(NW_ * 64), 0, stream,           \
                      (const bf16_t*)q, q_stride, (const bf16_t*)kc, (const bf16_t*)vc, bt, bt_stride, q_seq, q_ctx, \
                      fb_tok0, fb_ntok, NBF, (bf16_t*)out, (int64_t)nh * D, ws_o, ws_ml, nkv, nh, page_log2, PS, NP,  \
-                     scale_log2)
+                     scale_log2, pair)
 #define MP_FA_NW(HB_) \
   if (nw == 8) MP_FA(HB_, 8); else MP_FA(HB_, 4);
   switch (hb) {

@@ -42,7 +42,7 @@ int mp_attention_mfma(const void* q, int64_t q_stride, const void* kc, const voi
 int mp_attention_fa(const void* q, int64_t q_stride, const void* kc, const void* vc, const int32_t* bt, int bt_stride,
                     const int32_t* q_seq, const int32_t* q_ctx, const int32_t* fb_tok0, const int32_t* fb_ntok, int NBF,
                     void* out, float* workspace, int T, int nh, int nkv, int D, int page_size, int PS, int NP,
-                    float scale, int nw, hipStream_t stream);
+                    float scale, int nw, int pair, hipStream_t stream);
 int mp_quant_act_fp8(const void* ap, void* a8, float* scale, float* part, int M, int K, hipStream_t stream);
 int mp_gemm_fp8(const void* a8, const float* as, const void* wq, const float* ws, void* y, int64_t ys, const void* res,
                 int64_t rs, int M, int N, int K, int epilogue, int out_packed, int kind, float* part,
@@ -88,11 +88,11 @@ inline void check_rows(const at::Tensor& t, const char* name) {
 
 inline int64_t packed_numel(int64_t M, int64_t K) { return ((M + 15) / 16) * 16 * K; }
 
-// fused-norm row statistics: int64 [32 shards][128 rows] fixed-point sums (gemm.hip EpiArgs)
+// fused-norm row statistics: int64 [32 shards][256 rows] fixed-point sums (gemm.hip EpiArgs)
 inline void* opt_ss(const c10::optional<at::Tensor>& t, const char* name) {
   if (!t.has_value()) return nullptr;
   MP_CHECK(t->is_cuda() && t->scalar_type() == at::kLong && t->is_contiguous() && t->numel() >= mp_gemm_ss_elems(),
-           std::string(name) + ": int64 cuda contiguous [32, 128] (ops.norm_stats_buffer)");
+           std::string(name) + ": int64 cuda contiguous [32, 256] (ops.norm_stats_buffer)");
   return t->data_ptr();
 }
 
@@ -111,7 +111,7 @@ void rmsnorm(const at::Tensor& x, at::Tensor& residual, const at::Tensor& w, at:
   }
   MP_CHECK(mode >= 0 && mode <= 3, "mode");
   void* ssp = opt_ss(ss, "ss");
-  MP_CHECK(mode != 3 || (ssp != nullptr && x.size(0) <= 128), "mode 3 needs ss and <= 128 rows");
+  MP_CHECK(mode != 3 || (ssp != nullptr && x.size(0) <= 256), "mode 3 needs ss and <= 256 rows");
   if (mode != 0) {
     check_bf16_cuda(residual, "residual");
     check_rows(residual, "residual");
@@ -207,8 +207,8 @@ static bool qkv_part_args(const c10::optional<at::Tensor>& part, int64_t splits,
   MP_CHECK(splits >= 1 && splits <= 8, "qkv_part splits");
   const unsigned long long* ssp = nullptr;
   if (ss.has_value()) {
-    MP_CHECK(ss->is_cuda() && ss->scalar_type() == at::kLong && ss->is_contiguous() && ss->numel() >= 32 * 128,
-             "part_ss: row statistics [32, 128] int64");
+    MP_CHECK(ss->is_cuda() && ss->scalar_type() == at::kLong && ss->is_contiguous() && ss->numel() >= mp_gemm_ss_elems(),
+             "part_ss: row statistics [32, 256] int64");
     ssp = reinterpret_cast<const unsigned long long*>(ss->data_ptr<int64_t>());
   }
   a = QkvPartArgs{part->data_ptr<float>(), (int)splits, T * width, (int)width, ssp, (float)inv_k, (float)eps};
@@ -353,7 +353,7 @@ void attention_mfma(const at::Tensor& q, const at::Tensor& k_cache, const at::Te
 void attention_fa(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
                   const at::Tensor& block_tables, const at::Tensor& q_seq, const at::Tensor& q_ctx,
                   const at::Tensor& fablocks, at::Tensor& out, at::Tensor& workspace, int64_t nh, int64_t nkv,
-                  double scale, int64_t part_size, int64_t num_parts, int64_t waves) {
+                  double scale, int64_t part_size, int64_t num_parts, int64_t waves, int64_t pair) {
   check_bf16_cuda(q, "q");
   check_rows(q, "q");
   check_bf16_cuda(out, "out");
@@ -383,7 +383,7 @@ void attention_fa(const at::Tensor& q, const at::Tensor& k_cache, const at::Tens
                                q_ctx.data_ptr<int32_t>(), fablocks.data_ptr<int32_t>(),
                                fablocks.data_ptr<int32_t>() + NB, NB, out.data_ptr(), workspace.data_ptr<float>(), T,
                                nh, nkv, D, k_cache.size(2), part_size, num_parts, (float)scale, (int)waves,
-                               cur_stream()),
+                               (int)pair, cur_stream()),
                "attention_fa");
 }
 
@@ -732,7 +732,7 @@ TORCH_LIBRARY(mpamd, m) {
   m.def(
       "attention_fa(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor q_seq, Tensor q_ctx, "
       "Tensor fablocks, Tensor(a!) out, Tensor(b!) workspace, int nh, int nkv, float scale, int part_size, "
-      "int num_parts, int waves) -> ()");
+      "int num_parts, int waves, int pair=0) -> ()");
   m.def(
       "attention_mfma_rope(Tensor qkv, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor block_tables, Tensor q_seq, "
       "Tensor q_ctx, Tensor qblocks, Tensor positions, Tensor cos, Tensor sin, Tensor slots, Tensor(c!) out, "

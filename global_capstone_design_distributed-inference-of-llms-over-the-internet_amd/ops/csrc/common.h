@@ -84,7 +84,7 @@ __device__ __forceinline__ int64_t apk_off(int row, int col, int MT) {
 // read q / k / v through qkv_part_load8, which is the split-K reduce launch's epilogue 0 inlined:
 // the S slabs summed in split order from zero, times rsqrt(ss / K + eps), rounded to bf16 - the
 // same bits the reduce launch would have stored, without its launch.
-constexpr int QP_SS_NSH = 32, QP_SS_ROWS = 128;
+constexpr int QP_SS_NSH = 32, QP_SS_ROWS = 256;
 constexpr float QP_SS_FX = 1048576.f;
 struct QkvPart {
   const float* part;               // nullptr: read the bf16 qkv rows instead

@@ -44,7 +44,7 @@ extern "C" int mp_gemm_rwk_split(int M, int N, int K, int f8) {
   using namespace mp;
   if (M < 1 || M > 128 || N % 2048 || K % 128) return 0;
   int nt, S;
-  rwk_choose(N / 16, K / 32, sk_num_cus(), f8 != 0, nt, S);
+  rwk_choose(N / 16, K / 32, sk_num_cus(), f8 != 0, nt, S, rwk_nt_max(M));
   if (nt == 0 || (int64_t)S * M * N * 4 > RWK_SLAB_BYTES) return 0;
   return S;
 }
@@ -76,9 +76,9 @@ extern "C" int mp_gemm_bf16(const void* x, int64_t x_stride, const void* w, void
   if (epilogue == 3 && (ap == nullptr || res == nullptr)) return -5;
   EpiArgs ep{(bf16_t*)ap, (u64*)ss_out, (u64*)ss_zero, (const u64*)ss_in, inv_k, eps, (M + 15) / 16};
   ep.rot = (flags >> 10) & 1;
-  if (M > 128 || K % (32 * GU_MAX) || N % 16 || ((flags & 1) == 0 && x_stride % 8)) return -1;
+  if (M > 256 || K % (32 * GU_MAX) || N % 16 || ((flags & 1) == 0 && x_stride % 8)) return -1;
   int rc;
-  if (M > 64) {  // 65..128 rows: gemm_wide.hip (split-K ring / balanced ring, packed A, no gate)
+  if (M > 64) {  // 65..256 rows: gemm_wide.hip (split-K ring / balanced ring, packed A, no gate)
     if (!(flags & 1) || gate != nullptr) return -1;
     return mp_gemm_bf16_wide(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, ws, ep, stream);
   }

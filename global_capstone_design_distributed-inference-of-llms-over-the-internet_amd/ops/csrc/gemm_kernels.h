@@ -69,8 +69,8 @@ __device__ __forceinline__ u16x8 load_a_rows(const bf16_t* p, int lane, bool row
 // same-address atomics serialise at the memory side, 256 adders on one row cost ~20 us);
 // consumers sum the shards of every row once per workgroup into LDS.
 constexpr int SS_NSH = 32;
-constexpr int SS_ROWS = 128;        // rows per shard: decode steps of up to 128 sessions
-constexpr int SS_PG = 4;            // shard groups a RowScale reduction uses at most (512 / SS_ROWS)
+constexpr int SS_ROWS = 256;        // rows per shard: decode steps of up to 256 sessions
+constexpr int SS_PG = 512 / SS_ROWS;  // shard groups a RowScale reduction uses at most (512 threads)
 constexpr float SS_FX = 1048576.f;  // 2^20
 typedef unsigned long long u64;
 static_assert(SS_NSH == QP_SS_NSH && SS_ROWS == QP_SS_ROWS && SS_FX == QP_SS_FX,
@@ -460,7 +460,7 @@ __device__ __forceinline__ void tile_epilogue(int mt, int tile, const f32x4& v, 
       const int ncol = (tile >> 1) * 16 + c;
       const float gg = round_bf(v[r] * sc);
       const float a = round_bf(gg / (1.f + __expf(-gg)));
-      const int64_t yo = OPK ? apk_off(row, ncol, MT) : (int64_t)row * ys + ncol;
+      const int64_t yo = OPK ? apk_off(row, ncol, ep.mt_out) : (int64_t)row * ys + ncol;
       y[yo] = f2bf(a * round_bf(up[r] * sc));
     } else if constexpr (EPI == 3) {
       const bf16_t rv = rpv != nullptr ? (*rpv)[r] : res[(int64_t)row * rs + tile * 16 + c];
@@ -1047,7 +1047,8 @@ __device__ __forceinline__ void rw_body(const bf16_t* __restrict__ x, const bf16
       rb[s][t] = NTW ? __builtin_nontemporal_load(p_) : *p_;                                                 \
     }                                                                                                        \
     _Pragma("unroll") for (int mt = 0; mt < MT; ++mt) ra[s][mt] =                                            \
-        load_a_rows(xl + (((int64_t)k_ * mta + mt0 + mt) << 9), lane, (mt0 + mt) * 16 + (lane & 15) < M);   \
+        load_a_rows(xl + (((int64_t)k_ * mta + min(mt0 + mt, mta - 1)) << 9), lane,                         \
+                    (mt0 + mt) * 16 + (lane & 15) < M);                                                      \
   }
 #pragma unroll
   for (int s = 0; s < R; ++s) RW_LOAD(s, s)
@@ -1121,10 +1122,10 @@ __global__ __launch_bounds__(RW_WAVES * 64) void gemm_rw_kernel(const bf16_t* __
   __shared__ __attribute__((aligned(16))) f32x4 red[RW_WAVES * (MT * NTB < RW_QC ? MT * NTB : RW_QC) * 64];
   const int b = blockIdx.x;
   if (b < n_big) {
-    rw_body<MT, NTB, EPI, OPK, F8>(x, wp, y, ys, res, rs, M, K, b * NTB, ep, red, rs_part, rs_lds);
+    rw_body<MT, NTB, EPI, OPK, F8>(x, wp, y, ys, res, rs, M, K, b * NTB, ep, red, rs_part, rs_lds, 0, ep.mt_out);
   } else {
     rw_body<MT, NTS, EPI, OPK, F8>(x, wp, y, ys, res, rs, M, K, n_big * NTB + (b - n_big) * NTS, ep, red, rs_part,
-                                   rs_lds);
+                                   rs_lds, 0, ep.mt_out);
   }
 }
 
@@ -1154,9 +1155,9 @@ static int launch_gemm_rw_cfg(const void* x, const void* w, void* y, int64_t ys,
       return 0;
     }
   } else if constexpr (MT > 4) {
-    // M = 65..128 (the unfused packed decode path at 96 / 128 sessions): plain and packed-SwiGLU
-    // epilogues only, accumulators within 192 AGPRs
-    if constexpr (4 * MT * NTB > 192) {
+    // M = 65..256 (the packed decode path at 96..256 sessions): plain and packed-SwiGLU epilogues
+    // only, accumulators within 192 AGPRs (MT <= 8) or all 256 (MT 9..16: 129..256 rows)
+    if constexpr (4 * MT * NTB > (MT > 8 ? 256 : 192)) {
       return 1;
     } else {
       if (!(epi == 0 || (epi == 1 && opk)) || (epi == 1 && (NTB % 2 || NTS % 2))) return 1;
@@ -1205,7 +1206,13 @@ static int launch_gemm_rw(const void* x, const void* w, void* y, int64_t ys, con
   const int step = epi == 1 ? 2 : 1;
   const int units = (N / 16) / step;
   if ((N / 16) % step || units == 0) return 1;
-  const int G = units < sk_num_cus() ? units : sk_num_cus();
+  int G = units < sk_num_cus() ? units : sk_num_cus();
+  if constexpr (MT > 8) {
+    // 129..256 rows: at most 64 / MT column tiles per workgroup (256 accumulator AGPRs), so wide
+    // projections run more workgroups than CUs (gate/up at 256 rows: 344 groups of 4 tiles)
+    const int per = ((64 / MT) / step) > 0 ? (64 / MT) / step : 1;
+    if ((units + per - 1) / per > G) G = (units + per - 1) / per;
+  }
   const int base = units / G, rem = units % G;
   const int ntb = (base + (rem ? 1 : 0)) * step;
   const int n_big = rem ? rem : G;
@@ -1307,7 +1314,7 @@ static int launch_gemm_rwr(const void* x, const void* w, void* y, int64_t ys, co
 // slab; the sum over the S slabs and the epilogue (residual, packed copy, row sums of squares)
 // run in a small second launch - a kernel boundary instead of an in-launch seam (the stream-K
 // kernel's end-of-range hand-off costs ~7 us at these sizes).
-constexpr int64_t RWK_SLAB_BYTES = (int64_t)16 << 20;  // S x M x N fp32 partials (workspace tail)
+constexpr int64_t RWK_SLAB_BYTES = (int64_t)32 << 20;  // S x M x N fp32 partials (workspace tail)
 
 // INL >= 0: in-launch combine instead of the reduce launch - every split stores its summed
 // tiles as write-through (sc1) fp32 slabs in fragment order, takes an arrival ticket on its
@@ -1386,7 +1393,8 @@ __global__ __launch_bounds__(RW_WAVES * 64) void gemm_rwk_kernel(const bf16_t* _
     _Pragma("unroll") for (int t = 0; t < NT; ++t) rb[s][t] =                                                \
         __builtin_nontemporal_load(reinterpret_cast<const BT*>(wb + (((int64_t)t * nks + k_) << 9)));       \
     _Pragma("unroll") for (int mt = 0; mt < MT; ++mt) ra[s][mt] =                                            \
-        load_a_rows(xl + (((int64_t)k_ * MT + mt) << 9), lane, mt * 16 + (lane & 15) < M);                  \
+        load_a_rows(xl + (((int64_t)k_ * ep.mt_out + min(mt, ep.mt_out - 1)) << 9), lane,                  \
+                    mt * 16 + (lane & 15) < M);                                                              \
   }
 #pragma unroll
   for (int s = 0; s < R; ++s) RWK_LOAD(s, s)
@@ -1646,7 +1654,7 @@ static inline void launch_splitk_reduce(int S, int epi, dim3 g2, hipStream_t str
 // NT = 6, S = 2 fills 256 CUs where NT = 8, S = 2 leaves 64 idle).  fp8 weights: the bf16
 // activation block costs 2M / (16 NT) x the weight bytes per CU - the widest group first.
 // nt = 0 when no split applies.  MPAMD_RWK_NT (ablation) allows only that width.
-static inline void rwk_choose(int tiles, int nks, int C0, bool f8, int& nt, int& S) {
+static inline void rwk_choose(int tiles, int nks, int C0, bool f8, int& nt, int& S, int nt_max = 8) {
   static constexpr int kOrderBf16[5] = {4, 2, 8, 6, 1}, kOrderF8[5] = {8, 4, 2, 6, 1};
   static const int nt_only = [] {
     const char* v = getenv("MPAMD_RWK_NT");
@@ -1655,10 +1663,18 @@ static inline void rwk_choose(int tiles, int nks, int C0, bool f8, int& nt, int&
   nt = S = 0;
   int best_fill = 0;
   for (int cand : (f8 ? kOrderF8 : kOrderBf16)) {
-    if ((nt_only && cand != nt_only) || tiles % cand) continue;
+    if ((nt_only && cand != nt_only) || tiles % cand || cand > nt_max) continue;
     const int C = tiles / cand, s = C0 / C;
     if (s >= 2 && s <= 8 && nks >= 4 * s && C * s > best_fill) { nt = cand; S = s; best_fill = C * s; }
   }
+}
+
+// Widest split-K ring column group the instantiation for M rows holds in its accumulators: 192
+// AGPRs up to 128 rows (MT 5..8), all 256 at 129..256 rows (built at MT 12 and 16).
+constexpr int rwk_nt_max_mt(int MT) { return MT > 8 ? 64 / MT : (MT > 4 ? 192 / (4 * MT) : 8); }
+static inline int rwk_nt_max(int M) {
+  const int mt = (M + 15) / 16;
+  return rwk_nt_max_mt(mt <= 8 ? mt : (mt <= 12 ? 12 : 16));
 }
 
 // ``comb``: 0 = reduce launch, 1 = in-launch combine by the last arriver, 2 = symmetric in-launch
@@ -1679,12 +1695,11 @@ static int launch_gemm_rwk(const void* x, const void* w, void* y, int64_t ys, co
   if (epi == 1 || ws == nullptr || N % 2048 != 0) return 1;
   const int tiles = N / 16, C0 = sk_num_cus(), nks = K / 32;
   int nt = 0, S = 0;
-  rwk_choose(tiles, nks, C0, F8, nt, S);
+  // accumulators: 192 AGPRs up to 128 rows, all 256 beyond (MT 9..16 -> NT <= 64 / MT)
+  constexpr int nt_max = rwk_nt_max_mt(MT);
+  rwk_choose(tiles, nks, C0, F8, nt, S, nt_max);
   if (nt == 0) return 1;
   if ((int64_t)S * M * N * 4 > RWK_SLAB_BYTES) return 1;
-  if constexpr (4 * MT * 8 > 192) {
-    if (nt == 8) return 1;
-  }
   float* part = (float*)((char*)ws + (int64_t)SK_MAX_GROUPS * sizeof(int) + SK_ZERO_BYTES +
                          (int64_t)SK_MAX_BLOCKS * 2 * SK_MAX_S * 64 * sizeof(float));
   const dim3 g1((tiles / nt) * S);
@@ -1716,13 +1731,16 @@ static int launch_gemm_rwk(const void* x, const void* w, void* y, int64_t ys, co
   switch (nt) {
     case 1: hipLaunchKernelGGL((gemm_rwk_kernel<MT, 1, F8>), g1, dim3(RW_WAVES * 64), 0, stream, (const bf16_t*)x, (const bf16_t*)w, part, M, N, K, S, ep, nullptr, 0, nullptr, 0, nullptr); break;
     case 2: hipLaunchKernelGGL((gemm_rwk_kernel<MT, 2, F8>), g1, dim3(RW_WAVES * 64), 0, stream, (const bf16_t*)x, (const bf16_t*)w, part, M, N, K, S, ep, nullptr, 0, nullptr, 0, nullptr); break;
-    case 4: hipLaunchKernelGGL((gemm_rwk_kernel<MT, 4, F8>), g1, dim3(RW_WAVES * 64), 0, stream, (const bf16_t*)x, (const bf16_t*)w, part, M, N, K, S, ep, nullptr, 0, nullptr, 0, nullptr); break;
+    case 4:
+      if constexpr (4 <= nt_max)
+        hipLaunchKernelGGL((gemm_rwk_kernel<MT, 4, F8>), g1, dim3(RW_WAVES * 64), 0, stream, (const bf16_t*)x, (const bf16_t*)w, part, M, N, K, S, ep, nullptr, 0, nullptr, 0, nullptr);
+      break;
     case 6:
-      if constexpr (4 * MT * 6 <= 192)
+      if constexpr (6 <= nt_max)
         hipLaunchKernelGGL((gemm_rwk_kernel<MT, 6, F8>), g1, dim3(RW_WAVES * 64), 0, stream, (const bf16_t*)x, (const bf16_t*)w, part, M, N, K, S, ep, nullptr, 0, nullptr, 0, nullptr);
       break;
     default:
-      if constexpr (4 * MT * 8 <= 192)
+      if constexpr (8 <= nt_max)
         hipLaunchKernelGGL((gemm_rwk_kernel<MT, 8, F8>), g1, dim3(RW_WAVES * 64), 0, stream, (const bf16_t*)x, (const bf16_t*)w, part, M, N, K, S, ep, nullptr, 0, nullptr, 0, nullptr);
       break;
   }

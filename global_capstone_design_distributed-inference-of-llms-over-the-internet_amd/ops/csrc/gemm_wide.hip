@@ -1,5 +1,8 @@
-// Decode GEMM for 65..128 rows (the unfused packed decode path at 96 / 128 sessions): split-K
-// ring (o, down) and balanced ring kernels at MT = 5..8 (kernels: gemm_kernels.h).
+// Decode GEMM for 65..256 rows (the packed decode path at 96..256 sessions): split-K ring (o,
+// down) and balanced ring kernels at MT = 5..8, 12 and 16 (kernels: gemm_kernels.h).  129..256
+// rows run the 12- or 16-row-tile instantiation over the activation's own row tiles (the packed
+// layout's tile count is a runtime stride; tiles past it are masked rows), so the fused-norm
+// decode path no longer hands 129..256-session steps to hipBLASLt.
 #include "gemm_kernels.h"
 
 extern "C" int mp_gemm_bf16_wide(const void* x, const void* w, void* y, int64_t y_stride, const void* res,
@@ -14,7 +17,9 @@ extern "C" int mp_gemm_bf16_wide(const void* x, const void* w, void* y, int64_t 
       case 5: MP_RWK(5); break;
       case 6: MP_RWK(6); break;
       case 7: MP_RWK(7); break;
-      default: MP_RWK(8); break;
+      case 8: MP_RWK(8); break;
+      case 9: case 10: case 11: case 12: MP_RWK(12); break;
+      default: MP_RWK(16); break;
     }
 #undef MP_RWK
     if (rc < 0) return rc;
@@ -23,26 +28,31 @@ extern "C" int mp_gemm_bf16_wide(const void* x, const void* w, void* y, int64_t 
   if (M <= 80) rc = launch_gemm_rw<5>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, ep, stream);
   else if (M <= 96) rc = launch_gemm_rw<6>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, ep, stream);
   else if (M <= 112) rc = launch_gemm_rw<7>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, ep, stream);
-  else rc = launch_gemm_rw<8>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, ep, stream);
+  else if (M <= 128) rc = launch_gemm_rw<8>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, ep, stream);
+  else if (M <= 192) rc = launch_gemm_rw<12>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, ep, stream);
+  else rc = launch_gemm_rw<16>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, ep, stream);
   if (rc != 0) return rc < 0 ? rc : -1;
   return (int)hipGetLastError();
 }
 
-// 1 if mp_gemm_bf16 covers a packed-activation decode GEMM of M = 65..128 rows (balanced ring
+// 1 if mp_gemm_bf16 covers a packed-activation decode GEMM of M = 65..256 rows (balanced ring
 // kernel: the widths built, epilogue 0 or packed SwiGLU), else 0.  No launch.
 extern "C" int mp_gemm_rw_ok(int M, int N, int K, int epilogue, int out_packed) {
   using namespace mp;
-  if (M <= 64 || M > 128 || K % (32 * GU_MAX) || N % 16) return 0;
-  // the fused-norm producer (residual + packed copy + row statistics) at 65..128 rows runs as
+  if (M <= 64 || M > 256 || K % (32 * GU_MAX) || N % 16) return 0;
+  // the fused-norm producer (residual + packed copy + row statistics) at 65..256 rows runs as
   // the split-K ring + its reduce launch (the reduce applies the epilogue): o / down widths
   if (epilogue == 3) return !out_packed && N % 2048 == 0;
-  const EpiArgs ep{};
+  EpiArgs ep{};
+  ep.mt_out = (M + 15) / 16;
   const int flags = 1 | (out_packed ? 2 : 0) | 128;
   int rc;
   if (M <= 80) rc = launch_gemm_rw<5>(nullptr, nullptr, nullptr, 0, nullptr, 0, M, N, K, epilogue, flags, ep, 0, true);
   else if (M <= 96) rc = launch_gemm_rw<6>(nullptr, nullptr, nullptr, 0, nullptr, 0, M, N, K, epilogue, flags, ep, 0, true);
   else if (M <= 112) rc = launch_gemm_rw<7>(nullptr, nullptr, nullptr, 0, nullptr, 0, M, N, K, epilogue, flags, ep, 0, true);
-  else rc = launch_gemm_rw<8>(nullptr, nullptr, nullptr, 0, nullptr, 0, M, N, K, epilogue, flags, ep, 0, true);
+  else if (M <= 128) rc = launch_gemm_rw<8>(nullptr, nullptr, nullptr, 0, nullptr, 0, M, N, K, epilogue, flags, ep, 0, true);
+  else if (M <= 192) rc = launch_gemm_rw<12>(nullptr, nullptr, nullptr, 0, nullptr, 0, M, N, K, epilogue, flags, ep, 0, true);
+  else rc = launch_gemm_rw<16>(nullptr, nullptr, nullptr, 0, nullptr, 0, M, N, K, epilogue, flags, ep, 0, true);
   return rc == 0;
 }
 

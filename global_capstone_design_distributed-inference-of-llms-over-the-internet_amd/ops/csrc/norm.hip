@@ -86,7 +86,7 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(
       ssq = 0;
       for (int i = 0; i < NT / 64; ++i) ssq += redq[i];
     }
-    if (threadIdx.x < 32) ss_out[threadIdx.x * 128 + orow] = threadIdx.x == 0 ? ssq : 0ull;  // [32][128] shards
+    if (threadIdx.x < 32) ss_out[threadIdx.x * QP_SS_ROWS + orow] = threadIdx.x == 0 ? ssq : 0ull;  // [32][256] shards
   }
   bf16_t* yr = y + (int64_t)orow * y_stride;
   float amax = 0.f;
@@ -143,7 +143,7 @@ extern "C" int mp_rmsnorm(const void* x, int64_t x_stride, void* res, int64_t re
   (void)hipGetLastError();  // an earlier non-mpamd HIP call's stale error is not this launch's
   using namespace mp;
   if (H % 8 != 0 || H > 8 * 256 * 8) return -1;
-  if (mode == 3 && (ss_out == nullptr || nrows > 128)) return -2;
+  if (mode == 3 && (ss_out == nullptr || nrows > QP_SS_ROWS)) return -2;
   if (a8 != nullptr && (packed_mt <= 0 || H % 64 || a8_scale == nullptr || mode == 3)) return -3;
   if (nrows == 0) return 0;
   const int nch = H / 8;

@@ -37,7 +37,7 @@ def unpack_act(ap, M, K):
     return x[:M]
 
 
-SS_SHARDS, SS_ROWS, SS_FX = 32, 128, float(1 << 20)
+SS_SHARDS, SS_ROWS, SS_FX = 32, 256, float(1 << 20)
 
 
 def fx_sumsq(x):

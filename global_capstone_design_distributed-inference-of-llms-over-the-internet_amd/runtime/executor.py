@@ -743,7 +743,8 @@ class StageExecutor:
         done = self.__dict__.setdefault("_served_warm", set())
         if key in done:
             return False
-        prompt_len = int(min(prompt_len, self.max_seq_len - decode_steps - 2))
+        ab_steps = 48  # the fold A/B below: 2 rounds x 2 variants x (1 capture + 10 timed) steps
+        prompt_len = int(min(prompt_len, self.max_seq_len - decode_steps - 2 - ab_steps))
         if prompt_len < 1 or batch > self.sessions.max_sessions:
             return False
         sids = [f"__warm{i}__" for i in range(batch)]
@@ -769,6 +770,7 @@ class StageExecutor:
                     out = self.forward([(s, 1) for s in sids], x)
                     if self.is_last:
                         self._warm_sampler(out)
+                self._confirm_qkv_fold(sids, gen)
                 done.add(key)
             except Exception as e:  # noqa: BLE001 - e.g. no KV room: the first request warms itself
                 logger.info(f"serving warm-up ({batch} x {prompt_len}) skipped: {e}")
@@ -778,6 +780,46 @@ class StageExecutor:
                     self.sessions.close(s)
             torch.cuda.synchronize(self.device)
         return True
+
+    def _confirm_qkv_fold(self, sids, gen, reps: int = 10) -> Optional[dict]:
+        """End-to-end check of the qkv fold for this decode batch: ``ops.autotune_qkv_fold`` times
+        the qkv GEMM alone (partials vs the full projection), but the fold also moves work into the
+        attention kernel (its q / k / v loads sum the slabs), so the whole decode step - graph
+        replays of this batch bucket - is timed both ways and the fold kept only where the step
+        is >= 1 % faster.  The losing variant's graph is dropped.  Returns {fold: ms} or None."""
+        B = len(sids)
+        if not self.use_graphs or B > self.graph_max_batch or not self._qkv_fold(B):
+            return None
+        cfg = self.cfg
+        key = (ops._m_bucket(B), cfg.q_dim + 2 * cfg.kv_dim, cfg.hidden_size, bool(self._w8))
+        H = cfg.hidden_size
+
+        def step():
+            if self.is_first:
+                x = torch.randint(0, cfg.vocab_size, (B,), device=self.device, generator=gen)
+            else:
+                x = (0.1 * torch.randn(B, H, device=self.device, generator=gen)).to(self.dtype)
+            self.forward([(s, 1) for s in sids], x)
+
+        t = {True: float("inf"), False: float("inf")}
+        for _ in range(2):
+            for fold in (True, False):
+                ops._QKV_FOLD[key] = fold
+                step()  # capture (first time) / warm
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(reps):
+                    step()
+                e1.record()
+                e1.synchronize()
+                t[fold] = min(t[fold], e0.elapsed_time(e1) / reps)
+        keep = t[True] < 0.99 * t[False]
+        ops._QKV_FOLD[key] = keep
+        for k in [k for k in self._graphs if k[0] == self._bucket(B) and k[3] != keep]:
+            del self._graphs[k]
+        logger.info(f"qkv fold at batch {B}: {t[True]:.3f} ms/step folded vs {t[False]:.3f} unfolded -> "
+                    f"{'fold' if keep else 'reduce launch'}")
+        return t
 
     def _warm_sampler(self, logits: torch.Tensor) -> None:
         """The sampling kernel at this row count, on scratch parameters (no session state)."""
@@ -904,11 +946,11 @@ class StageExecutor:
         logger.info(f"CPU offload: {n_stream} layers streamed from pinned host memory, {keep} resident")
 
     def _fused_wide_ok(self, M: int) -> bool:
-        """Fused-norm decode path at 65..128 rows (bf16): the wide kernels cover every
+        """Fused-norm decode path at 65..256 rows (bf16): the wide kernels cover every
         projection with its fused epilogue - qkv and gate/up consume the row statistics
         (balanced ring or split-K ring + reduce), o and down produce them (split-K ring, the
         reduce launch applies the residual / packed copy / statistics epilogue)."""
-        if not 64 < M <= 128 or self.device.type != "cuda" or not self._packed_ok(M):
+        if not 64 < M <= 256 or self.device.type != "cuda" or not self._packed_ok(M):
             return False
         cfg = self.cfg
         H, F = cfg.hidden_size, cfg.intermediate_size
@@ -927,9 +969,9 @@ class StageExecutor:
             (cfg.q_dim + 2 * cfg.kv_dim) % 32 == 0
 
     def _packed_ok(self, M: int) -> bool:
-        """Packed-activation decode path: GPU, native GEMM allowed, all projections packed; 65..128
+        """Packed-activation decode path: GPU, native GEMM allowed, all projections packed; 65..256
         rows when the balanced ring kernel covers every projection of the layer (dense Llama)."""
-        if self.device.type != "cuda" or ops.gemm_policy() == "hipblaslt" or not 0 < M <= 128:
+        if self.device.type != "cuda" or ops.gemm_policy() == "hipblaslt" or not 0 < M <= 256:
             return False
         if getattr(self, "_packed_ready", None) is None:
             cfg = self.cfg
@@ -990,7 +1032,7 @@ class StageExecutor:
         B = self._bucket(plan.T)
         ctxb = min(self._ctx_bucket(plan.max_ctx), self._ctx_bucket(self.max_seq_len))
         part = ops.attention_partition(B, self.nkv, ctxb, min_part=self._attn_min_part)
-        key = (B, part[0], part[1], hooked)
+        key = (B, part[0], part[1], self._qkv_fold(B), hooked)  # (hooked last: _drop_hooked)
         g = self._graphs.get(key)
         if g is None:
             if self._graph_pool is None:

@@ -67,13 +67,15 @@ def main():
                     sb = torch.from_numpy(ops.query_superblocks(ntoks, nh // nkv)).to(dev)
                     fn = lambda: ops.attention_mfma(q, kc, vc, bt, q_seq, q_ctx, qb, nh, nkv, scale, out=out,  # noqa
                                                     max_ctx=L, superblocks=sb)
-                else:  # fa<waves>[:p<parts>] (parts: explicit context split; "auto": the library's rule)
-                    name, _, pp = k.partition(":")
+                else:  # fa<waves>[:p<parts>][:z|:n] (parts: explicit context split; z / n: causal block
+                    #       pairing forced on / off, default the library's rule)
+                    name, *opts = k.split(":")
                     w = int(name[2:])
-                    nparts = int(pp[1:]) if pp.startswith("p") else None
+                    nparts = next((int(o[1:]) for o in opts if o.startswith("p")), None)
+                    pair = True if "z" in opts else (False if "n" in opts else None)
                     fb = torch.from_numpy(ops.fa_blocks(ntoks, nh // nkv, w)).to(dev)
                     fn = lambda: ops.attention_fa(q, kc, vc, bt, q_seq, q_ctx, fb, nh, nkv, scale, out=out,  # noqa
-                                                  max_ctx=L, waves=w, num_parts=nparts)
+                                                  max_ctx=L, waves=w, num_parts=nparts, pair=pair)
                 us = timeit(fn)
                 o = out.float().clone()
                 if ref_out is None:

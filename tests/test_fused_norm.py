@@ -115,11 +115,12 @@ def test_producer_epilogue_residual_pack_and_sumsq(kern, M):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("M", [65, 96, 128])
+@pytest.mark.parametrize("M", [65, 96, 128, 129, 192, 200, 256])
 def test_wide_rows_consumer_and_producer(M):
-    """65..128 rows (decode steps of 65..128 sessions): the consumers (qkv: split-K ring +
+    """65..256 rows (decode steps of 65..256 sessions): the consumers (qkv: split-K ring +
     reduce with the row scale; gate/up: balanced ring with the row scale and packed SwiGLU) and
-    the producer (split-K ring + the reduce launch's residual / packed copy / statistics)."""
+    the producer (split-K ring + the reduce launch's residual / packed copy / statistics), against
+    fp32 oracles.  129..256 rows run the 12 / 16 row-tile kernels over fewer real row tiles."""
     dev = "cuda"
     g = torch.Generator(device=dev).manual_seed(500 + M)
     K, N = 2048, 2048
@@ -161,8 +162,9 @@ def test_wide_rows_consumer_and_producer(M):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("graphs", [False, True])
-def test_fused_executor_wide_batch_matches_unfused(graphs, monkeypatch):
-    """A 100-session decode step takes the fused-norm path (wide kernels) and matches the
+@pytest.mark.parametrize("n", [100, 200])
+def test_fused_executor_wide_batch_matches_unfused(graphs, n, monkeypatch):
+    """A 100- / 200-session decode step takes the fused-norm path (wide kernels) and matches the
     unfused packed path step by step."""
     import dataclasses
 
@@ -173,7 +175,6 @@ def test_fused_executor_wide_batch_matches_unfused(graphs, monkeypatch):
     cfg = dataclasses.replace(resolve_model("small-llama"), hidden_size=2048, intermediate_size=4096,
                               num_attention_heads=16, num_key_value_heads=16, num_hidden_layers=2,
                               name="wide-test")
-    n = 100
 
     def build(fused):
         monkeypatch.setenv("MPAMD_FUSED_NORM", "1" if fused else "0")
@@ -182,8 +183,8 @@ def test_fused_executor_wide_batch_matches_unfused(graphs, monkeypatch):
             gen = torch.Generator(device="cuda").manual_seed(70 + i)
             lay.input_norm = (torch.rand(cfg.hidden_size, device="cuda", generator=gen) + 0.5).to(torch.bfloat16)
             lay.post_norm = (torch.rand(cfg.hidden_size, device="cuda", generator=gen) + 0.5).to(torch.bfloat16)
-        return StageExecutor(cfg, w, "cuda", kv_cache_bytes=512 << 20, max_sessions=128, max_seq_len=64,
-                             use_graphs=graphs)
+        return StageExecutor(cfg, w, "cuda", kv_cache_bytes=512 << 20, max_sessions=256, max_seq_len=64,
+                             use_graphs=graphs, graph_max_batch=256)
 
     fx, ux = build(True), build(False)
     assert fx._fused and fx._fused_wide_ok(n)

@@ -628,12 +628,14 @@ def test_attention_mfma_grouped_prefill(nh, nkv, D, ntoks, prefix, parts):
 @pytest.mark.parametrize("nh,nkv", [(32, 32), (32, 8), (64, 8), (16, 8), (8, 4)])
 @pytest.mark.parametrize("ntoks,prefix", [([70, 9, 1, 33, 130], [0, 0, 0, 0, 0]), ([300, 17], [64, 5]),
                                           ([1000], [0]), ([48, 64], [1, 200]), ([129, 256], [0, 63])])
-@pytest.mark.parametrize("waves,parts", [(4, None), (8, None), (4, 3)])
-def test_attention_fa_prefill(nh, nkv, ntoks, prefix, waves, parts):
+@pytest.mark.parametrize("waves,parts,pair", [(4, None, False), (8, None, False), (4, 3, False), (4, None, True),
+                                             (8, None, True)])
+def test_attention_fa_prefill(nh, nkv, ntoks, prefix, waves, parts, pair):
     """FA2 prefill kernel (32x32x16 MFMA, transposed LDS reads of V) vs the fp32 reference:
     ragged prompts, chunked prefill over an existing prefix (ctx = prefix + i + 1), 4- and
-    8-wave workgroups, context split over parts.  Cache slots past every context hold NaN:
-    they must never reach the output."""
+    8-wave workgroups, context split over parts, causal block pairing (a workgroup runs a long
+    block and its short mirror; odd block counts leave one unpaired).  Cache slots past every
+    context hold NaN: they must never reach the output."""
     D = 128
     ctxs = [p + n for p, n in zip(prefix, ntoks)]
     q, kc, vc, bt, _, _ = _attn_case(nh, nkv, D, ctxs)
@@ -649,7 +651,7 @@ def test_attention_fa_prefill(nh, nkv, ntoks, prefix, waves, parts):
     fb = torch.from_numpy(ops.fa_blocks(ntoks, nh // nkv, waves)).to(DEV)
     assert int(fb[1].sum()) == T
     scale = 1 / math.sqrt(D)
-    out = ops.attention_fa(q, kc, vc, bt, q_seq, q_ctx, fb, nh, nkv, scale, waves=waves, num_parts=parts)
+    out = ops.attention_fa(q, kc, vc, bt, q_seq, q_ctx, fb, nh, nkv, scale, waves=waves, num_parts=parts, pair=pair)
     kr, vr = kc.clone(), vc.clone()
     kr[kr.isnan()] = 0
     vr[vr.isnan()] = 0

@@ -1,0 +1,41 @@
+"""Stage-local recovery building blocks (CPU): the per-stage replay cache of output rows
+(``parallel.engine.ReplayCache``) and session adoption by rename (``SessionManager.rename``)."""
+import numpy as np
+import torch
+
+from src.parallel.engine import ReplayCache
+from src.runtime.kv_cache import PagedKVCache
+from src.runtime.session import SessionManager
+
+
+def test_replay_cache_stores_rows_by_handle_and_position():
+    rc = ReplayCache(max_handles=4, max_len=8, hidden=3, dtype=torch.float32, device="cpu")
+    # a step: handle 2 prefills 3 tokens from position 0, handle 0 decodes 1 token at position 5
+    out = torch.arange(12, dtype=torch.float32).view(4, 3)
+    rc.store([(2, 3, 0, 0, 0), (0, 1, 5, 0, 0)], out)
+    assert torch.equal(rc.rows(2, 3), out[:3])
+    assert torch.equal(rc.buf[0 * 8 + 5], out[3])
+    # a later step appends at positions 3, 4 of handle 2; rows past max_len are dropped, not wrapped
+    rc.store([(2, 2, 3, 0, 0), (1, 3, 6, 0, 0)], torch.ones(5, 3))
+    assert torch.equal(rc.rows(2, 5)[3:], torch.ones(2, 3))
+    assert torch.equal(rc.buf[1 * 8 + 6:1 * 8 + 8], torch.ones(2, 3))
+    assert torch.equal(rc.buf[2 * 8], out[0])  # handle 1's overflow did not reach handle 2
+
+
+def test_session_rename_moves_kv_and_closes_target():
+    cache = PagedKVCache(num_layers=1, num_pages=16, page_size=4, num_kv_heads=1, head_dim=8,
+                         dtype=torch.float32, device="cpu")
+    sm = SessionManager(cache, max_sessions=4, max_seq_len=32)
+    s = sm.open("chan-a:3")
+    sm.reserve(s, 10)
+    s.length = 10
+    pages = list(s.pages)
+    other = sm.open("chan-b:0")
+    sm.reserve(other, 4)
+    free0 = sm.free_pages
+    moved = sm.rename("chan-a:3", "chan-b:0")
+    assert moved is s and moved.sid == "chan-b:0" and moved.pages == pages and moved.length == 10
+    assert "chan-a:3" not in sm.sessions and sm.get("chan-b:0") is s
+    assert sm.free_pages == free0 + 1  # the replaced target's page went back
+    assert sm.rename("missing", "x") is None
+    assert int(np.sum(sm.table[s.row] >= 0)) == len(pages)

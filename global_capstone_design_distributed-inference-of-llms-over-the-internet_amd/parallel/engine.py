@@ -310,6 +310,25 @@ class ReplayCache:
     def __init__(self, max_handles: int, max_len: int, hidden: int, dtype, device):
         self.max_len = int(max_len)
         self.buf = torch.zeros(int(max_handles) * self.max_len, hidden, dtype=dtype, device=device)
+        pin = self.buf.is_cuda
+        self._pin = [torch.empty(1 << 14, dtype=torch.int64, pin_memory=pin) for _ in range(2)]
+        self._pin_ev: List[Optional[object]] = [None, None]
+        self._k = 0
+
+    def _to_device(self, a: np.ndarray) -> torch.Tensor:
+        """Row indices to the device without a host block (double-buffered pinned staging)."""
+        if not self.buf.is_cuda or len(a) > self._pin[0].numel():
+            return torch.from_numpy(a).to(self.buf.device)
+        self._k ^= 1
+        if self._pin_ev[self._k] is not None:
+            self._pin_ev[self._k].synchronize()
+        host = self._pin[self._k]
+        host.numpy()[: len(a)] = a
+        dev = host[: len(a)].to(self.buf.device, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._pin_ev[self._k] = ev
+        return dev
 
     def store(self, recs, out: torch.Tensor) -> None:
         """``recs``: the step's (handle, n_tokens, start, ...) records, ``out`` its [T, H] rows."""
@@ -323,10 +342,10 @@ class ReplayCache:
             off += n
         if not idx:
             return
-        idx, keep = np.concatenate(idx), np.concatenate(keep)
-        dev = self.buf.device
-        src = out if len(keep) == out.shape[0] else out.index_select(0, torch.from_numpy(keep).to(dev))
-        self.buf.index_copy_(0, torch.from_numpy(idx.astype(np.int64)).to(dev), src)
+        idx, keep = np.concatenate(idx).astype(np.int64), np.concatenate(keep).astype(np.int64)
+        src = out[: len(keep)] if np.array_equal(keep, np.arange(len(keep))) else \
+            out.index_select(0, self._to_device(keep))
+        self.buf.index_copy_(0, self._to_device(idx), src)
 
     def rows(self, handle: int, n: int) -> torch.Tensor:
         return self.buf[int(handle) * self.max_len: int(handle) * self.max_len + int(n)]

@@ -770,10 +770,14 @@ def wide_gemm_ok(M: int, N: int, K: int, epilogue: int = 0, out_packed: bool = F
     return _RW_OK[key]
 
 
+# decode rows the hand-written GEMMs take (MPAMD_WIDE_ROWS=128: hipBLASLt above 128, the round-3 split)
+WIDE_ROWS = int(os.environ.get("MPAMD_WIDE_ROWS", "256"))
+
+
 def native_gemm_ok(M: int, N: int, K: int, epilogue: int = 0, out_packed: bool = False) -> bool:
     if not (K % 128 == 0 and N % (32 if epilogue == 1 else 16) == 0):
         return False
-    if 64 < M <= 256:
+    if 64 < M <= WIDE_ROWS:
         return wide_gemm_ok(M, N, K, epilogue, out_packed)
     return 0 < M <= 64
 

@@ -511,6 +511,8 @@ def main(argv=None):
             "hop_bytes_sent_per_rank": [int(p[3]) for p in per_stage],
             "hop_sends_per_rank": [int(p[4]) for p in per_stage],
             "hop_recv_wait_ms_per_rank": [round(p[5], 4) for p in per_stage],
+            # the qkv fold per decode row bucket, as the warm-up's decode-graph A/B left it
+            "qkv_fold": {f"M{k[0]}": bool(v) for k, v in sorted(ops._QKV_FOLD.items())},
             "prefill_plus_first_token_s": round(prefill_s, 3),
             # the prefill round alone: every session's prompt through the whole pipeline
             # (micro-batch slots x batch x prompt-len tokens), max over ranks

@@ -517,11 +517,14 @@ FA_PAIR = os.environ.get("MPAMD_FA_PAIR", "auto")
 
 def fa_pair(nblocks: int, nh: int, nkv: int, num_parts: int, n_cu: int = 256) -> bool:
     """Pair each long causal query block with its short mirror in one workgroup (csrc/attention_fa.hip
-    ``pair``) when the grid is at most 2 workgroups per CU: there the longest blocks, not the total
-    work, set the kernel time.  MPAMD_FA_PAIR=0/1 forces it."""
+    ``pair``): every workgroup then streams the same context, so the longest blocks no longer set
+    the kernel time, and there are half as many workgroups to launch.  Measured faster or equal
+    in every case of profiles/r4d/attn_pair.jsonl (1 x 2048 MHA 116.6 -> 80.9 us, 1 x 4096 MHA
+    231.7 -> 159.8, 64 x 128 GQA 59.3 -> 54.5), so it is on whenever the context is not split.
+    MPAMD_FA_PAIR=0/1 forces it."""
     if FA_PAIR in ("0", "1"):
         return FA_PAIR == "1" and num_parts == 1
-    return num_parts == 1 and nblocks >= 4 and nblocks * nkv <= 2 * n_cu
+    return num_parts == 1 and nblocks >= 2
 
 
 def fa_ok(nh: int, nkv: int, D: int, page_size: int) -> bool:
@@ -770,8 +773,12 @@ def wide_gemm_ok(M: int, N: int, K: int, epilogue: int = 0, out_packed: bool = F
     return _RW_OK[key]
 
 
-# decode rows the hand-written GEMMs take (MPAMD_WIDE_ROWS=128: hipBLASLt above 128, the round-3 split)
-WIDE_ROWS = int(os.environ.get("MPAMD_WIDE_ROWS", "256"))
+# decode rows the hand-written GEMMs take.  The ring / split-K ring kernels are built and tested up
+# to 256 rows (12 / 16 row tiles), but at 256 sessions they measured slower than hipBLASLt + the
+# unfused path (11.18 vs ~9.5 ms/step, profiles/r4d: one column group per workgroup takes in the
+# whole 256-row activation block, 5x its weight bytes) - so 128 stays the default split;
+# MPAMD_WIDE_ROWS=256 turns them on above it.
+WIDE_ROWS = int(os.environ.get("MPAMD_WIDE_ROWS", "128"))
 
 
 def native_gemm_ok(M: int, N: int, K: int, epilogue: int = 0, out_packed: bool = False) -> bool:

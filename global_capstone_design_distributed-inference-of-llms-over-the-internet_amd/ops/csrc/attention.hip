@@ -446,7 +446,7 @@ __global__ __launch_bounds__(NW * 64) void paged_attn1_kernel(
     float scale_log2, int packed_mt, RopeFuse rf, int* __restrict__ cnt) {
   constexpr int LPT = D / 8;
   constexpr int TPI = 64 / LPT;
-  // U: tokens per lane group per iteration (U = 8: half the dependent K / V round trips at short contexts)
+  // U: tokens per lane group per iteration (U = 8 measured 32 -> 43 us at 64 x 170, profiles/r4d)
   constexpr int TPW = TPI * U;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int NT_ = NW * 64;
@@ -758,17 +758,10 @@ static void launch_attn(const void* q, int64_t q_stride, const void* kc, const v
     const char* v = getenv("MPAMD_ATTN_PIPE");
     return !(v && v[0] == '0');
   }();
-  // MPAMD_ATTN_U=8 (ablation): 8 tokens per lane group per iteration on the pipelined path
-  static const bool u8 = [] {
-    const char* v = getenv("MPAMD_ATTN_U");
-    return v && atoi(v) == 8;
-  }();
+
   if (one_pass && wide) {
     if (rf.pos) go(paged_attn1_kernel<D, NREP, true, 16, false>);
     else go(paged_attn1_kernel<D, NREP, false, 16, false>);
-  } else if (one_pass && pipe && u8) {
-    if (rf.pos) go(paged_attn1_kernel<D, NREP, true, 4, true, 8>);
-    else go(paged_attn1_kernel<D, NREP, false, 4, true, 8>);
   } else if (one_pass && pipe) {
     if (rf.pos) go(paged_attn1_kernel<D, NREP, true, 4, true>);
     else go(paged_attn1_kernel<D, NREP, false, 4, true>);

@@ -116,11 +116,12 @@ def test_producer_epilogue_residual_pack_and_sumsq(kern, M):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("M", [65, 96, 128, 129, 192, 200, 256])
-def test_wide_rows_consumer_and_producer(M):
+def test_wide_rows_consumer_and_producer(M, monkeypatch):
     """65..256 rows (decode steps of 65..256 sessions): the consumers (qkv: split-K ring +
     reduce with the row scale; gate/up: balanced ring with the row scale and packed SwiGLU) and
     the producer (split-K ring + the reduce launch's residual / packed copy / statistics), against
     fp32 oracles.  129..256 rows run the 12 / 16 row-tile kernels over fewer real row tiles."""
+    monkeypatch.setattr(ops, "WIDE_ROWS", 256)  # above 128 rows the hand-written forms are opt-in
     dev = "cuda"
     g = torch.Generator(device=dev).manual_seed(500 + M)
     K, N = 2048, 2048
@@ -167,6 +168,8 @@ def test_fused_executor_wide_batch_matches_unfused(graphs, n, monkeypatch):
     """A 100- / 200-session decode step takes the fused-norm path (wide kernels) and matches the
     unfused packed path step by step."""
     import dataclasses
+
+    monkeypatch.setattr(ops, "WIDE_ROWS", 256)
 
     from src.models.config import resolve_model
     from src.models.weights import random_stage_weights

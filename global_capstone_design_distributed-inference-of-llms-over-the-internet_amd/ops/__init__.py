@@ -135,7 +135,7 @@ _SK_CHOICE = {}  # (m_bucket, N, K, epilogue) -> kernel name (see _KERNEL_FLAGS)
 # in-launch combines "rwki" (last arriver) / "rwks" (symmetric), and the row-split ring "rwr"
 # (a pair of workgroups per column group, half the rows each: no K split, no combine)
 _KERNEL_FLAGS = {"pk": 0, "sk": 4, "lds22": 16, "lds24": 16 | 32, "lds42": 16 | 96, "rw": 128, "rwk": 256,
-                 "rwki": 256 | 512, "rwks": 256 | 2048, "rwr": 4096}
+                 "rwki": 256 | 512, "rwks": 256 | 2048, "rwr": 4096, "mw": 32768}
 _LDS_CFG = {"lds22": (2, 2), "lds24": (2, 4), "lds42": (4, 2)}
 # "<kernel>+r": the same kernel with every workgroup's k walk rotated (csrc/gemm_kernels.h
 # rw_krot, flags bit 10) - kept by the autotuners per shape only where it measures faster
@@ -144,6 +144,9 @@ ROT_FLAG = 1024
 
 # 65..128-row steps (not autotuned): rotated k walk (MPAMD_WIDE_ROT=1) or the lock-step one
 _WIDE_ROT = os.environ.get("MPAMD_WIDE_ROT", "0") == "1"
+# 65..128-row steps on the row-split form (csrc/gemm_mw.h) instead of the ring kernels
+# (MPAMD_WIDE_KERNEL=mw); 129..256 rows always run it
+_WIDE_MW = os.environ.get("MPAMD_WIDE_KERNEL", "") == "mw"
 
 
 def _base(name: str) -> str:
@@ -840,7 +843,9 @@ def linear(x, w, out=None, epilogue=0, residual=None, policy=None, wp=None, a_ro
                    else torch.empty(M, ncols, dtype=x.dtype, device=x.device))
         if gate is not None:
             kern = "pk"
-        elif M > 64:  # 65..256 rows: split-K ring where it applies (o, down), else the ring kernel
+        elif M > 128 or (M > 64 and _WIDE_MW):  # row-split form (its own geometry per shape)
+            kern = "mw"
+        elif M > 64:  # 65..128 rows: split-K ring where it applies (o, down), else the ring kernel
             kern = "rwk" if (not out_packed and _covered("rwk", M, N, K, epilogue)
                              and os.environ.get("MPAMD_WIDE_SPLITK", "1") != "0") else "rw"
             if _WIDE_ROT:
@@ -848,7 +853,7 @@ def linear(x, w, out=None, epilogue=0, residual=None, policy=None, wp=None, a_ro
         else:
             kern = _kernel_for(M, N, K, epilogue)
         flags = 1 | (2 if out_packed else 0) | _kflags(kern)
-        ws = gemm_workspace(x.device) if _base(kern) in ("sk", "rwk", "rwki", "rwks") else None
+        ws = gemm_workspace(x.device) if _base(kern) in ("sk", "rwk", "rwki", "rwks", "mw") else None
         torch.ops.mpamd.gemm(x, wp, out, residual, int(epilogue), M, flags, ws, gate, ap_out, ss_out, ss_zero, ss_in,
                              1.0 / K, float(eps))
         return out

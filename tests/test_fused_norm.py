@@ -115,13 +115,15 @@ def test_producer_epilogue_residual_pack_and_sumsq(kern, M):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("M", [65, 96, 128, 129, 192, 200, 256])
-def test_wide_rows_consumer_and_producer(M, monkeypatch):
+@pytest.mark.parametrize("M,mw", [(65, False), (96, False), (128, False), (65, True), (96, True), (128, True),
+                                  (129, True), (192, True), (200, True), (256, True)])
+def test_wide_rows_consumer_and_producer(M, mw, monkeypatch):
     """65..256 rows (decode steps of 65..256 sessions): the consumers (qkv: split-K ring +
     reduce with the row scale; gate/up: balanced ring with the row scale and packed SwiGLU) and
     the producer (split-K ring + the reduce launch's residual / packed copy / statistics), against
-    fp32 oracles.  129..256 rows run the 12 / 16 row-tile kernels over fewer real row tiles."""
+    fp32 oracles.  mw: the row-split form (csrc/gemm_mw.h), which every step above 128 rows runs."""
     monkeypatch.setattr(ops, "WIDE_ROWS", 256)  # above 128 rows the hand-written forms are opt-in
+    monkeypatch.setattr(ops, "_WIDE_MW", mw)     # the row-split form (csrc/gemm_mw.h); > 128 rows always
     dev = "cuda"
     g = torch.Generator(device=dev).manual_seed(500 + M)
     K, N = 2048, 2048

@@ -411,6 +411,7 @@ def _run_rank0_channel(args, device, ex, tok, tx, route, ids, on_token=None, res
 
     fe = ReplicaFrontend(len(engines), locals=engines, throughputs=thrs if known else None, timeout_s=timeout,
                          recover=recover)
+    engines[0]._settle_heap()  # the one-time heap freeze before t0, not inside the first round (TTFT)
     progress = {"n": 0, "t": time.perf_counter()}
 
     def _on_token(req, tok_id):

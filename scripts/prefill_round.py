@@ -45,6 +45,7 @@ def main():
     t0 = time.perf_counter()
     eng = PipelineServingEngine(ex, None, n_slots=1, batch=B, name="pr")
     eng.freeze_heap = True
+    eng._settle_heap()  # as bench.py / the CLI do before their first round
     t_init = time.perf_counter() - t0
     gpu = []
     orig = ex.forward

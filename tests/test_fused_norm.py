@@ -164,6 +164,37 @@ def test_wide_rows_consumer_and_producer(M, mw, monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("M", [200, 256])
+def test_row_split_in_kernel_epilogues(M, monkeypatch):
+    """The row-split form's S = 1 geometry (csrc/gemm_mw.h: every column group in one workgroup,
+    the decode epilogue in the kernel) - what the Llama-2-7B qkv (N = 12288) and gate/up
+    (N = 22016) widths choose at 129..256 rows: row-scaled consumer and packed SwiGLU vs fp32."""
+    monkeypatch.setattr(ops, "WIDE_ROWS", 256)
+    dev = "cuda"
+    g = torch.Generator(device=dev).manual_seed(900 + M)
+    K = 1024
+    x = (torch.randn(M, K, device=dev, generator=g) * 0.7).to(torch.bfloat16)
+    gw = (torch.rand(K, device=dev, generator=g) + 0.5).to(torch.bfloat16)
+    ss = ops.norm_stats_buffer(dev)[0]
+    res = torch.empty_like(x)
+    xp = torch.zeros(ops.packed_numel(M, K), dtype=torch.bfloat16, device=dev)
+    ops.rmsnorm(x, gw, EPS, out=xp, residual=res, mode=3, packed=True, ss=ss)
+    xn = _rms_ref(x, gw).float()
+    N = 12288
+    w = (torch.randn(N, K, device=dev, generator=g) * 0.03).to(torch.bfloat16)
+    wp = ops.pack_weight((w.float() * gw.float()[None, :]).to(torch.bfloat16).contiguous())
+    y = ops.linear(xp, None, wp=wp, a_rows=M, ss_in=ss, eps=EPS)
+    torch.testing.assert_close(y.float(), xn @ w.float().t(), atol=3e-2, rtol=3e-2)
+    F = 11008
+    wgu = (torch.randn(2 * F, K, device=dev, generator=g) * 0.03).to(torch.bfloat16)
+    wgup = ops.pack_weight((wgu.float() * gw.float()[None, :]).to(torch.bfloat16).contiguous())
+    act = torch.zeros(ops.packed_numel(M, F), dtype=torch.bfloat16, device=dev)
+    ops.linear(xp, None, out=act, epilogue=1, wp=wgup, a_rows=M, out_packed=True, ss_in=ss, eps=EPS)
+    exp = ref.swiglu((xn @ wgu.float().t()).to(torch.bfloat16)).float()
+    torch.testing.assert_close(ref.unpack_act(act, M, F).float(), exp, atol=5e-2, rtol=3e-2)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("graphs", [False, True])
 @pytest.mark.parametrize("n", [100, 200])
 def test_fused_executor_wide_batch_matches_unfused(graphs, n, monkeypatch):

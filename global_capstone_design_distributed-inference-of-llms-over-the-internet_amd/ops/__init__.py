@@ -214,6 +214,8 @@ def _covered(name: str, M: int, N: int, K: int, epilogue: int) -> bool:
         return epilogue != 1 and N % 2048 == 0
     if name in ("rwki", "rwks"):  # the same with an in-launch combine (M <= 64)
         return epilogue != 1 and N % 2048 == 0 and M <= 64
+    if name == "mw":  # row-split wide form: chosen by row count (linear), never by the autotuner
+        return False
     if name == "rwr":  # row-split ring: 2 or 4 row tiles split over a workgroup pair
         return epilogue != 1 and N % 2048 == 0 and (M + 15) // 16 in (2, 4)
     return _lds_covered(name, M, N, K, epilogue)

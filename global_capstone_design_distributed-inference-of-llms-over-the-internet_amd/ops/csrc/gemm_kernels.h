@@ -119,41 +119,52 @@ __device__ __forceinline__ void clear_other(const EpiArgs& ep) {
 }
 
 // Consumer side (EPI 0 / 1 only; compiled out of the producer epilogues), in two halves around
-// the main loop: thread t owns row t % SS_ROWS and shard group t / SS_ROWS (G = NW * 64 /
-// SS_ROWS groups), loads its SS_NSH / G shard words right AFTER the kernel's first weight loads
+// the main loop: thread t owns row t % R and shard group t / R (R: the step's row window, G =
+// threads / R groups), loads its SS_NSH / G shard words right AFTER the kernel's first weight loads
 // and folds them into one 64-bit partial (in-order vmcnt: waiting for them costs nothing beyond
 // the first weight chunk the loop waits for anyway, and only 2 VGPRs stay live through the
 // loop); the G partials of a row are reduced through LDS in the epilogue, after the main loop's
 // last barrier.  Rows past the step's M read zeroed shards: their scale is never used.
 template <bool ON, int NW = 8>
 struct RowScale {
-  static constexpr int G = NW * 64 / SS_ROWS;
-  static_assert(G >= 1 && G <= SS_PG && SS_NSH % G == 0, "shard groups");
+  // The step's rows use a power-of-two window R >= 16 x row tiles (at most SS_ROWS) and the
+  // workgroup's threads form G = threads / R shard groups, so a small step spreads its 32 shard
+  // words over more threads (batch 1: 16 rows x 16 groups, 2 loads a thread) while 256 rows
+  // still fit (1 group of 256 at 4 waves).
+  static constexpr int NT = NW * 64;
+  static_assert(NT <= SS_PG * SS_ROWS, "shard partials fit the shared scratch");
   u64 v = 0;
+  int R = SS_ROWS;
+  __device__ __forceinline__ static int window(int mt_out) {
+    int r = 16;
+    while (r < 16 * mt_out && r < SS_ROWS) r <<= 1;
+    return r;
+  }
+  __device__ __forceinline__ int groups() const { return NT / R < SS_NSH ? NT / R : SS_NSH; }
   __device__ __forceinline__ void load(const EpiArgs& ep, const void* any_valid) {
     if constexpr (ON) {
+      R = window(ep.mt_out);
       const u64* src = ep.ss_in != nullptr ? ep.ss_in : reinterpret_cast<const u64*>(any_valid);
-      const int tid = threadIdx.x;
-      const int row = tid % SS_ROWS, grp = tid / SS_ROWS;
+      const int tid = threadIdx.x, G = groups();
+      const int row = tid % R, grp = tid / R;
       u64 t = 0;
-      if (row < 16 * ep.mt_out) {  // rows past the step's row tiles: never scaled, not loaded
-#pragma unroll
+      if (grp < G && row < 16 * ep.mt_out) {  // rows past the step's row tiles: never scaled, not loaded
         for (int j = 0; j < SS_NSH / G; ++j) t += src[ep.ss_in != nullptr ? (grp + G * j) * SS_ROWS + row : 0];
       }
       v = t;
     }
   }
   // every thread of the workgroup calls this (two barriers inside when ss_in is set)
-  __device__ __forceinline__ void finish(const EpiArgs& ep, u64 (*part)[SS_ROWS], float* rs) {
+  __device__ __forceinline__ void finish(const EpiArgs& ep, u64 (*part2)[SS_ROWS], float* rs) {
     if constexpr (ON) {
       if (ep.ss_in == nullptr) return;
-      const int tid = threadIdx.x;
-      part[tid / SS_ROWS][tid % SS_ROWS] = v;
+      u64* part = &part2[0][0];
+      const int tid = threadIdx.x, G = groups();
+      if (tid / R < G) part[tid] = v;  // [grp][row] = grp * R + row = tid
       __syncthreads();
-      if (tid < SS_ROWS) {
+      if (tid < R) {
         u64 s = 0;
-#pragma unroll
-        for (int w = 0; w < G; ++w) s += part[w][tid];
+        for (int w = 0; w < G; ++w) s += part[w * R + tid];
         rs[tid] = rsqrtf((float)s * (1.f / SS_FX) * ep.inv_k + ep.eps);
       }
       __syncthreads();

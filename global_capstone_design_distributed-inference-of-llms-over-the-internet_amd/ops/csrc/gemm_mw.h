@@ -4,15 +4,12 @@
 // its 4 waves: at 256 rows every workgroup then takes in the whole 256 x K activation block (2 MB
 // at K = 4096) for 192-384 KB of weights, and 256 accumulator AGPRs cap the group at 4 column
 // tiles - measured slower than hipBLASLt (profiles/r4d: gate/up 116 vs 60 us).  Here the 4 waves
-// split the ROWS instead (wave w owns row tiles [MTW w, MTW (w + 1))), so the accumulators are
-// MTW x NT quads per wave and a column group can be 4x wider; the weight fragments every wave
-// needs are staged ONCE per workgroup through LDS:
+// split the ROWS instead (wave w owns row tiles [MTW w, MTW (w + 1))) and each walks all of the
+// split's k-slices through its own register ring (A: its MTW fragments, B: the group's NT weight
+// fragments, R slots in flight); the four waves read the same weight fragments together, so
+// three of the four come from L2.  (A first version staged the weights once per workgroup
+// through LDS with one barrier per 2 k-slices: latency-bound at 3-5x hipBLASLt, profiles/r4f.)
 //
-//   * per chunk of KC k-slices the 256 threads load the group's NT x KC weight fragments (1 KiB
-//     each, fragment order: ops.pack_weight) and store them to an LDS stage (two stages, one
-//     barrier per chunk); each wave reads them back with conflict-free ds_read_b128 (64 lanes x
-//     16 B contiguous) while its own A fragments (the packed activation, 1 KiB each) come
-//     straight from global memory, prefetched a chunk ahead in registers;
 //   * K may be split over S workgroups of the same column group (ks0..ks1): S == 1 runs the
 //     decode epilogues in the kernel (row-scaled consumer, packed SwiGLU, residual-stream
 //     producer - tile_epilogue, every quad owned by exactly one wave, no cross-wave reduction);
@@ -26,7 +23,11 @@
 
 namespace mp {
 
-constexpr int MW_KC = 2;  // k-slices per LDS stage
+constexpr int MW_KC = 2;  // (geometry granularity: a split keeps at least 2 x MW_KC k-slices)
+
+// Register ring depth: 4 slots of one k-slice (A: MTW fragments, B: NT) while they fit ~160 VGPRs.
+template <int MTW, int NT>
+constexpr int mw_depth() { return 16 * (MTW + NT) <= 160 ? 4 : 2; }
 
 template <int MTW, int NT, int EPI, bool OPK>
 __global__ __launch_bounds__(256) void gemm_mw_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ wp,
@@ -35,9 +36,7 @@ __global__ __launch_bounds__(256) void gemm_mw_kernel(const bf16_t* __restrict__
                                                       float* __restrict__ part, int M, int N, int K, int S,
                                                       int tiles, const EpiArgs ep) {
   // EPI -1: partial slabs only (S > 1); else the epilogue runs here (S == 1)
-  constexpr int KC = MW_KC, NB = KC * NT / 4;  // B fragments each thread stages per chunk
-  static_assert((KC * NT) % 4 == 0, "B chunk splits evenly over the 4 waves");
-  __shared__ __attribute__((aligned(16))) u16x8 sb[2][KC * NT][64];
+  constexpr int R = mw_depth<MTW, NT>();
   __shared__ u64 rs_part[SS_PG][SS_ROWS];
   __shared__ float rs_lds[SS_ROWS];
   clear_other(ep);
@@ -47,75 +46,47 @@ __global__ __launch_bounds__(256) void gemm_mw_kernel(const bf16_t* __restrict__
   const int tile0 = c * NT;
   const int nks = K >> 5;
   const int ks0 = (int)((int64_t)sp * nks / S), ks1 = (int)((int64_t)(sp + 1) * nks / S);
-  const int nch = (ks1 - ks0 + KC - 1) / KC;
+  const int cnt = ks1 - ks0;  // every wave walks every k-slice of the split, over its own rows
   const int mta = ep.mt_out;  // row tiles of the packed activation (a runtime stride)
   const int mt0 = wid * MTW;
   const bf16_t* xl = x + lane * 8;
   const bf16_t* wl = wp + lane * 8;
-
-  u16x8 bst[NB];
-  auto load_b = [&](int kc0) {
+  int trow[NT];  // clamped column tiles (a partial last group re-reads its last tile, never stores it)
 #pragma unroll
-    for (int j = 0; j < NB; ++j) {
-      const int f = wid + 4 * j, k = f / NT, t = f - k * NT;
-      const int ks = min(kc0 + k, ks1 - 1), tile = min(tile0 + t, tiles - 1);
-      bst[j] = __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(wl + (((int64_t)tile * nks + ks) << 9)));
-    }
-  };
-  auto store_b = [&](int buf) {
-#pragma unroll
-    for (int j = 0; j < NB; ++j) sb[buf][wid + 4 * j][lane] = bst[j];
-  };
-  auto load_a = [&](int kc0, u16x8 (&ar)[KC][MTW]) {
-#pragma unroll
-    for (int k = 0; k < KC; ++k)
-#pragma unroll
-      for (int mt = 0; mt < MTW; ++mt) {
-        const int ks = min(kc0 + k, ks1 - 1);
-        ar[k][mt] = load_a_rows(xl + (((int64_t)ks * mta + min(mt0 + mt, mta - 1)) << 9), lane,
-                                (mt0 + mt) * 16 + (lane & 15) < M);
-      }
-  };
+  for (int t = 0; t < NT; ++t) trow[t] = min(tile0 + t, tiles - 1);
 
   f32x4 acc[MTW][NT];
 #pragma unroll
   for (int mt = 0; mt < MTW; ++mt)
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[mt][t] = (f32x4)(0.f);
-  u16x8 a0[KC][MTW], a1[KC][MTW];
-  load_b(ks0);
-  load_a(ks0, a0);
+  u16x8 ra[R][MTW], rb[R][NT];
+  // the 4 waves read the same weight fragments at about the same time: default cache policy, so
+  // the other three get them from L2 (a non-temporal load would not leave them there)
+#define MW_LOAD(s_, i_)                                                                                   \
+  {                                                                                                       \
+    const int k_ = ks0 + min((i_), cnt - 1);                                                              \
+    _Pragma("unroll") for (int t = 0; t < NT; ++t) rb[s_][t] =                                            \
+        *reinterpret_cast<const u16x8*>(wl + (((int64_t)trow[t] * nks + k_) << 9));                       \
+    _Pragma("unroll") for (int mt = 0; mt < MTW; ++mt) ra[s_][mt] =                                       \
+        load_a_rows(xl + (((int64_t)k_ * mta + min(mt0 + mt, mta - 1)) << 9), lane, (mt0 + mt) * 16 + (lane & 15) < M); \
+  }
+#pragma unroll
+  for (int s = 0; s < R; ++s) MW_LOAD(s, s)
   rsc.load(ep, wp);
-  store_b(0);
-  __syncthreads();
-  // one chunk: MFMAs on stage CUR with A registers AR while the next chunk's B (registers) and A
-  // (the other register set) are in flight; then B goes to the other stage and one barrier
-#define MW_STEP(CUR, AR, AN)                                                                   \
-  {                                                                                            \
-    const bool more = i + 1 < nch;                                                             \
-    const int kn = ks0 + (i + 1) * KC;                                                         \
-    if (more) {                                                                                \
-      load_b(kn);                                                                              \
-      load_a(kn, AN);                                                                          \
-    }                                                                                          \
-    _Pragma("unroll") for (int k = 0; k < KC; ++k) {                                           \
-      if (ks0 + i * KC + k < ks1) {                                                            \
-        _Pragma("unroll") for (int t = 0; t < NT; ++t) {                                       \
-          const u16x8 b = sb[CUR][k * NT + t][lane];                                           \
-          _Pragma("unroll") for (int mt = 0; mt < MTW; ++mt) acc[mt][t] = mfma16(AR[k][mt], b, acc[mt][t]); \
-        }                                                                                      \
-      }                                                                                        \
-    }                                                                                          \
-    if (more) store_b(CUR ^ 1);                                                                \
-    __syncthreads();                                                                           \
-    ++i;                                                                                       \
+  for (int i0 = 0; i0 < cnt; i0 += R) {
+#pragma unroll
+    for (int s = 0; s < R; ++s) {
+      if (i0 + s < cnt) {
+#pragma unroll
+        for (int mt = 0; mt < MTW; ++mt)
+#pragma unroll
+          for (int t = 0; t < NT; ++t) acc[mt][t] = mfma16(ra[s][mt], rb[s][t], acc[mt][t]);
+      }
+      MW_LOAD(s, i0 + s + R)
+    }
   }
-  for (int i = 0; i < nch;) {
-    MW_STEP(0, a0, a1)
-    if (i >= nch) break;
-    MW_STEP(1, a1, a0)
-  }
-#undef MW_STEP
+#undef MW_LOAD
   if constexpr (EPI < 0) {
     // fp32 partial slab of split sp: rows < M of this wave's tiles, columns of the group's tiles
 #pragma unroll
@@ -196,10 +167,10 @@ __global__ __launch_bounds__(256) void splitk_swiglu_kernel(const float* __restr
 }
 
 // Geometry of the mw form for a shape: the column-group width NT and split count S with the
-// lowest modelled time - per wave of workgroups the larger of the activation intake per CU (the
-// L2 -> CU path, ~64 B / clk) and the MFMA issue of one wave (MTW x NT quads x k-slices, 16
-// clk each), plus the slab round trip of a split (S x M x N fp32 written and read, ~3 KB / clk
-// for the chip).  MPAMD_MW="NTxS" pins it (ablation).  nt = 0: no form fits.
+// lowest modelled time - per wave of workgroups the larger of the intake per CU (activation
+// slice + the 4 waves' weight reads, the L2 -> CU path at ~64 B / clk) and the MFMA issue of one
+// wave (MTW x NT quads x k-slices, 16 clk each), plus the slab round trip of a split (S x M x N
+// fp32 written and read, ~3 KB / clk for the chip).  MPAMD_MW="NTxS" pins it (ablation).  nt = 0: no form fits.
 static inline void mw_choose(int tiles, int nks, int M, int N, int MTW, int C0, int nt_max_s1, int& nt, int& S) {
   static const int pin_nt = [] { const char* v = getenv("MPAMD_MW"); return v ? atoi(v) : 0; }();
   static const int pin_s = [] {
@@ -207,7 +178,7 @@ static inline void mw_choose(int tiles, int nks, int M, int N, int MTW, int C0, 
     const char* xp = v ? strchr(v, 'x') : nullptr;
     return xp ? atoi(xp + 1) : 0;
   }();
-  static constexpr int kNT[5] = {16, 12, 8, 6, 4};
+  static constexpr int kNT[3] = {8, 6, 4};  // wider groups spill the register ring (12 / 16: scratch)
   nt = S = 0;
   double best = 1e30;
   for (int cand : kNT) {
@@ -221,7 +192,8 @@ static inline void mw_choose(int tiles, int nks, int M, int N, int MTW, int C0, 
       if (s > 1 && C * s > C0) break;  // split only to fill the chip
       if (s == 1 && cand > nt_max_s1) continue;
       const double ks = (double)nks / s;
-      const double intake = (double)M * 64.0 * ks / 64.0;  // activation bytes per workgroup / (64 B / clk)
+      // bytes into the CU per k-slice / (64 B / clk): the M-row activation slice + 4 waves x NT KiB
+      const double intake = ks * ((double)M + 64.0 * cand);
       const double mfma = (double)MTW * cand * ks * 16.0;
       const double waves = (double)((C * s + C0 - 1) / C0);
       double t = waves * (intake > mfma ? intake : mfma);
@@ -243,8 +215,7 @@ static int launch_gemm_mw(const void* x, const void* w, void* y, int64_t ys, con
   if (!mw_ok(N, K, epi, opk)) return 1;
   const int tiles = N / 16, nks = K / 32, C0 = sk_num_cus();
   int nt = 0, S = 0;
-  // the in-kernel producer epilogue (EPI 3) spills beyond 8 column tiles at 12 / 16 row tiles
-  mw_choose(tiles, nks, M, N, MTW, C0, epi == 3 ? 8 : 16, nt, S);
+  mw_choose(tiles, nks, M, N, MTW, C0, 8, nt, S);
   if (nt == 0 || (S > 1 && ws == nullptr)) return 1;
   float* part = S > 1 ? (float*)((char*)ws + (int64_t)SK_MAX_GROUPS * sizeof(int) + SK_ZERO_BYTES +
                                  (int64_t)SK_MAX_BLOCKS * 2 * SK_MAX_S * 64 * sizeof(float))
@@ -264,8 +235,6 @@ static int launch_gemm_mw(const void* x, const void* w, void* y, int64_t ys, con
     MW_GO(NT_, 0, false);                                 \
   }
   switch (nt) {
-    case 16: if constexpr (4 * MTW * 16 <= 256) { MW_NT(16) } break;
-    case 12: if constexpr (4 * MTW * 12 <= 256) { MW_NT(12) } break;
     case 8: MW_NT(8) break;
     case 6: MW_NT(6) break;
     default: MW_NT(4) break;

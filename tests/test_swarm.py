@@ -311,7 +311,7 @@ def test_lb_placement_follows_measured_throughput():
     """Load-balanced servers announce MEASURED throughput (batched compute probe, network term
     from a measured link): a 2-block span measures slower than a 1-block span, so the next
     server fills the slow span's blocks, not the lowest uncovered-by-one index."""
-    extra = "--use_load_balancing --mean_balance_check_period 1000 --throughput_batch 4"
+    extra = "--use_load_balancing --mean_balance_check_period 1000 --throughput_batch 16"
     a = ServerThread(server_argv(MODEL, "1", 1, extra=extra + " --num_blocks 1")).wait()
     b = ServerThread(server_argv(MODEL, "1", 1, peers=a.addr, extra=extra + " --num_blocks 2")).wait()
     c = None

@@ -886,7 +886,12 @@ def linear(x, w, out=None, epilogue=0, residual=None, policy=None, wp=None, a_ro
 # reduce launch would have stored (csrc/common.h qkv_part_load8).
 PART_FLAG = 16384
 _RWK_SPLIT = {}
-_QKV_FOLD = {}  # (m_bucket, N, K, fp8) -> True where partials + fold beat the chosen kernel
+# (m_bucket, N, K, fp8) -> bool.  _QKV_FOLD_CAND: the qkv GEMM alone measured faster as partial
+# slabs (autotune_qkv_fold); _QKV_FOLD: the decision the decode path uses - set only by the
+# executor's end-to-end decode-graph A/B (the fold also moves work into the attention kernel), so
+# an unconfirmed bucket keeps the reduce launch
+_QKV_FOLD_CAND = {}
+_QKV_FOLD = {}
 
 
 def rwk_split(M: int, N: int, K: int, fp8: bool = False) -> int:
@@ -947,7 +952,7 @@ def autotune_qkv_fold(N: int, K: int, device, fp8: bool = False, ms=(16, 32, 48,
         ws = [(torch.randn(N // 16, K // 32, 64, 8, device=device) * 0.02).to(torch.bfloat16) for _ in range(copies)]
     for M in ms:
         key = (_m_bucket(M), N, K, bool(fp8))
-        if key in _QKV_FOLD or rwk_split(M, N, K, fp8) <= 0:
+        if key in _QKV_FOLD_CAND or rwk_split(M, N, K, fp8) <= 0:
             continue
         xp = pack_act(torch.randn(M, K, device=device).to(torch.bfloat16))
         y = torch.empty(M, N, dtype=torch.bfloat16, device=device)
@@ -976,9 +981,9 @@ def autotune_qkv_fold(N: int, K: int, device, fp8: bool = False, ms=(16, 32, 48,
                 e1.record()
                 e1.synchronize()
                 t[name] = min(t[name], e0.elapsed_time(e1) / iters)
-        _QKV_FOLD[key] = t["part"] < 0.97 * t["full"]
+        _QKV_FOLD_CAND[key] = t["part"] < 0.97 * t["full"]
     del ws
-    return dict(_QKV_FOLD)
+    return dict(_QKV_FOLD_CAND)
 
 
 # ---------------------------------------------------------------------------------------

@@ -503,7 +503,7 @@ class StageExecutor:
 
     def _qkv_fold(self, T: int) -> bool:
         """Decode steps of T rows: qkv as split-K partial slabs folded into the attention kernel's
-        loads (``ops.autotune_qkv_fold`` measured it faster than the chosen qkv GEMM)."""
+        loads - where ``_confirm_qkv_fold``'s decode-step A/B found it faster (``ops.qkv_fold``)."""
         if not (self._fuse_rope and self._fused and self.device.type == "cuda") or \
                 os.environ.get("MPAMD_QKV_FOLD", "1") == "0":
             return False
@@ -788,10 +788,11 @@ class StageExecutor:
         replays of this batch bucket - is timed both ways and the fold kept only where the step
         is >= 1 % faster.  The losing variant's graph is dropped.  Returns {fold: ms} or None."""
         B = len(sids)
-        if not self.use_graphs or B > self.graph_max_batch or not self._qkv_fold(B):
-            return None
         cfg = self.cfg
         key = (ops._m_bucket(B), cfg.q_dim + 2 * cfg.kv_dim, cfg.hidden_size, bool(self._w8))
+        if not self.use_graphs or B > self.graph_max_batch or not ops._QKV_FOLD_CAND.get(key) or \
+                not (self._fuse_rope and self._fused) or os.environ.get("MPAMD_QKV_FOLD", "1") == "0":
+            return None
         H = cfg.hidden_size
 
         def step():

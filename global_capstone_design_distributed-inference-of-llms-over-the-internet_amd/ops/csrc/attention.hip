@@ -759,16 +759,9 @@ static void launch_attn(const void* q, int64_t q_stride, const void* kc, const v
     return !(v && v[0] == '0');
   }();
 
-  // MPAMD_ATTN_WIDE_PIPE=1 (ablation): the 16-wave form with the first K / V issued ahead of the
-  // query / RoPE prologue, as the 4-wave form does
-  static const bool wide_pipe = [] {
-    const char* v = getenv("MPAMD_ATTN_WIDE_PIPE");
-    return v && v[0] == '1';
-  }();
-  if (one_pass && wide && wide_pipe) {
-    if (rf.pos) go(paged_attn1_kernel<D, NREP, true, 16, true>);
-    else go(paged_attn1_kernel<D, NREP, false, 16, true>);
-  } else if (one_pass && wide) {
+  // (the 16-wave form keeps the plain prologue: issuing its first K / V ahead of the query / RoPE
+  // loads, as the 4-wave form does, measured no faster at batch 1 / 4 / 8, profiles/r4n)
+  if (one_pass && wide) {
     if (rf.pos) go(paged_attn1_kernel<D, NREP, true, 16, false>);
     else go(paged_attn1_kernel<D, NREP, false, 16, false>);
   } else if (one_pass && pipe) {

@@ -1,6 +1,7 @@
 """Stage-local recovery building blocks (CPU): the per-stage replay cache of output rows
 (``parallel.engine.ReplayCache``) and session adoption by rename (``SessionManager.rename``)."""
 import numpy as np
+import pytest
 import torch
 
 from src.parallel.engine import ReplayCache
@@ -39,3 +40,21 @@ def test_session_rename_moves_kv_and_closes_target():
     assert sm.free_pages == free0 + 1  # the replaced target's page went back
     assert sm.rename("missing", "x") is None
     assert int(np.sum(sm.table[s.row] >= 0)) == len(pages)
+
+
+@pytest.mark.gpu
+def test_replay_cache_on_gpu_pinned_staging():
+    """The device path: row indices staged through the double-buffered pinned area (no host block),
+    many steps in a row so both staging buffers are reused."""
+    rc = ReplayCache(max_handles=8, max_len=64, hidden=16, dtype=torch.bfloat16, device="cuda")
+    ref = torch.zeros(8 * 64, 16, dtype=torch.bfloat16)
+    g = torch.Generator().manual_seed(0)
+    for step in range(40):
+        recs = [(h, 1, step, 0, 0) for h in range(8)]
+        out = torch.randn(8, 16, generator=g).to(torch.bfloat16)
+        rc.store(recs, out.cuda())
+        for h in range(8):
+            ref[h * 64 + step] = out[h]
+    torch.cuda.synchronize()
+    assert torch.equal(rc.buf.cpu(), ref)
+    assert torch.equal(rc.rows(3, 40).cpu(), ref[3 * 64: 3 * 64 + 40])

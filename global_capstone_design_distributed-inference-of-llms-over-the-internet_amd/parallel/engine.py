@@ -946,8 +946,7 @@ class PipelineServingEngine:
             if lost:
                 self._fail(f"replay: {lost} session state(s) missing on rank {self.rank}")
             if self.rank == target - 1:
-                x = torch.cat([self.replay.rows(int(h), int(L)) for h, L, _ in recs])
-                self.ch.send(self.rank + 1, x)
+                self._replay_send(torch.cat([self.replay.rows(int(h), int(L)) for h, L, _ in recs]))
             elif self.rank == target:
                 _, waiter = self.ch.recv(self.rank - 1, (T, self.H), self.ex.dtype)
                 x = waiter()
@@ -960,6 +959,14 @@ class PipelineServingEngine:
         logger.info(f"[{self.name} rank {self.rank}] replay: " +
                     (f"rebuilt the KV of {n} session(s) from {T} replayed rows" if self.rank == target
                      else f"adopted {n} session(s)"))
+
+    def _replay_send(self, x: torch.Tensor) -> None:
+        """Replayed rows to the next rank, in the same op order as the data plane's hidden-state
+        hops (with the graph hop those go on the compute stream, not the channel's side stream)."""
+        if self.graph_hop:
+            self.ch.send_on_stream(self.rank + 1, x.contiguous())
+        else:
+            self.ch.send(self.rank + 1, x)
 
     def resume_sessions(self, items: Sequence[Tuple[Request, int, int]], target: int) -> List[Request]:
         """Head of the channel that replaced a failed one (same surviving servers, a spare in
@@ -1010,7 +1017,7 @@ class PipelineServingEngine:
         try:
             self.ch.send_msg(1, hdr)
             if target == 1:
-                self.ch.send(1, torch.cat([self.replay.rows(lv.handle, lv.fed) for lv, _ in done]))
+                self._replay_send(torch.cat([self.replay.rows(lv.handle, lv.fed) for lv, _ in done]))
         except ChannelError as e:
             self._fail(str(e))
         logger.info(f"[{self.name}] stage-local recovery: {len(done)} session(s) resumed, stage {target} "

@@ -740,10 +740,13 @@ static void launch_attn(const void* q, int64_t q_stride, const void* kc, const v
     const char* v = getenv("MPAMD_ATTN_1PASS");
     return !(v && v[0] == '0');
   }();
-  // 16-wave workgroups when the grid cannot fill the chip with 4-wave ones
+  // 16-wave workgroups when the grid is at most MPAMD_ATTN_WIDE_WGS workgroups (default 0: never).
+  // With the pipelined 4-wave form they no longer pay: batch 1..16 x ctx 170 / 1024, 32 heads,
+  // sum of 10 cases 171.5 us at a 512 threshold vs 167.9 us without (4 x 170: 13.9 -> 10.8 us),
+  // profiles/r4o
   static const int wide_max = [] {
     const char* v = getenv("MPAMD_ATTN_WIDE_WGS");
-    return v ? atoi(v) : 512;
+    return v ? atoi(v) : 0;
   }();
   const bool wide = one_pass && (int64_t)NP * (nh / NREP) * T <= wide_max;
   const int nw = wide ? 16 : 4;

@@ -571,8 +571,8 @@ def attention_mfma_rope(qkv, k_cache, v_cache, block_tables, q_seq, q_ctx, qbloc
                         nkv, scale, out=None, workspace=None, part_size=None, num_parts=None, max_ctx=None,
                         packed=False, qkv_part=None):
     """GQA decode step on the MFMA kernel with RoPE of q / new k and the new token's page-slot
-    write folded in (csrc/attention_mfma.hip ROPE path).  ``qblocks`` holds one token per block
-    (``decode_qblocks``); ``qkv`` is the unrotated fused projection and is not modified; with
+    write folded in (csrc/attention_mfma.hip ROPE path).  ``qblocks`` must hold one token per block,
+    block i = token i (``decode_qblocks``: the kernel takes that as given and reads no qblocks); ``qkv`` is the unrotated fused projection and is not modified; with
     ``qkv_part`` the kernel reads q / k / v from the qkv GEMM's partial slabs instead."""
     if qkv_part is not None and not _native(qkv):
         qkv = reduce_qkv_part(qkv_part, qkv.dtype)

@@ -76,7 +76,10 @@ __global__ __launch_bounds__(256, 2) void attn_mfma_kernel(
   const int g = hbase / (nh / nkv);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int c = lane & 15, qd = lane >> 4;
-  const int tok0 = qb_tok0[b], ntok = qb_ntok[b];
+  // ROPE (decode): block b is token b (``decode_qblocks``: one token per block, in order), so the
+  // block-table walk starts from q_seq / q_ctx directly - one dependent global load fewer in the
+  // chain (q_seq -> page id -> K / V) that sets the decode kernel's time
+  const int tok0 = ROPE ? b : qb_tok0[b], ntok = ROPE ? 1 : qb_ntok[b];
   const int seq = q_seq[tok0];
   const int32_t* bt = block_tables + (int64_t)seq * bt_stride;
   const int page_size = 1 << page_log2;

@@ -387,7 +387,8 @@ void attention_fa(const at::Tensor& q, const at::Tensor& k_cache, const at::Tens
                "attention_fa");
 }
 
-// GQA decode with RoPE + KV write fused (attention_mfma.hip ROPE path): one token per query block.
+// GQA decode with RoPE + KV write fused (attention_mfma.hip ROPE path): one token per query block,
+// block b = token b (the kernel reads no qblocks on this path; ``decode_qblocks`` builds exactly that).
 void attention_mfma_rope(const at::Tensor& qkv, at::Tensor& k_cache, at::Tensor& v_cache,
                          const at::Tensor& block_tables, const at::Tensor& q_seq, const at::Tensor& q_ctx,
                          const at::Tensor& qblocks, const at::Tensor& positions, const at::Tensor& cos,

@@ -989,14 +989,15 @@ constexpr int rw_depth() {
 // fp8 weights: a slot is 4 MT + 2 NT VGPRs.  The 8-column split-K forms of the 70B shapes
 // (MT 4, NT 8: 32 VGPRs a slot) keep 2 slots by the 190-VGPR rule, i.e. ~16 KB per wave in flight
 // for ~1 MB of activations + weights per CU: latency-bound (qkv ~2.6 TB/s).  MP_F8_DEEP keeps 4
-// slots whenever 4 slots fit beside ~60 other VGPRs and the column group is at most 8 tiles.
+// slots whenever 4 slots fit beside ~60 other VGPRs and the column group is at most 8 tiles
+// (MP_F8_DEEP=2: only the wider groups, i.e. the 14-tile Llama-3-70B gate/up form).
 #ifndef MP_F8_DEEP
 #define MP_F8_DEEP 0
 #endif
 template <int MT, int NT, bool F8>
 constexpr int rw_depth2() {
   if constexpr (F8) {
-    if (MP_F8_DEEP && NT <= 8 && 4 * (4 * MT + 2 * NT) + 60 <= 256) return 4;
+    if (((MP_F8_DEEP == 1 && NT <= 8) || (MP_F8_DEEP == 2 && NT > 8)) && 4 * (4 * MT + 2 * NT) + 60 <= 256) return 4;
     return 190 / (4 * MT + 2 * NT) >= 8 ? 4 : 2;
   } else {
     return rw_depth<MT, NT>();

@@ -408,8 +408,8 @@ def attention_partition(num_queries: int, nkv: int, max_ctx: int, target_wgs: in
     ``MPAMD_ATTN_MIN_PART`` overrides every caller."""
     max_ctx = max(int(max_ctx), 1)
     if not _ATTN_MIN_PART_ENV and min_part < 256 and num_queries * nkv <= 64:
-        # few (query, head) pairs: the flash-decoding kernel runs 16-wave workgroups over
-        # 256-token slices (one iteration each), so short contexts need no split-K / reduce
+        # few (query, head) pairs: 256-token slices, so short contexts need no split-K combine
+        # (its cost exceeds what 64 / 128-token slices save at batch 1 / 2: profiles/r4t)
         min_part, target_wgs = 256, 256
     min_part = int(_ATTN_MIN_PART_ENV) if _ATTN_MIN_PART_ENV else int(min_part)
     want = max(1, math.ceil(target_wgs / max(1, num_queries * nkv)))

@@ -435,8 +435,9 @@ __global__ __launch_bounds__(256) void paged_attn_kernel(
 // while the current one computes (no dependent page-table round trip on the critical path).  The
 // 4 token groups of a wave merge by xor shuffles, the 4 waves through LDS (rescaled by their
 // maxima), and the output / split-K partials (o, m, l) have the two-pass kernel's format.
-// NW = waves per workgroup: 4, or 16 when the grid is small (batch 1: one workgroup per head
-// over the whole context, each wave a 16-token slice; no split-K, no reduce launch).
+// NW = waves per workgroup: 4 (software-pipelined, PIPE), or 16 for grids of at most
+// MPAMD_ATTN_WIDE_WGS workgroups (default 0: never - it stopped paying once the 4-wave form was
+// pipelined, profiles/r4o).
 template <int D, int NREP, bool ROPE, int NW, bool PIPE, int U = 4>
 __global__ __launch_bounds__(NW * 64) void paged_attn1_kernel(
     const bf16_t* __restrict__ q, int64_t q_stride, const bf16_t* __restrict__ kc,

@@ -1378,7 +1378,8 @@ __global__ __launch_bounds__(RW_WAVES * 64) void gemm_rwk_kernel(const bf16_t* _
   const WT* wb = reinterpret_cast<const WT*>(wp) + ((int64_t)tile0 * nks) * 512 + lane * 8;
   const bf16_t* xl = x + lane * 8;
   float wsc[NT];
-  if constexpr (F8) {
+  // (the 16-tile fp8 group loads its column scales after the loop: 16 VGPRs less across it)
+  if constexpr (F8 && NT <= 8) {
 #pragma unroll
     for (int t = 0; t < NT; ++t) wsc[t] = ep.wsc[(tile0 + t) * 16 + (lane & 15)];
   }
@@ -1433,6 +1434,10 @@ __global__ __launch_bounds__(RW_WAVES * 64) void gemm_rwk_kernel(const bf16_t* _
   }
 #undef RWK_LOAD
   if constexpr (F8) {
+    if constexpr (NT > 8) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) wsc[t] = ep.wsc[(tile0 + t) * 16 + (lane & 15)];
+    }
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -1666,15 +1671,24 @@ static inline void launch_splitk_reduce(int S, int epi, dim3 g2, hipStream_t str
 // NT = 6, S = 2 fills 256 CUs where NT = 8, S = 2 leaves 64 idle).  fp8 weights: the bf16
 // activation block costs 2M / (16 NT) x the weight bytes per CU - the widest group first.
 // nt = 0 when no split applies.  MPAMD_RWK_NT (ablation) allows only that width.
+// fp8 weights at <= 64 rows also have a 16-tile group (all 256 AGPRs hold the accumulators), taken
+// only when MPAMD_RWK_F8_WIDE=1 or MPAMD_RWK_NT=16 (A/B: it halves the activation intake per CU
+// against the 8-tile group, at twice the slab bytes).
 static inline void rwk_choose(int tiles, int nks, int C0, bool f8, int& nt, int& S, int nt_max = 8) {
-  static constexpr int kOrderBf16[5] = {4, 2, 8, 6, 1}, kOrderF8[5] = {8, 4, 2, 6, 1};
+  static constexpr int kOrderBf16[6] = {4, 2, 8, 6, 1, 0}, kOrderF8[6] = {16, 8, 4, 2, 6, 1};
   static const int nt_only = [] {
     const char* v = getenv("MPAMD_RWK_NT");
     return v ? atoi(v) : 0;
   }();
+  static const bool f8_wide = [] {
+    const char* v = getenv("MPAMD_RWK_F8_WIDE");
+    return v && v[0] == '1';
+  }();
   nt = S = 0;
   int best_fill = 0;
   for (int cand : (f8 ? kOrderF8 : kOrderBf16)) {
+    if (cand == 0) continue;
+    if (cand == 16 && !(f8 && nt_max >= 16 && (f8_wide || nt_only == 16))) continue;
     if ((nt_only && cand != nt_only) || tiles % cand || cand > nt_max) continue;
     const int C = tiles / cand, s = C0 / C;
     if (s >= 2 && s <= 8 && nks >= 4 * s && C * s > best_fill) { nt = cand; S = s; best_fill = C * s; }
@@ -1707,10 +1721,12 @@ static int launch_gemm_rwk(const void* x, const void* w, void* y, int64_t ys, co
   if (epi == 1 || ws == nullptr || N % 2048 != 0) return 1;
   const int tiles = N / 16, C0 = sk_num_cus(), nks = K / 32;
   int nt = 0, S = 0;
-  // accumulators: 192 AGPRs up to 128 rows, all 256 beyond (MT 9..16 -> NT <= 64 / MT)
-  constexpr int nt_max = rwk_nt_max_mt(MT);
+  // accumulators: 192 AGPRs up to 128 rows, all 256 beyond (MT 9..16 -> NT <= 64 / MT); fp8 weights
+  // at <= 64 rows: a 16-tile group (256 AGPRs) as an opt-in candidate
+  constexpr int nt_max = (F8 && MT == 4) ? 16 : rwk_nt_max_mt(MT);
   rwk_choose(tiles, nks, C0, F8, nt, S, nt_max);
   if (nt == 0) return 1;
+  if (nt == 16 && inl) return 1;  // the in-launch combines are built up to 8-tile groups
   if ((int64_t)S * M * N * 4 > RWK_SLAB_BYTES) return 1;
   float* part = (float*)((char*)ws + (int64_t)SK_MAX_GROUPS * sizeof(int) + SK_ZERO_BYTES +
                          (int64_t)SK_MAX_BLOCKS * 2 * SK_MAX_S * 64 * sizeof(float));
@@ -1750,6 +1766,10 @@ static int launch_gemm_rwk(const void* x, const void* w, void* y, int64_t ys, co
     case 6:
       if constexpr (6 <= nt_max)
         hipLaunchKernelGGL((gemm_rwk_kernel<MT, 6, F8>), g1, dim3(RW_WAVES * 64), 0, stream, (const bf16_t*)x, (const bf16_t*)w, part, M, N, K, S, ep, nullptr, 0, nullptr, 0, nullptr);
+      break;
+    case 16:
+      if constexpr (F8 && MT == 4)
+        hipLaunchKernelGGL((gemm_rwk_kernel<MT, 16, F8>), g1, dim3(RW_WAVES * 64), 0, stream, (const bf16_t*)x, (const bf16_t*)w, part, M, N, K, S, ep, nullptr, 0, nullptr, 0, nullptr);
       break;
     default:
       if constexpr (8 <= nt_max)

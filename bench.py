@@ -118,10 +118,15 @@ def run_failover_drill(a, cfg, eng, ex, rank, world, S, R, M, B, device, load_s)
         after = sum(1 for ts, _ in stamps if t_rec is not None and ts >= t_rec)
         done = sum(1 for r in reqs if r.done and len(r.generated) >= a.steps)
         total_tokens = sum(len(r.generated) for r in reqs)
+        # ms per decode step of the pre-failure window (every session advances one token per step):
+        # wall time before the kill / tokens delivered per session in it; the whole drill without a kill
+        win_s, win_tok = ((t_fail - t0), before) if t_fail is not None else ((t1 - t0), total_tokens)
+        ms_step = round(1000.0 * win_s / (win_tok / n_total), 3) if win_tok else None
         out = {
             "metric": METRIC, "value": round(total_tokens / (t1 - t0), 2), "unit": "tokens/s", "n_gpus": world,
-            "steps": a.steps, "warmup": 0, "ms_per_step": None, "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "bf16", "data": f"synthetic (random-init {cfg.name} weights, random prompt ids)",
+            "steps": a.steps, "warmup": 0, "ms_per_step": ms_step, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": fp8_label(ex) if a.fp8 else "bf16",
+            "data": f"synthetic (random-init {cfg.name} weights, random prompt ids)",
             "config": {"model": cfg.name, "global_batch": n_total, "seq_len": a.prompt_len,
                        "parallelism": f"pp{S}xdp{R}", "micro_batches": M, "sessions_per_micro_batch": B,
                        "engine": "ReplicaFrontend over PipelineServingEngine replicas (failover drill)"},

@@ -132,21 +132,15 @@ _SK_CHOICE = {}  # (m_bucket, N, K, epilogue) -> kernel name (see _KERNEL_FLAGS)
 # form with (NT column tiles per wave, CH column waves sharing each k-split's A) = (2,2)/(2,4)/(4,2),
 # the balanced ring form "rw" (every CU one workgroup with ceil/floor of tiles / CUs) and its
 # split-K variant "rwk" (+ a reduce / epilogue launch) for the narrow projections, with the
-# in-launch combines "rwki" (last arriver) / "rwks" (symmetric), and the row-split ring "rwr"
+# in-launch combine "rwki" (the last arriving split sums the slabs), and the row-split ring "rwr"
 # (a pair of workgroups per column group, half the rows each: no K split, no combine)
 _KERNEL_FLAGS = {"pk": 0, "sk": 4, "lds22": 16, "lds24": 16 | 32, "lds42": 16 | 96, "rw": 128, "rwk": 256,
-                 "rwki": 256 | 512, "rwks": 256 | 2048, "rwr": 4096, "mw": 32768}
+                 "rwki": 256 | 512, "rwr": 4096}
 _LDS_CFG = {"lds22": (2, 2), "lds24": (2, 4), "lds42": (4, 2)}
 # "<kernel>+r": the same kernel with every workgroup's k walk rotated (csrc/gemm_kernels.h
 # rw_krot, flags bit 10) - kept by the autotuners per shape only where it measures faster
 ROT_FLAG = 1024
 
-
-# 65..128-row steps (not autotuned): rotated k walk (MPAMD_WIDE_ROT=1) or the lock-step one
-_WIDE_ROT = os.environ.get("MPAMD_WIDE_ROT", "0") == "1"
-# 65..128-row steps on the row-split form (csrc/gemm_mw.h) instead of the ring kernels
-# (MPAMD_WIDE_KERNEL=mw); 129..256 rows always run it
-_WIDE_MW = os.environ.get("MPAMD_WIDE_KERNEL", "") == "mw"
 
 
 def _base(name: str) -> str:
@@ -212,10 +206,8 @@ def _covered(name: str, M: int, N: int, K: int, epilogue: int) -> bool:
         return True
     if name == "rwk":  # split-K ring + reduce launch: plain / residual / fused-norm producer epilogues
         return epilogue != 1 and N % 2048 == 0
-    if name in ("rwki", "rwks"):  # the same with an in-launch combine (M <= 64)
+    if name == "rwki":  # the same with an in-launch combine (M <= 64)
         return epilogue != 1 and N % 2048 == 0 and M <= 64
-    if name == "mw":  # row-split wide form: chosen by row count (linear), never by the autotuner
-        return False
     if name == "rwr":  # row-split ring: 2 or 4 row tiles split over a workgroup pair
         return epilogue != 1 and N % 2048 == 0 and (M + 15) // 16 in (2, 4)
     return _lds_covered(name, M, N, K, epilogue)
@@ -770,8 +762,6 @@ def wide_gemm_ok(M: int, N: int, K: int, epilogue: int = 0, out_packed: bool = F
     """65..256 decode rows: the balanced ring kernel covers (packed A; epilogue 0 or packed SwiGLU,
     the widths it is built for; 129..256 rows at 12 / 16 row tiles)."""
     key = (M, N, K, int(epilogue), bool(out_packed))
-    if epilogue == 3 and os.environ.get("MPAMD_WIDE_SPLITK", "1") == "0":
-        return False  # the fused-norm producer only exists as the split-K ring + reduce form
     if key not in _RW_OK:
         _RW_OK[key] = bool(native_available() and
                            torch.ops.mpamd.gemm_rw_ok(int(M), int(N), int(K), int(epilogue), int(bool(out_packed))))
@@ -845,17 +835,12 @@ def linear(x, w, out=None, epilogue=0, residual=None, policy=None, wp=None, a_ro
                    else torch.empty(M, ncols, dtype=x.dtype, device=x.device))
         if gate is not None:
             kern = "pk"
-        elif M > 128 or (M > 64 and _WIDE_MW):  # row-split form (its own geometry per shape)
-            kern = "mw"
-        elif M > 64:  # 65..128 rows: split-K ring where it applies (o, down), else the ring kernel
-            kern = "rwk" if (not out_packed and _covered("rwk", M, N, K, epilogue)
-                             and os.environ.get("MPAMD_WIDE_SPLITK", "1") != "0") else "rw"
-            if _WIDE_ROT:
-                kern += "+r"
+        elif M > 64:  # 65..256 rows: split-K ring where it applies (o, down), else the ring kernel
+            kern = "rwk" if (not out_packed and _covered("rwk", M, N, K, epilogue)) else "rw"
         else:
             kern = _kernel_for(M, N, K, epilogue)
         flags = 1 | (2 if out_packed else 0) | _kflags(kern)
-        ws = gemm_workspace(x.device) if _base(kern) in ("sk", "rwk", "rwki", "rwks", "mw") else None
+        ws = gemm_workspace(x.device) if _base(kern) in ("sk", "rwk", "rwki") else None
         torch.ops.mpamd.gemm(x, wp, out, residual, int(epilogue), M, flags, ws, gate, ap_out, ss_out, ss_zero, ss_in,
                              1.0 / K, float(eps))
         return out
@@ -1146,7 +1131,7 @@ def unpack_weight_w8(w8: torch.Tensor, w_scale: torch.Tensor, dtype=torch.bfloat
     return ref.unpack_weight_fp8(fp8_from_w8(w8), w_scale, dtype)
 
 
-_W8_KERNELS = {"rw": 128, "rwk": 256, "rwki": 256 | 512, "rwks": 256 | 2048}
+_W8_KERNELS = {"rw": 128, "rwk": 256, "rwki": 256 | 512}
 _W8_CHOICE = {}  # (m_bucket, N, K, epilogue) -> "rw" / "rwk", from autotune_w8
 _W8_MODE = os.environ.get("MPAMD_W8_KERNEL", "auto")
 
@@ -1154,7 +1139,7 @@ _W8_MODE = os.environ.get("MPAMD_W8_KERNEL", "auto")
 def _w8_kernel(M: int, N: int, K: int, epilogue: int) -> str:
     rwk_ok = epilogue != 1 and N % 2048 == 0
     mode = _W8_MODE if _W8_MODE != "auto" else _W8_CHOICE.get((_m_bucket(M), N, K, int(epilogue)), "rw")
-    if _base(mode) in ("rwk", "rwki", "rwks") and rwk_ok:
+    if _base(mode) in ("rwk", "rwki") and rwk_ok:
         return mode
     return "rw+r" if mode.endswith("+r") else "rw"
 
@@ -1177,7 +1162,7 @@ def linear_w8(x, w8, w_scale, a_rows: int, out=None, epilogue: int = 0, residual
     kern = _w8_kernel(M, N, K, epilogue)
     flags = 1 | (2 if out_packed else 0) | _W8_KERNELS[_base(kern)] | (ROT_FLAG if kern.endswith("+r") else 0)
     torch.ops.mpamd.gemm_w8(x, w8, w_scale, out, residual, int(epilogue), M, flags,
-                            gemm_workspace(x.device) if _base(kern) in ("rwk", "rwki", "rwks") else None, ap_out, ss_out,
+                            gemm_workspace(x.device) if _base(kern) in ("rwk", "rwki") else None, ap_out, ss_out,
                             ss_zero, ss_in,
                             1.0 / K, float(eps))
     return out

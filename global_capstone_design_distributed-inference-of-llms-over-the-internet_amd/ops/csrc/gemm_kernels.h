@@ -986,18 +986,11 @@ constexpr int rw_depth() {
   if (MP_RW_DEEP1 && MT + NT <= 2) return 8;
   return 190 / (4 * (MT + NT)) >= 8 ? 4 : 2;
 }
-// fp8 weights: a slot is 4 MT + 2 NT VGPRs.  The 8-column split-K forms of the 70B shapes
-// (MT 4, NT 8: 32 VGPRs a slot) keep 2 slots by the 190-VGPR rule, i.e. ~16 KB per wave in flight
-// for ~1 MB of activations + weights per CU: latency-bound (qkv ~2.6 TB/s).  MP_F8_DEEP keeps 4
-// slots whenever 4 slots fit beside ~60 other VGPRs and the column group is at most 8 tiles
-// (MP_F8_DEEP=2: only the wider groups, i.e. the 14-tile Llama-3-70B gate/up form).
-#ifndef MP_F8_DEEP
-#define MP_F8_DEEP 0
-#endif
+// fp8 weights: a slot is 4 MT + 2 NT VGPRs.  (4 slots for the 14-tile Llama-3-70B gate/up group
+// measured 17.30-17.34 vs 17.23-17.25 ms with 2: profiles/r4ab2.)
 template <int MT, int NT, bool F8>
 constexpr int rw_depth2() {
   if constexpr (F8) {
-    if (((MP_F8_DEEP == 1 && NT <= 8) || (MP_F8_DEEP == 2 && NT > 8)) && 4 * (4 * MT + 2 * NT) + 60 <= 256) return 4;
     return 190 / (4 * MT + 2 * NT) >= 8 ? 4 : 2;
   } else {
     return rw_depth<MT, NT>();
@@ -1334,16 +1327,13 @@ constexpr int64_t RWK_SLAB_BYTES = (int64_t)32 << 20;  // S x M x N fp32 partial
 // deterministic) and runs epilogue INL (0 with the optional row scale, 2, 3) itself - the
 // stream-K kernel's hand-off protocol (guide: splitk-seam, publish-large).
 //
-// COMB (INL >= 0 only) picks the combine: 1 = the last arriver of the S splits sums all S slabs
-// and runs the whole epilogue (arrival ticket); 2 = symmetric (reduce-scatter): quad qd belongs
-// to split qd % S, every split publishes only the quads the others own, keeps its own in LDS,
-// waits until all S splits of its column group have published (arrive counter + bounded sc1 poll;
-// the S splits are co-resident: the grid is at most one workgroup per CU) and finalises its own
-// quads - 1/S of the slab reads and of the epilogue per workgroup, no serial tail on one CU.
-// Both sum the S partials in split order (0..S-1) from zero: the reduce launch's order, so every
-// combine gives the same bits.  Residual quads of EPI 3 are prefetched before the main loop.
-constexpr int RWK_SPIN_LIMIT = 1 << 25;  // symmetric combine: bounded poll (~1 s), then flag an error
-template <int MT, int NT, bool F8 = false, int INL = -1, int COMB = 1>
+// The last arriver of the S splits (arrival ticket) sums all S slabs in split order (0..S-1) from
+// zero - the reduce launch's order, so both give the same bits - and runs the whole epilogue; no
+// workgroup ever waits for another, so the result never depends on co-residency.  (A symmetric
+// reduce-scatter combine, in which every split polled for its partners, was measured 2-3.5 us
+// slower than the reduce launch and needed all S splits resident at once: removed, profiles/r4_seam.)
+// Residual quads of EPI 3 are prefetched before the main loop.
+template <int MT, int NT, bool F8 = false, int INL = -1>
 __global__ __launch_bounds__(RW_WAVES * 64) void gemm_rwk_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ wp,
                                                        float* __restrict__ part, int M, int N, int K, int S,
                                                        const EpiArgs ep, bf16_t* __restrict__ y, int64_t ys,
@@ -1378,18 +1368,17 @@ __global__ __launch_bounds__(RW_WAVES * 64) void gemm_rwk_kernel(const bf16_t* _
   const WT* wb = reinterpret_cast<const WT*>(wp) + ((int64_t)tile0 * nks) * 512 + lane * 8;
   const bf16_t* xl = x + lane * 8;
   float wsc[NT];
-  // (the 16-tile fp8 group loads its column scales after the loop: 16 VGPRs less across it)
-  if constexpr (F8 && NT <= 8) {
+  if constexpr (F8) {
 #pragma unroll
     for (int t = 0; t < NT; ++t) wsc[t] = ep.wsc[(tile0 + t) * 16 + (lane & 15)];
   }
-  // EPI 3 in-launch: the residual quads this wave may finalise (COMB 1: qd = wid + 4 j of the
-  // whole group; COMB 2: this split's own quads qd = S (wid + 4 j) + sp), in flight during the loop
+  // EPI 3 in-launch: the residual quads this wave may finalise (qd = wid + 4 j of the whole
+  // group), in flight during the loop
   u16x4 rpre[NQ];
   if constexpr (INL == 3) {
 #pragma unroll
     for (int j = 0; j < NQ; ++j) {
-      const int qd = COMB == 2 ? S * (wid + RW_WAVES * j) + sp : wid + RW_WAVES * j;
+      const int qd = wid + RW_WAVES * j;
       rpre[j] = res_quad<NT>(res, rs, min(qd, Q - 1), c, M, lane);
     }
   }
@@ -1434,10 +1423,6 @@ __global__ __launch_bounds__(RW_WAVES * 64) void gemm_rwk_kernel(const bf16_t* _
   }
 #undef RWK_LOAD
   if constexpr (F8) {
-    if constexpr (NT > 8) {
-#pragma unroll
-      for (int t = 0; t < NT; ++t) wsc[t] = ep.wsc[(tile0 + t) * 16 + (lane & 15)];
-    }
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -1451,8 +1436,6 @@ __global__ __launch_bounds__(RW_WAVES * 64) void gemm_rwk_kernel(const bf16_t* _
     rsc.load(ep, wp);
     const __amdgpu_buffer_rsrc_t rsrc =
         __builtin_amdgcn_make_buffer_rsrc(part, (short)0, (int)RWK_SLAB_BYTES, 0x00020000);
-    // COMB 2: this split's own quads (qd % S == sp) stay in LDS, slot qd / S
-    __shared__ __attribute__((aligned(16))) f32x4 own[COMB == 2 ? ((Q + 1) / 2) * 64 : 1];
 #pragma unroll
     for (int p0 = 0; p0 < Q; p0 += QC) {
       if (p0 > 0) __syncthreads();
@@ -1463,55 +1446,12 @@ __global__ __launch_bounds__(RW_WAVES * 64) void gemm_rwk_kernel(const bf16_t* _
         f32x4 v = red[(qd - p0) * 64 + lane];
 #pragma unroll
         for (int w = 1; w < RW_WAVES; ++w) v += red[(w * QC + qd - p0) * 64 + lane];
-        if (COMB == 2 && qd % S == sp)
-          own[(qd / S) * 64 + lane] = v;
-        else
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rsrc,
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rsrc,
                                                  (((c * S + sp) * Q + qd) * 64 + lane) * 16, 0, 16);
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 slab stores landed
     __syncthreads();
-    if constexpr (COMB == 2) {
-      // tick: [2 c] arrivals, [2 c + 1] departures; the last to depart re-zeroes both (every split
-      // has seen all S arrivals by then), so the zeroed workspace stays valid across launches
-      if (threadIdx.x == 0) {
-        __hip_atomic_fetch_add(tick + 2 * c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        int spins = 0;
-        while (__hip_atomic_load(tick + 2 * c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < S) {
-          __builtin_amdgcn_s_sleep(1);
-          if (++spins > RWK_SPIN_LIMIT) {  // a partner never ran: flag it, never hang the GPU
-            __hip_atomic_store(tick - 1 + 2 * (SK_MAX_GROUPS / 8), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            break;
-          }
-        }
-        const int old = __hip_atomic_fetch_add(tick + 2 * c + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (old == S - 1) {
-          __hip_atomic_store(tick + 2 * c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_store(tick + 2 * c + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      }
-      __syncthreads();
-      rsc.finish(ep, rs_part, rs_lds);
-#pragma unroll
-      for (int j = 0; j < NQ; ++j) {
-        const int jo = wid + RW_WAVES * j, qd = S * jo + sp;
-        if (qd >= Q) break;
-        f32x4 pv[8];
-#pragma unroll
-        for (int s2 = 0; s2 < 8; ++s2)
-          if (s2 < S && s2 != sp)
-            pv[s2] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                   rsrc, (((c * S + s2) * Q + qd) * 64 + lane) * 16, 0, 16));
-        f32x4 v = (f32x4)(0.f);
-#pragma unroll
-        for (int s2 = 0; s2 < 8; ++s2)
-          if (s2 < S) v += s2 == sp ? own[jo * 64 + lane] : pv[s2];
-        tile_epilogue<MT, INL, false>(qd / NT, tile0 + qd % NT, v, (f32x4)(0.f), y, ys, res, rs, M, lane, ep, rs_lds,
-                                      INL == 3 ? &rpre[j] : nullptr);
-      }
-      return;
-    }
     if (threadIdx.x == 0) {
       const int old = __hip_atomic_fetch_add(tick + c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       s_last = old == S - 1;
@@ -1664,32 +1604,18 @@ static inline void launch_splitk_reduce(int S, int epi, dim3 g2, hipStream_t str
   else launch_splitk_reduce_e<0>(S, g2, stream, part, M, N, y, ys, res, rs, ep);
 }
 
-// Column-group width NT and split count S with C x S <= #CUs (prefer NT = 4, then 2, 8, 1;
-// 2 <= S <= 8); returns 1 when no split applies (the caller falls back).
 // Split-K ring geometry: column-group width NT and split count S (C x S <= #CUs, 2 <= S <= 8):
 // the width whose grid C x S fills the most CUs, ties to the earlier candidate (qkv, 768 tiles:
 // NT = 6, S = 2 fills 256 CUs where NT = 8, S = 2 leaves 64 idle).  fp8 weights: the bf16
 // activation block costs 2M / (16 NT) x the weight bytes per CU - the widest group first.
-// nt = 0 when no split applies.  MPAMD_RWK_NT (ablation) allows only that width.
-// fp8 weights at <= 64 rows also have a 16-tile group (all 256 AGPRs hold the accumulators), taken
-// only when MPAMD_RWK_F8_WIDE=1 or MPAMD_RWK_NT=16 (A/B: it halves the activation intake per CU
-// against the 8-tile group, at twice the slab bytes).
+// nt = 0 when no split applies.  (Widths 4 / 2 / 16 for the fp8 70B shapes were measured against 8:
+// 8 is the optimum, profiles/r4ac, r4ad.)
 static inline void rwk_choose(int tiles, int nks, int C0, bool f8, int& nt, int& S, int nt_max = 8) {
-  static constexpr int kOrderBf16[6] = {4, 2, 8, 6, 1, 0}, kOrderF8[6] = {16, 8, 4, 2, 6, 1};
-  static const int nt_only = [] {
-    const char* v = getenv("MPAMD_RWK_NT");
-    return v ? atoi(v) : 0;
-  }();
-  static const bool f8_wide = [] {
-    const char* v = getenv("MPAMD_RWK_F8_WIDE");
-    return v && v[0] == '1';
-  }();
+  static constexpr int kOrderBf16[5] = {4, 2, 8, 6, 1}, kOrderF8[5] = {8, 4, 2, 6, 1};
   nt = S = 0;
   int best_fill = 0;
   for (int cand : (f8 ? kOrderF8 : kOrderBf16)) {
-    if (cand == 0) continue;
-    if (cand == 16 && !(f8 && nt_max >= 16 && (f8_wide || nt_only == 16))) continue;
-    if ((nt_only && cand != nt_only) || tiles % cand || cand > nt_max) continue;
+    if (tiles % cand || cand > nt_max) continue;
     const int C = tiles / cand, s = C0 / C;
     if (s >= 2 && s <= 8 && nks >= 4 * s && C * s > best_fill) { nt = cand; S = s; best_fill = C * s; }
   }
@@ -1703,15 +1629,12 @@ static inline int rwk_nt_max(int M) {
   return rwk_nt_max_mt(mt <= 8 ? mt : (mt <= 12 ? 12 : 16));
 }
 
-// ``comb``: 0 = reduce launch, 1 = in-launch combine by the last arriver, 2 = symmetric in-launch
-// combine (gemm_rwk_kernel COMB).  Flags: 256 = split-K ring, + 512 -> comb 1, + 2048 -> comb 2.
+// ``comb``: 0 = reduce launch, 1 = in-launch combine by the last arriver (flags 256 = split-K ring,
+// + 512 -> comb 1), -1 = partial slabs only (flags bit 14).
 static inline int rwk_comb(int flags) {
   if (flags & 16384) return -1;  // bit 14: fp32 partial slabs only, no reduce launch
-  return (flags & 2048) ? 2 : ((flags & 512) ? 1 : 0);
+  return (flags & 512) ? 1 : 0;
 }
-
-// symmetric-combine counters [2 per column group] and the error word (last int of the region)
-static inline int* rwk_sym_counters(void* ws) { return (int*)ws + 3 * (SK_MAX_GROUPS / 4); }
 
 template <int MT, bool F8 = false>
 static int launch_gemm_rwk(const void* x, const void* w, void* y, int64_t ys, const void* res, int64_t rs, int M,
@@ -1721,28 +1644,21 @@ static int launch_gemm_rwk(const void* x, const void* w, void* y, int64_t ys, co
   if (epi == 1 || ws == nullptr || N % 2048 != 0) return 1;
   const int tiles = N / 16, C0 = sk_num_cus(), nks = K / 32;
   int nt = 0, S = 0;
-  // accumulators: 192 AGPRs up to 128 rows, all 256 beyond (MT 9..16 -> NT <= 64 / MT); fp8 weights
-  // at <= 64 rows: a 16-tile group (256 AGPRs) as an opt-in candidate
-  constexpr int nt_max = (F8 && MT == 4) ? 16 : rwk_nt_max_mt(MT);
+  // accumulators: 192 AGPRs up to 128 rows, all 256 beyond (MT 9..16 -> NT <= 64 / MT)
+  constexpr int nt_max = rwk_nt_max_mt(MT);
   rwk_choose(tiles, nks, C0, F8, nt, S, nt_max);
   if (nt == 0) return 1;
-  if (nt == 16 && inl) return 1;  // the in-launch combines are built up to 8-tile groups
   if ((int64_t)S * M * N * 4 > RWK_SLAB_BYTES) return 1;
   float* part = (float*)((char*)ws + (int64_t)SK_MAX_GROUPS * sizeof(int) + SK_ZERO_BYTES +
                          (int64_t)SK_MAX_BLOCKS * 2 * SK_MAX_S * 64 * sizeof(float));
   const dim3 g1((tiles / nt) * S);
   int* tick = (int*)ws + SK_MAX_GROUPS / 2;  // rwk arrival tickets (the stream-K kernel uses the low half)
-  if (comb == 2) tick = rwk_sym_counters(ws);
   if (inl && MT <= 4 && nt >= 2 && tiles / nt <= SK_MAX_GROUPS / 8 - 1 &&
       (int64_t)tiles * MT * S * 1024 <= RWK_SLAB_BYTES) {
     if constexpr (MT <= 4) {
 #define MP_RWKI(NT_, E_)                                                                                       \
-  if (comb == 2)                                                                                               \
-    hipLaunchKernelGGL((gemm_rwk_kernel<MT, NT_, F8, E_, 2>), g1, dim3(RW_WAVES * 64), 0, stream, (const bf16_t*)x,       \
-                       (const bf16_t*)w, part, M, N, K, S, ep, (bf16_t*)y, ys, (const bf16_t*)res, rs, tick);  \
-  else                                                                                                         \
-    hipLaunchKernelGGL((gemm_rwk_kernel<MT, NT_, F8, E_, 1>), g1, dim3(RW_WAVES * 64), 0, stream, (const bf16_t*)x,       \
-                       (const bf16_t*)w, part, M, N, K, S, ep, (bf16_t*)y, ys, (const bf16_t*)res, rs, tick)
+  hipLaunchKernelGGL((gemm_rwk_kernel<MT, NT_, F8, E_>), g1, dim3(RW_WAVES * 64), 0, stream, (const bf16_t*)x,    \
+                     (const bf16_t*)w, part, M, N, K, S, ep, (bf16_t*)y, ys, (const bf16_t*)res, rs, tick)
 #define MP_RWKI_E(NT_) \
   { if (epi == 3) MP_RWKI(NT_, 3); else if (epi == 2) MP_RWKI(NT_, 2); else MP_RWKI(NT_, 0); }
       switch (nt) {
@@ -1766,10 +1682,6 @@ static int launch_gemm_rwk(const void* x, const void* w, void* y, int64_t ys, co
     case 6:
       if constexpr (6 <= nt_max)
         hipLaunchKernelGGL((gemm_rwk_kernel<MT, 6, F8>), g1, dim3(RW_WAVES * 64), 0, stream, (const bf16_t*)x, (const bf16_t*)w, part, M, N, K, S, ep, nullptr, 0, nullptr, 0, nullptr);
-      break;
-    case 16:
-      if constexpr (F8 && MT == 4)
-        hipLaunchKernelGGL((gemm_rwk_kernel<MT, 16, F8>), g1, dim3(RW_WAVES * 64), 0, stream, (const bf16_t*)x, (const bf16_t*)w, part, M, N, K, S, ep, nullptr, 0, nullptr, 0, nullptr);
       break;
     default:
       if constexpr (8 <= nt_max)

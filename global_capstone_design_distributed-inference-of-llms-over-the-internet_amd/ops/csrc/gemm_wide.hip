@@ -1,23 +1,15 @@
 // Decode GEMM for 65..256 rows (the packed decode path at 96..256 sessions): split-K ring (o,
 // down) and balanced ring kernels at MT = 5..8, 12 and 16 (kernels: gemm_kernels.h).  129..256
 // rows run the 12- or 16-row-tile instantiation over the activation's own row tiles (the packed
-// layout's tile count is a runtime stride; tiles past it are masked rows), so the fused-norm
-// decode path no longer hands 129..256-session steps to hipBLASLt.
-#include "gemm_mw.h"
+// layout's tile count is a runtime stride; tiles past it are masked rows).  Above ops.WIDE_ROWS
+// (128 by default) the decode step stays on hipBLASLt, which measured faster there (profiles/r4d).
+#include "gemm_kernels.h"
 
 extern "C" int mp_gemm_bf16_wide(const void* x, const void* w, void* y, int64_t y_stride, const void* res,
                                  int64_t res_stride, int M, int N, int K, int epilogue, int flags, void* ws,
                                  const mp::EpiArgs& ep, hipStream_t stream) {
   using namespace mp;
   int rc = 1;
-  if ((flags & 32768) || M > 128) {  // row-split form: the 129..256-row default, opt-in below
-    const int mtw = ((M + 15) / 16 + 3) / 4;
-    if (mtw <= 2) rc = launch_gemm_mw<2>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags & 2, ep, ws, stream);
-    else if (mtw == 3) rc = launch_gemm_mw<3>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags & 2, ep, ws, stream);
-    else rc = launch_gemm_mw<4>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags & 2, ep, ws, stream);
-    if (rc < 0) return rc;
-    if (rc == 0) return (int)hipGetLastError();
-  }
   if ((flags & 256) && !(flags & 2) && ws != nullptr) {  // split-K ring
 #define MP_RWK(MT_) \
   rc = launch_gemm_rwk<MT_>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, ep, ws, stream, rwk_comb(flags))
@@ -48,7 +40,6 @@ extern "C" int mp_gemm_bf16_wide(const void* x, const void* w, void* y, int64_t 
 extern "C" int mp_gemm_rw_ok(int M, int N, int K, int epilogue, int out_packed) {
   using namespace mp;
   if (M <= 64 || M > 256 || K % (32 * GU_MAX) || N % 16) return 0;
-  if (M > 128) return mw_ok(N, K, epilogue, out_packed != 0);  // the row-split form (gemm_mw.h)
   // the fused-norm producer (residual + packed copy + row statistics) at 65..256 rows runs as
   // the split-K ring + its reduce launch (the reduce applies the epilogue): o / down widths
   if (epilogue == 3) return !out_packed && N % 2048 == 0;

@@ -425,7 +425,9 @@ class Channel:
 
     def stats(self, reset: bool = True) -> dict:
         """Hop statistics since the last reset: backend, payload bytes / sends, and the mean
-        ms this rank's stream (device) or host (gloo) waited for an incoming payload."""
+        ms this rank's stream (device) or host (gloo) waited for an incoming payload.  ``reset``
+        starts a new window for ALL of them (byte and send counters included), so a caller that
+        resets before a timed region reads exactly that region's traffic afterwards."""
         waits = [1e3 * x for x in self._wait_host_s]
         if self._wait_events:
             self._wait_events[-1][1].synchronize()
@@ -436,6 +438,8 @@ class Channel:
         if reset:
             self._wait_events.clear()
             self._wait_host_s.clear()
+            self.bytes_sent = 0
+            self.sends = 0
         return out
 
     def flush(self, timeout_s: Optional[float] = None) -> None:

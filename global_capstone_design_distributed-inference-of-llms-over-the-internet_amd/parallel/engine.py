@@ -767,15 +767,23 @@ class PipelineServingEngine:
             self.ch.send_msg(self.rank + 1, hdr)  # the successor plans while we compute
         recs = hdr[HDR:HDR + SEQ_REC * n_seq].reshape(n_seq, SEQ_REC)
         closes = hdr[HDR + SEQ_REC * n_seq:HDR + SEQ_REC * n_seq + n_close]
+        x = None
+        if n_seq:
+            # the payload wait happens OUTSIDE exec_lock: a predecessor that dies between its header
+            # and its payload leaves this thread blocked here until the channel times out or is
+            # aborted, and the executor must stay usable meanwhile (stage-local recovery adopts this
+            # channel's sessions into a new one, the TCP handler keeps serving)
+            rows = self._hop_rows(T, bool((recs[:, 1] == 1).all()))
+            _, waiter = self.ch.recv(self.rank - 1, (rows, self.H), self.ex.dtype)
+            x = waiter()
+            if x is not None and rows != T:
+                x = x[:T]
+        if self.ch.closed:
+            raise ChannelError("channel aborted while waiting for a payload")
         with self.ex.exec_lock:
             for c in closes:  # before the compute: a closed handle may be re-admitted in this very step
                 self.ex.sessions.close(self._key(int(c)))
             if n_seq:
-                rows = self._hop_rows(T, bool((recs[:, 1] == 1).all()))
-                _, waiter = self.ch.recv(self.rank - 1, (rows, self.H), self.ex.dtype)
-                x = waiter()
-                if x is not None and rows != T:
-                    x = x[:T]
                 out = self._compute(recs.tolist(), x, m)
                 if self.is_tail:
                     tok = self._sample_tail(hdr, out)
@@ -924,7 +932,8 @@ class PipelineServingEngine:
                 s.length = min(s.length, int(length))
                 break
         cache = self.resume.get("cache")
-        rows = self.replay is not None and cache is not None and 0 < length <= cache.max_len
+        rows = (self.replay is not None and cache is not None and 0 < length <= cache.max_len and
+                length <= self.replay.max_len)
         if rows:
             self.replay.rows(handle, length).copy_(cache.rows(old_handle, length))
         return s is not None, rows
@@ -943,6 +952,7 @@ class PipelineServingEngine:
             for h, L, oh in recs:
                 kv, rows = self._adopt(int(h), int(L), int(oh))
                 lost += int(self.rank != target and not kv) + int(self.rank == target - 1 and not rows)
+            self.resume.pop("cache", None)  # every row is copied: the failed channel's cache can go
             if lost:
                 self._fail(f"replay: {lost} session state(s) missing on rank {self.rank}")
             if self.rank == target - 1:
@@ -1000,6 +1010,7 @@ class PipelineServingEngine:
                 self.live[req.rid] = lv
                 req._repeat = repeat_run(req.generated)
                 done.append((lv, int(oh)))
+        self.resume.pop("cache", None)  # adopted rows are in this engine's own cache now
         if not done:
             return []
         recs = np.asarray([(lv.handle, lv.fed, oh) for lv, oh in done], dtype=np.int64)

@@ -221,8 +221,15 @@ class StageConnectionHandler:
                 with self._chan_lock:
                     prev = self._chan_engines.pop(str(old), None)
                 if prev is not None:
-                    prev.release()  # a failed channel's thread may still be blocked: free the executor's hook
+                    # the replaced channel has failed even if its thread has not noticed yet (it may
+                    # be blocked on a payload from the dead stage): abort it so that wait returns now
+                    # and its serving loop ends, then free the executor's graph hook
+                    if prev.ch is not None:
+                        prev.ch.abort()
+                    prev.release()
                 resume = {"prefix": str(old), "cache": getattr(prev, "replay", None)}
+                if prev is not None:
+                    prev.replay = None  # the new engine owns it now and drops it once adopted
             eng = PipelineServingEngine(ex, ch, n_slots=int(md.get("n_slots", 1)), batch=int(md.get("batch", 64)),
                                         name=name, replay_cache=bool(md.get("replay_cache", False)), resume=resume)
             with self._chan_lock:
@@ -244,8 +251,10 @@ class StageConnectionHandler:
                     if eng.failed is None or not eng.park_on_fail:
                         self._chan_engines.pop(name, None)
                     dead = [k for k, e in self._chan_engines.items() if getattr(e, "failed", None) is not None]
-                    for k in dead[:-4]:  # keep the 4 newest failed channels nobody adopted
-                        self._chan_engines.pop(k)
+                    # keep only the newest failed channel nobody adopted: each holds a replay cache of
+                    # max_handles x max_len x hidden in HBM that the KV capacity exchange never counted
+                    for k in dead[:-1]:
+                        self._chan_engines.pop(k).replay = None
             with ex.exec_lock:  # (parked sessions - ``park:`` keys - wait for adoption or the session TTL)
                 for sid in [k for k in ex.sessions.sessions if k.startswith(name + ":")]:
                     ex.sessions.close(sid)

@@ -47,6 +47,14 @@ def test_bench_spawns_its_own_ranks():
     rec = json.loads(lines[0])
     assert KEYS <= set(rec) and rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "pp2"
     assert rec["data_plane"].startswith("gloo") and rec["graph_hop"] is False
+    # hop statistics cover exactly the timed steps: rank 0 sends one [B, H] bf16 hidden-state hop
+    # per micro-batch slot per step (tiny-llama H = 256; M = stages + 1 = 3 slots, B = 2), nothing
+    # from the prefill or warm-up rounds
+    steps, M, B, H = 3, rec["config"]["micro_batches"], 2, 256
+    assert rec["hop_sends_per_rank"][0] == steps * M
+    assert rec["hop_bytes_sent_per_rank"][0] == steps * M * B * H * 2
+    assert rec["hop_sends_per_rank"][1] == steps * M  # the tail's token returns
+    assert rec["hop_bytes_sent_per_rank"][1] == steps * M * B * 8
 
 
 def test_bench_spawn_fails_loudly():

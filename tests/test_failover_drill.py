@@ -37,6 +37,7 @@ def _drill(tmp_path, name, extra, device, model, env_extra=None, timeout=300):
 
 def _check(ref, ref_dump, rec, dump, exact):
     fo = rec["failover"]
+    assert rec["ms_per_step"] is not None and rec["ms_per_step"] > 0  # the pre-failure window's step time
     assert fo["failed_replicas"] == [1]
     assert fo["sessions_completed"] == fo["sessions_total"] == 12
     assert fo["sessions_replaced"] > 0 and fo["recovery_s"] is not None and fo["recovery_s"] < 30

@@ -50,7 +50,7 @@ def test_reference_fold_identity_cpu():
     assert int(ssz.abs().sum()) == 0
 
 
-KERNELS = ["pk", "sk", "lds22", "lds24", "lds42", "rw", "rwk", "rwki", "rwks", "rwr"]
+KERNELS = ["pk", "sk", "lds22", "lds24", "lds42", "rw", "rwk", "rwki", "rwr"]
 
 
 @pytest.mark.gpu
@@ -115,15 +115,13 @@ def test_producer_epilogue_residual_pack_and_sumsq(kern, M):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("M,mw", [(65, False), (96, False), (128, False), (65, True), (96, True), (128, True),
-                                  (129, True), (192, True), (200, True), (256, True)])
-def test_wide_rows_consumer_and_producer(M, mw, monkeypatch):
+@pytest.mark.parametrize("M", [65, 96, 128, 129, 192, 200, 256])
+def test_wide_rows_consumer_and_producer(M, monkeypatch):
     """65..256 rows (decode steps of 65..256 sessions): the consumers (qkv: split-K ring +
     reduce with the row scale; gate/up: balanced ring with the row scale and packed SwiGLU) and
     the producer (split-K ring + the reduce launch's residual / packed copy / statistics), against
-    fp32 oracles.  mw: the row-split form (csrc/gemm_mw.h), which every step above 128 rows runs."""
+    fp32 oracles.  Above 128 rows: the 12 / 16-row-tile ring instantiations."""
     monkeypatch.setattr(ops, "WIDE_ROWS", 256)  # above 128 rows the hand-written forms are opt-in
-    monkeypatch.setattr(ops, "_WIDE_MW", mw)     # the row-split form (csrc/gemm_mw.h); > 128 rows always
     dev = "cuda"
     g = torch.Generator(device=dev).manual_seed(500 + M)
     K, N = 2048, 2048
@@ -165,10 +163,10 @@ def test_wide_rows_consumer_and_producer(M, mw, monkeypatch):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("M", [200, 256])
-def test_row_split_in_kernel_epilogues(M, monkeypatch):
-    """The row-split form's S = 1 geometry (csrc/gemm_mw.h: every column group in one workgroup,
-    the decode epilogue in the kernel) - what the Llama-2-7B qkv (N = 12288) and gate/up
-    (N = 22016) widths choose at 129..256 rows: row-scaled consumer and packed SwiGLU vs fp32."""
+def test_wide_ring_in_kernel_epilogues(M, monkeypatch):
+    """The ring kernel's 12 / 16-row-tile forms with the decode epilogue in the kernel, at the
+    Llama-2-7B qkv (N = 12288) and gate/up (N = 22016) widths and 129..256 rows: row-scaled
+    consumer and packed SwiGLU vs fp32."""
     monkeypatch.setattr(ops, "WIDE_ROWS", 256)
     dev = "cuda"
     g = torch.Generator(device=dev).manual_seed(900 + M)

@@ -125,7 +125,7 @@ def use_tuned_gemms(path: Optional[str] = None) -> bool:
 # kernel.  "auto" = per (M bucket, N, K, epilogue) choice measured by ``autotune_gemm`` (the
 # executor tunes its own shapes at start-up; untuned shapes use the first kernel); "on" /
 # "off" force the stream-K kernel on / off wherever it applies.
-_GEMM_SK = os.environ.get("MPAMD_GEMM_SK", "auto")
+_GEMM_SK = "auto"
 _GEMM_WS = {}
 _SK_CHOICE = {}  # (m_bucket, N, K, epilogue) -> kernel name (see _KERNEL_FLAGS)
 # decode-GEMM kernels (csrc/gemm.hip): one-group-per-workgroup, stream-K, and the shared-A (LDS)
@@ -387,23 +387,19 @@ def kv_write(k, v, k_cache, v_cache, slots):
     torch.ops.mpamd.kv_write(k, v, k_cache, v_cache, slots)
 
 
-_ATTN_MIN_PART_ENV = os.environ.get("MPAMD_ATTN_MIN_PART")
-
-
 def attention_partition(num_queries: int, nkv: int, max_ctx: int, target_wgs: int = 1024,
                         min_part: int = 64) -> Tuple[int, int]:
     """(part_size, num_parts) for split-K flash decoding: enough workgroups to fill 256 CUs,
     but no slice shorter than ``min_part`` tokens.  The executor asks for 256-token slices on
     the MFMA GQA decode kernel (Llama-3-8B, 64 sessions: 13147 -> 13675 tok/s; batch 1:
     278 -> 281) and keeps 64 on the flash-decoding kernel, where short slices + the reduce
-    launch measured slightly faster at batch 1 (334 vs 327 tok/s, Llama-2-7B).
-    ``MPAMD_ATTN_MIN_PART`` overrides every caller."""
+    launch measured slightly faster at batch 1 (334 vs 327 tok/s, Llama-2-7B)."""
     max_ctx = max(int(max_ctx), 1)
-    if not _ATTN_MIN_PART_ENV and min_part < 256 and num_queries * nkv <= 64:
+    if min_part < 256 and num_queries * nkv <= 64:
         # few (query, head) pairs: 256-token slices, so short contexts need no split-K combine
         # (its cost exceeds what 64 / 128-token slices save at batch 1 / 2: profiles/r4t)
         min_part, target_wgs = 256, 256
-    min_part = int(_ATTN_MIN_PART_ENV) if _ATTN_MIN_PART_ENV else int(min_part)
+    min_part = int(min_part)
     want = max(1, math.ceil(target_wgs / max(1, num_queries * nkv)))
     np_ = max(1, min(want, math.ceil(max_ctx / 64)))
     ps = 64 * math.ceil(math.ceil(max_ctx / np_) / 64)
@@ -476,7 +472,8 @@ def attention_mfma(q, k_cache, v_cache, block_tables, q_seq, q_ctx, qblocks, nh,
     return out
 
 
-FA_WAVES = int(os.environ.get("MPAMD_FA_WAVES", "4"))  # waves per prefill workgroup (32 query rows each)
+FA_WAVES = 4  # default waves per prefill workgroup (32 query rows each); fa_plan picks 4 or 8 per step
+FA_WAVES_FORCE = None  # 4 / 8: every prefill step on that workgroup size (A/B runs)
 
 
 def fa_blocks(ntoks, nrep: int, waves: int = None):
@@ -502,14 +499,14 @@ def fa_plan(ntoks, nh: int, nkv: int, n_cu: int = 256):
     (a single 2K GQA prompt: 4 waves measured 74.7 vs 91.7 us, profiles/r3_fa2/attn.jsonl)."""
     nrep = max(1, nh // nkv)
     fb8 = fa_blocks(ntoks, nrep, 8)
-    if FA_WAVES in (4, 8) and os.environ.get("MPAMD_FA_WAVES"):
-        return (fb8 if FA_WAVES == 8 else fa_blocks(ntoks, nrep, 4)), FA_WAVES
+    if FA_WAVES_FORCE in (4, 8):
+        return (fb8 if FA_WAVES_FORCE == 8 else fa_blocks(ntoks, nrep, 4)), FA_WAVES_FORCE
     if fb8.shape[1] * nkv > n_cu:
         return fb8, 8
     return fa_blocks(ntoks, nrep, 4), 4
 
 
-FA_PAIR = os.environ.get("MPAMD_FA_PAIR", "auto")
+FA_PAIR = "auto"  # "0" / "1" force the pairing off / on (A/B runs)
 
 
 def fa_pair(nblocks: int, nh: int, nkv: int, num_parts: int, n_cu: int = 256) -> bool:
@@ -517,8 +514,7 @@ def fa_pair(nblocks: int, nh: int, nkv: int, num_parts: int, n_cu: int = 256) ->
     ``pair``): every workgroup then streams the same context, so the longest blocks no longer set
     the kernel time, and there are half as many workgroups to launch.  Measured faster or equal
     in every case of profiles/r4d/attn_pair.jsonl (1 x 2048 MHA 116.6 -> 80.9 us, 1 x 4096 MHA
-    231.7 -> 159.8, 64 x 128 GQA 59.3 -> 54.5), so it is on whenever the context is not split.
-    MPAMD_FA_PAIR=0/1 forces it."""
+    231.7 -> 159.8, 64 x 128 GQA 59.3 -> 54.5), so it is on whenever the context is not split."""
     if FA_PAIR in ("0", "1"):
         return FA_PAIR == "1" and num_parts == 1
     return num_parts == 1 and nblocks >= 2
@@ -608,11 +604,14 @@ def attention_counters(device) -> torch.Tensor:
     return c
 
 
+# the flash-decoding split-K combine inside the attention launch (last-arriving slice) instead of
+# the reduce launch: off - measured at batch 1 (Llama-2-7B, 1 MI355X) 2.984 ms/step with it vs
+# 2.921 with the separate reduce launch (profiles/r2_attn_combine); kept bit-identical and tested
+ATTN_INLAUNCH_REDUCE = False
+
+
 def _attn_cnt(device):
-    # off by default: measured at batch 1 (Llama-2-7B, 1 MI355X) 2.984 ms/step with the in-launch
-    # combine vs 2.921 with the separate reduce launch - the release / ticket / acquire chain of
-    # the last-arriving slice costs more than the launch it removes (profiles/r2_attn_combine)
-    if os.environ.get("MPAMD_ATTN_INLAUNCH_REDUCE", "0") == "0":
+    if not ATTN_INLAUNCH_REDUCE:
         return None
     return attention_counters(device)
 
@@ -1133,7 +1132,7 @@ def unpack_weight_w8(w8: torch.Tensor, w_scale: torch.Tensor, dtype=torch.bfloat
 
 _W8_KERNELS = {"rw": 128, "rwk": 256, "rwki": 256 | 512}
 _W8_CHOICE = {}  # (m_bucket, N, K, epilogue) -> "rw" / "rwk", from autotune_w8
-_W8_MODE = os.environ.get("MPAMD_W8_KERNEL", "auto")
+_W8_MODE = "auto"  # or a _W8_KERNELS name forced everywhere it applies (tests, A/B runs)
 
 
 def _w8_kernel(M: int, N: int, K: int, epilogue: int) -> str:

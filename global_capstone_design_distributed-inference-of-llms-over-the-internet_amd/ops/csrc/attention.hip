@@ -161,283 +161,17 @@ __device__ __forceinline__ void split_combine(int* cnt_slot, int NP, const float
   }
 }
 
-template <int D, int NREP, bool ROPE>
-__global__ __launch_bounds__(256) void paged_attn_kernel(
-    const bf16_t* __restrict__ q, int64_t q_stride, const bf16_t* __restrict__ kc,
-    const bf16_t* __restrict__ vc, const int32_t* __restrict__ block_tables, int bt_stride,
-    const int32_t* __restrict__ q_seq, const int32_t* __restrict__ q_ctx, bf16_t* __restrict__ out,
-    float* __restrict__ part_o, float* __restrict__ part_ml, int nkv, int nh, int page_log2, int PS, int NP,
-    float scale_log2, int packed_mt, RopeFuse rf, int* __restrict__ cnt) {
-  constexpr int LPT = D / 8;
-  constexpr int TPI = 64 / LPT;
-  constexpr int U = 4;
-  constexpr int TPW = TPI * U;
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* s_p = smem;                  // [NREP][PS] scores -> probabilities
-  float* s_red = smem + NREP * PS;    // [4][NREP] per-wave maxes, then [4][NREP] sums
-  float* s_o = s_red + 8 * NREP;      // [4][NREP][D]
-
-  const int t = blockIdx.z, p = blockIdx.x;
-  const int hbase = blockIdx.y * NREP;  // first query head of this workgroup
-  const int g = hbase / (nh / nkv);      // its kv head
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int sl = lane % LPT, tg = lane / LPT;
-  const int ctx = q_ctx[t];
-  const int start = p * PS;
-  const int end = min(start + PS, ctx);
-  const int64_t obase = ((int64_t)t * nh + hbase) * D;
-  if (start >= end) {
-    if (NP == 1) {
-      for (int i = tid; i < NREP * D; i += 256)
-        out[packed_mt > 0 ? apk_off(t, hbase * D + i, packed_mt) : obase + i] = 0;
-    } else {
-      if (tid < NREP) {
-        float* ml = part_ml + (((int64_t)t * nh + hbase + tid) * NP + p) * 2;
-        ml[0] = -INFINITY;
-        ml[1] = 0.f;
-      }
-      if (cnt != nullptr)
-        split_combine<D, NREP>(cnt + (int64_t)t * (nh / NREP) + blockIdx.y, NP, part_o, part_ml, t, hbase, nh, out,
-                               packed_mt, smem);
-    }
-    return;
-  }
-  const int page_size = 1 << page_log2;
-  const int32_t* bt = block_tables + (int64_t)q_seq[t] * bt_stride;
-  const int64_t head_off = (int64_t)g * page_size * D + sl * 8;
-  const int64_t page_stride = (int64_t)nkv * page_size * D;
-
-  float qf[NREP][8];
-  u16x8 kn = (u16x8)(0), vn = (u16x8)(0);  // ROPE: the new token's rotated k / v chunk
-  int tnew = -1;
-  if constexpr (ROPE) {
-    constexpr int HALF = D / 2;
-    const bf16_t* row = q + (int64_t)t * q_stride;
-    const int c0 = (sl * 8) & (HALF - 1);
-    const bool lo = sl * 8 < HALF;
-    const int po = lo ? HALF : -HALF;
-    if (rf.qp.part != nullptr) {
-      // the qkv split-K partials: this workgroup's q / k / v chunks built once into LDS (every slab
-      // element read once per workgroup, not once per token group of every wave)
-      __shared__ u16x8 s_fold[(NREP + 2) * LPT];
-      fold_qkv_lds<D, NREP>(rf, t, hbase, g, nh, nkv, qkv_part_scale(rf.qp, t), s_fold);
-#pragma unroll
-      for (int r = 0; r < NREP; ++r) {
-        const u16x8 v = s_fold[r * LPT + sl];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) qf[r][j] = bf2f(v[j]) * scale_log2;
-      }
-      kn = s_fold[NREP * LPT + sl];
-      vn = s_fold[(NREP + 1) * LPT + sl];
-    } else {
-      const int64_t ps_ = rf.pos[t];
-      const f32x4 ca = *reinterpret_cast<const f32x4*>(rf.cos_t + ps_ * HALF + c0);
-      const f32x4 cb = *reinterpret_cast<const f32x4*>(rf.cos_t + ps_ * HALF + c0 + 4);
-      const f32x4 sa = *reinterpret_cast<const f32x4*>(rf.sin_t + ps_ * HALF + c0);
-      const f32x4 sb = *reinterpret_cast<const f32x4*>(rf.sin_t + ps_ * HALF + c0 + 4);
-      auto rot = [&](int hc) {  // hc: first column of the head in the qkv row
-        const u16x8 me = *reinterpret_cast<const u16x8*>(row + hc + sl * 8);
-        const u16x8 ot = *reinterpret_cast<const u16x8*>(row + hc + sl * 8 + po);
-        return rope8(me, ot, ca, cb, sa, sb, lo);
-      };
-#pragma unroll
-      for (int r = 0; r < NREP; ++r) {
-        const u16x8 v = rot((hbase + r) * D);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) qf[r][j] = bf2f(v[j]) * scale_log2;
-      }
-      kn = rot((nh + g) * D);
-      vn = *reinterpret_cast<const u16x8*>(row + (nh + nkv + g) * D + sl * 8);
-    }
-    tnew = ctx - 1;
-    const int64_t slot = rf.slots[t];
-    if (tnew >= start && tnew < end && slot >= 0 && tid < LPT && hbase % (nh / nkv) == 0) {
-      const int64_t pg = slot >> page_log2, off = slot & (page_size - 1);
-      const int64_t dst = pg * page_stride + head_off + off * D;
-      *reinterpret_cast<u16x8*>(rf.kw + dst) = kn;
-      *reinterpret_cast<u16x8*>(rf.vw + dst) = vn;
-    }
-  } else {
-#pragma unroll
-    for (int r = 0; r < NREP; ++r) {
-      const u16x8 v = *reinterpret_cast<const u16x8*>(q + (int64_t)t * q_stride + (hbase + r) * D + sl * 8);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) qf[r][j] = bf2f(v[j]) * scale_log2;
-    }
-  }
-
-  // ---- pass 1: scores (log2 domain) into LDS, running max per head ----
-  float mloc[NREP];
-#pragma unroll
-  for (int r = 0; r < NREP; ++r) mloc[r] = -INFINITY;
-  for (int base = start + w * TPW; base < end; base += 4 * TPW) {
-    u16x8 kv[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int tok = base + u * TPI + tg;
-      // unconditional load of a clamped token (no exec-masked branch between the U loads),
-      // then select: the ROPE path's new token comes from registers, past the end is 0
-      const int tc = min(tok, end - 1);
-      const int64_t pg = bt[tc >> page_log2];
-      const u16x8 ld = *reinterpret_cast<const u16x8*>(kc + pg * page_stride + head_off +
-                                                        (int64_t)(tc & (page_size - 1)) * D);
-      kv[u] = ROPE ? ld : (tok < end ? ld : (u16x8)(0));
-    }
-    if constexpr (ROPE) {
-      // pin the U loads as unconditional (otherwise the compiler sinks each into a
-      // tok != tnew branch with a full vmcnt(0) wait), then substitute the new token
-#pragma unroll
-      for (int u = 0; u < U; ++u) asm volatile("" : "+v"(kv[u]));
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int tok = base + u * TPI + tg;
-        kv[u] = tok == tnew ? kn : (tok < end ? kv[u] : (u16x8)(0));
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int tok = base + u * TPI + tg;
-#pragma unroll
-      for (int r = 0; r < NREP; ++r) {
-        float d = 0.f;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) d += qf[r][j] * bf2f(kv[u][j]);
-        d = group_sum<LPT>(d);
-        if (sl == 0 && tok < end) {
-          s_p[r * PS + (tok - start)] = d;
-          mloc[r] = fmaxf(mloc[r], d);
-        }
-      }
-    }
-  }
-#pragma unroll
-  for (int r = 0; r < NREP; ++r) {
-    const float m = wave_max(mloc[r]);
-    if (lane == 0) s_red[w * NREP + r] = m;
-  }
-  __syncthreads();
-  float mrow[NREP];
-#pragma unroll
-  for (int r = 0; r < NREP; ++r)
-    mrow[r] = fmaxf(fmaxf(s_red[r], s_red[NREP + r]), fmaxf(s_red[2 * NREP + r], s_red[3 * NREP + r]));
-
-  // ---- pass 2: probabilities p = exp2(s - m) in place ----
-  const int n = end - start;
-  for (int i = tid; i < NREP * n; i += 256) {
-    const int r = i / n, j = i - r * n;
-    float m = mrow[0];
-#pragma unroll
-    for (int rr = 1; rr < NREP; ++rr)
-      if (r == rr) m = mrow[rr];
-    s_p[r * PS + j] = exp2f(s_p[r * PS + j] - m);
-  }
-  __syncthreads();
-
-  // ---- pass 3: o = sum_t p_t * V_t, l = sum_t p_t ----
-  float acc[NREP][8];
-  float lsum[NREP];
-#pragma unroll
-  for (int r = 0; r < NREP; ++r) {
-    lsum[r] = 0.f;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[r][j] = 0.f;
-  }
-  for (int base = start + w * TPW; base < end; base += 4 * TPW) {
-    u16x8 vv[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int tok = base + u * TPI + tg;
-      // unconditional load of a clamped token (no exec-masked branch between the U loads),
-      // then select: the ROPE path's new token comes from registers, past the end is 0
-      const int tc = min(tok, end - 1);
-      const int64_t pg = bt[tc >> page_log2];
-      const u16x8 ld = *reinterpret_cast<const u16x8*>(vc + pg * page_stride + head_off +
-                                                        (int64_t)(tc & (page_size - 1)) * D);
-      vv[u] = ROPE ? ld : (tok < end ? ld : (u16x8)(0));
-    }
-    if constexpr (ROPE) {
-      // pin the U loads as unconditional (otherwise the compiler sinks each into a
-      // tok != tnew branch with a full vmcnt(0) wait), then substitute the new token
-#pragma unroll
-      for (int u = 0; u < U; ++u) asm volatile("" : "+v"(vv[u]));
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int tok = base + u * TPI + tg;
-        vv[u] = tok == tnew ? vn : (tok < end ? vv[u] : (u16x8)(0));
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int tok = base + u * TPI + tg;
-      if (tok < end) {
-#pragma unroll
-        for (int r = 0; r < NREP; ++r) {
-          const float pr = s_p[r * PS + (tok - start)];
-          lsum[r] += pr;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) acc[r][j] += pr * bf2f(vv[u][j]);
-        }
-      }
-    }
-  }
-  // reduce over the token groups of the wave (lanes sl, sl+LPT, ...)
-#pragma unroll
-  for (int o = LPT; o < 64; o <<= 1) {
-#pragma unroll
-    for (int r = 0; r < NREP; ++r) {
-      lsum[r] += __shfl_xor(lsum[r], o, 64);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc[r][j] += __shfl_xor(acc[r][j], o, 64);
-    }
-  }
-  float* s_l = s_red + 4 * NREP;
-  if (tg == 0) {
-#pragma unroll
-    for (int r = 0; r < NREP; ++r) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) s_o[(w * NREP + r) * D + sl * 8 + j] = acc[r][j];
-      if (sl == 0) s_l[w * NREP + r] = lsum[r];
-    }
-  }
-  __syncthreads();
-  for (int i = tid; i < NREP * D; i += 256) {
-    const int r = i / D, d = i - r * D;
-    const float o = s_o[r * D + d] + s_o[(NREP + r) * D + d] + s_o[(2 * NREP + r) * D + d] +
-                    s_o[(3 * NREP + r) * D + d];
-    const float l = s_l[r] + s_l[NREP + r] + s_l[2 * NREP + r] + s_l[3 * NREP + r];
-    if (NP == 1) {
-      out[packed_mt > 0 ? apk_off(t, hbase * D + i, packed_mt) : obase + i] = f2bf(o / l);
-    } else {
-      const int64_t hp = ((int64_t)t * nh + hbase + r) * NP + p;
-      part_o[hp * D + d] = o;
-      if (d == 0) {
-        float m = mrow[0];
-#pragma unroll
-        for (int rr = 1; rr < NREP; ++rr)
-          if (r == rr) m = mrow[rr];
-        part_ml[hp * 2] = m;
-        part_ml[hp * 2 + 1] = l;
-      }
-    }
-  }
-  if (NP > 1 && cnt != nullptr)
-    split_combine<D, NREP>(cnt + (int64_t)t * (nh / NREP) + blockIdx.y, NP, part_o, part_ml, t, hbase, nh, out,
-                           packed_mt, s_red);
-}
-
-// Single-pass form of the kernel above (the default; MPAMD_ATTN_1PASS=0 selects the two-pass
-// one).  The two-pass kernel reads K, publishes scores to LDS, waits at a barrier, and only then
-// starts the V stream: every workgroup has ONE stream in flight at a time and the whole grid idles
-// at the barrier (at 64 sessions all 2048 workgroups are resident at once and hit it together).
-// Here each lane keeps an ONLINE softmax over the tokens it sees (running max m, sum l and the
+// The decode kernel is single-pass.  (A two-pass form - K read, scores published to LDS, a
+// barrier, then the V stream - kept ONE stream in flight per workgroup and idled the whole grid
+// at the barrier; it was measured slower and removed.)  Each lane keeps an ONLINE softmax over the tokens it sees (running max m, sum l and the
 // 8-dim P.V accumulator, exp2 domain), so the K and V loads of an iteration are issued together
 // (8 x 16 B per lane in flight) and the page ids of the next iteration are fetched into registers
 // while the current one computes (no dependent page-table round trip on the critical path).  The
 // 4 token groups of a wave merge by xor shuffles, the 4 waves through LDS (rescaled by their
 // maxima), and the output / split-K partials (o, m, l) have the two-pass kernel's format.
-// NW = waves per workgroup: 4 (software-pipelined, PIPE), or 16 for grids of at most
-// MPAMD_ATTN_WIDE_WGS workgroups (default 0: never - it stopped paying once the 4-wave form was
-// pipelined, profiles/r4o).
+// NW = waves per workgroup, PIPE = software-pipelined K / V stream: the launcher uses (4, true).
+// (16-wave workgroups for small grids stopped paying once the 4-wave form was pipelined,
+// profiles/r4o; the unpipelined form measured slower: both removed.)
 template <int D, int NREP, bool ROPE, int NW, bool PIPE, int U = 4>
 __global__ __launch_bounds__(NW * 64) void paged_attn1_kernel(
     const bf16_t* __restrict__ q, int64_t q_stride, const bf16_t* __restrict__ kc,
@@ -737,48 +471,15 @@ static void launch_attn(const void* q, int64_t q_stride, const void* kc, const v
                         int bt_stride, const int32_t* q_seq, const int32_t* q_ctx, void* out, float* ws_o,
                         float* ws_ml, int T, int nkv, int nh, int page_log2, int PS, int NP, float scale_log2,
                         int packed_mt, const RopeFuse& rf, int* cnt, hipStream_t stream) {
-  static const bool one_pass = [] {
-    const char* v = getenv("MPAMD_ATTN_1PASS");
-    return !(v && v[0] == '0');
-  }();
-  // 16-wave workgroups when the grid is at most MPAMD_ATTN_WIDE_WGS workgroups (default 0: never).
-  // With the pipelined 4-wave form they no longer pay: batch 1..16 x ctx 170 / 1024, 32 heads,
-  // sum of 10 cases 171.5 us at a 512 threshold vs 167.9 us without (4 x 170: 13.9 -> 10.8 us),
-  // profiles/r4o
-  static const int wide_max = [] {
-    const char* v = getenv("MPAMD_ATTN_WIDE_WGS");
-    return v ? atoi(v) : 0;
-  }();
-  const bool wide = one_pass && (int64_t)NP * (nh / NREP) * T <= wide_max;
-  const int nw = wide ? 16 : 4;
-  const size_t lds = one_pass ? (size_t)(nw * NREP * D + 2 * nw * NREP + 4) * sizeof(float)
-                              : (size_t)(NREP * PS + 8 * NREP + 4 * NREP * D) * sizeof(float);
+  constexpr int nw = 4;
+  const size_t lds = (size_t)(nw * NREP * D + 2 * nw * NREP + 4) * sizeof(float);
   auto go = [&](auto kern) {
     hipLaunchKernelGGL(kern, dim3(NP, nh / NREP, T), dim3(64 * nw), lds, stream, (const bf16_t*)q, q_stride,
                        (const bf16_t*)kc, (const bf16_t*)vc, bt, bt_stride, q_seq, q_ctx, (bf16_t*)out, ws_o, ws_ml,
                        nkv, nh, page_log2, PS, NP, scale_log2, packed_mt, rf, cnt);
   };
-  static const bool pipe = [] {
-    const char* v = getenv("MPAMD_ATTN_PIPE");
-    return !(v && v[0] == '0');
-  }();
-
-  // (the 16-wave form keeps the plain prologue: issuing its first K / V ahead of the query / RoPE
-  // loads, as the 4-wave form does, measured no faster at batch 1 / 4 / 8, profiles/r4n)
-  if (one_pass && wide) {
-    if (rf.pos) go(paged_attn1_kernel<D, NREP, true, 16, false>);
-    else go(paged_attn1_kernel<D, NREP, false, 16, false>);
-  } else if (one_pass && pipe) {
-    if (rf.pos) go(paged_attn1_kernel<D, NREP, true, 4, true>);
-    else go(paged_attn1_kernel<D, NREP, false, 4, true>);
-  } else if (one_pass) {
-    if (rf.pos) go(paged_attn1_kernel<D, NREP, true, 4, false>);
-    else go(paged_attn1_kernel<D, NREP, false, 4, false>);
-  } else if (rf.pos) {
-    go(paged_attn_kernel<D, NREP, true>);
-  } else {
-    go(paged_attn_kernel<D, NREP, false>);
-  }
+  if (rf.pos) go(paged_attn1_kernel<D, NREP, true, nw, true>);
+  else go(paged_attn1_kernel<D, NREP, false, nw, true>);
 }
 
 }  // namespace mp
@@ -807,11 +508,8 @@ extern "C" int mp_paged_attention(const void* q, int64_t q_stride, const void* k
   const float scale_log2 = scale * 1.4426950408889634f;
   float* ws_o = workspace;
   float* ws_ml = workspace + (int64_t)T * nh * NP * D;
-  // heads per workgroup: at most ATTN_HPB of a GQA group (register budget), a divisor of nrep
-  static const int hpb_max = [] {
-    const char* v = getenv("MPAMD_ATTN_HPB");
-    return v ? atoi(v) : 4;
-  }();
+  // heads per workgroup: at most 4 of a GQA group (register budget), a divisor of nrep
+  constexpr int hpb_max = 4;
   int hpb = 1;
   while (hpb * 2 <= hpb_max && nrep % (hpb * 2) == 0) hpb *= 2;
   // in-launch combine when the caller's zeroed counters cover every (query, head group)
@@ -825,11 +523,9 @@ extern "C" int mp_paged_attention(const void* q, int64_t q_stride, const void* k
   MP_ATTN_CASE(128, 1)
   MP_ATTN_CASE(128, 2)
   MP_ATTN_CASE(128, 4)
-  MP_ATTN_CASE(128, 8)
   MP_ATTN_CASE(64, 1)
   MP_ATTN_CASE(64, 2)
   MP_ATTN_CASE(64, 4)
-  MP_ATTN_CASE(64, 8)
 #undef MP_ATTN_CASE
   return -3;
 launched:

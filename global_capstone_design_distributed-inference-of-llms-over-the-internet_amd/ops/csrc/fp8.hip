@@ -662,12 +662,9 @@ static int launch_gemm_fp8_rwk(const void* a8, const float* as, const void* wq, 
   return 0;
 }
 
-// 0 = one-group kernel, 1 = balanced ring kernel where it applies (M > 16; default);
-// MPAMD_FP8_GEMM=pk selects the one-group kernel at start-up (A/B runs of bench.py)
-static int g_fp8_kernel = [] {
-  const char* v = getenv("MPAMD_FP8_GEMM");
-  return (v && v[0] == 'p') ? 0 : 1;
-}();
+// 0 = one-group kernel, 1 = balanced ring kernel where it applies (M > 16; default); the autotuner
+// (ops.autotune_fp8) sets it through mp_fp8_set_kernel
+static int g_fp8_kernel = 1;
 
 }  // namespace mp
 

@@ -150,15 +150,9 @@ extern "C" int mp_rmsnorm(const void* x, int64_t x_stride, void* res, int64_t re
   // threads per row: 512 (one 16-B chunk per thread at H = 4096) measured best in the decode
   // step, 64 -> 512: 13433 / 13493 / 13615 / 13719 tok/s (Llama-2-7B, 64 sessions, one box,
   // profiles/r1_norm_threads/); the kernel itself only moves 5.06 -> 4.99 us, it is latency
-  // bound at 64 rows.  MPAMD_NORM_THREADS = 64 / 128 / 256 overrides
-  static const int nt_env = [] {
-    const char* v = getenv("MPAMD_NORM_THREADS");
-    const int t = v ? atoi(v) : 0;
-    return (t == 64 || t == 128 || t == 256 || t == 512 || t == 1024) ? t : 0;
-  }();
-  // default: 512 threads (one 16-B chunk each at H = 4096); 1024 for wider rows (H = 8192:
-  // Llama-3-70B), so every thread still owns one chunk
-  const int nt = nt_env ? nt_env : (nch > 512 ? 1024 : 512);
+  // bound at 64 rows.  1024 threads for wider rows (H = 8192: Llama-3-70B), so every thread still
+  // owns one chunk
+  const int nt = nch > 512 ? 1024 : 512;
   dim3 grid(nrows), block(nt);
   auto args = [&](auto kern) {
     hipLaunchKernelGGL(kern, grid, block, 0, stream, (const bf16_t*)x, x_stride, (bf16_t*)res, res_stride,
@@ -167,28 +161,13 @@ extern "C" int mp_rmsnorm(const void* x, int64_t x_stride, void* res, int64_t re
   };
   // MAXC = chunks of 8 per thread; nch <= MAXC * nt
   const int per = (nch + nt - 1) / nt;
-  if (nt == 64) {
-    if (per <= 4) args(rmsnorm_kernel<4, 64>);
-    else if (per <= 8) args(rmsnorm_kernel<8, 64>);
-    else if (per <= 16) args(rmsnorm_kernel<16, 64>);
-    else args(rmsnorm_kernel<32, 64>);
-  } else if (nt == 128) {
-    if (per <= 2) args(rmsnorm_kernel<2, 128>);
-    else if (per <= 4) args(rmsnorm_kernel<4, 128>);
-    else if (per <= 8) args(rmsnorm_kernel<8, 128>);
-    else args(rmsnorm_kernel<16, 128>);
-  } else if (nt == 1024) {
+  if (nt == 1024) {
     if (per <= 1) args(rmsnorm_kernel<1, 1024>);
     else args(rmsnorm_kernel<2, 1024>);
-  } else if (nt == 512) {
+  } else {
     if (per <= 1) args(rmsnorm_kernel<1, 512>);
     else if (per <= 2) args(rmsnorm_kernel<2, 512>);
     else args(rmsnorm_kernel<4, 512>);
-  } else {
-    if (per <= 1) args(rmsnorm_kernel<1>);
-    else if (per <= 2) args(rmsnorm_kernel<2>);
-    else if (per <= 4) args(rmsnorm_kernel<4>);
-    else args(rmsnorm_kernel<8>);
   }
   return (int)hipGetLastError();
 }

@@ -852,14 +852,11 @@ extern "C" int mp_sample(const void* logits, int64_t stride, int R, int V, const
   if (recent_stride > SB) return -1;
   const size_t lds = (size_t)V * sizeof(float);
   const int use_lds = lds <= 136 * 1024;  // + ~23 KB of histogram / candidate arrays
-  // split path for wide vocabularies (MPAMD_SAMPLE_SPLIT: 0 = never, else the smallest V that
-  // takes it; default 65536, i.e. the 128K Llama-3 vocabulary but not Llama-2's 32K)
-  static const int split_min = [] {
-    const char* v = getenv("MPAMD_SAMPLE_SPLIT");
-    return v ? atoi(v) : 65536;
-  }();
+  // split path for wide vocabularies: the 128K Llama-3 vocabulary takes it, Llama-2's 32K does not
+  // (splitting the 32K rows measured no gain, profiles/r4m)
+  constexpr int split_min = 65536;
   const int C = (V + SPLIT_CH - 1) / SPLIT_CH;
-  const bool split = split_min > 0 && V >= split_min && C <= SPLIT_MAXC && recent_stride <= SPLIT_NT &&
+  const bool split = V >= split_min && C <= SPLIT_MAXC && recent_stride <= SPLIT_NT &&
                      (int64_t)R * V >= (int64_t)R * C * SPLIT_REC;  // the records fit the workspace
   if (split) {
     hipLaunchKernelGGL(sample_split_chunk_kernel, dim3(C, R), dim3(SPLIT_NT), 0, stream, (const bf16_t*)logits,

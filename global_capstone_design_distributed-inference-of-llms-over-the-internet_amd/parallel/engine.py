@@ -149,9 +149,9 @@ def settle_heap() -> bool:
     (every few dozen steps) walks the whole setup heap and stalls the step loop for milliseconds.
     Only drivers call it (engines with ``freeze_heap``): frozen objects are never collected, so a
     server that builds an engine per client channel must not freeze each one's transient state.
-    ``MPAMD_GC_FREEZE=0`` keeps the default collector.  Returns True if this call froze the heap."""
+    Returns True if this call froze the heap."""
     global _HEAP_FROZEN
-    if _HEAP_FROZEN or os.environ.get("MPAMD_GC_FREEZE", "1") == "0":
+    if _HEAP_FROZEN:
         return False
     _HEAP_FROZEN = True
     gc.collect()

@@ -173,8 +173,7 @@ class StageExecutor:
         self.use_graphs = (self.device.type == "cuda") if use_graphs is None else bool(use_graphs)
         self.use_graphs = self.use_graphs and self.device.type == "cuda" and cfg.model_type != "gpt2" and \
             os.environ.get("MPAMD_GRAPHS", "1") != "0"
-        if self._tp is not None and not getattr(self._tp, "capturable", False) and \
-                os.environ.get("MPAMD_TP_GRAPHS", "0") != "1":
+        if self._tp is not None and not getattr(self._tp, "capturable", False):
             # torch's all-reduce (gloo, or ProcessGroupNCCL's private stream) is not replayable:
             # graphs under TP need the direct RCCL communicator (parallel/rccl.py)
             self.use_graphs = False
@@ -189,29 +188,27 @@ class StageExecutor:
         self.graph_hook = None
         self._hook_owner = None
         self.last_graphed = self.last_hooked = False
-        # MFMA flash attention for prefill steps (csrc/attention_mfma.hip); MPAMD_ATTN_MFMA=off disables
-        self._attn_mfma_prefill = os.environ.get("MPAMD_ATTN_MFMA", "prefill") != "off" and \
-            cfg.model_type != "gpt2" and cfg.head_dim in (64, 128)
+        # MFMA flash attention for prefill steps (csrc/attention_mfma.hip)
+        self._attn_mfma_prefill = cfg.model_type != "gpt2" and cfg.head_dim in (64, 128)
         # GQA decode: the whole group of a kv head in the MFMA rows (2x the VALU kernel at nrep 8)
-        # MHA decode stays on the flash-decoding kernel: forcing it onto the MFMA kernel
-        # (MPAMD_ATTN_MFMA_DECODE=1, 15 of 16 MFMA rows idle) measured 11005 vs 13617 tok/s at 64
-        # sessions and 13847 vs 16248 at 128 (Llama-2-7B, profiles/r1_attn_mha_mfma_vs_simt/)
-        self._attn_mfma_gqa = self._attn_mfma_prefill and (
-            self.nh // self.nkv >= 4 or os.environ.get("MPAMD_ATTN_MFMA_DECODE", "0") == "1")
+        # MHA decode stays on the flash-decoding kernel: forcing it onto the MFMA kernel (15 of 16
+        # MFMA rows idle) measured 11005 vs 13617 tok/s at 64 sessions and 13847 vs 16248 at 128
+        # (Llama-2-7B, profiles/r1_attn_mha_mfma_vs_simt/)
+        self._attn_mfma_gqa = self._attn_mfma_prefill and self.nh // self.nkv >= 4
         # prefill: up to 4 query blocks of a sequence per workgroup share each K/V step
-        # (csrc/attention_mfma.hip attn_mfma_grp_kernel); MPAMD_ATTN_GROUPED=0 = one block each
-        self._attn_grouped = os.environ.get("MPAMD_ATTN_GROUPED", "1") != "0"
+        # (csrc/attention_mfma.hip attn_mfma_grp_kernel)
+        self._attn_grouped = True
         self._cur_sb = None
         # prefill steps with a row-major attention output: the FA2 kernel on 32x32x16 MFMA with
-        # transposed LDS reads of V (csrc/attention_fa.hip); MPAMD_ATTN_FA=0 keeps the 16x16 one
-        self._attn_fa = self._attn_mfma_prefill and os.environ.get("MPAMD_ATTN_FA", "1") != "0" and \
+        # transposed LDS reads of V (csrc/attention_fa.hip); other shapes keep the 16x16 one
+        self._attn_fa = self._attn_mfma_prefill and \
             ops.fa_ok(cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim, page_size)
         self._cur_fb = None
         self._cur_fw = 4
         self._n_cu = torch.cuda.get_device_properties(self.device).multi_processor_count \
             if self.device.type == "cuda" else 256
         # decode steps on the flash-decoding kernel fold RoPE + the KV page write into it
-        self._fuse_rope = os.environ.get("MPAMD_FUSE_ROPE", "1") != "0"
+        self._fuse_rope = True
         # shortest split-K context slice (ops.attention_partition): longer on the MFMA GQA kernel
         self._attn_min_part = 256 if self._attn_mfma_gqa else 64
         self._decode_qb: Dict[int, torch.Tensor] = {}

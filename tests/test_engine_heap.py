@@ -3,7 +3,7 @@
 * ``settle_heap``: the setup heap is collected and frozen at most once per PROCESS, and only by
   driver engines (``freeze_heap``: bench.py, the CLI client); server engines built per client
   channel never freeze, so opening and closing many channels does not grow the permanent
-  generation (``MPAMD_GC_FREEZE=0`` keeps the default collector everywhere).
+  generation.
 * graph hook: one owner at a time on an executor; ``release`` (stop / failure / end of serve)
   removes the owner's hook."""
 import gc
@@ -25,7 +25,6 @@ def fresh(monkeypatch):
     monkeypatch.setattr(engmod, "_HEAP_FROZEN", False)
     monkeypatch.setattr(gc, "freeze", lambda: calls.append("freeze"))
     monkeypatch.setattr(gc, "collect", lambda *a: calls.append("collect") or 0)
-    monkeypatch.delenv("MPAMD_GC_FREEZE", raising=False)
     return calls
 
 
@@ -40,12 +39,6 @@ def test_driver_freezes_once_per_process(fresh):
 def test_server_engines_never_freeze(fresh):
     for _ in range(5):  # one engine per client channel
         _Probe(freeze=False)._settle_heap()
-    assert fresh == []
-
-
-def test_freeze_disabled(fresh, monkeypatch):
-    monkeypatch.setenv("MPAMD_GC_FREEZE", "0")
-    _Probe(freeze=True)._settle_heap()
     assert fresh == []
 
 

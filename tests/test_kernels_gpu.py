@@ -125,7 +125,7 @@ def test_paged_attention_inlaunch_combine_equals_reduce_kernel(ctxs, parts, pack
     ps, np_ = parts
     outs = []
     for flag in ("0", "1", "1"):
-        monkeypatch.setenv("MPAMD_ATTN_INLAUNCH_REDUCE", flag)
+        monkeypatch.setattr(ops, "ATTN_INLAUNCH_REDUCE", flag == "1")
         outs.append(ops.paged_attention(q, kc, vc, bt, q_seq, q_ctx, nh, nkv, 0.088, part_size=ps, num_parts=np_,
                                         packed=packed))
     torch.cuda.synchronize()

@@ -26,6 +26,7 @@ import math
 import os
 import sys
 import time
+from typing import Optional
 
 import torch
 
@@ -284,6 +285,20 @@ def main(argv=None):
                     help="stage-hop data plane: ProcessGroupNCCL (nccl, the GPU default), the framework's own "
                          "RCCL communicators (rccl; + MPAMD_GRAPH_HOP=1 records the hop inside the decode graph), "
                          "or host-staged gloo")
+    ap.add_argument("--phase2", default="auto", choices=["auto", "off", "rccl", "nccl", "gloo"],
+                    help="after the headline phase, a second timed phase of the same pipelines on another stage-hop "
+                         "data plane, in the same processes: auto = the framework's RCCL communicators with the hop "
+                         "recorded in the decode graphs (rccl + graph hop) whenever the headline ran on "
+                         "ProcessGroupNCCL with >= 2 stages; reported under 'phase2' (ok or the failure reason), "
+                         "never replacing the headline value")
+    ap.add_argument("--phase2-timeout", type=float, default=240.0,
+                    help="wall-clock bound of the second phase: past it every rank leaves (rank 0 printing the "
+                         "headline line with phase2 = timeout)")
+    ap.add_argument("--phase2-hop-timeout", type=float, default=60.0,
+                    help="second phase: timeout of every channel wait (a dead or stuck peer becomes a failure)")
+    ap.add_argument("--phase2-inject", default="none", choices=["none", "init", "run"],
+                    help="test hook: make the second phase fail on the last stage rank at communicator set-up "
+                         "(init) or in the middle of its timed steps (run)")
     a = ap.parse_args(argv)
 
     from src import ops
@@ -393,15 +408,16 @@ def main(argv=None):
         if rank == 0:
             print(f"replica throughput (tok/s, probe batch {min(B, 16)}): {[round(t, 1) for t in thr]} -> "
                   f"sessions {counts}", file=sys.stderr)
+    reqs1 = []
+    sp = SamplingParams(a.temperature, a.top_p, a.top_k, a.repetition_penalty)
     if stage == 0:
         # synthetic requests: every pipeline of a TP group submits the same ones (same seeds),
         # so its shards take identical scheduling decisions and sample identical tokens
-        sp = SamplingParams(a.temperature, a.top_p, a.top_k, a.repetition_penalty)
         gen = torch.Generator().manual_seed(1234 + (lane // TP))
         for i in range(n_sessions):
             prompt = torch.randint(0, cfg.vocab_size, (a.prompt_len,), generator=gen).tolist()
-            eng.submit(Request(prompt, max_new_tokens=rounds + 8, params=sp, stop_on_repeat=0,
-                               seed=a.seed * 1000003 + (lane // TP) * 7919 + i, rid=f"s{i}"))
+            reqs1.append(eng.submit(Request(prompt, max_new_tokens=rounds + 8, params=sp, stop_on_repeat=0,
+                                            seed=a.seed * 1000003 + (lane // TP) * 7919 + i, rid=f"s{i}")))
     load_s = time.time() - t0
 
     def sync():
@@ -519,7 +535,7 @@ def main(argv=None):
             "hop_sends_per_rank": [int(p[4]) for p in per_stage],
             "hop_recv_wait_ms_per_rank": [round(p[5], 4) for p in per_stage],
             # the qkv fold per decode row bucket, as the warm-up's decode-graph A/B left it
-            "qkv_fold": {f"M{k[0]}": bool(v) for k, v in sorted(ops._QKV_FOLD.items())},
+            "qkv_fold": {f"M{k}": bool(v) for k, v in sorted(ex.qkv_fold_by_bucket.items())},
             "prefill_plus_first_token_s": round(prefill_s, 3),
             # the prefill round alone: every session's prompt through the whole pipeline
             # (micro-batch slots x batch x prompt-len tokens), max over ranks
@@ -527,8 +543,179 @@ def main(argv=None):
             "prefill_tokens_per_s": round(n_sessions_total * a.prompt_len / max(prefill_only_s, 1e-9), 1),
             "load_s": round(load_s, 1),
         }
+    p2 = phase2_backend(a, S, R, TP, device, data_plane)
+    if p2 is not None:
+        ctx = dict(ex=ex, rank=rank, world=world, S=S, stage=stage, lane=lane, M=M, B=B, device=device,
+                   rounds=rounds, reqs1=reqs1, sp=sp)
+        guard = _Phase2Guard(a.phase2_timeout, rec if rank == 0 else None)
+        phase2 = run_phase2(a, p2, ctx)
+        if rank == 0:
+            rec["phase2"] = phase2
+            guard.print_once(rec)
+        guard.cancel()
+    elif rank == 0:
         print(json.dumps(rec), flush=True)
     pdist.shutdown()
+
+
+def phase2_backend(a, S, R, TP, device, data_plane):
+    """The second phase's data plane, or None: only pure pipelines (no replicas / TP)."""
+    if a.phase2 == "off" or S < 2 or R != 1 or TP != 1:
+        return None
+    if a.phase2 == "auto":
+        return "rccl" if (device.type == "cuda" and data_plane == "pgnccl") else None
+    return a.phase2
+
+
+class _Phase2Guard:
+    """Wall-clock bound of the second phase: a peer stuck inside a device wait (an RCCL receive that
+    never completes blocks ``torch.cuda.synchronize``) must not cost the run its headline line.  Past
+    the deadline rank 0 prints the headline record with ``phase2 = timeout`` and every rank leaves
+    with exit code 0 (no exec, no GPU call from this thread)."""
+
+    def __init__(self, limit_s: float, rec: Optional[dict]):
+        import threading
+
+        self.rec = rec
+        self.printed = False
+        self.lock = threading.Lock()
+        self.timer = threading.Timer(max(1.0, float(limit_s)), self._fire)
+        self.timer.daemon = True
+        self.timer.start()
+
+    def print_once(self, rec: dict) -> None:
+        with self.lock:
+            if not self.printed:
+                self.printed = True
+                print(json.dumps(rec), flush=True)
+
+    def _fire(self) -> None:
+        if self.rec is not None:
+            out = dict(self.rec)
+            out["phase2"] = {"ok": False, "stage": "timeout",
+                             "reason": "the second phase did not finish within --phase2-timeout"}
+            self.print_once(out)
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0)
+
+    def cancel(self) -> None:
+        self.timer.cancel()
+
+
+def run_phase2(a, backend: str, ctx: dict) -> dict:
+    """Second timed phase: the same pipeline, the same synthetic sessions (same prompts and seeds,
+    so the same tokens), on another stage-hop data plane - by default the designed one, the
+    framework's own RCCL communicators with every hop recorded inside the sender's decode graph
+    and received straight into the receiver's graph input (the reference hop it
+    replaces: /root/reference/src/rpc_transport.py:738-766).  Built only after the headline phase
+    has been timed and reported; every wait is bounded (channel timeouts, the host agreement link,
+    ``_Phase2Guard``), a failure aborts this phase's communicators and is reported, never raised.
+    Returns the phase's record (rank 0's is the one printed)."""
+    from torch.distributed import distributed_c10d as c10d
+
+    from src.parallel.channel import Channel, HostLink
+    from src.parallel.engine import PipelineServingEngine, Request
+
+    ex, rank, world, S, stage, lane = ctx["ex"], ctx["rank"], ctx["world"], ctx["S"], ctx["stage"], ctx["lane"]
+    M, B, device = ctx["M"], ctx["B"], ctx["device"]
+    store = c10d._get_default_store()
+    link = HostLink(store, "bench/p2ctl", rank, world, timeout_s=max(30.0, 2 * a.phase2_hop_timeout))
+
+    def sync():
+        if device.type == "cuda":
+            torch.cuda.synchronize()
+
+    def agree(vals):
+        return link.all_gather_floats([float(v) for v in vals])
+
+    out = {"data_plane": None, "ok": False}
+    ch2 = eng2 = None
+    ok, reason, where = 1.0, "", "init"
+    try:
+        with ex.exec_lock:  # the headline phase's sessions (never finished) give their rows / pages back
+            for sid in list(ex.sessions.sessions):
+                ex.sessions.close(sid)
+        if a.phase2_inject == "init" and stage == S - 1:
+            raise RuntimeError("injected communicator set-up failure (--phase2-inject init)")
+        if backend == "rccl":
+            os.environ["MPAMD_GRAPH_HOP"] = "1"  # record the send in the decode graphs (every stage agrees)
+        ch2 = Channel(store, f"bench/p2pipe{lane}", stage, S, device, timeout_s=a.phase2_hop_timeout,
+                      data_backend=backend)
+    except Exception as e:  # noqa: BLE001 - reported in the JSON, never fatal to the headline
+        ok, reason = 0.0, f"rank {rank}: {type(e).__name__}: {e}"
+    try:
+        allv = agree([ok])
+    except Exception as e:  # noqa: BLE001
+        allv, reason = [[0.0]], reason or f"rank {rank}: agreement failed: {e}"
+    if not all(v[0] for v in allv):
+        if ch2 is not None:
+            ch2.abort()
+        out.update(stage="init", reason=reason or "another rank failed to set up its communicators",
+                   ranks_failed=[r for r, v in enumerate(allv) if not v[0]])
+        link.close()
+        return out
+    dt_local, tokens_match, n_cmp, hop = 0.0, None, 0, {"bytes_sent": 0, "sends": 0}
+    try:
+        where = "warmup"
+        eng2 = PipelineServingEngine(ex, ch2, n_slots=M, batch=B, max_step_tokens=B * a.prompt_len,
+                                     timeout_s=a.phase2_hop_timeout, name=f"q{lane}")
+        out["data_plane"] = data_plane_name(ch2, eng2)
+        out["graph_hop"] = bool(eng2.graph_hop)
+        reqs2 = []
+        if stage == 0:
+            for r in ctx["reqs1"]:
+                reqs2.append(eng2.submit(Request(list(r.prompt), max_new_tokens=r.max_new_tokens, params=ctx["sp"],
+                                                 stop_on_repeat=0, seed=r.seed, rid=r.rid)))
+        eng2.run_rounds(2 + a.warmup)
+        if eng2.failed:
+            raise RuntimeError(eng2.failed)
+        sync()
+        agree([1])  # host barrier
+        ch2.stats(reset=True)
+        where = "timed"
+        t1 = time.perf_counter()
+        if a.phase2_inject == "run" and stage == S - 1:
+            eng2.run_rounds(max(1, a.steps // 2))
+            raise RuntimeError("injected failure in the middle of the timed steps (--phase2-inject run)")
+        eng2.run_rounds(a.steps)
+        if eng2.failed:
+            raise RuntimeError(eng2.failed)
+        sync()
+        dt_local = time.perf_counter() - t1
+        hop = ch2.stats()
+        where = "drain"
+        if stage == 0:
+            eng2.drain()
+            n_cmp = len(reqs2)
+            tokens_match = all(list(r2.generated) == list(r1.generated) for r1, r2 in zip(ctx["reqs1"], reqs2))
+            eng2.stop()
+        else:
+            eng2.serve()
+        ch2.close()
+    except Exception as e:  # noqa: BLE001 - a peer failure of this phase: abort, report
+        ok, reason = 0.0, f"rank {rank} ({where}): {type(e).__name__}: {e}"
+        if ch2 is not None:
+            ch2.abort()
+    try:
+        rows = agree([ok, dt_local, float(hop["bytes_sent"]), float(hop["sends"]),
+                      float(bool(tokens_match)) if tokens_match is not None else -1.0])
+    except Exception as e:  # noqa: BLE001
+        rows = [[0.0, 0.0, 0.0, 0.0, -1.0]]
+        reason = reason or f"rank {rank}: agreement failed: {e}"
+    link.close()
+    if not all(r[0] for r in rows):
+        out.update(stage=where if not ok else "peer", reason=reason or "another rank's second phase failed",
+                   ranks_failed=[r for r, v in enumerate(rows) if not v[0]])
+        return out
+    dt = max(r[1] for r in rows)
+    n_sess = len(ctx["reqs1"]) if stage == 0 else 0
+    out.update(ok=True, value=round(a.steps * n_sess / dt, 2) if n_sess else None,
+               ms_per_step=round(1000 * dt / a.steps, 3), steps=a.steps, warmup=a.warmup,
+               hop_bytes_sent_per_rank=[int(r[2]) for r in rows], hop_sends_per_rank=[int(r[3]) for r in rows],
+               tokens_match_headline=bool(tokens_match) if tokens_match is not None else None,
+               sessions_compared=n_cmp)
+    return out
 
 
 if __name__ == "__main__":

@@ -870,12 +870,11 @@ def linear(x, w, out=None, epilogue=0, residual=None, policy=None, wp=None, a_ro
 # reduce launch would have stored (csrc/common.h qkv_part_load8).
 PART_FLAG = 16384
 _RWK_SPLIT = {}
-# (m_bucket, N, K, fp8) -> bool.  _QKV_FOLD_CAND: the qkv GEMM alone measured faster as partial
-# slabs (autotune_qkv_fold); _QKV_FOLD: the decision the decode path uses - set only by the
-# executor's end-to-end decode-graph A/B (the fold also moves work into the attention kernel), so
-# an unconfirmed bucket keeps the reduce launch
+# (m_bucket, N, K, fp8) -> bool: the qkv GEMM alone measured faster as partial slabs
+# (autotune_qkv_fold).  A candidate only: the decision the decode path uses is each executor's
+# end-to-end decode-graph A/B per batch bucket (StageExecutor.qkv_fold_by_bucket), because the fold
+# also moves work into the attention kernel
 _QKV_FOLD_CAND = {}
-_QKV_FOLD = {}
 
 
 def rwk_split(M: int, N: int, K: int, fp8: bool = False) -> int:
@@ -912,10 +911,6 @@ def linear_partials(x, M: int, wp=None, w8=None, w_scale=None, out=None, rot: bo
     else:
         torch.ops.mpamd.gemm(x, wp, out, None, 0, M, flags, ws, None, None, None, None, None, 1.0 / K, 0.0)
     return _slab_view(x.device, S, M, N)
-
-
-def qkv_fold(M: int, N: int, K: int, fp8: bool = False) -> bool:
-    return bool(_QKV_FOLD.get((_m_bucket(M), N, K, bool(fp8)), False)) and rwk_split(M, N, K, fp8) > 0
 
 
 def autotune_qkv_fold(N: int, K: int, device, fp8: bool = False, ms=(16, 32, 48, 64), iters: int = 24,

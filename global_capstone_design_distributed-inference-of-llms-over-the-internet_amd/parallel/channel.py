@@ -292,12 +292,14 @@ class Channel:
         except RuntimeError as e:
             raise ChannelError(f"{which} send to {dst} failed: {e}") from e
 
-    def recv(self, src: int, shape, dtype, which: str = "data", timeout_s: Optional[float] = None):
+    def recv(self, src: int, shape, dtype, which: str = "data", timeout_s: Optional[float] = None, into=None):
         """Post a receive; returns ``(tensor, waiter)``.  ``waiter()`` makes the tensor usable
         on the current stream: on RCCL it is a stream dependency (no host block), on gloo a
-        blocking wait bounded by the timeout."""
+        blocking wait bounded by the timeout.  ``into = (buffer, free_event)`` (direct RCCL only):
+        receive straight into ``buffer`` - a decode graph's static input - once ``free_event`` (its
+        last reader's completion, None = free now) has passed; other backends ignore it."""
         if self._rc:
-            return self._rccl_recv(src, shape, dtype, which)
+            return self._rccl_recv(src, shape, dtype, which, into)
         pg = self._pg(which)
         t = self.timeout_s if timeout_s is None else timeout_s
         try:
@@ -393,21 +395,29 @@ class Channel:
         self.bytes_sent += int(nbytes)
         self.sends += 1
 
-    def _rccl_recv(self, src: int, shape, dtype, which: str):
+    def _rccl_recv(self, src: int, shape, dtype, which: str, into=None):
         comm, peer, st = self._rccl_pair(which, "recv", src)
         ring = self._rings[(which, "recv")]
+        k = None
         try:
-            k, buf = ring.take(tuple(shape), dtype)
-            free = torch.cuda.Event()  # the slab's previous readers are on the compute stream
-            free.record()
-            st.wait_event(free)
+            if into is not None and tuple(into[0].shape) == tuple(shape) and into[0].dtype == dtype and \
+                    into[0].is_contiguous():
+                buf, free = into
+                if free is not None:  # the buffer's last reader (an earlier replay) must be done
+                    st.wait_event(free)
+            else:
+                k, buf = ring.take(tuple(shape), dtype)
+                free = torch.cuda.Event()  # the slab's previous readers are on the compute stream
+                free.record()
+                st.wait_event(free)
             comm.recv(buf, peer, stream=st)
             done = torch.cuda.Event()
             done.record(st)
         except RuntimeError as e:
             raise ChannelError(f"{which} recv from {src} failed: {e}") from e
         work = _EventWork(done)
-        ring.done(k, work)
+        if k is not None:
+            ring.done(k, work)
 
         def waiter():
             e0 = None

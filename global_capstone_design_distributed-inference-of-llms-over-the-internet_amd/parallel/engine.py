@@ -773,8 +773,12 @@ class PipelineServingEngine:
             # and its payload leaves this thread blocked here until the channel times out or is
             # aborted, and the executor must stay usable meanwhile (stage-local recovery adopts this
             # channel's sessions into a new one, the TCP handler keeps serving)
-            rows = self._hop_rows(T, bool((recs[:, 1] == 1).all()))
-            _, waiter = self.ch.recv(self.rank - 1, (rows, self.H), self.ex.dtype)
+            is_dec = bool((recs[:, 1] == 1).all())
+            rows = self._hop_rows(T, is_dec)
+            into = None
+            if self.graph_hop and is_dec:  # straight into the static input of the graph this step replays
+                into = self.ex.graph_input(T, int((recs[:, 2] + recs[:, 1]).max()), owner=self)
+            _, waiter = self.ch.recv(self.rank - 1, (rows, self.H), self.ex.dtype, into=into)
             x = waiter()
             if x is not None and rows != T:
                 x = x[:T]

@@ -178,8 +178,12 @@ class StageExecutor:
             # graphs under TP need the direct RCCL communicator (parallel/rccl.py)
             self.use_graphs = False
         self.graph_max_batch = graph_max_batch
-        self._graphs: Dict[Tuple[int, int, int], "_DecodeGraph"] = {}
+        self._graphs: Dict[tuple, "_DecodeGraph"] = {}
         self._graph_pool = None
+        self._recv_slot: Dict[tuple, int] = {}  # graph_input: last receive graph handed out per key
+        self._recv_pin = None                   # (owner, graph key) the owner's next step replays
+        # qkv fold per decode-graph batch bucket (_confirm_qkv_fold's end-to-end A/B on THIS executor)
+        self.qkv_fold_by_bucket: Dict[int, bool] = {}
         self._pinned = _Pinned(2 * max_tokens_per_step, 2 * max_tokens_per_step + max_sessions, self.device)
         self.last_step_ms: Optional[float] = None
         # graph_hook(out): recorded at the END of every decode graph capture (the static output
@@ -443,7 +447,7 @@ class StageExecutor:
         self.last_graphed = self.last_hooked = False
         if prompt is None and self.use_graphs and plan.is_decode and plan.T <= self.graph_max_batch:
             hooked = self.graph_hook is not None and hook_owner is not None and hook_owner is self._hook_owner
-            out = self._run_graph(plan, x, hooked)
+            out = self._run_graph(plan, x, hooked, owner=hook_owner)
             self.last_graphed, self.last_hooked = True, hooked
         elif self.cfg.model_type == "gpt2":
             out = self._forward_gpt2(plan, x, prompt=prompt)
@@ -500,12 +504,14 @@ class StageExecutor:
 
     def _qkv_fold(self, T: int) -> bool:
         """Decode steps of T rows: qkv as split-K partial slabs folded into the attention kernel's
-        loads - where ``_confirm_qkv_fold``'s decode-step A/B found it faster (``ops.qkv_fold``)."""
+        loads - where ``_confirm_qkv_fold``'s decode-step A/B on this executor found it faster for
+        the batch bucket the step replays (an unconfirmed bucket keeps the reduce launch)."""
         if not (self._fuse_rope and self._fused and self.device.type == "cuda") or \
                 os.environ.get("MPAMD_QKV_FOLD", "1") == "0":
             return False
         cfg = self.cfg
-        return ops.qkv_fold(T, cfg.q_dim + 2 * cfg.kv_dim, cfg.hidden_size, bool(self._w8))
+        return bool(self.qkv_fold_by_bucket.get(self._bucket(T), False)) and \
+            ops.rwk_split(T, cfg.q_dim + 2 * cfg.kv_dim, cfg.hidden_size, bool(self._w8)) > 0
 
     def _rope_attend(self, qkv, positions, slots, kc, vc, q_seq, q_ctx, out, ws, ps, np_, packed, qblocks, max_ctx,
                      decode, qkv_part=None):
@@ -799,10 +805,11 @@ class StageExecutor:
                 x = (0.1 * torch.randn(B, H, device=self.device, generator=gen)).to(self.dtype)
             self.forward([(s, 1) for s in sids], x)
 
+        Bb = self._bucket(B)
         t = {True: float("inf"), False: float("inf")}
         for _ in range(2):
             for fold in (True, False):
-                ops._QKV_FOLD[key] = fold
+                self.qkv_fold_by_bucket[Bb] = fold
                 step()  # capture (first time) / warm
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
@@ -812,8 +819,8 @@ class StageExecutor:
                 e1.synchronize()
                 t[fold] = min(t[fold], e0.elapsed_time(e1) / reps)
         keep = t[True] < 0.99 * t[False]
-        ops._QKV_FOLD[key] = keep
-        for k in [k for k in self._graphs if k[0] == self._bucket(B) and k[3] != keep]:
+        self.qkv_fold_by_bucket[Bb] = keep
+        for k in [k for k in self._graphs if k[0] == Bb and k[3] != keep]:
             del self._graphs[k]
         logger.info(f"qkv fold at batch {B}: {t[True]:.3f} ms/step folded vs {t[False]:.3f} unfolded -> "
                     f"{'fold' if keep else 'reduce launch'}")
@@ -1026,18 +1033,54 @@ class StageExecutor:
         c = max(c, 256)
         return 1 << (c - 1).bit_length()
 
-    def _run_graph(self, plan: Plan, x: torch.Tensor, hooked: bool = False) -> torch.Tensor:
-        B = self._bucket(plan.T)
-        ctxb = min(self._ctx_bucket(plan.max_ctx), self._ctx_bucket(self.max_seq_len))
+    def _graph_key(self, T: int, max_ctx: int, hooked: bool, slot: int = 0) -> tuple:
+        """(batch bucket, attention part size, parts, qkv fold, hooked, input slot).  Input slot 0 is
+        the graph every caller replays; 1 / 2 are a stage hop's two receive graphs (``graph_input``)."""
+        B = self._bucket(T)
+        ctxb = min(self._ctx_bucket(max_ctx), self._ctx_bucket(self.max_seq_len))
         part = ops.attention_partition(B, self.nkv, ctxb, min_part=self._attn_min_part)
-        key = (B, part[0], part[1], self._qkv_fold(B), hooked)  # (hooked last: _drop_hooked)
+        return (B, part[0], part[1], self._qkv_fold(B), bool(hooked), int(slot))
+
+    def _graph(self, key: tuple) -> "_DecodeGraph":
         g = self._graphs.get(key)
         if g is None:
             if self._graph_pool is None:
                 self._graph_pool = torch.cuda.graph_pool_handle()
-            g = _DecodeGraph(self, B, part, self._graph_pool, hook=self.graph_hook if hooked else None)
+            g = _DecodeGraph(self, key[0], (key[1], key[2]), self._graph_pool, hook=self.graph_hook if key[4] else None)
             self._graphs[key] = g
-        return g.replay(plan, x)
+        return g
+
+    def _run_graph(self, plan: Plan, x: torch.Tensor, hooked: bool = False, owner=None) -> torch.Tensor:
+        key = self._graph_key(plan.T, plan.max_ctx, hooked)
+        pin = self._recv_pin
+        if pin is not None and pin[0] is owner and owner is not None:
+            self._recv_pin = None
+            if pin[1][:5] == key[:5]:
+                key = pin[1]  # the receive graph whose static input the hop landed in
+        g = self._graph(key)
+        out = g.replay(plan, x)
+        g.mark_replayed()
+        return out
+
+    def graph_input(self, T: int, max_ctx: int, owner=None):
+        """Receive target of a stage hop (``PipelineServingEngine`` with the graph hop): the static
+        input of the decode graph the owner's NEXT step of ``T`` rows will replay, and the event after
+        which that buffer is free (the end of its last replay), or None when that step runs eagerly.
+        The hidden states then land where the graph reads them: no receive slab, no copy.  Two
+        receive graphs per bucket alternate, so the hop of step k lands in one while step k - 1
+        still replays the other (a single buffer would serialise every receive behind the previous
+        step's compute); other callers of the executor never replay them."""
+        if self.is_first or not (self.use_graphs and T <= self.graph_max_batch) or owner is None:
+            return None
+        with self.exec_lock:
+            hooked = self.graph_hook is not None and owner is self._hook_owner
+            base = self._graph_key(T, max_ctx, hooked)
+            slot = 3 - self._recv_slot.get(base, 2)  # 1, 2, 1, ...
+            self._recv_slot[base] = slot
+            key = base[:5] + (slot,)
+            g = self._graph(key)
+            self._recv_pin = (owner, key)
+            return g.x, g.done_ev
 
     def graph_rows(self, T: int, is_decode: bool) -> Optional[int]:
         """Rows of the static output a step of ``T`` tokens would replay into (its batch bucket),
@@ -1072,7 +1115,7 @@ class StageExecutor:
                 self._hook_owner = None
 
     def _drop_hooked(self) -> None:
-        for k in [k for k in self._graphs if k[-1]]:
+        for k in [k for k in self._graphs if k[4]]:
             del self._graphs[k]
 
     def clear_graphs(self):
@@ -1113,6 +1156,7 @@ class _DecodeGraph:
         if ex._attn_mfma_gqa:
             ex.decode_qblocks(B)  # allocated outside the capture
         self.bufs: dict = {}
+        self.done_ev = None  # end of the last replay on the compute stream (graph_input)
         args = (self.x, self.meta64[0], self.meta64[1], self.meta32[:B], self.meta32[B:2 * B], self.meta32[2 * B:], B,
                 0, part)
         s = torch.cuda.Stream()
@@ -1126,6 +1170,7 @@ class _DecodeGraph:
             self.out = ex._forward_llama(*args, decode=True)
             if hook is not None:  # recorded only: the warm-up runs above never call it
                 hook(self.out)
+        self.mark_replayed()  # the warm-up runs read ``x``: a receive into it waits for them
 
     def replay(self, plan: Plan, x: torch.Tensor) -> torch.Tensor:
         b, B = plan.T, self.B
@@ -1149,7 +1194,12 @@ class _DecodeGraph:
         self._stage_ev[k] = ev
         if self.ex.is_first:
             self.x[:b].copy_(x.view(-1))
-        else:
+        elif x.data_ptr() != self.x.data_ptr():  # (a hop received into the static input: no copy)
             self.x[:b].copy_(x)
         self.graph.replay()
         return self.out[:b]
+
+    def mark_replayed(self) -> None:
+        ev = torch.cuda.Event()
+        ev.record()
+        self.done_ev = ev

@@ -112,7 +112,7 @@ def test_executor_fold_on_off_same_logits(monkeypatch):
         w = random_stage_weights(cfg, 0, cfg.num_hidden_layers, has_embed=True, has_head=True, device=DEV, seed=3)
         ex = StageExecutor(cfg, w, DEV, kv_cache_bytes=64 << 20, max_sessions=16, max_seq_len=256, use_graphs=False)
         N, K = cfg.q_dim + 2 * cfg.kv_dim, cfg.hidden_size
-        monkeypatch.setattr(ops, "_QKV_FOLD", {(ops._m_bucket(8), N, K, False): fold})
+        ex.qkv_fold_by_bucket = {ex._bucket(8): fold}
         monkeypatch.setattr(ops, "_SK_CHOICE", {(ops._m_bucket(8), N, K, 0): "rwk"})
         ids = torch.arange(8 * 12, device=DEV) % cfg.vocab_size
         ex.forward([(f"s{i}", 12) for i in range(8)], ids)

@@ -199,6 +199,9 @@ class StageExecutor:
         # MFMA rows idle) measured 11005 vs 13617 tok/s at 64 sessions and 13847 vs 16248 at 128
         # (Llama-2-7B, profiles/r1_attn_mha_mfma_vs_simt/)
         self._attn_mfma_gqa = self._attn_mfma_prefill and self.nh // self.nkv >= 4
+        # decode steps of GQA models on the MFMA kernel (a lab script may flip this before the
+        # first decode step to A/B the flash-decoding kernel)
+        self.gqa_decode_mfma = self._attn_mfma_gqa
         # prefill: up to 4 query blocks of a sequence per workgroup share each K/V step
         # (csrc/attention_mfma.hip attn_mfma_grp_kernel)
         self._attn_grouped = True
@@ -214,7 +217,7 @@ class StageExecutor:
         # decode steps on the flash-decoding kernel fold RoPE + the KV page write into it
         self._fuse_rope = True
         # shortest split-K context slice (ops.attention_partition): longer on the MFMA GQA kernel
-        self._attn_min_part = 256 if self._attn_mfma_gqa else 64
+        self._attn_min_part = 256 if self.gqa_decode_mfma else 64
         self._decode_qb: Dict[int, torch.Tensor] = {}
         self._moe_y: Dict[int, torch.Tensor] = {}
         self.timing = False
@@ -484,7 +487,7 @@ class StageExecutor:
         """Paged attention: MFMA flash attention for prefill blocks (``qblocks``) and GQA decode,
         else the flash-decoding kernel."""
         table = self.sessions.table_dev
-        if qblocks is None and self._attn_mfma_gqa and self.device.type == "cuda":
+        if qblocks is None and self.gqa_decode_mfma and self.device.type == "cuda":
             T = qkv.shape[0]
             ps2 = 128 * math.ceil(ps / 128)
             np2 = max(1, math.ceil(ps * np_ / ps2))
@@ -518,7 +521,7 @@ class StageExecutor:
         """RoPE + KV write + attention.  Decode steps that run on the flash-decoding kernel do all
         three in one launch (ops.paged_attention_rope); everything else keeps rope_kv_write.
         ``qkv_part``: q / k / v as the qkv GEMM's split-K slabs (decode RoPE paths only)."""
-        if decode and qblocks is None and self._fuse_rope and self._attn_mfma_gqa and self.device.type == "cuda":
+        if decode and qblocks is None and self._fuse_rope and self.gqa_decode_mfma and self.device.type == "cuda":
             T = qkv.shape[0]
             ps2 = 128 * math.ceil(ps / 128)
             np2 = max(1, math.ceil(ps * np_ / ps2))
@@ -527,7 +530,7 @@ class StageExecutor:
                                            out=out, workspace=ws, part_size=ps2, num_parts=np2, packed=packed,
                                            qkv_part=qkv_part)
         if decode and qblocks is None and self._fuse_rope and not (
-                self._attn_mfma_gqa and self.device.type == "cuda"):
+                self.gqa_decode_mfma and self.device.type == "cuda"):
             return ops.paged_attention_rope(qkv, kc, vc, self.sessions.table_dev, q_seq, q_ctx, positions, self.cos,
                                             self.sin, slots, self.nh, self.nkv, self.scale, out=out, workspace=ws,
                                             part_size=ps, num_parts=np_, packed=packed, qkv_part=qkv_part)
@@ -1153,7 +1156,7 @@ class _DecodeGraph:
         h32[2 * B:] = np.arange(B, dtype=np.int32)
         self.blob.copy_(self._stage[0])
         self._stage[1].copy_(self._stage[0])
-        if ex._attn_mfma_gqa:
+        if ex.gqa_decode_mfma:
             ex.decode_qblocks(B)  # allocated outside the capture
         self.bufs: dict = {}
         self.done_ev = None  # end of the last replay on the compute stream (graph_input)

@@ -35,6 +35,21 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
 
 typedef unsigned long long u64;
 constexpr int SB = 1024;   // threads per block
+
+// Phase timestamps of sample_kernel for the lab driver scripts/sampler_prof.hip (compiled out of
+// the package build): thread 0 of block b stores clock64() at mark i into mp_sprof[b * 16 + i].
+#ifdef MP_SAMPLE_PROF
+__device__ unsigned long long mp_sprof[1024 * 16];
+#define MP_PROF(i) \
+  if (threadIdx.x == 0 && blockIdx.x < 1024) mp_sprof[blockIdx.x * 16 + (i)] = clock64()
+#else
+#define MP_PROF(i) ((void)0)
+#endif
+#ifdef MP_SAMPLE_PROF
+#define MP_PROF_CNT(c) (mp_sprof[blockIdx.x * 16 + 15] = (unsigned long long)(c))
+#else
+#define MP_PROF_CNT(c) ((void)0)
+#endif
 constexpr int CAND = 1024;  // top-k candidate capacity of the fast path
 
 // order-preserving unsigned key of a float (ascending key == ascending value)
@@ -54,32 +69,159 @@ __device__ __forceinline__ void push_history(int32_t* rec, int32_t* len, int cap
   *len = n + 1;
 }
 
+// The block appends `tok` to its row's left-aligned history of the last `cap` ids, in parallel:
+// thread j < cap holds the old rec[j + 1] (`h_next`, loaded at kernel start), so a full history
+// shifts by one store per thread instead of a serial load/store chain in one thread.  Every
+// thread of the block calls it with the same tok / n_old.
+__device__ __forceinline__ void push_history_block(int32_t* rec, int32_t* len, int cap, int n_old, int tok,
+                                                   int h_next) {
+  const int tid = threadIdx.x;
+  if (n_old >= cap) {
+    if (tid + 1 < cap) rec[tid] = h_next;
+    else if (tid + 1 == cap) rec[tid] = tok;
+  } else if (tid == n_old) {
+    rec[tid] = tok;
+  }
+  if (tid == 0) *len = min(n_old + 1, cap);
+}
+
+// Wave-wide reductions and scans on DPP (register-only lane moves: quad_perm, row mirrors,
+// row_shr, row_bcast15/31 - CDNA keeps the gfx9 row broadcasts) instead of __shfl_xor, which
+// lowers to ds_bpermute: an LDS round trip per step, six dependent ones per reduction.
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ float dppf(float v, float old) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(v), CTRL, ROW_MASK, 0xF, false));
+}
+__device__ __forceinline__ float wave_max_dpp(float v) {  // every lane gets the wave maximum
+  v = fmaxf(v, dppf<0xB1>(v, -INFINITY));        // quad_perm [1,0,3,2]
+  v = fmaxf(v, dppf<0x4E>(v, -INFINITY));        // quad_perm [2,3,0,1]
+  v = fmaxf(v, dppf<0x141>(v, -INFINITY));       // row_half_mirror
+  v = fmaxf(v, dppf<0x140>(v, -INFINITY));       // row_mirror: each row of 16 holds its max
+  v = fmaxf(v, dppf<0x142, 0xA>(v, -INFINITY));  // row_bcast15 into rows 1, 3
+  v = fmaxf(v, dppf<0x143, 0xC>(v, -INFINITY));  // row_bcast31 into rows 2, 3: lane 63 = total
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+  v += dppf<0xB1>(v, 0.f);
+  v += dppf<0x4E>(v, 0.f);
+  v += dppf<0x141>(v, 0.f);
+  v += dppf<0x140>(v, 0.f);
+  v += dppf<0x142, 0xA>(v, 0.f);
+  v += dppf<0x143, 0xC>(v, 0.f);
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+__device__ __forceinline__ float wave_incl_scan_dpp(float v) {  // inclusive prefix sum over the lanes
+  v += dppf<0x111>(v, 0.f);        // row_shr:1
+  v += dppf<0x112>(v, 0.f);        // row_shr:2
+  v += dppf<0x114>(v, 0.f);        // row_shr:4
+  v += dppf<0x118>(v, 0.f);        // row_shr:8: inclusive within each row of 16
+  v += dppf<0x142, 0xA>(v, 0.f);   // + the previous row's total (rows 1, 3)
+  v += dppf<0x143, 0xC>(v, 0.f);   // + rows 0-1's total (rows 2, 3)
+  return v;
+}
+
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ unsigned dppu(unsigned v) {  // identity 0 for unsigned max
+  return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROW_MASK, 0xF, false);
+}
+__device__ __forceinline__ unsigned wave_umax_dpp(unsigned v) {
+  v = max(v, dppu<0xB1>(v));
+  v = max(v, dppu<0x4E>(v));
+  v = max(v, dppu<0x141>(v));
+  v = max(v, dppu<0x140>(v));
+  v = max(v, dppu<0x142, 0xA>(v));
+  v = max(v, dppu<0x143, 0xC>(v));
+  return (unsigned)__builtin_amdgcn_readlane((int)v, 63);
+}
+
+// Exact k-th largest (k >= 1) of the keys of the wave's lanes with `act`, by a ballot radix
+// over the 32 key bits: uniform ballots and popcounts, no LDS.
+__device__ __forceinline__ unsigned wave_kth_largest(unsigned key, bool act, int k) {
+  unsigned prefix = 0u;
+  for (int b = 31; b >= 0; --b) {
+    const unsigned hi = (prefix >> b) | 1u;  // higher bits as decided, bit b = 1
+    const int cnt = __popcll(__ballot(act && (key >> b) == hi));
+    if (cnt >= k) prefix |= 1u << b;
+    else k -= cnt;
+  }
+  return prefix;
+}
+
+// Rank of each active lane's (key desc, index asc) among the wave's active lanes: a ballot radix
+// over the key bits, then the low IBITS bits of ~index (the index breaks ties like a stable sort).
+template <int IBITS>
+__device__ __forceinline__ int wave_rank_desc(unsigned key, unsigned idx, bool act) {
+  unsigned long long eq = __ballot(act);  // lanes equal to this one on the bits so far
+  int r = 0;
+  for (int b = 31; b >= 0; --b) {
+    const unsigned long long g = __ballot(act && ((key >> b) & 1u));
+    if ((key >> b) & 1u) eq &= g;
+    else {
+      r += __popcll(eq & g);
+      eq &= ~g;
+    }
+  }
+  const unsigned ni = ~idx;
+  for (int b = IBITS - 1; b >= 0; --b) {
+    const unsigned long long g = __ballot(act && ((ni >> b) & 1u));
+    if ((ni >> b) & 1u) eq &= g;
+    else {
+      r += __popcll(eq & g);
+      eq &= ~g;
+    }
+  }
+  return r;
+}
+
+// Block max / sum over SB threads: DPP wave reductions, then every lane reads the 16 wave totals
+// with four 16-B LDS reads.
+__device__ __forceinline__ float sb_max(float v, float* red) {
+  v = wave_max_dpp(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  const f32x4* r4 = reinterpret_cast<const f32x4*>(red);
+  const f32x4 a = r4[0], b = r4[1], c = r4[2], d = r4[3];
+  float t = -INFINITY;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) t = fmaxf(t, fmaxf(fmaxf(a[j], b[j]), fmaxf(c[j], d[j])));
+  return t;
+}
+__device__ __forceinline__ float sb_sum(float v, float* red) {
+  v = wave_sum_dpp(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  const f32x4* r4 = reinterpret_cast<const f32x4*>(red);
+  const f32x4 a = r4[0], b = r4[1], c = r4[2], d = r4[3];
+  float t = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) t += (a[j] + b[j]) + (c[j] + d[j]);
+  return t;
+}
+
 // Exclusive block scan of one float per thread (blockDim == SB).
 __device__ __forceinline__ float block_excl_scan(float v, float* red, float* total) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  float inc = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const float n = __shfl_up(inc, o, 64);
-    if (lane >= o) inc += n;
-  }
+  const float inc = wave_incl_scan_dpp(v);
   __syncthreads();
   if (lane == 63) red[w] = inc;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    float acc = 0.f;
-    for (int i = 0; i < SB / 64; ++i) {
-      const float t = red[i];
-      red[i] = acc;
-      acc += t;
-    }
-    red[SB / 64] = acc;
+  if (w == 0) {  // wave 0 scans the SB / 64 wave totals (one row of 16 lanes: DPP row shifts)
+    constexpr int NW = SB / 64;
+    const float t = lane < NW ? red[lane] : 0.f;
+    const float s = wave_incl_scan_dpp(t);
+    if (lane < NW) red[lane] = s - t;
+    if (lane == NW - 1) red[NW] = s;
   }
   __syncthreads();
   *total = red[SB / 64];
   return red[w] + inc - v;
 }
 
+// LDS = the working row lives in LDS (V <= 34K): a compile-time choice, so every access to it is
+// a ds_* op (a run-time choice left `x` a generic pointer: flat loads / stores on every sweep)
+template <bool LDS>
 __global__ __launch_bounds__(SB) void sample_kernel(const bf16_t* __restrict__ logits, int64_t stride, int V,
                                                     const float* __restrict__ temps, const float* __restrict__ top_ps,
                                                     const int32_t* __restrict__ top_ks,
@@ -89,7 +231,7 @@ __global__ __launch_bounds__(SB) void sample_kernel(const bf16_t* __restrict__ l
                                                     const int64_t* __restrict__ seeds, float* __restrict__ ws,
                                                     int64_t* __restrict__ out, int use_lds, int update,
                                                     int only_unset) {
-  __shared__ float red[SB / 64 + 1];
+  __shared__ __attribute__((aligned(16))) float red[SB / 64 + 4];
   __shared__ unsigned hist[256];
   __shared__ float mass[256];
   __shared__ unsigned s_u[4];  // scratch: selected bin, fallback flag, remaining rank
@@ -97,11 +239,19 @@ __global__ __launch_bounds__(SB) void sample_kernel(const bf16_t* __restrict__ l
   extern __shared__ __attribute__((aligned(16))) float s_row[];
   const int row = blockIdx.x, tid = threadIdx.x;
   if (only_unset && out[row] >= 0) return;  // the split sampler already drew this row
+  MP_PROF(0);
   const bf16_t* lrow = logits + (int64_t)row * stride;
   // the working row lives in LDS when it fits (V <= 38K: every pass is an LDS sweep),
   // otherwise in the global workspace (L2-resident)
-  float* x = (use_lds ? s_row : ws + (int64_t)row * V);
+  (void)use_lds;
+  float* x = LDS ? s_row : ws + (int64_t)row * V;
   const float temp = temps[row];
+  // the row's history, loaded now so its round trip overlaps the row copy: rec[tid] (penalty)
+  // and rec[tid + 1] (the shift of a full history on append)
+  int32_t* hrow = recent + (int64_t)row * recent_stride;
+  const int n_hist = recent_len[row];
+  const int h_mine = tid < recent_stride ? hrow[tid] : 0;
+  const int h_next = tid + 1 < recent_stride ? hrow[tid + 1] : 0;
 
   // ---- fp32 copy + max (max is needed by both the greedy and the sampling path) ----
   // 16-B loads, 4 in flight per thread before any use (one latency, not V/1024 of them)
@@ -153,20 +303,24 @@ __global__ __launch_bounds__(SB) void sample_kernel(const bf16_t* __restrict__ l
       for (int k = 1; k < SB / 64; ++k)
         if (bv[k] > b || (bv[k] == b && bi[k] < ix)) { b = bv[k]; ix = bi[k]; }
       out[row] = ix == 0x7fffffff ? 0 : ix;
-      if (update) push_history(recent + (int64_t)row * recent_stride, recent_len + row, recent_stride,
-                               ix == 0x7fffffff ? 0 : ix);
+      s_i[1] = ix == 0x7fffffff ? 0 : ix;
+    }
+    if (update) {
+      __syncthreads();
+      push_history_block(hrow, recent_len + row, recent_stride, n_hist, s_i[1], h_next);
     }
     return;
   }
+  // the history, staged in LDS (each thread scans all of it) under the copy's barrier
+  const int nrec = min(n_hist, recent_stride);
+  __shared__ int s_rec[SB];
+  if (tid < nrec) s_rec[tid] = h_mine;
   __syncthreads();
+  MP_PROF(1);
 
   // ---- repetition penalty (reference src/rpc_handler.py:345-374) ----
   const float rp = rep_pens[row];
-  const int nrec = min((int)recent_len[row], recent_stride);
-  __shared__ int s_rec[SB];
-  if (tid < nrec) s_rec[tid] = recent[(int64_t)row * recent_stride + tid];
-  __syncthreads();
-  const int* rec = s_rec;  // the history, staged in LDS (each thread scans all of it)
+  const int* rec = s_rec;
   if (rp != 1.f && nrec > 0) {
     if (tid < nrec) {
       const int tok = rec[tid];
@@ -180,30 +334,53 @@ __global__ __launch_bounds__(SB) void sample_kernel(const bf16_t* __restrict__ l
       }
       if (first && tok >= 0 && tok < V) {
         const float pen = powf(rp, (float)count);
-        const float v = x[tok];
-        x[tok] = v > 0.f ? v / pen : v * pen;
-      }
-    }
-    __syncthreads();
-    if (tid == 0 && nrec >= 3) {
-      const int a = rec[nrec - 1];
-      if (rec[nrec - 2] == a && rec[nrec - 3] == a && a >= 0 && a < V) {
-        const float pen = rp * rp * rp;
-        const float v = x[a];
-        x[a] = v > 0.f ? v / pen : v * pen;
+        float v = x[tok];
+        v = v > 0.f ? v / pen : v * pen;
+        // the last three ids equal: that id gets rp**3 more, applied after the count penalty
+        // by the same thread (no second barrier / serial pass)
+        if (nrec >= 3 && tok == rec[nrec - 1] && rec[nrec - 2] == tok && rec[nrec - 3] == tok) {
+          const float pen3 = rp * rp * rp;
+          v = v > 0.f ? v / pen3 : v * pen3;
+        }
+        x[tok] = v;
       }
     }
     __syncthreads();
   }
 
   // ---- softmax(x / T): max and normaliser (x keeps the penalised logits) ----
+  MP_PROF(2);
   const float inv_t = 1.f / fmaxf(temp, 1e-5f);
+  // The sweeps below read the row in the copy's layout when it has one: thread tid owns the
+  // 8-float chunks at tid * 8 + u * SB * 8 (two 16-B LDS reads each, unrolled, so a sweep is a
+  // few LDS round trips per thread instead of V / SB dependent scalar reads).
   float lm = -INFINITY;
-  for (int i = tid; i < V; i += SB) lm = fmaxf(lm, x[i]);
-  const float m = block_max(lm, red);
+  if (vec) {
+#pragma unroll 4
+    for (int base = tid * 8; base < V; base += SB * 8) {
+      const f32x4 a = *reinterpret_cast<const f32x4*>(x + base), b = *reinterpret_cast<const f32x4*>(x + base + 4);
+      lm = fmaxf(lm, fmaxf(fmaxf(fmaxf(a[0], a[1]), fmaxf(a[2], a[3])), fmaxf(fmaxf(b[0], b[1]), fmaxf(b[2], b[3]))));
+    }
+  } else {
+    for (int i = tid; i < V; i += SB) lm = fmaxf(lm, x[i]);
+  }
+  // this thread's maximum as an order-preserving key (the top-k bound below; 0 = no element)
+  const unsigned tmax = lm > -INFINITY ? okey(lm) : 0u;
+  const float m = sb_max(lm, red);
+  MP_PROF(3);
   float ls = 0.f;
-  for (int i = tid; i < V; i += SB) ls += __expf((x[i] - m) * inv_t);
-  const float inv_s = 1.f / block_sum(ls, red);
+  if (vec) {
+#pragma unroll 4
+    for (int base = tid * 8; base < V; base += SB * 8) {
+      const f32x4 a = *reinterpret_cast<const f32x4*>(x + base), b = *reinterpret_cast<const f32x4*>(x + base + 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ls += __expf((a[j] - m) * inv_t) + __expf((b[j] - m) * inv_t);
+    }
+  } else {
+    for (int i = tid; i < V; i += SB) ls += __expf((x[i] - m) * inv_t);
+  }
+  const float inv_s = 1.f / sb_sum(ls, red);
+  MP_PROF(4);
   const int k = top_ks[row];
   const float tp = top_ps[row];
   const uint64_t rnd = splitmix64((uint64_t)seeds[row] * 0x9E3779B97F4A7C15ull + (uint64_t)row);
@@ -214,24 +391,49 @@ __global__ __launch_bounds__(SB) void sample_kernel(const bf16_t* __restrict__ l
     //      largest value (those k maxima are values of the row), so every top-k id has
     //      key >= tau, and few others do.  Selecting among 1024 maxima instead of V keys
     //      avoids the LDS-atomic pile-up on the few bins dense logits fall into. ----
-    __shared__ unsigned h2k[2048];
-    __shared__ unsigned c_key[CAND];
+    __shared__ __attribute__((aligned(16))) unsigned h2k[2 * CAND];  // radix bins, then (key, index) candidates
+    uint2* c_ki = reinterpret_cast<uint2*>(h2k);
     __shared__ int c_idx[CAND];
     __shared__ float c_p[CAND];
     __shared__ int s_cnt;
     if (tid == 0) { s_cnt = 0; s_u[1] = 0u; }
-    unsigned tmax = 0u;
-    for (int i = tid; i < V; i += SB) tmax = max(tmax, okey(x[i]));
-    // exact k-th largest of the per-thread maxima: radix select over 1024 keys (11 + 11 + 10
-    // bits), cheap however flat the row is (random-init logits are nearly uniform)
     unsigned prefix = 0u, msk = 0u;
     int kk = k;
-    for (int round = 0; round < 3; ++round) {
+    constexpr int NW = SB / 64, QW = 64 / NW;  // 16 waves x their top 4 maxima = 64 keys
+    const bool wave_bound = k <= 64;
+    if (wave_bound) {
+      // tau = the k-th largest of U, the union of every wave's QW largest thread maxima.  U is a
+      // subset of the maxima, so tau <= their k-th largest <= the row's k-th largest value, and
+      // it is close to it (the top k maxima rarely crowd into a few waves).  Wave shuffles and
+      // two barriers instead of the radix select's ~18 (the exact ranking below makes the result
+      // independent of how tight tau is; a loose one only costs candidates)
+      const int lane = tid & 63;
+      unsigned cur = tmax, mine = 0u;
+#pragma unroll
+      for (int j = 0; j < QW; ++j) {  // this wave's QW largest maxima, one DPP reduction each
+        const unsigned mxk = wave_umax_dpp(cur);
+        const unsigned long long hit = __ballot(cur == mxk);
+        if (lane == __ffsll((long long)hit) - 1) cur = 0u;  // remove one holder of the maximum
+        if (lane == j) mine = mxk;
+      }
+      if (lane < QW) h2k[(tid >> 6) * QW + lane] = mine;
+      __syncthreads();
+      if (tid < 64) {  // wave 0: the k-th largest of the 64 keys
+        const unsigned t = wave_kth_largest(h2k[tid], true, k);
+        if (tid == 0) s_u[0] = t;
+      }
+      __syncthreads();
+      prefix = s_u[0];
+      __syncthreads();  // h2k / s_u are reused below
+    }
+    // else: exact k-th largest of the per-thread maxima: radix select over 1024 keys (11 + 11 +
+    // 10 bits), cheap however flat the row is (random-init logits are nearly uniform)
+    for (int round = 0; round < (wave_bound ? 0 : 3); ++round) {
       const int shift = round == 0 ? 21 : (round == 1 ? 10 : 0);
       const unsigned nb = round < 2 ? 2048u : 1024u;
       for (int i = tid; i < 2048; i += SB) h2k[i] = 0;
       __syncthreads();
-      if (tid < V && (tmax & msk) == prefix) atomicAdd(&h2k[(tmax >> shift) & (nb - 1)], 1u);
+      if (tmax != 0u && (tmax & msk) == prefix) atomicAdd(&h2k[(tmax >> shift) & (nb - 1)], 1u);
       __syncthreads();
       const float own0 = (float)h2k[2 * tid], own1 = (float)h2k[2 * tid + 1];
       float tot;
@@ -250,39 +452,72 @@ __global__ __launch_bounds__(SB) void sample_kernel(const bf16_t* __restrict__ l
     }
     const unsigned tau = prefix;  // a value of the row <= the k-th largest value
     bool fast = s_u[1] == 0u;
+    MP_PROF(5);
     if (fast) {
-      for (int i = tid; i < V; i += SB) {
-        const unsigned key = okey(x[i]);
-        if (key >= tau) {
-          const int pos = atomicAdd(&s_cnt, 1);
-          if (pos < CAND) {
-            c_key[pos] = key;
-            c_idx[pos] = i;
+      if (vec) {
+        // a thread whose maximum is below tau holds no candidate
+#pragma unroll 4
+        for (int base = tid * 8; base < (tmax >= tau ? V : 0); base += SB * 8) {
+          const f32x4 a = *reinterpret_cast<const f32x4*>(x + base), b = *reinterpret_cast<const f32x4*>(x + base + 4);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const unsigned key = okey(j < 4 ? a[j & 3] : b[j & 3]);
+            if (key >= tau) {
+              const int pos = atomicAdd(&s_cnt, 1);
+              if (pos < CAND) c_ki[pos] = make_uint2(key, (unsigned)(base + j));
+            }
+          }
+        }
+      } else {
+        for (int i = tid; i < V; i += SB) {
+          const unsigned key = okey(x[i]);
+          if (key >= tau) {
+            const int pos = atomicAdd(&s_cnt, 1);
+            if (pos < CAND) c_ki[pos] = make_uint2(key, (unsigned)i);
           }
         }
       }
       __syncthreads();
       fast = s_cnt <= CAND;
+      MP_PROF(6);
+      if (threadIdx.x == 0 && blockIdx.x < 1024) MP_PROF_CNT(s_cnt);
     }
     if (fast) {
       const int c = s_cnt;
       // rank by (value desc, index asc); rank < k survives top-k
       int rank = CAND, my_idx = 0;
-      if (tid < c) {
-        const unsigned kt = c_key[tid];
-        my_idx = c_idx[tid];
+      if (c <= 64 && V <= (1 << 20) && tid < 64) {  // wave 0 holds every candidate: ballot radix ranks
+        const uint2 me = tid < c ? c_ki[tid] : make_uint2(0u, 0u);
+        const int r = wave_rank_desc<20>(me.x, me.y, tid < c);
+        if (tid < c) {
+          rank = r;
+          my_idx = (int)me.y;
+        }
+      } else if (tid < c) {
+        const uint2 me = c_ki[tid];
+        my_idx = (int)me.y;
         rank = 0;
-        for (int j = 0; j < c; ++j) {
-          const unsigned kj = c_key[j];
-          rank += (kj > kt) || (kj == kt && c_idx[j] < my_idx);
+        int j = 0;
+        for (; j + 8 <= c; j += 8) {  // 8 broadcast 8-B LDS reads in flight per batch
+          uint2 o[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) o[u] = c_ki[j + u];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) rank += (o[u].x > me.x) || (o[u].x == me.x && o[u].y < me.y);
+        }
+        for (; j < c; ++j) {
+          const uint2 o = c_ki[j];
+          rank += (o.x > me.x) || (o.x == me.x && o.y < me.y);
         }
       }
       __syncthreads();
+      MP_PROF(7);
       if (rank < k) {  // sorted (descending) survivors: index and FULL-softmax probability
         c_idx[rank] = my_idx;
         c_p[rank] = __expf((x[my_idx] - m) * inv_t) * inv_s;
       }
       __syncthreads();
+      MP_PROF(8);
       const int kk = min(k, c);
       const float pv = tid < kk ? c_p[tid] : 0.f;
       float t1;
@@ -297,10 +532,10 @@ __global__ __launch_bounds__(SB) void sample_kernel(const bf16_t* __restrict__ l
       __syncthreads();
       if (q > 0.f && uu >= ex2 && uu < ex2 + q) s_i[1] = c_idx[tid];
       __syncthreads();
-      if (tid == 0) {
-        out[row] = s_i[1];
-        if (update) push_history(recent + (int64_t)row * recent_stride, recent_len + row, recent_stride, s_i[1]);
-      }
+      MP_PROF(9);
+      if (tid == 0) out[row] = s_i[1];
+      if (update) push_history_block(hrow, recent_len + row, recent_stride, n_hist, s_i[1], h_next);
+      MP_PROF(10);
       return;
     }
     // degenerate row (too many candidates at the k-th value): general path below
@@ -470,8 +705,11 @@ __global__ __launch_bounds__(SB) void sample_kernel(const bf16_t* __restrict__ l
         if (__float_as_uint(x[i]) == maxbits) { pick = i; break; }
     }
     out[row] = pick < 0 ? 0 : pick;
-    if (update) push_history(recent + (int64_t)row * recent_stride, recent_len + row, recent_stride,
-                             pick < 0 ? 0 : pick);
+    s_i[0] = pick < 0 ? 0 : pick;
+  }
+  if (update) {
+    __syncthreads();
+    push_history_block(hrow, recent_len + row, recent_stride, n_hist, s_i[0], h_next);
   }
 }
 
@@ -866,8 +1104,13 @@ extern "C" int mp_sample(const void* logits, int64_t stride, int R, int V, const
     // rows the split could not take (out = -1) run the single-workgroup kernel; the others exit
     // at once.  (Its global-workspace rows overlap the split records: only -1 rows use them.)
   }
-  hipLaunchKernelGGL(sample_kernel, dim3(R), dim3(SB), use_lds ? lds : 0, stream, (const bf16_t*)logits, stride, V,
-                     temps, top_ps, top_ks, rep_pens, recent, recent_stride, recent_len, seeds, ws, out, use_lds, update,
-                     split ? 1 : 0);
+  if (use_lds)
+    hipLaunchKernelGGL(sample_kernel<true>, dim3(R), dim3(SB), lds, stream, (const bf16_t*)logits, stride, V, temps,
+                       top_ps, top_ks, rep_pens, recent, recent_stride, recent_len, seeds, ws, out, 1, update,
+                       split ? 1 : 0);
+  else
+    hipLaunchKernelGGL(sample_kernel<false>, dim3(R), dim3(SB), 0, stream, (const bf16_t*)logits, stride, V, temps,
+                       top_ps, top_ks, rep_pens, recent, recent_stride, recent_len, seeds, ws, out, 0, update,
+                       split ? 1 : 0);
   return (int)hipGetLastError();
 }

@@ -519,10 +519,11 @@ def _fp8_gemm_case(M, N, K, epi, ref, interleave_gate_up):
         assert float((y.float() - exact).norm() / exact.norm()) < 0.06
 
 
-@pytest.mark.parametrize("k,tp", [(50, 0.92), (0, 0.92), (50, 1.0)])
+@pytest.mark.parametrize("k,tp", [(50, 0.92), (0, 0.92), (50, 1.0), (200, 0.92)])
 def test_sampler_large_vocab_distribution(k, tp):
-    """V = 32000 at the reference CLI defaults: fast top-k candidate path (k > 0) and the
-    general radix path (k = 0) both sample the reference's filtered distribution."""
+    """V = 32000 at the reference CLI defaults: fast top-k candidate path (k > 0; its candidate
+    bound from the per-wave maxima for k <= 128, the exact radix select above) and the general
+    radix path (k = 0) all sample the reference's filtered distribution."""
     V, R = 32000, 8192
     g = torch.Generator().manual_seed(11)
     base = torch.randn(V, generator=g) * 1.5

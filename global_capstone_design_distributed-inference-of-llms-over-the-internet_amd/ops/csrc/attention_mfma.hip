@@ -57,7 +57,11 @@ __device__ __forceinline__ f32x4 mfma_bf16(const u16x8& a, const u16x8& b, const
 
 constexpr int VT_PITCH = 36;  // bf16 per LDS row of the transposed V tile (32 tokens + pad; 8-B aligned rows)
 
-template <int D, int HB, bool ROPE>
+// FOLD (ROPE only): q / k / v come from the qkv GEMM's split-K slabs through LDS (s_fold).  A
+// compile-time choice: as a run-time one the LDS-or-global q / k / v loads compiled to flat
+// loads, which count against vmcnt, so the RoPE prologue waited for the K / V stream issued
+// before them.
+template <int D, int HB, bool ROPE, bool FOLD = false>
 __global__ __launch_bounds__(256, 2) void attn_mfma_kernel(
     const bf16_t* __restrict__ q, int64_t q_stride, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
     const int32_t* __restrict__ block_tables, int bt_stride, const int32_t* __restrict__ q_seq,
@@ -130,7 +134,7 @@ __global__ __launch_bounds__(256, 2) void attn_mfma_kernel(
   // lane group of every wave; the RoPE below then reads them as it would the bf16 qkv row
   constexpr int CK = D / 8;  // 8-column chunks per head
   __shared__ u16x8 s_fold[(HB + 2) * CK];
-  const bool from_part = ROPE && rf.qp.part != nullptr;
+  constexpr bool from_part = ROPE && FOLD;
   if (from_part) {
     const float qrs = qkv_part_scale(rf.qp, tok0);
     for (int i = tid; i < (HB + 2) * CK; i += blockDim.x) {
@@ -571,8 +575,9 @@ static void launch_attn_mfma(const void* q, int64_t q_stride, const void* kc, co
                        (const bf16_t*)kc, (const bf16_t*)vc, bt, bt_stride, q_seq, q_ctx, qb_tok0, qb_ntok,
                        (bf16_t*)out, ws_o, ws_ml, nkv, nh, page_log2, PS, NP, scale_log2, packed_mt, rf);
   };
-  if (rf.pos) go(attn_mfma_kernel<D, HB, true>);
-  else go(attn_mfma_kernel<D, HB, false>);
+  if (rf.pos && rf.qp.part) go(attn_mfma_kernel<D, HB, true, true>);
+  else if (rf.pos) go(attn_mfma_kernel<D, HB, true, false>);
+  else go(attn_mfma_kernel<D, HB, false, false>);
 }
 
 __global__ void paged_attn_reduce_kernel(const float* __restrict__ part_o, const float* __restrict__ part_ml,

@@ -137,6 +137,7 @@ class StageWeights:
     final_norm_b: Optional[torch.Tensor] = None  # gpt2 ln_f bias
     lm_head: Optional[torch.Tensor] = None      # [V, H]
     lm_head_p: Optional[torch.Tensor] = None    # packed lm_head (V padded to a multiple of 16)
+    lm_head_folded: bool = False                # lm_head_p carries final_norm in its K columns
 
     @property
     def has_embed(self) -> bool:
@@ -190,7 +191,14 @@ class StageWeights:
             if H % 32 == 0:
                 pad = (-V) % 16
                 w = self.lm_head if pad == 0 else torch.cat([self.lm_head, self.lm_head.new_zeros(pad, H)])
+                # fused-norm decode: the final RMSNorm weight folded in as for qkv / gate_up, so a
+                # decode step's lm_head reads the packed residual stream + its row statistics
+                # (no final norm launch); other steps normalise with a unit weight first
+                fold = fold_norms and self.final_norm is not None
+                if fold:
+                    w = (w.float() * self.final_norm.float()[None, :]).to(w.dtype)
                 self.lm_head_p = ops.pack_weight(w.contiguous())
+                self.lm_head_folded = fold
 
     def quantize_fp8(self, drop_dense: bool = True) -> None:
         """fp8 (OCP e4m3) W8A8 weights for every projection (the 70B fp8 MFMA path).

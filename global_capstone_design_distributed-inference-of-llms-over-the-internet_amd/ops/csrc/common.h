@@ -35,16 +35,62 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
 
 __device__ __forceinline__ float round_bf(float f) { return bf2f(f2bf(f)); }
 
+// Wave-wide reductions on DPP lane moves (quad_perm, row mirrors, row_bcast15/31 - CDNA keeps
+// the gfx9 row broadcasts): register-only steps.  __shfl_xor lowers to ds_bpermute, an LDS round
+// trip per step, six dependent ones per 64-lane reduction.  `old` fills lanes a move leaves
+// without a source (the reduction's identity).
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ unsigned dpp_u32(unsigned old, unsigned v) {
+  return (unsigned)__builtin_amdgcn_update_dpp((int)old, (int)v, CTRL, ROW_MASK, 0xF, false);
+}
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ float dppf(float v, float old) {
+  return __uint_as_float(dpp_u32<CTRL, ROW_MASK>(__float_as_uint(old), __float_as_uint(v)));
+}
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ unsigned long long dpp_u64z(unsigned long long v) {  // 0 where no source
+  const unsigned lo = dpp_u32<CTRL, ROW_MASK>(0u, (unsigned)v);
+  const unsigned hi = dpp_u32<CTRL, ROW_MASK>(0u, (unsigned)(v >> 32));
+  return ((unsigned long long)hi << 32) | lo;
+}
+
+// every lane gets the sum / max of the wave (lane 63 collects it, then a readlane broadcast)
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, WAVE);
-  return v;
+  v += dppf<0xB1>(v, 0.f);        // quad_perm [1,0,3,2]
+  v += dppf<0x4E>(v, 0.f);        // quad_perm [2,3,0,1]
+  v += dppf<0x141>(v, 0.f);       // row_half_mirror
+  v += dppf<0x140>(v, 0.f);       // row_mirror: every lane of a row holds the row's sum
+  v += dppf<0x142, 0xA>(v, 0.f);  // row_bcast15 into rows 1, 3
+  v += dppf<0x143, 0xC>(v, 0.f);  // row_bcast31 into rows 2, 3: lane 63 holds the total
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
 }
 
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, WAVE));
+  v = fmaxf(v, dppf<0xB1>(v, -INFINITY));
+  v = fmaxf(v, dppf<0x4E>(v, -INFINITY));
+  v = fmaxf(v, dppf<0x141>(v, -INFINITY));
+  v = fmaxf(v, dppf<0x140>(v, -INFINITY));
+  v = fmaxf(v, dppf<0x142, 0xA>(v, -INFINITY));
+  v = fmaxf(v, dppf<0x143, 0xC>(v, -INFINITY));
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+
+// exact integer sums (fixed-point row statistics): over the 16 lanes of each row of the wave
+// (every lane gets its row's sum), and over the whole wave (every lane gets the total)
+__device__ __forceinline__ unsigned long long sum16_u64(unsigned long long v) {
+  v += dpp_u64z<0xB1>(v);
+  v += dpp_u64z<0x4E>(v);
+  v += dpp_u64z<0x141>(v);
+  v += dpp_u64z<0x140>(v);
   return v;
+}
+__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
+  v = sum16_u64(v);
+  v += dpp_u64z<0x142, 0xA>(v);
+  v += dpp_u64z<0x143, 0xC>(v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)v, 63);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v >> 32), 63);
+  return ((unsigned long long)hi << 32) | lo;
 }
 
 // Block-wide sum for blockDim.x <= 1024 (multiple of 64). `red` needs >= 16 floats.

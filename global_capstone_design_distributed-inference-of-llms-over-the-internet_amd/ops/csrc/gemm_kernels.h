@@ -179,13 +179,7 @@ __device__ __forceinline__ float row_scale(const EpiArgs& ep, const float* rs, i
 }
 
 // sum over the 16 lanes that share lane >> 4 (one accumulator row of a 16x16 MFMA tile)
-__device__ __forceinline__ u64 sum16(u64 v) {
-  v += __shfl_xor(v, 1, 64);
-  v += __shfl_xor(v, 2, 64);
-  v += __shfl_xor(v, 4, 64);
-  v += __shfl_xor(v, 8, 64);
-  return v;
-}
+__device__ __forceinline__ u64 sum16(u64 v) { return sum16_u64(v); }
 
 // EPI 3 store of one element (called by all 16 lanes of a row group together: sum16 inside).
 // ``rv`` is the old residual value, PREFETCHED by the caller before its main loop: loaded here
@@ -1524,8 +1518,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
     if (ep.ss_in != nullptr) {
       if (threadIdx.x < 64) {
         u64 t = threadIdx.x < SS_NSH ? ep.ss_in[threadIdx.x * SS_ROWS + row] : 0ull;
-#pragma unroll
-        for (int o2 = 32; o2 > 0; o2 >>= 1) t += __shfl_xor(t, o2, 64);
+        t = wave_sum_u64(t);
         if (threadIdx.x == 0) s_rs = rsqrtf((float)t * (1.f / SS_FX) * ep.inv_k + ep.eps);
       }
       __syncthreads();
@@ -1568,8 +1561,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   }
   if constexpr (EPI == 3) {
     if (ep.ss_out == nullptr) return;
-#pragma unroll
-    for (int o2 = 32; o2 > 0; o2 >>= 1) sq += __shfl_xor(sq, o2, 64);
+    sq = wave_sum_u64(sq);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sq;
     __syncthreads();
     if (threadIdx.x == 0)

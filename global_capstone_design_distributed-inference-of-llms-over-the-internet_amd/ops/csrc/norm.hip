@@ -77,8 +77,7 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(
   const float tot = NT == 64 ? wave_sum(ss) : block_sum(ss, red);
   const float r = rsqrtf(tot / (float)H + eps);
   if (mode == 3) {  // exact integer block sum (order-independent), then the 32 shards of this row
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) ssq += __shfl_xor(ssq, o, WAVE);
+    ssq = wave_sum_u64(ssq);
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     if (NT > 64) {
       if (lane == 0) redq[wid] = ssq;

@@ -85,31 +85,7 @@ __device__ __forceinline__ void push_history_block(int32_t* rec, int32_t* len, i
   if (tid == 0) *len = min(n_old + 1, cap);
 }
 
-// Wave-wide reductions and scans on DPP (register-only lane moves: quad_perm, row mirrors,
-// row_shr, row_bcast15/31 - CDNA keeps the gfx9 row broadcasts) instead of __shfl_xor, which
-// lowers to ds_bpermute: an LDS round trip per step, six dependent ones per reduction.
-template <int CTRL, int ROW_MASK = 0xF>
-__device__ __forceinline__ float dppf(float v, float old) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(v), CTRL, ROW_MASK, 0xF, false));
-}
-__device__ __forceinline__ float wave_max_dpp(float v) {  // every lane gets the wave maximum
-  v = fmaxf(v, dppf<0xB1>(v, -INFINITY));        // quad_perm [1,0,3,2]
-  v = fmaxf(v, dppf<0x4E>(v, -INFINITY));        // quad_perm [2,3,0,1]
-  v = fmaxf(v, dppf<0x141>(v, -INFINITY));       // row_half_mirror
-  v = fmaxf(v, dppf<0x140>(v, -INFINITY));       // row_mirror: each row of 16 holds its max
-  v = fmaxf(v, dppf<0x142, 0xA>(v, -INFINITY));  // row_bcast15 into rows 1, 3
-  v = fmaxf(v, dppf<0x143, 0xC>(v, -INFINITY));  // row_bcast31 into rows 2, 3: lane 63 = total
-  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
-}
-__device__ __forceinline__ float wave_sum_dpp(float v) {
-  v += dppf<0xB1>(v, 0.f);
-  v += dppf<0x4E>(v, 0.f);
-  v += dppf<0x141>(v, 0.f);
-  v += dppf<0x140>(v, 0.f);
-  v += dppf<0x142, 0xA>(v, 0.f);
-  v += dppf<0x143, 0xC>(v, 0.f);
-  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
-}
+// Wave reductions / scans: DPP lane moves (common.h), no ds_bpermute round trips.
 __device__ __forceinline__ float wave_incl_scan_dpp(float v) {  // inclusive prefix sum over the lanes
   v += dppf<0x111>(v, 0.f);        // row_shr:1
   v += dppf<0x112>(v, 0.f);        // row_shr:2
@@ -122,7 +98,7 @@ __device__ __forceinline__ float wave_incl_scan_dpp(float v) {  // inclusive pre
 
 template <int CTRL, int ROW_MASK = 0xF>
 __device__ __forceinline__ unsigned dppu(unsigned v) {  // identity 0 for unsigned max
-  return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROW_MASK, 0xF, false);
+  return dpp_u32<CTRL, ROW_MASK>(0u, v);
 }
 __device__ __forceinline__ unsigned wave_umax_dpp(unsigned v) {
   v = max(v, dppu<0xB1>(v));
@@ -176,7 +152,7 @@ __device__ __forceinline__ int wave_rank_desc(unsigned key, unsigned idx, bool a
 // Block max / sum over SB threads: DPP wave reductions, then every lane reads the 16 wave totals
 // with four 16-B LDS reads.
 __device__ __forceinline__ float sb_max(float v, float* red) {
-  v = wave_max_dpp(v);
+  v = wave_max(v);
   __syncthreads();
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
   __syncthreads();
@@ -188,7 +164,7 @@ __device__ __forceinline__ float sb_max(float v, float* red) {
   return t;
 }
 __device__ __forceinline__ float sb_sum(float v, float* red) {
-  v = wave_sum_dpp(v);
+  v = wave_sum(v);
   __syncthreads();
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
   __syncthreads();

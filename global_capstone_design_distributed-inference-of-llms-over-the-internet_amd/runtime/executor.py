@@ -702,9 +702,16 @@ class StageExecutor:
         S = last_rows.numel()
         V = cfg.vocab_size
         if w.lm_head_p is not None and self._head_packed_ok(S):
-            fn = ops.rmsnorm(hout, w.final_norm, eps, out=e("fn_p", (ops.packed_numel(S, H),)), rows=last_rows,
-                             packed=True)
             Vp = 16 * w.lm_head_p.shape[0]
+            if w.lm_head_folded and mlp is None and S == T:
+                # fused-norm path, every row a last row (decode): lm_head (final norm folded in)
+                # reads the packed residual stream the last down GEMM left in ``xr`` and scales
+                # each row by its rsqrt(mean r^2 + eps) from ``ss_in`` - no final norm launch
+                logits = ops.linear(xr, None, out=e("logits", (S, Vp)), wp=w.lm_head_p, a_rows=S, ss_in=ss_in,
+                                    eps=eps)
+                return logits[:, :V]
+            fn = ops.rmsnorm(hout, self._unit_norm() if w.lm_head_folded else w.final_norm, eps,
+                             out=e("fn_p", (ops.packed_numel(S, H),)), rows=last_rows, packed=True)
             logits = ops.linear(fn, None, out=e("logits", (S, Vp)), wp=w.lm_head_p, a_rows=S)
             return logits[:, :V]
         fn = ops.rmsnorm(hout, w.final_norm, eps, out=e("fn", (S, H)), rows=last_rows)

@@ -291,7 +291,7 @@ def main(argv=None):
                          "recorded in the decode graphs (rccl + graph hop) whenever the headline ran on "
                          "ProcessGroupNCCL with >= 2 stages; reported under 'phase2' (ok or the failure reason), "
                          "never replacing the headline value")
-    ap.add_argument("--phase2-timeout", type=float, default=240.0,
+    ap.add_argument("--phase2-timeout", type=float, default=180.0,
                     help="wall-clock bound of the second phase: past it every rank leaves (rank 0 printing the "
                          "headline line with phase2 = timeout)")
     ap.add_argument("--phase2-hop-timeout", type=float, default=60.0,

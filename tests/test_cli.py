@@ -116,3 +116,31 @@ def test_lb_swarm_recipe(tmp_path):
     spans = sorted(set(__import__("re").findall(r"Selected blocks \[(\d+), (\d+)\)", r.stdout)))
     assert spans == [("1", "2"), ("2", "3"), ("3", "4")], r.stdout
     assert "GENERATED:" in r.stdout
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_run_all_launcher_on_gpu_matches_single_process(tmp_path):
+    """The reference's main flow on the GPU: two stage servers and the CLI client (stage 0) as
+    separate processes on cuda:0 (all stages on one node: the client opens a device channel to
+    them), greedy decoding; the text is a prefix of the single-process generator's
+    (scripts/single_gpu_check.py, the reference's S4 tool) for the same synthetic weights - the
+    CLI stops early on repeated tokens, as the reference client does (src/main.py:160-204).  Synthetic weights are
+    seeded per device (the CUDA generator is not the CPU one), so GPU runs compare with GPU runs.
+    Reference flow: src/main.py:776-819, scripts/run_all.py; single-GPU check:
+    scripts/single_gpu_check.py."""
+    import ast
+    import re
+
+    ref = subprocess.run([sys.executable, "scripts/single_gpu_check.py", "--model", "small-llama", "--max_new_tokens",
+                          "12", "--device", "cuda"], cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert ref.returncode == 0, ref.stderr[-3000:]
+    want = ast.literal_eval(re.search(r"Generated: (.*)", ref.stdout).group(1))
+    r = subprocess.run([sys.executable, "scripts/run_all.py", "--model", "small-llama", "--splits", "2,4", "--gpus",
+                        "--max_new_tokens", "12", "--base_port", "29890", "--log_dir", str(tmp_path),
+                        "--extra", "--kv_cache_gb 1"], cwd=ROOT, capture_output=True, text=True, timeout=540)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+    assert "TTFT" in r.stdout and ("device channel" in r.stdout or "hop mini_petals:stage2" in r.stdout), \
+        r.stdout[-3000:]
+    got = re.search(r"GENERATED: (.*?)\n={10,}", r.stdout, re.S).group(1)
+    assert got and want.startswith(got), (got, want)

@@ -135,7 +135,7 @@ _SK_CHOICE = {}  # (m_bucket, N, K, epilogue) -> kernel name (see _KERNEL_FLAGS)
 # in-launch combine "rwki" (the last arriving split sums the slabs), and the row-split ring "rwr"
 # (a pair of workgroups per column group, half the rows each: no K split, no combine)
 _KERNEL_FLAGS = {"pk": 0, "sk": 4, "lds22": 16, "lds24": 16 | 32, "lds42": 16 | 96, "rw": 128, "rwk": 256,
-                 "rwki": 256 | 512, "rwr": 4096}
+                 "rwki": 256 | 512, "rwr": 4096, "t2d": 32768}
 _LDS_CFG = {"lds22": (2, 2), "lds24": (2, 4), "lds42": (4, 2)}
 # "<kernel>+r": the same kernel with every workgroup's k walk rotated (csrc/gemm_kernels.h
 # rw_krot, flags bit 10) - kept by the autotuners per shape only where it measures faster
@@ -210,6 +210,8 @@ def _covered(name: str, M: int, N: int, K: int, epilogue: int) -> bool:
         return epilogue != 1 and N % 2048 == 0 and M <= 64
     if name == "rwr":  # row-split ring: 2 or 4 row tiles split over a workgroup pair
         return epilogue != 1 and N % 2048 == 0 and (M + 15) // 16 in (2, 4)
+    if name == "t2d":  # row blocks x column groups: more than 64 rows only (picked by linear itself)
+        return 64 < M <= 256 and t2d_ok(M, N, K, epilogue, epilogue == 1)
     return _lds_covered(name, M, N, K, epilogue)
 
 
@@ -759,7 +761,10 @@ _RW_OK = {}
 
 def wide_gemm_ok(M: int, N: int, K: int, epilogue: int = 0, out_packed: bool = False) -> bool:
     """65..256 decode rows: the balanced ring kernel covers (packed A; epilogue 0 or packed SwiGLU,
-    the widths it is built for; 129..256 rows at 12 / 16 row tiles)."""
+    the widths it is built for; 129..256 rows at 12 / 16 row tiles) - or, from ``T2D_MIN`` rows
+    up, the two-dimensionally tiled kernel (every decode epilogue)."""
+    if t2d_rows(M):
+        return t2d_ok(M, N, K, epilogue, out_packed)
     key = (M, N, K, int(epilogue), bool(out_packed))
     if key not in _RW_OK:
         _RW_OK[key] = bool(native_available() and
@@ -773,12 +778,34 @@ def wide_gemm_ok(M: int, N: int, K: int, epilogue: int = 0, out_packed: bool = F
 # whole 256-row activation block, 5x its weight bytes) - so 128 stays the default split;
 # MPAMD_WIDE_ROWS=256 turns them on above it.
 WIDE_ROWS = int(os.environ.get("MPAMD_WIDE_ROWS", "128"))
+# Decode rows from which the two-dimensionally tiled kernel (csrc/gemm_t2d.h: row blocks x column
+# groups, both operands shared through LDS) runs every projection of the packed / fused-norm path,
+# up to 256 (MPAMD_T2D_MIN; 257 = never).
+T2D_MIN = int(os.environ.get("MPAMD_T2D_MIN", "257"))
+_T2D_OK = {}
+
+
+def t2d_rows(M: int) -> bool:
+    return max(T2D_MIN, 65) <= M <= 256
+
+
+def wide_rows() -> int:
+    """Largest decode row count the packed (hand-written GEMM) path takes."""
+    return 256 if T2D_MIN <= 256 else WIDE_ROWS
+
+
+def t2d_ok(M: int, N: int, K: int, epilogue: int = 0, out_packed: bool = False) -> bool:
+    key = (M, N, K, int(epilogue), bool(out_packed))
+    if key not in _T2D_OK:
+        _T2D_OK[key] = bool(native_available() and
+                            torch.ops.mpamd.gemm_t2d_ok(int(M), int(N), int(K), int(epilogue), int(bool(out_packed))))
+    return _T2D_OK[key]
 
 
 def native_gemm_ok(M: int, N: int, K: int, epilogue: int = 0, out_packed: bool = False) -> bool:
     if not (K % 128 == 0 and N % (32 if epilogue == 1 else 16) == 0):
         return False
-    if 64 < M <= WIDE_ROWS:
+    if 64 < M <= wide_rows():
         return wide_gemm_ok(M, N, K, epilogue, out_packed)
     return 0 < M <= 64
 
@@ -834,12 +861,14 @@ def linear(x, w, out=None, epilogue=0, residual=None, policy=None, wp=None, a_ro
                    else torch.empty(M, ncols, dtype=x.dtype, device=x.device))
         if gate is not None:
             kern = "pk"
+        elif M > 64 and t2d_rows(M) and t2d_ok(M, N, K, epilogue, out_packed):
+            kern = "t2d"  # row blocks x column groups (129..256 rows)
         elif M > 64:  # 65..256 rows: split-K ring where it applies (o, down), else the ring kernel
             kern = "rwk" if (not out_packed and _covered("rwk", M, N, K, epilogue)) else "rw"
         else:
             kern = _kernel_for(M, N, K, epilogue)
         flags = 1 | (2 if out_packed else 0) | _kflags(kern)
-        ws = gemm_workspace(x.device) if _base(kern) in ("sk", "rwk", "rwki") else None
+        ws = gemm_workspace(x.device) if _base(kern) in ("sk", "rwk", "rwki", "t2d") else None
         torch.ops.mpamd.gemm(x, wp, out, residual, int(epilogue), M, flags, ws, gate, ap_out, ss_out, ss_zero, ss_in,
                              1.0 / K, float(eps))
         return out

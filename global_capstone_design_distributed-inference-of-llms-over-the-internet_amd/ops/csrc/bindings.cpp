@@ -51,6 +51,7 @@ int64_t mp_gemm_slab_offset();
 int64_t mp_gemm_slab_bytes();
 void mp_fp8_set_kernel(int kind);
 int mp_gemm_rw_ok(int M, int N, int K, int epilogue, int out_packed);
+int mp_gemm_t2d_ok(int M, int N, int K, int epilogue, int out_packed, int with_ws);
 int mp_quant_rows_fp8(const void* x, int64_t xs, void* a8, float* scale, int M, int K, hipStream_t stream);
 int mp_gemm_bf16(const void* x, int64_t x_stride, const void* w, void* y, int64_t y_stride, const void* res,
                  int64_t res_stride, int M, int N, int K, int epilogue, int flags, void* ws, const int* gate,
@@ -626,6 +627,10 @@ int64_t gemm_rwk_split(int64_t M, int64_t N, int64_t K, int64_t f8) {
   return mp_gemm_rwk_split((int)M, (int)N, (int)K, (int)f8);
 }
 void fp8_gemm_kernel(int64_t kind) { mp_fp8_set_kernel((int)kind); }
+bool gemm_t2d_ok(int64_t M, int64_t N, int64_t K, int64_t epilogue, int64_t out_packed) {
+  return mp_gemm_t2d_ok((int)M, (int)N, (int)K, (int)epilogue, (int)out_packed, 1) != 0;
+}
+
 bool gemm_rw_ok(int64_t M, int64_t N, int64_t K, int64_t epilogue, int64_t out_packed) {
   return mp_gemm_rw_ok((int)M, (int)N, (int)K, (int)epilogue, (int)out_packed) != 0;
 }
@@ -710,6 +715,7 @@ TORCH_LIBRARY(mpamd, m) {
   m.def("gemm_rwk_split(int M, int N, int K, int f8) -> int", &gemm_rwk_split);
   m.def("fp8_gemm_kernel(int kind) -> ()", &fp8_gemm_kernel);
   m.def("gemm_rw_ok(int M, int N, int K, int epilogue, int out_packed) -> bool", &gemm_rw_ok);
+  m.def("gemm_t2d_ok(int M, int N, int K, int epilogue, int out_packed) -> bool", &gemm_t2d_ok);
   m.def(
       "rmsnorm(Tensor x, Tensor(a!) residual, Tensor w, Tensor(b!) y, float eps, int mode, Tensor? rows, "
       "int packed, Tensor(c!)? ss=None, Tensor(d!)? a8=None, Tensor(e!)? a8_scale=None) -> ()");

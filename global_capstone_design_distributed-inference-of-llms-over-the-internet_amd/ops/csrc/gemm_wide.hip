@@ -3,13 +3,20 @@
 // rows run the 12- or 16-row-tile instantiation over the activation's own row tiles (the packed
 // layout's tile count is a runtime stride; tiles past it are masked rows).  Above ops.WIDE_ROWS
 // (128 by default) the decode step stays on hipBLASLt, which measured faster there (profiles/r4d).
-#include "gemm_kernels.h"
+#include "gemm_t2d.h"
 
 extern "C" int mp_gemm_bf16_wide(const void* x, const void* w, void* y, int64_t y_stride, const void* res,
                                  int64_t res_stride, int M, int N, int K, int epilogue, int flags, void* ws,
                                  const mp::EpiArgs& ep, hipStream_t stream) {
   using namespace mp;
   int rc = 1;
+  if (flags & 32768) {  // two-dimensionally tiled form (gemm_t2d.h); bits 16-17: forced k split
+    rc = launch_gemm_t2d(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, ep, ws, stream,
+                         (flags >> 16) & 3);
+    if (rc == 1 && ((flags >> 16) & 3)) return -7;  // a forced split this shape does not take (lab)
+    if (rc < 0) return rc;
+    if (rc == 0) return (int)hipGetLastError();
+  }
   if ((flags & 256) && !(flags & 2) && ws != nullptr) {  // split-K ring
 #define MP_RWK(MT_) \
   rc = launch_gemm_rwk<MT_>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, ep, ws, stream, rwk_comb(flags))
@@ -33,6 +40,16 @@ extern "C" int mp_gemm_bf16_wide(const void* x, const void* w, void* y, int64_t 
   else rc = launch_gemm_rw<16>(x, w, y, y_stride, res, res_stride, M, N, K, epilogue, flags, ep, stream);
   if (rc != 0) return rc < 0 ? rc : -1;
   return (int)hipGetLastError();
+}
+
+// 1 if the two-dimensionally tiled form covers this shape (flags as mp_gemm_bf16; no launch).
+extern "C" int mp_gemm_t2d_ok(int M, int N, int K, int epilogue, int out_packed, int with_ws) {
+  using namespace mp;
+  EpiArgs ep{};
+  ep.mt_out = (M + 15) / 16;
+  char dummy = 0;
+  return launch_gemm_t2d(nullptr, nullptr, nullptr, 0, nullptr, 0, M, N, K, epilogue, 1 | (out_packed ? 2 : 0), ep,
+                         with_ws ? &dummy : nullptr, 0, 0, true) == 0;
 }
 
 // 1 if mp_gemm_bf16 covers a packed-activation decode GEMM of M = 65..256 rows (balanced ring

@@ -965,7 +965,7 @@ class StageExecutor:
         projection with its fused epilogue - qkv and gate/up consume the row statistics
         (balanced ring or split-K ring + reduce), o and down produce them (split-K ring, the
         reduce launch applies the residual / packed copy / statistics epilogue)."""
-        if not 64 < M <= ops.WIDE_ROWS or self.device.type != "cuda" or not self._packed_ok(M):
+        if not 64 < M <= ops.wide_rows() or self.device.type != "cuda" or not self._packed_ok(M):
             return False
         cfg = self.cfg
         H, F = cfg.hidden_size, cfg.intermediate_size
@@ -986,7 +986,7 @@ class StageExecutor:
     def _packed_ok(self, M: int) -> bool:
         """Packed-activation decode path: GPU, native GEMM allowed, all projections packed; 65..256
         rows when the balanced ring kernel covers every projection of the layer (dense Llama)."""
-        if self.device.type != "cuda" or ops.gemm_policy() == "hipblaslt" or not 0 < M <= ops.WIDE_ROWS:
+        if self.device.type != "cuda" or ops.gemm_policy() == "hipblaslt" or not 0 < M <= ops.wide_rows():
             return False
         if getattr(self, "_packed_ready", None) is None:
             cfg = self.cfg

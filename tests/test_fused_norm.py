@@ -193,14 +193,65 @@ def test_wide_ring_in_kernel_epilogues(M, monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("M", [129, 200, 256])
+@pytest.mark.parametrize("dims", [(2048, 2048, 2048), (4096, 12288, 11008)])
+def test_t2d_consumers_and_producers(M, dims, monkeypatch):
+    """The two-dimensionally tiled kernel (csrc/gemm_t2d.h) at 129..256 rows, every decode
+    epilogue against fp32 oracles: the row-scaled consumer (qkv), the row-scaled packed SwiGLU
+    (gate/up: 12- and 10-tile column groups at F = 11008), the residual-stream producer straight
+    from the accumulators (o) and as split-K slabs + the reduce launch (down, K = 11008)."""
+    monkeypatch.setattr(ops, "T2D_MIN", 129)
+    dev = "cuda"
+    H, Nq, F = dims
+    g = torch.Generator(device=dev).manual_seed(1300 + M + H)
+    for N, K, epi, pk in ((Nq, H, 0, False), (2 * F, H, 1, True), (H, H, 3, False), (H, F, 3, False)):
+        assert ops.t2d_ok(M, N, K, epi, pk), (N, K, epi)
+    x = (torch.randn(M, H, device=dev, generator=g) * 0.7).to(torch.bfloat16)
+    gw = (torch.rand(H, device=dev, generator=g) + 0.5).to(torch.bfloat16)
+    ss = ops.norm_stats_buffer(dev)[0] + 3
+    res = torch.empty_like(x)
+    xp = torch.zeros(ops.packed_numel(M, H), dtype=torch.bfloat16, device=dev)
+    ops.rmsnorm(x, gw, EPS, out=xp, residual=res, mode=3, packed=True, ss=ss)
+    xn = _rms_ref(x, gw).float()
+    sd = 0.03 * (1024 / H) ** 0.5  # outputs of the size the K = 1024 tests above see
+    w = (torch.randn(Nq, H, device=dev, generator=g) * sd).to(torch.bfloat16)
+    wp = ops.pack_weight((w.float() * gw.float()[None, :]).to(torch.bfloat16).contiguous())
+    y = ops.linear(xp, None, wp=wp, a_rows=M, ss_in=ss, eps=EPS)
+    torch.testing.assert_close(y.float(), xn @ w.float().t(), atol=3e-2, rtol=3e-2)
+    wgu = (torch.randn(2 * F, H, device=dev, generator=g) * sd).to(torch.bfloat16)
+    wgup = ops.pack_weight((wgu.float() * gw.float()[None, :]).to(torch.bfloat16).contiguous())
+    act = torch.zeros(ops.packed_numel(M, F), dtype=torch.bfloat16, device=dev)
+    ops.linear(xp, None, out=act, epilogue=1, wp=wgup, a_rows=M, out_packed=True, ss_in=ss, eps=EPS)
+    exp = ref.swiglu((xn @ wgu.float().t()).to(torch.bfloat16)).float()
+    torch.testing.assert_close(ref.unpack_act(act, M, F).float(), exp, atol=5e-2, rtol=3e-2)
+    for K in (H, F):  # o (direct producer epilogue), down (split-K slabs + reduce)
+        a = (torch.randn(M, K, device=dev, generator=g) * 0.5).to(torch.bfloat16)
+        wo = (torch.randn(H, K, device=dev, generator=g) * 0.03 * (2048 / K) ** 0.5).to(torch.bfloat16)
+        r = torch.randn(M, H, device=dev, generator=g).to(torch.bfloat16)
+        r0 = r.clone()
+        ap = torch.zeros(ops.packed_numel(M, H), dtype=torch.bfloat16, device=dev)
+        sso, ssz = ops.norm_stats_buffer(dev)[0], ops.norm_stats_buffer(dev)[0] + 7
+        ops.linear(ops.pack_act(a), None, out=r, epilogue=3, residual=r, wp=ops.pack_weight(wo), a_rows=M,
+                   ap_out=ap, ss_out=sso, ss_zero=ssz)
+        exp = (r0.float() + (a.float() @ wo.float().t()).to(torch.bfloat16).float()).to(torch.bfloat16)
+        torch.testing.assert_close(r.float(), exp.float(), atol=2e-2, rtol=2e-2)
+        assert torch.equal(ref.unpack_act(ap, M, H), r)
+        assert torch.equal(sso.sum(0)[:M].cpu(), ref.fx_sumsq(r.cpu()))
+        assert int(ssz.abs().sum()) == 0
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("graphs", [False, True])
 @pytest.mark.parametrize("n", [100, 200])
-def test_fused_executor_wide_batch_matches_unfused(graphs, n, monkeypatch):
-    """A 100- / 200-session decode step takes the fused-norm path (wide kernels) and matches the
-    unfused packed path step by step."""
+@pytest.mark.parametrize("t2d", [False, True])
+def test_fused_executor_wide_batch_matches_unfused(graphs, n, t2d, monkeypatch):
+    """A 100- / 200-session decode step takes the fused-norm path (wide kernels; with ``t2d`` the
+    two-dimensionally tiled kernel from 129 rows) and matches the unfused packed path step by step."""
     import dataclasses
 
     monkeypatch.setattr(ops, "WIDE_ROWS", 256)
+    if t2d:
+        monkeypatch.setattr(ops, "T2D_MIN", 129)
 
     from src.models.config import resolve_model
     from src.models.weights import random_stage_weights

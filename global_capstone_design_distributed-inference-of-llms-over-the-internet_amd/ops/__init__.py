@@ -772,16 +772,19 @@ def wide_gemm_ok(M: int, N: int, K: int, epilogue: int = 0, out_packed: bool = F
     return _RW_OK[key]
 
 
-# decode rows the hand-written GEMMs take.  The ring / split-K ring kernels are built and tested up
-# to 256 rows (12 / 16 row tiles), but at 256 sessions they measured slower than hipBLASLt + the
-# unfused path (11.18 vs ~9.5 ms/step, profiles/r4d: one column group per workgroup takes in the
-# whole 256-row activation block, 5x its weight bytes) - so 128 stays the default split;
-# MPAMD_WIDE_ROWS=256 turns them on above it.
+# decode rows the ring kernels take.  They are built and tested up to 256 rows (12 / 16 row tiles),
+# but at 256 sessions they measured slower than hipBLASLt + the unfused path (11.18 vs ~9.5
+# ms/step, profiles/r4d: one column group per workgroup takes in the whole 256-row activation
+# block, 5x its weight bytes); MPAMD_WIDE_ROWS=256 turns them on above 128.
 WIDE_ROWS = int(os.environ.get("MPAMD_WIDE_ROWS", "128"))
 # Decode rows from which the two-dimensionally tiled kernel (csrc/gemm_t2d.h: row blocks x column
 # groups, both operands shared through LDS) runs every projection of the packed / fused-norm path,
-# up to 256 (MPAMD_T2D_MIN; 257 = never).
-T2D_MIN = int(os.environ.get("MPAMD_T2D_MIN", "257"))
+# up to 256 (MPAMD_T2D_MIN; 257 = never: hipBLASLt + the unfused path above WIDE_ROWS).  Measured
+# on the whole decode step against hipBLASLt (profiles/r5x): 136 / 160 / 192 / 224 / 256 sessions
+# 7.49 / 7.85 / 8.35 / 8.95 / 9.53 ms vs 7.61 / 8.91 / 10.01 / 9.37 / 9.78.
+T2D_MIN = int(os.environ.get("MPAMD_T2D_MIN", "129"))
+# its operand stages arrive by LDS-DMA (global_load_lds) instead of a register ring + ds_write
+T2D_GL = os.environ.get("MPAMD_T2D_GL", "1") == "1"
 _T2D_OK = {}
 
 
@@ -867,7 +870,7 @@ def linear(x, w, out=None, epilogue=0, residual=None, policy=None, wp=None, a_ro
             kern = "rwk" if (not out_packed and _covered("rwk", M, N, K, epilogue)) else "rw"
         else:
             kern = _kernel_for(M, N, K, epilogue)
-        flags = 1 | (2 if out_packed else 0) | _kflags(kern)
+        flags = 1 | (2 if out_packed else 0) | _kflags(kern) | (262144 if kern == "t2d" and T2D_GL else 0)
         ws = gemm_workspace(x.device) if _base(kern) in ("sk", "rwk", "rwki", "t2d") else None
         torch.ops.mpamd.gemm(x, wp, out, residual, int(epilogue), M, flags, ws, gate, ap_out, ss_out, ss_zero, ss_in,
                              1.0 / K, float(eps))

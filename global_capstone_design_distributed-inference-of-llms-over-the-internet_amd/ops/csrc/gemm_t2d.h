@@ -31,17 +31,27 @@
 
 namespace mp {
 
-constexpr int T2D_KU = 2;  // k-slices per stage (64 k): one barrier per 2 x 8 or 2 x 12 MFMA rounds
+// LDS budget of one workgroup: the staging buffers + the RowScale scratch, in ONE __shared__ array
+// (guide §5 trap (a): a second __shared__ object beside an LDS-DMA staging array can make hipcc
+// wait vmcnt(0) before every k-step's first ds_read).
+constexpr int T2D_SS_BYTES = SS_PG * SS_ROWS * 8 + SS_ROWS * 4;
+constexpr int T2D_LDS_BYTES = 160 * 1024;
 
-template <int MW, int NW, int WM, int WN, int D>
+// KU: k-slices (of 32) per stage.  GL: stages arrive by LDS-DMA (global_load_lds_dwordx4) into a
+// P-slot LDS ring instead of through a D-deep register ring and ds_write.
+template <int MW, int NW, int WM, int WN, int D, int KU, bool GL>
 struct T2dGeom {
   static constexpr int BMT = WM * MW;                    // row tiles per block
   static constexpr int NBMAX = WN * NW;                  // column tiles per block (at most)
-  static constexpr int FA = BMT * T2D_KU;                // activation fragments per stage
-  static constexpr int FMAX = FA + NBMAX * T2D_KU;       // fragments per stage (at most)
+  static constexpr int FA = BMT * KU;                    // activation fragments per stage
+  static constexpr int FMAX = FA + NBMAX * KU;           // fragments per stage (at most)
   static constexpr int J = (FMAX + 7) / 8;               // fragment loads per wave per stage
   static constexpr int STAGE_BYTES = FMAX * 1024;
+  static constexpr int PMAX = (T2D_LDS_BYTES - T2D_SS_BYTES) / STAGE_BYTES;
+  static constexpr int P = GL ? (PMAX > 6 ? 6 : PMAX) : 2;  // LDS stages
+  static constexpr int LDS_BYTES = P * STAGE_BYTES + T2D_SS_BYTES;
   static_assert(WM * WN == 8, "8 waves per workgroup");
+  static_assert(!GL || (P >= 3 && J * (P - 2) <= 63), "LDS-DMA ring: 3+ stages, vmcnt is 6 bits");
 };
 
 // blockIdx -> (column group, row block, k split): the MB x S blocks of one column group share
@@ -61,18 +71,23 @@ __device__ __forceinline__ void t2d_place(int MB, int S, int& cg, int& mb, int& 
   sp = u - mb * S;
 }
 
-template <int MW, int NW, int WM, int WN, int D, int EPI, bool OPK, bool SPLIT>
+template <int N>
+__device__ __forceinline__ void t2d_wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int MW, int NW, int WM, int WN, int D, int KU, bool GL, int EPI, bool OPK, bool SPLIT>
 __global__ __launch_bounds__(512) void gemm_t2d_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ wp,
                                                        bf16_t* __restrict__ y, int64_t ys,
                                                        const bf16_t* __restrict__ res, int64_t rs,
                                                        float* __restrict__ part, int M, int N, int K, int MB, int S,
                                                        int nbig, int NBB, int NBS, const EpiArgs ep) {
-  using G = T2dGeom<MW, NW, WM, WN, D>;
-  constexpr int KU = T2D_KU, BMT = G::BMT, FA = G::FA, J = G::J;
+  using G = T2dGeom<MW, NW, WM, WN, D, KU, GL>;
+  constexpr int BMT = G::BMT, FA = G::FA, J = G::J, P = G::P, SB = G::STAGE_BYTES;
   clear_other(ep);
-  __shared__ u64 rs_part[SS_PG][SS_ROWS];
-  __shared__ float rs_lds[SS_ROWS];
-  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * G::STAGE_BYTES];
+  __shared__ __attribute__((aligned(16))) unsigned char smem[G::LDS_BYTES];
+  auto* rs_part = reinterpret_cast<u64(*)[SS_ROWS]>(smem + P * SB);
+  float* rs_lds = reinterpret_cast<float*>(smem + P * SB + SS_PG * SS_ROWS * 8);
   RowScale<(EPI < 2) && !SPLIT> rsc;
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wid % WM, wn = wid / WM;
@@ -111,7 +126,8 @@ __global__ __launch_bounds__(512) void gemm_t2d_kernel(const bf16_t* __restrict_
   const int ntw = min(NW, ntl - wn * NW);                  // column tiles of this wave (may be <= 0)
   const int mtw = min(MW, mto - (mt0 + wm * MW));          // row tiles of this wave
 
-  // EPI 3: this wave's residual quads, in flight during the main loop
+  // loads whose results are used only after the loop go first (vmcnt retires in issue order: the
+  // ring's counted waits never wait for them).  EPI 3: this wave's residual quads.
   u16x4 rpre[MW][NW];
   if constexpr (EPI == 3 && !SPLIT) {
 #pragma unroll
@@ -124,6 +140,7 @@ __global__ __launch_bounds__(512) void gemm_t2d_kernel(const bf16_t* __restrict_
           rpre[mt][t][r] = res[(int64_t)min((mt0 + wm * MW + mt) * 16 + (lane >> 4) * 4 + r, M - 1) * rs + col];
       }
   }
+  rsc.load(ep, wp);
 
   f32x4 acc[MW][NW];
 #pragma unroll
@@ -131,21 +148,11 @@ __global__ __launch_bounds__(512) void gemm_t2d_kernel(const bf16_t* __restrict_
 #pragma unroll
     for (int t = 0; t < NW; ++t) acc[mt][t] = (f32x4)(0.f);
 
-  u16x8 stg[D][J];
-#define T2D_LOAD(d, st)                                                                                  \
+  // compute one stage from LDS stage buffer at byte offset ``off`` (every tile of the wave: tiles
+  // past the block's rows / columns compute on stale LDS and are never stored - no per-MFMA branches)
+#define T2D_MMA(off)                                                                                     \
   {                                                                                                      \
-    const int64_t s_ = min(st, n - 1);                                                                   \
-    _Pragma("unroll") for (int j = 0; j < J; ++j) stg[d][j] =                                         \
-        *reinterpret_cast<__attribute__((address_space(1))) const u16x8*>(gp[j] + s_ * ginc[j]);          \
-  }
-#define T2D_STORE(d, buf)                                                                                \
-  _Pragma("unroll") for (int j = 0; j < J; ++j) *reinterpret_cast<u16x8*>(                              \
-      smem + (buf) * G::STAGE_BYTES + slot[j] * 1024 + lane * 16) = stg[d][j];
-  // compute one stage from LDS buffer ``buf`` (every tile of the wave: tiles past the block's
-  // rows / columns compute on stale LDS and are never stored - no per-MFMA branches)
-#define T2D_MMA(buf)                                                                                     \
-  {                                                                                                      \
-    const unsigned char* sb_ = smem + (buf) * G::STAGE_BYTES + lane * 16;                               \
+    const unsigned char* sb_ = smem + (off) + lane * 16;                                                 \
     u16x8 a_[KU][MW], b_[KU][NW];                                                                        \
     _Pragma("unroll") for (int u = 0; u < KU; ++u) {                                                     \
       _Pragma("unroll") for (int mt = 0; mt < MW; ++mt) a_[u][mt] =                                      \
@@ -157,30 +164,66 @@ __global__ __launch_bounds__(512) void gemm_t2d_kernel(const bf16_t* __restrict_
         _Pragma("unroll") for (int t = 0; t < NW; ++t) acc[mt][t] = mfma16(a_[u][mt], b_[u][t], acc[mt][t]); \
   }
 
+  if constexpr (GL) {
+    // LDS-DMA ring of P stages: stage s lives in slot s % P.  At step s: wait for this wave's part
+    // of stage s (counted: the P - 2 younger stages stay in flight), barrier (everyone's part of
+    // stage s landed, everyone finished step s - 1), refill the slot step s - 1 used with stage
+    // s + P - 1, compute stage s.  The LDS image of a fragment is lane-linear (64 lanes x 16 B),
+    // exactly what one global_load_lds_dwordx4 writes.
+    typedef __attribute__((address_space(3))) void* lptr_t;
+    auto issue = [&](int sl, int st) {
+      const int64_t s_ = min(st, n - 1);
 #pragma unroll
-  for (int d = 0; d < D; ++d) T2D_LOAD(d, d)
-  rsc.load(ep, wp);
-  T2D_STORE(0, 0)
-  T2D_LOAD(0, D)
-  lds_barrier();
-  // invariant at the top of step s: LDS buffer s & 1 holds stage s; the ring holds stages
-  // s + 1 .. s + D (slot (s + 1) % D is the oldest)
-  for (int s0 = 0; s0 < n; s0 += D) {
+      for (int j = 0; j < J; ++j)
+        __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) const void*)(gp[j] + s_ * ginc[j]),
+                                         (lptr_t)(smem + sl * SB + slot[j] * 1024), 16, 0, 0);
+    };
 #pragma unroll
-    for (int d = 0; d < D; ++d) {
-      const int s = s0 + d;
-      if (s >= n) break;
-      // D even: the LDS buffer of step s is d & 1
-      T2D_MMA(d & 1)
-      // (at s = n - 1 this stages a clamped copy nobody reads: no branch around the ring)
-      T2D_STORE((d + 1) % D, (d + 1) & 1)
-      T2D_LOAD((d + 1) % D, s + 1 + D)
+    for (int p = 0; p < P - 1; ++p) issue(p, p);
+    int cur = 0;  // slot of stage s
+    for (int s = 0; s < n; ++s) {
+      t2d_wait_vm<J * (P - 2)>();
       lds_barrier();
+      issue(cur == 0 ? P - 1 : cur - 1, s + P - 1);
+      T2D_MMA(cur * SB)
+      cur = cur + 1 == P ? 0 : cur + 1;
     }
+    t2d_wait_vm<0>();  // the clamped refills of the last steps
+  } else {
+    u16x8 stg[D][J];
+#define T2D_LOAD(d, st)                                                                                  \
+  {                                                                                                      \
+    const int64_t s_ = min(st, n - 1);                                                                   \
+    _Pragma("unroll") for (int j = 0; j < J; ++j) stg[d][j] =                                            \
+        *reinterpret_cast<__attribute__((address_space(1))) const u16x8*>(gp[j] + s_ * ginc[j]);          \
   }
-#undef T2D_MMA
+#define T2D_STORE(d, buf)                                                                                \
+  _Pragma("unroll") for (int j = 0; j < J; ++j) *reinterpret_cast<u16x8*>(                              \
+      smem + (buf) * SB + slot[j] * 1024 + lane * 16) = stg[d][j];
+#pragma unroll
+    for (int d = 0; d < D; ++d) T2D_LOAD(d, d)
+    T2D_STORE(0, 0)
+    T2D_LOAD(0, D)
+    lds_barrier();
+    // invariant at the top of step s: LDS buffer s & 1 holds stage s; the ring holds stages
+    // s + 1 .. s + D (slot (s + 1) % D is the oldest)
+    for (int s0 = 0; s0 < n; s0 += D) {
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        const int s = s0 + d;
+        if (s >= n) break;
+        // D even: the LDS buffer of step s is d & 1
+        T2D_MMA((d & 1) * SB)
+        // (at s = n - 1 this stages a clamped copy nobody reads: no branch around the ring)
+        T2D_STORE((d + 1) % D, (d + 1) & 1)
+        T2D_LOAD((d + 1) % D, s + 1 + D)
+        lds_barrier();
+      }
+    }
 #undef T2D_STORE
 #undef T2D_LOAD
+  }
+#undef T2D_MMA
 
   if constexpr (SPLIT) {
     float* slab = part + (int64_t)sp * M * N;
@@ -215,12 +258,12 @@ __global__ __launch_bounds__(512) void gemm_t2d_kernel(const bf16_t* __restrict_
 // Geometry chooser + launcher.  Returns 1 (caller falls back) when the shape is not covered.
 // ``S_force`` > 0 forces the k split (lab); 0 picks (t2d_pick_split).
 // ``dry``: only report coverage.
-template <int MW, int NW, int WM, int WN, int D>
+template <int MW, int NW, int WM, int WN, int D, int KU, bool GL>
 static int launch_t2d_cfg(const void* x, const void* w, void* y, int64_t ys, const void* res, int64_t rs, float* part,
                           int M, int N, int K, int epi, bool opk, int MB, int S, int G, int nbig, int NBB, int NBS,
                           const EpiArgs& ep, hipStream_t stream) {
 #define T2D_L(EPI_, OPK_, SPLIT_)                                                                                  \
-  hipLaunchKernelGGL((gemm_t2d_kernel<MW, NW, WM, WN, D, EPI_, OPK_, SPLIT_>), dim3(G), dim3(512), 0, stream,       \
+  hipLaunchKernelGGL((gemm_t2d_kernel<MW, NW, WM, WN, D, KU, GL, EPI_, OPK_, SPLIT_>), dim3(G), dim3(512), 0, stream, \
                      (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, ys, (const bf16_t*)res, rs, part, M, N, K, MB, \
                      S, nbig, NBB, NBS, ep)
   if (S > 1) {
@@ -242,27 +285,32 @@ static int launch_t2d_cfg(const void* x, const void* w, void* y, int64_t ys, con
   return 0;
 }
 
-// Two k splits wherever the epilogue allows (0 / 3: the reduce launch applies it): the column
-// groups double in width, so per CU the activation intake halves for 1.5x the weight intake -
-// qkv 50.0 -> 45.9 us, o 30.4 -> 24.5 us, down 70.6 -> 50.2 us at 256 rows (reduce included).
-static inline int t2d_pick_split(int K, int epi, int S_force) {
+// K split: two for the residual-stream producers (o, down: the reduce launch applies the epilogue)
+// - the column groups double in width, so per CU the activation intake halves for 1.5x the weight
+// intake: LDS-DMA form at 256 rows o 28.0 -> 23.5 us, down 60.7 -> 44.0 us (reduce included).  The
+// row-scaled qkv consumer splits only in the register-ring form (49.9 -> 46.2 us; LDS-DMA form 44.0
+// unsplit vs 45.7 split).  SwiGLU never (its epilogue needs the whole sum).
+static inline int t2d_pick_split(int K, int epi, bool gl, int S_force) {
   if (S_force > 0) return S_force;
-  return epi != 1 ? 2 : 1;
+  if (epi == 3) return 2;
+  return (epi == 0 && !gl) ? 2 : 1;
 }
 
-// MW = 2, WM = 4 (128-row blocks), WN = 2; NW by the column-group width
+// MW = 2, WM = 4 (128-row blocks), WN = 2; NW by the column-group width.  flags bit 18: the
+// LDS-DMA ring (2 k-slices per stage up to 4-tile waves, 1 beyond, so 3+ stages fit in LDS).
 static int launch_gemm_t2d(const void* x, const void* w, void* y, int64_t ys, const void* res, int64_t rs, int M,
                            int N, int K, int epi, int flags, const EpiArgs& ep, void* ws, hipStream_t stream,
                            int S_force = 0, bool dry = false) {
   constexpr int D = 4;
   const int mto = (M + 15) / 16;
-  if (M <= 64 || M > 256 || N % 16 || K % (32 * T2D_KU) || (flags & 2 && epi != 1)) return 1;
+  if (M <= 64 || M > 256 || N % 16 || K % 128 || (flags & 2 && epi != 1)) return 1;
   if (!(epi == 0 || epi == 1 || epi == 3)) return 1;
   const int MB = (mto + 7) / 8;
-  const int S = t2d_pick_split(K, epi, S_force);
+  const bool gl = flags & 262144;
+  const int S = t2d_pick_split(K, epi, gl, S_force);
   if (S > 1 && (epi == 1 || ws == nullptr || (int64_t)S * M * N * 4 > RWK_SLAB_BYTES || N % (256 * SKR_CPT)))
     return 1;
-  if (K / 32 / T2D_KU < 2 * S) return 1;
+  if (K / 64 < 2 * S) return 1;
   const int step = epi == 1 ? 2 : 1;
   const int units = (N / 16) / step;
   const int C0 = sk_num_cus();
@@ -281,9 +329,12 @@ static int launch_gemm_t2d(const void* x, const void* w, void* y, int64_t ys, co
   int nw = (NBB + 1) / 2;
   if (epi == 1 && nw % 2) ++nw;
   int rc;
-#define T2D_C(NW_)                                                                                               \
-  rc = dry ? 0 : launch_t2d_cfg<2, NW_, 4, 2, D>(x, w, y, ys, res, rs, part, M, N, K, epi, opk, MB, S, G, nbig, NBB, \
-                                                NBS, ep, stream)
+#define T2D_C(NW_)                                                                                                 \
+  rc = dry ? 0                                                                                                     \
+     : gl  ? launch_t2d_cfg<2, NW_, 4, 2, D, (NW_ > 4 ? 1 : 2), true>(x, w, y, ys, res, rs, part, M, N, K, epi, opk, \
+                                                                     MB, S, G, nbig, NBB, NBS, ep, stream)          \
+           : launch_t2d_cfg<2, NW_, 4, 2, D, 2, false>(x, w, y, ys, res, rs, part, M, N, K, epi, opk, MB, S, G, nbig, \
+                                                      NBB, NBS, ep, stream)
   switch (nw) {
     case 1: if (epi == 1) return 1; T2D_C(1); break;
     case 2: T2D_C(2); break;

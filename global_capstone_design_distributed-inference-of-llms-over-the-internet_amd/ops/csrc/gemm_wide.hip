@@ -1,8 +1,8 @@
 // Decode GEMM for 65..256 rows (the packed decode path at 96..256 sessions): split-K ring (o,
-// down) and balanced ring kernels at MT = 5..8, 12 and 16 (kernels: gemm_kernels.h).  129..256
-// rows run the 12- or 16-row-tile instantiation over the activation's own row tiles (the packed
-// layout's tile count is a runtime stride; tiles past it are masked rows).  Above ops.WIDE_ROWS
-// (128 by default) the decode step stays on hipBLASLt, which measured faster there (profiles/r4d).
+// down) and balanced ring kernels at MT = 5..8, 12 and 16 (kernels: gemm_kernels.h), and the
+// two-dimensionally tiled kernel (gemm_t2d.h, flags bit 15), which ops picks from ops.T2D_MIN
+// (129) rows up: there the ring forms measured slower than hipBLASLt (profiles/r4d) and the tiled
+// form faster (profiles/r5x).
 #include "gemm_t2d.h"
 
 extern "C" int mp_gemm_bf16_wide(const void* x, const void* w, void* y, int64_t y_stride, const void* res,
@@ -49,7 +49,9 @@ extern "C" int mp_gemm_t2d_ok(int M, int N, int K, int epilogue, int out_packed,
   ep.mt_out = (M + 15) / 16;
   char dummy = 0;
   return launch_gemm_t2d(nullptr, nullptr, nullptr, 0, nullptr, 0, M, N, K, epilogue, 1 | (out_packed ? 2 : 0), ep,
-                         with_ws ? &dummy : nullptr, 0, 0, true) == 0;
+                         with_ws ? &dummy : nullptr, 0, 0, true) == 0 &&
+         launch_gemm_t2d(nullptr, nullptr, nullptr, 0, nullptr, 0, M, N, K, epilogue,
+                         1 | (out_packed ? 2 : 0) | 262144, ep, with_ws ? &dummy : nullptr, 0, 0, true) == 0;
 }
 
 // 1 if mp_gemm_bf16 covers a packed-activation decode GEMM of M = 65..256 rows (balanced ring

@@ -46,6 +46,7 @@ def main():
     ap.add_argument("--splits", type=int, nargs="+", default=[0, 1, 2])
     ap.add_argument("--shapes", nargs="+", default=[s[0] for s in SHAPES])
     ap.add_argument("--ring", action="store_true", help="also time the 12 / 16-row-tile ring kernels")
+    ap.add_argument("--gl", action="store_true", help="also time the LDS-DMA staging form")
     a = ap.parse_args()
     dev = torch.device("cuda")
     ws_buf = ops.gemm_workspace(dev)
@@ -73,6 +74,8 @@ def main():
             ss_in = ss[2] if epi in (0, 1) else None
             flags0 = 1 | (2 if epi == 1 else 0)
             cands = [("t2d" + (f"/S{s}" if s else ""), flags0 | 32768 | (s << 16)) for s in a.splits]
+            if a.gl:
+                cands += [("t2d-gl" + (f"/S{s}" if s else ""), flags0 | 32768 | 262144 | (s << 16)) for s in a.splits]
             if a.ring:
                 ring = 256 if (epi != 1 and N % 2048 == 0) else 128
                 cands.append(("ring", flags0 | ring))

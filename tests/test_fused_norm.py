@@ -121,7 +121,8 @@ def test_wide_rows_consumer_and_producer(M, monkeypatch):
     reduce with the row scale; gate/up: balanced ring with the row scale and packed SwiGLU) and
     the producer (split-K ring + the reduce launch's residual / packed copy / statistics), against
     fp32 oracles.  Above 128 rows: the 12 / 16-row-tile ring instantiations."""
-    monkeypatch.setattr(ops, "WIDE_ROWS", 256)  # above 128 rows the hand-written forms are opt-in
+    monkeypatch.setattr(ops, "WIDE_ROWS", 256)  # above 128 rows the ring forms are opt-in
+    monkeypatch.setattr(ops, "T2D_MIN", 257)  # (the tiled kernel's own test is below)
     dev = "cuda"
     g = torch.Generator(device=dev).manual_seed(500 + M)
     K, N = 2048, 2048
@@ -168,6 +169,7 @@ def test_wide_ring_in_kernel_epilogues(M, monkeypatch):
     Llama-2-7B qkv (N = 12288) and gate/up (N = 22016) widths and 129..256 rows: row-scaled
     consumer and packed SwiGLU vs fp32."""
     monkeypatch.setattr(ops, "WIDE_ROWS", 256)
+    monkeypatch.setattr(ops, "T2D_MIN", 257)
     dev = "cuda"
     g = torch.Generator(device=dev).manual_seed(900 + M)
     K = 1024
@@ -195,12 +197,15 @@ def test_wide_ring_in_kernel_epilogues(M, monkeypatch):
 @pytest.mark.gpu
 @pytest.mark.parametrize("M", [129, 200, 256])
 @pytest.mark.parametrize("dims", [(2048, 2048, 2048), (4096, 12288, 11008)])
-def test_t2d_consumers_and_producers(M, dims, monkeypatch):
+@pytest.mark.parametrize("gl", [False, True])
+def test_t2d_consumers_and_producers(M, dims, gl, monkeypatch):
     """The two-dimensionally tiled kernel (csrc/gemm_t2d.h) at 129..256 rows, every decode
     epilogue against fp32 oracles: the row-scaled consumer (qkv), the row-scaled packed SwiGLU
     (gate/up: 12- and 10-tile column groups at F = 11008), the residual-stream producer straight
-    from the accumulators (o) and as split-K slabs + the reduce launch (down, K = 11008)."""
+    from the accumulators (o) and as split-K slabs + the reduce launch (down, K = 11008); ``gl``:
+    the LDS-DMA staging ring."""
     monkeypatch.setattr(ops, "T2D_MIN", 129)
+    monkeypatch.setattr(ops, "T2D_GL", gl)
     dev = "cuda"
     H, Nq, F = dims
     g = torch.Generator(device=dev).manual_seed(1300 + M + H)
@@ -250,8 +255,7 @@ def test_fused_executor_wide_batch_matches_unfused(graphs, n, t2d, monkeypatch):
     import dataclasses
 
     monkeypatch.setattr(ops, "WIDE_ROWS", 256)
-    if t2d:
-        monkeypatch.setattr(ops, "T2D_MIN", 129)
+    monkeypatch.setattr(ops, "T2D_MIN", 129 if t2d else 257)
 
     from src.models.config import resolve_model
     from src.models.weights import random_stage_weights

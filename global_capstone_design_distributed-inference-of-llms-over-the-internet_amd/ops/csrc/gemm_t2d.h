@@ -275,7 +275,7 @@ static int launch_t2d_cfg(const void* x, const void* w, void* y, int64_t ys, con
       return 1;
     }
   } else if (epi == 3) {
-    if constexpr (NW <= 4) T2D_L(3, false, false); else return 1;  // (the 6-wide producer would spill)
+    if constexpr (MW * NW <= 8) T2D_L(3, false, false); else return 1;  // (wider producers would spill)
   } else if (epi == 0) {
     T2D_L(0, false, false);
   } else {
@@ -296,8 +296,10 @@ static inline int t2d_pick_split(int K, int epi, bool gl, int S_force) {
   return (epi == 0 && !gl) ? 2 : 1;
 }
 
-// MW = 2, WM = 4 (128-row blocks), WN = 2; NW by the column-group width.  flags bit 18: the
-// LDS-DMA ring (2 k-slices per stage up to 4-tile waves, 1 beyond, so 3+ stages fit in LDS).
+// WM = 4 x WN = 2 waves; MW = 2 (128-row blocks) or, with flags bit 19 (LDS-DMA form only), MW = 1
+// (64-row blocks: twice the column-group width, a quarter of the activation intake per block for
+// twice the weight intake); NW by the column-group width.  flags bit 18: the LDS-DMA ring (2
+// k-slices per stage while a stage fits in 32 KB, else 1, so 4+ stages fit in LDS).
 static int launch_gemm_t2d(const void* x, const void* w, void* y, int64_t ys, const void* res, int64_t rs, int M,
                            int N, int K, int epi, int flags, const EpiArgs& ep, void* ws, hipStream_t stream,
                            int S_force = 0, bool dry = false) {
@@ -305,8 +307,10 @@ static int launch_gemm_t2d(const void* x, const void* w, void* y, int64_t ys, co
   const int mto = (M + 15) / 16;
   if (M <= 64 || M > 256 || N % 16 || K % 128 || (flags & 2 && epi != 1)) return 1;
   if (!(epi == 0 || epi == 1 || epi == 3)) return 1;
-  const int MB = (mto + 7) / 8;
-  const bool gl = flags & 262144;
+  // the SwiGLU consumer (gate/up: 6-tile waves) keeps the register ring: 4 stages of 40 KB in
+  // registers against the LDS-DMA ring's 5 of 20 KB, 1-4 % faster at 192 / 256 rows (profiles/r5x)
+  const bool gl = (flags & 262144) && (epi != 1 || (flags & 524288)), bm64 = gl && (flags & 524288);
+  const int MB = bm64 ? (mto + 3) / 4 : (mto + 7) / 8;
   const int S = t2d_pick_split(K, epi, gl, S_force);
   if (S > 1 && (epi == 1 || ws == nullptr || (int64_t)S * M * N * 4 > RWK_SLAB_BYTES || N % (256 * SKR_CPT)))
     return 1;
@@ -329,21 +333,41 @@ static int launch_gemm_t2d(const void* x, const void* w, void* y, int64_t ys, co
   int nw = (NBB + 1) / 2;
   if (epi == 1 && nw % 2) ++nw;
   int rc;
+#define T2D_KU(MW_, NW_) ((4 * MW_ + 2 * NW_) * 2 <= 32 ? 2 : 1)
 #define T2D_C(NW_)                                                                                                 \
   rc = dry ? 0                                                                                                     \
-     : gl  ? launch_t2d_cfg<2, NW_, 4, 2, D, (NW_ > 4 ? 1 : 2), true>(x, w, y, ys, res, rs, part, M, N, K, epi, opk, \
-                                                                     MB, S, G, nbig, NBB, NBS, ep, stream)          \
+     : gl  ? launch_t2d_cfg<2, NW_, 4, 2, D, T2D_KU(2, NW_), true>(x, w, y, ys, res, rs, part, M, N, K, epi, opk,   \
+                                                                  MB, S, G, nbig, NBB, NBS, ep, stream)             \
            : launch_t2d_cfg<2, NW_, 4, 2, D, 2, false>(x, w, y, ys, res, rs, part, M, N, K, epi, opk, MB, S, G, nbig, \
                                                       NBB, NBS, ep, stream)
-  switch (nw) {
-    case 1: if (epi == 1) return 1; T2D_C(1); break;
-    case 2: T2D_C(2); break;
-    case 3: if (epi == 1) return 1; T2D_C(3); break;
-    case 4: T2D_C(4); break;
-    case 6: T2D_C(6); break;
-    default: return 1;
+#define T2D_C1(NW_)                                                                                                \
+  rc = dry ? 0                                                                                                     \
+           : launch_t2d_cfg<1, NW_, 4, 2, D, T2D_KU(1, NW_), true>(x, w, y, ys, res, rs, part, M, N, K, epi, opk, MB, \
+                                                                  S, G, nbig, NBB, NBS, ep, stream)
+  if (bm64) {
+    switch (nw) {
+      case 1: if (epi == 1) return 1; T2D_C1(1); break;
+      case 2: T2D_C1(2); break;
+      case 3: if (epi == 1) return 1; T2D_C1(3); break;
+      case 4: T2D_C1(4); break;
+      case 6: T2D_C1(6); break;
+      case 8: T2D_C1(8); break;
+      case 12: T2D_C1(12); break;
+      default: return 1;
+    }
+  } else {
+    switch (nw) {
+      case 1: if (epi == 1) return 1; T2D_C(1); break;
+      case 2: T2D_C(2); break;
+      case 3: if (epi == 1) return 1; T2D_C(3); break;
+      case 4: T2D_C(4); break;
+      case 6: T2D_C(6); break;
+      default: return 1;
+    }
   }
+#undef T2D_C1
 #undef T2D_C
+#undef T2D_KU
   if (rc != 0 || dry) return rc;
   if (S > 1) {
     const dim3 g2(N / (256 * SKR_CPT), M);

@@ -309,7 +309,8 @@ static int launch_gemm_t2d(const void* x, const void* w, void* y, int64_t ys, co
   if (!(epi == 0 || epi == 1 || epi == 3)) return 1;
   // the SwiGLU consumer (gate/up: 6-tile waves) keeps the register ring: 4 stages of 40 KB in
   // registers against the LDS-DMA ring's 5 of 20 KB, 1-4 % faster at 192 / 256 rows (profiles/r5x)
-  const bool gl = (flags & 262144) && (epi != 1 || (flags & 524288)), bm64 = gl && (flags & 524288);
+  bool gl = (flags & 262144) && (epi != 1 || (flags & 524288));
+  const bool bm64 = gl && (flags & 524288);
   const int MB = bm64 ? (mto + 3) / 4 : (mto + 7) / 8;
   const int S = t2d_pick_split(K, epi, gl, S_force);
   if (S > 1 && (epi == 1 || ws == nullptr || (int64_t)S * M * N * 4 > RWK_SLAB_BYTES || N % (256 * SKR_CPT)))
@@ -332,6 +333,7 @@ static int launch_gemm_t2d(const void* x, const void* w, void* y, int64_t ys, co
   // the narrowest wave width that holds NBB tiles on 2 column waves (even for SwiGLU pairs)
   int nw = (NBB + 1) / 2;
   if (epi == 1 && nw % 2) ++nw;
+  if (nw == 8 && !bm64) gl = true;  // 8-tile waves (Llama-3-8B gate/up): a register ring would spill
   int rc;
 #define T2D_KU(MW_, NW_) ((4 * MW_ + 2 * NW_) * 2 <= 32 ? 2 : 1)
 #define T2D_C(NW_)                                                                                                 \
@@ -362,6 +364,10 @@ static int launch_gemm_t2d(const void* x, const void* w, void* y, int64_t ys, co
       case 3: if (epi == 1) return 1; T2D_C(3); break;
       case 4: T2D_C(4); break;
       case 6: T2D_C(6); break;
+      case 8:
+        rc = dry ? 0 : launch_t2d_cfg<2, 8, 4, 2, D, 1, true>(x, w, y, ys, res, rs, part, M, N, K, epi, opk, MB, S, G,
+                                                             nbig, NBB, NBS, ep, stream);
+        break;
       default: return 1;
     }
   }

@@ -196,14 +196,14 @@ def test_wide_ring_in_kernel_epilogues(M, monkeypatch):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("M", [129, 200, 256])
-@pytest.mark.parametrize("dims", [(2048, 2048, 2048), (4096, 12288, 11008)])
+@pytest.mark.parametrize("dims", [(2048, 2048, 2048), (4096, 12288, 11008), (4096, 6144, 14336)])
 @pytest.mark.parametrize("gl", [False, True])
 def test_t2d_consumers_and_producers(M, dims, gl, monkeypatch):
     """The two-dimensionally tiled kernel (csrc/gemm_t2d.h) at 129..256 rows, every decode
     epilogue against fp32 oracles: the row-scaled consumer (qkv), the row-scaled packed SwiGLU
     (gate/up: 12- and 10-tile column groups at F = 11008), the residual-stream producer straight
-    from the accumulators (o) and as split-K slabs + the reduce launch (down, K = 11008); ``gl``:
-    the LDS-DMA staging ring."""
+    from the accumulators (o) and as split-K slabs + the reduce launch (down, K = 11008); the
+    Llama-3-8B widths (8-tile waves for gate/up); ``gl``: the LDS-DMA staging ring."""
     monkeypatch.setattr(ops, "T2D_MIN", 129)
     monkeypatch.setattr(ops, "T2D_GL", gl)
     dev = "cuda"

@@ -50,6 +50,20 @@ def test_reference_fold_identity_cpu():
     assert int(ssz.abs().sum()) == 0
 
 
+def test_t2d_row_range_policy_cpu(monkeypatch):
+    """Which decode row counts the two-dimensionally tiled kernel owns (ops.T2D_MIN .. 256), and
+    how far the packed (hand-written GEMM) path reaches with and without it."""
+    monkeypatch.setattr(ops, "T2D_MIN", 129)
+    assert [ops.t2d_rows(m) for m in (64, 128, 129, 200, 256, 257)] == [False, False, True, True, True, False]
+    assert ops.wide_rows() == 256
+    monkeypatch.setattr(ops, "T2D_MIN", 257)  # off: the ring kernels up to WIDE_ROWS, hipBLASLt above
+    assert not any(ops.t2d_rows(m) for m in (129, 256))
+    assert ops.wide_rows() == ops.WIDE_ROWS
+    monkeypatch.setattr(ops, "T2D_MIN", 10)  # never below 65 rows (the M <= 64 kernels own that range)
+    assert not ops.t2d_rows(64) and ops.t2d_rows(65)
+    assert "t2d" in ops._KERNEL_FLAGS and not ops._covered("t2d", 64, 4096, 4096, 0)
+
+
 KERNELS = ["pk", "sk", "lds22", "lds24", "lds42", "rw", "rwk", "rwki", "rwr"]
 
 

@@ -129,30 +129,59 @@ __global__ __launch_bounds__(256, 2) void attn_mfma_kernel(
   if (b_first + 128 < end) pg_next = bt[(b_first + 128) >> page_log2];
 
   // ROPE with qkv partials (decode blocks, one token): the block's HB query heads, its key and its
-  // value summed from the split-K slabs, row-scaled and rounded (common.h qkv_part_load8: the
+  // value summed from the split-K slabs, row-scaled and rounded (common.h qkv_part_finish8: the
   // reduce launch's bits) ONCE per block into LDS - every slab element read once, not once per
-  // lane group of every wave; the RoPE below then reads them as it would the bf16 qkv row
+  // lane group of every wave; the RoPE below then reads them as it would the bf16 qkv row.
+  // Issue order = need order (vmcnt retires in order): row-statistics shards and slab loads, the
+  // rotary table, then the first step's K / V - so the fold's and the RoPE's waits leave the K / V
+  // stream in flight, and its round trip overlaps theirs instead of following the fold's barrier.
   constexpr int CK = D / 8;  // 8-column chunks per head
-  __shared__ u16x8 s_fold[(HB + 2) * CK];
+  constexpr int NFOLD = (HB + 2) * CK;
+  constexpr int NI = (NFOLD + 255) / 256;  // fold items per thread (256 threads)
+  __shared__ u16x8 s_fold[NFOLD];
   constexpr bool from_part = ROPE && FOLD;
-  if (from_part) {
-    const float qrs = qkv_part_scale(rf.qp, tok0);
-    for (int i = tid; i < (HB + 2) * CK; i += blockDim.x) {
-      const int item = i / CK, cc = (i % CK) * 8;
-      const int col = (item < HB ? (hbase + item) * D : item == HB ? (nh + g) * D : (nh + nkv + g) * D) + cc;
-      s_fold[i] = qkv_part_load8(rf.qp, tok0, col, qrs);
-    }
-    __syncthreads();
-  }
-  u16x8 qf[KD];
+  int fcol[NI];
 #pragma unroll
-  for (int kd = 0; kd < KD; ++kd) {
-    if (row_ok) {
-      qf[kd] = from_part ? s_fold[(my_h - hbase) * CK + kd * 4 + qd]
-                         : *reinterpret_cast<const u16x8*>(q + (int64_t)(tok0 + my_t) * q_stride + (int64_t)my_h * D +
-                                                           kd * 32 + qd * 8);
-    } else {
-      qf[kd] = (u16x8)(0);
+  for (int j = 0; j < NI; ++j) {
+    const int fi = min(tid + 256 * j, NFOLD - 1);  // (threads past the items fetch the last one again, unused)
+    fcol[j] = (fi / CK < HB ? (hbase + fi / CK) * D : fi / CK == HB ? (nh + g) * D : (nh + nkv + g) * D) +
+              (fi % CK) * 8;
+  }
+  unsigned long long ssv = 0;
+  QkvPart8 ff[NI];
+  if constexpr (from_part) {
+    ssv = qkv_part_ss_load(rf.qp, tok0);
+#pragma unroll
+    for (int j = 0; j < NI; ++j) qkv_part_fetch8(rf.qp, tok0, fcol[j], ff[j]);
+  }
+  u16x8 qf[KD], kr[KD];
+  u16x8 vn = (u16x8)(0);
+  if constexpr (!from_part) {
+#pragma unroll
+    for (int kd = 0; kd < KD; ++kd)
+      qf[kd] = row_ok ? *reinterpret_cast<const u16x8*>(q + (int64_t)(tok0 + my_t) * q_stride + (int64_t)my_h * D +
+                                                        kd * 32 + qd * 8)
+                      : (u16x8)(0);
+    if constexpr (ROPE) {  // the new token's key and value from the bf16 qkv row
+      const bf16_t* qrow = q + (int64_t)tok0 * q_stride;
+#pragma unroll
+      for (int kd = 0; kd < KD; ++kd) kr[kd] = *reinterpret_cast<const u16x8*>(qrow + (nh + g) * D + kd * 32 + qd * 8);
+      vn = *reinterpret_cast<const u16x8*>(qrow + (nh + nkv + g) * D + ((lane * 8) % D));
+    }
+  }
+  constexpr int HK = KD / 2, HALF = D / 2;
+  f32x4 cs[ROPE ? HK : 1][2], sn[ROPE ? HK : 1][2];
+  int64_t kv_slot = -1;
+  if constexpr (ROPE) {
+    kv_slot = rf.slots[tok0];
+    const int64_t ps_ = rf.pos[tok0];
+#pragma unroll
+    for (int h = 0; h < HK; ++h) {
+      const int64_t ci = ps_ * HALF + h * 32 + qd * 8;
+      cs[h][0] = *reinterpret_cast<const f32x4*>(rf.cos_t + ci);
+      cs[h][1] = *reinterpret_cast<const f32x4*>(rf.cos_t + ci + 4);
+      sn[h][0] = *reinterpret_cast<const f32x4*>(rf.sin_t + ci);
+      sn[h][1] = *reinterpret_cast<const f32x4*>(rf.sin_t + ci + 4);
     }
   }
 
@@ -161,28 +190,23 @@ __global__ __launch_bounds__(256, 2) void attn_mfma_kernel(
     load_v(b_first, pg_cur, vr);
   }
 
+  if constexpr (from_part) {
+    const float qrs = qkv_part_ss_scale(rf.qp, ssv);
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+      if (tid + 256 * j < NFOLD) s_fold[tid + 256 * j] = qkv_part_finish8(rf.qp, tok0, fcol[j], ff[j], qrs);
+    lds_wait_barrier();  // (lgkmcnt only: the K / V loads stay in flight)
+#pragma unroll
+    for (int kd = 0; kd < KD; ++kd) qf[kd] = row_ok ? s_fold[(my_h - hbase) * CK + kd * 4 + qd] : (u16x8)(0);
+  }
+
   int tnew = -1;
   float qk_new = 0.f;
-  u16x8 vn = (u16x8)(0);
   if constexpr (ROPE) {
-    constexpr int HK = KD / 2, HALF = D / 2;
-    const int64_t ps_ = rf.pos[tok0];
-    u16x8 kr[KD];
-    const bf16_t* qrow = q + (int64_t)tok0 * q_stride;
+    if constexpr (from_part) {
 #pragma unroll
-    for (int kd = 0; kd < KD; ++kd)
-      kr[kd] = from_part ? s_fold[HB * CK + kd * 4 + qd]
-                         : *reinterpret_cast<const u16x8*>(qrow + (nh + g) * D + kd * 32 + qd * 8);
-    vn = from_part ? s_fold[(HB + 1) * CK + ((lane * 8) % D) / 8]
-                   : *reinterpret_cast<const u16x8*>(qrow + (nh + nkv + g) * D + ((lane * 8) % D));
-    f32x4 cs[HK][2], sn[HK][2];
-#pragma unroll
-    for (int h = 0; h < HK; ++h) {
-      const int64_t ci = ps_ * HALF + h * 32 + qd * 8;
-      cs[h][0] = *reinterpret_cast<const f32x4*>(rf.cos_t + ci);
-      cs[h][1] = *reinterpret_cast<const f32x4*>(rf.cos_t + ci + 4);
-      sn[h][0] = *reinterpret_cast<const f32x4*>(rf.sin_t + ci);
-      sn[h][1] = *reinterpret_cast<const f32x4*>(rf.sin_t + ci + 4);
+      for (int kd = 0; kd < KD; ++kd) kr[kd] = s_fold[HB * CK + kd * 4 + qd];
+      vn = s_fold[(HB + 1) * CK + ((lane * 8) % D) / 8];
     }
     auto rot = [&](const u16x8 (&a)[KD], u16x8 (&r)[KD]) {
 #pragma unroll
@@ -210,7 +234,7 @@ __global__ __launch_bounds__(256, 2) void attn_mfma_kernel(
     part += __shfl_xor(part, 32, 64);
     qk_new = part;
     tnew = blk_ctx - 1;
-    const int64_t slot = rf.slots[tok0];
+    const int64_t slot = kv_slot;
     if (w == 0 && tnew >= start && tnew < end && slot >= 0 && hbase % (nh / nkv) == 0) {
       const int64_t dst = (slot >> page_log2) * page_stride + head_off + (slot & (page_size - 1)) * D;
       if (c == 0) {

@@ -75,6 +75,10 @@ __device__ __forceinline__ float wave_max(float v) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
 }
 
+// workgroup barrier that waits for this wave's LDS operations only: global loads in flight (a
+// register-staged stream) stay in flight across it, unlike __syncthreads()
+__device__ __forceinline__ void lds_wait_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 // exact integer sums (fixed-point row statistics): over the 16 lanes of each row of the wave
 // (every lane gets its row's sum), and over the whole wave (every lane gets the total)
 __device__ __forceinline__ unsigned long long sum16_u64(unsigned long long v) {
@@ -141,23 +145,54 @@ struct QkvPart {
   float inv_k, eps;
 };
 
-// Every lane of the wave must call it (a wave reduction): lane j < QP_SS_NSH loads shard j, the
-// integer sum is exact in any order.
-__device__ __forceinline__ float qkv_part_scale(const QkvPart& qp, int row) {
-  if (qp.ss == nullptr) return 1.f;
+// The row scale in two halves, so a kernel can issue the shard loads early and reduce late:
+// lane j < QP_SS_NSH loads shard j; every lane of the wave must call the reduction (the integer
+// sum is exact in any order).
+__device__ __forceinline__ unsigned long long qkv_part_ss_load(const QkvPart& qp, int row) {
   const int lane = threadIdx.x & 63;
-  unsigned long long t = lane < QP_SS_NSH ? qp.ss[lane * QP_SS_ROWS + row] : 0ull;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
-  return rsqrtf((float)t * (1.f / QP_SS_FX) * qp.inv_k + qp.eps);
+  return (qp.ss != nullptr && lane < QP_SS_NSH) ? qp.ss[lane * QP_SS_ROWS + row] : 0ull;
+}
+__device__ __forceinline__ float qkv_part_ss_scale(const QkvPart& qp, unsigned long long v) {
+  if (qp.ss == nullptr) return 1.f;
+  return rsqrtf((float)wave_sum_u64(v) * (1.f / QP_SS_FX) * qp.inv_k + qp.eps);
+}
+__device__ __forceinline__ float qkv_part_scale(const QkvPart& qp, int row) {
+  return qkv_part_ss_scale(qp, qkv_part_ss_load(qp, row));
 }
 
-__device__ __forceinline__ u16x8 qkv_part_load8(const QkvPart& qp, int row, int col, float rs) {
+// The S slabs' 8 columns (col .. col + 7 of ``row``), fetched and summed in two halves.  Up to
+// QP_SMAX splits every slab load is issued at once (one memory round trip, not S dependent ones;
+// slabs past S re-read the last one, an L2 hit, and are not added); qkv folds run S = 2 or 3.
+constexpr int QP_SMAX = 4;
+struct QkvPart8 {
+  f32x4 a[QP_SMAX], b[QP_SMAX];
+};
+__device__ __forceinline__ void qkv_part_fetch8(const QkvPart& qp, int row, int col, QkvPart8& f) {
+  const float* p0 = qp.part + (int64_t)row * qp.ldn + col;
+#pragma unroll
+  for (int s = 0; s < QP_SMAX; ++s) {
+    const float* p = p0 + (int64_t)min(s, qp.S - 1) * qp.slab;
+    f.a[s] = *reinterpret_cast<const f32x4*>(p);
+    f.b[s] = *reinterpret_cast<const f32x4*>(p + 4);
+  }
+}
+// bf16(sum * rs): the S slabs summed in split order from zero - the reduce launch's bits
+__device__ __forceinline__ u16x8 qkv_part_finish8(const QkvPart& qp, int row, int col, const QkvPart8& f, float rs) {
   f32x4 a = (f32x4)(0.f), b = (f32x4)(0.f);
-  for (int s = 0; s < qp.S; ++s) {  // fixed split order: the reduce launch's sum
-    const float* p = qp.part + s * qp.slab + (int64_t)row * qp.ldn + col;
-    a += *reinterpret_cast<const f32x4*>(p);
-    b += *reinterpret_cast<const f32x4*>(p + 4);
+  if (qp.S <= QP_SMAX) {
+#pragma unroll
+    for (int s = 0; s < QP_SMAX; ++s) {
+      if (s < qp.S) {  // (a select on registers: the loads are already issued)
+        a += f.a[s];
+        b += f.b[s];
+      }
+    }
+  } else {
+    for (int s = 0; s < qp.S; ++s) {  // more splits than the unrolled fetch holds: a plain loop
+      const float* p = qp.part + s * qp.slab + (int64_t)row * qp.ldn + col;
+      a += *reinterpret_cast<const f32x4*>(p);
+      b += *reinterpret_cast<const f32x4*>(p + 4);
+    }
   }
   u16x8 r;
 #pragma unroll
@@ -166,6 +201,11 @@ __device__ __forceinline__ u16x8 qkv_part_load8(const QkvPart& qp, int row, int 
     r[j + 4] = f2bf(b[j] * rs);
   }
   return r;
+}
+__device__ __forceinline__ u16x8 qkv_part_load8(const QkvPart& qp, int row, int col, float rs) {
+  QkvPart8 f;
+  qkv_part_fetch8(qp, row, col, f);
+  return qkv_part_finish8(qp, row, col, f, rs);
 }
 
 }  // namespace mp

@@ -536,6 +536,8 @@ def main(argv=None):
             "hop_recv_wait_ms_per_rank": [round(p[5], 4) for p in per_stage],
             # the qkv fold per decode row bucket, as the warm-up's decode-graph A/B left it
             "qkv_fold": {f"M{k}": bool(v) for k, v in sorted(ex.qkv_fold_by_bucket.items())},
+            # the warm-up A/B behind it: (folded, unfolded) ms per step
+            "qkv_fold_ab_ms": {f"M{k}": v for k, v in sorted(getattr(ex, "qkv_fold_ab_ms", {}).items())},
             "prefill_plus_first_token_s": round(prefill_s, 3),
             # the prefill round alone: every session's prompt through the whole pipeline
             # (micro-batch slots x batch x prompt-len tokens), max over ranks

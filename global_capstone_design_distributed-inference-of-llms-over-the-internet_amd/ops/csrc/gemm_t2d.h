@@ -296,10 +296,10 @@ static inline int t2d_pick_split(int K, int epi, bool gl, int S_force) {
   return (epi == 0 && !gl) ? 2 : 1;
 }
 
-// WM = 4 x WN = 2 waves; MW = 2 (128-row blocks) or, with flags bit 19 (LDS-DMA form only), MW = 1
-// (64-row blocks: twice the column-group width, a quarter of the activation intake per block for
-// twice the weight intake); NW by the column-group width.  flags bit 18: the LDS-DMA ring (2
-// k-slices per stage while a stage fits in 32 KB, else 1, so 4+ stages fit in LDS).
+// WM = 4 x WN = 2 waves, MW = 2 (128-row blocks); NW by the column-group width.  flags bit 18:
+// the LDS-DMA ring (2 k-slices per stage while a stage fits in 32 KB, else 1, so 4+ stages fit in
+// LDS).  (64-row blocks - a quarter of the activation intake per block for twice the weight
+// intake - measured slower on every shape, profiles/r5x, and were removed.)
 static int launch_gemm_t2d(const void* x, const void* w, void* y, int64_t ys, const void* res, int64_t rs, int M,
                            int N, int K, int epi, int flags, const EpiArgs& ep, void* ws, hipStream_t stream,
                            int S_force = 0, bool dry = false) {
@@ -309,9 +309,8 @@ static int launch_gemm_t2d(const void* x, const void* w, void* y, int64_t ys, co
   if (!(epi == 0 || epi == 1 || epi == 3)) return 1;
   // the SwiGLU consumer (gate/up: 6-tile waves) keeps the register ring: 4 stages of 40 KB in
   // registers against the LDS-DMA ring's 5 of 20 KB, 1-4 % faster at 192 / 256 rows (profiles/r5x)
-  bool gl = (flags & 262144) && (epi != 1 || (flags & 524288));
-  const bool bm64 = gl && (flags & 524288);
-  const int MB = bm64 ? (mto + 3) / 4 : (mto + 7) / 8;
+  bool gl = (flags & 262144) && epi != 1;
+  const int MB = (mto + 7) / 8;
   const int S = t2d_pick_split(K, epi, gl, S_force);
   if (S > 1 && (epi == 1 || ws == nullptr || (int64_t)S * M * N * 4 > RWK_SLAB_BYTES || N % (256 * SKR_CPT)))
     return 1;
@@ -333,7 +332,7 @@ static int launch_gemm_t2d(const void* x, const void* w, void* y, int64_t ys, co
   // the narrowest wave width that holds NBB tiles on 2 column waves (even for SwiGLU pairs)
   int nw = (NBB + 1) / 2;
   if (epi == 1 && nw % 2) ++nw;
-  if (nw == 8 && !bm64) gl = true;  // 8-tile waves (Llama-3-8B gate/up): a register ring would spill
+  if (nw == 8) gl = true;  // 8-tile waves (Llama-3-8B gate/up): a register ring would spill
   int rc;
 #define T2D_KU(MW_, NW_) ((4 * MW_ + 2 * NW_) * 2 <= 32 ? 2 : 1)
 #define T2D_C(NW_)                                                                                                 \
@@ -342,36 +341,18 @@ static int launch_gemm_t2d(const void* x, const void* w, void* y, int64_t ys, co
                                                                   MB, S, G, nbig, NBB, NBS, ep, stream)             \
            : launch_t2d_cfg<2, NW_, 4, 2, D, 2, false>(x, w, y, ys, res, rs, part, M, N, K, epi, opk, MB, S, G, nbig, \
                                                       NBB, NBS, ep, stream)
-#define T2D_C1(NW_)                                                                                                \
-  rc = dry ? 0                                                                                                     \
-           : launch_t2d_cfg<1, NW_, 4, 2, D, T2D_KU(1, NW_), true>(x, w, y, ys, res, rs, part, M, N, K, epi, opk, MB, \
-                                                                  S, G, nbig, NBB, NBS, ep, stream)
-  if (bm64) {
-    switch (nw) {
-      case 1: if (epi == 1) return 1; T2D_C1(1); break;
-      case 2: T2D_C1(2); break;
-      case 3: if (epi == 1) return 1; T2D_C1(3); break;
-      case 4: T2D_C1(4); break;
-      case 6: T2D_C1(6); break;
-      case 8: T2D_C1(8); break;
-      case 12: T2D_C1(12); break;
-      default: return 1;
-    }
-  } else {
-    switch (nw) {
-      case 1: if (epi == 1) return 1; T2D_C(1); break;
-      case 2: T2D_C(2); break;
-      case 3: if (epi == 1) return 1; T2D_C(3); break;
-      case 4: T2D_C(4); break;
-      case 6: T2D_C(6); break;
-      case 8:
-        rc = dry ? 0 : launch_t2d_cfg<2, 8, 4, 2, D, 1, true>(x, w, y, ys, res, rs, part, M, N, K, epi, opk, MB, S, G,
-                                                             nbig, NBB, NBS, ep, stream);
-        break;
-      default: return 1;
-    }
+  switch (nw) {
+    case 1: if (epi == 1) return 1; T2D_C(1); break;
+    case 2: T2D_C(2); break;
+    case 3: if (epi == 1) return 1; T2D_C(3); break;
+    case 4: T2D_C(4); break;
+    case 6: T2D_C(6); break;
+    case 8:
+      rc = dry ? 0 : launch_t2d_cfg<2, 8, 4, 2, D, 1, true>(x, w, y, ys, res, rs, part, M, N, K, epi, opk, MB, S, G,
+                                                           nbig, NBB, NBS, ep, stream);
+      break;
+    default: return 1;
   }
-#undef T2D_C1
 #undef T2D_C
 #undef T2D_KU
   if (rc != 0 || dry) return rc;

@@ -47,7 +47,6 @@ def main():
     ap.add_argument("--shapes", nargs="+", default=[s[0] for s in SHAPES])
     ap.add_argument("--ring", action="store_true", help="also time the 12 / 16-row-tile ring kernels")
     ap.add_argument("--gl", action="store_true", help="also time the LDS-DMA staging form")
-    ap.add_argument("--bm64", action="store_true", help="also time the 64-row-block LDS-DMA form")
     a = ap.parse_args()
     dev = torch.device("cuda")
     ws_buf = ops.gemm_workspace(dev)
@@ -77,9 +76,6 @@ def main():
             cands = [("t2d" + (f"/S{s}" if s else ""), flags0 | 32768 | (s << 16)) for s in a.splits]
             if a.gl:
                 cands += [("t2d-gl" + (f"/S{s}" if s else ""), flags0 | 32768 | 262144 | (s << 16)) for s in a.splits]
-            if a.bm64:
-                cands += [("t2d-gl64" + (f"/S{s}" if s else ""), flags0 | 32768 | 262144 | 524288 | (s << 16))
-                          for s in a.splits]
             if a.ring:
                 ring = 256 if (epi != 1 and N % 2048 == 0) else 128
                 cands.append(("ring", flags0 | ring))

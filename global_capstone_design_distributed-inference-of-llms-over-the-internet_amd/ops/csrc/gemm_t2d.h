@@ -17,15 +17,19 @@
 // Pipeline: each k-stage (KU k-slices of 32) is FA = (BM/16) KU activation fragments + NB KU weight
 // fragments of 1 KiB (both operands are stored in MFMA fragment order: ops.pack_weight /
 // the packed activation layout, so a fragment is one contiguous 1 KiB wave load).  The 8 waves
-// load the stage's fragments round-robin into a D-deep register ring (D stages in flight per CU),
-// write the oldest into one of two LDS buffers, and one barrier per stage (lgkmcnt only: the
-// register ring's loads stay in flight across it) hands it to the MFMA phase.  Wave (wm, wn) of
-// the WM x WN grid computes MW x NW 16 x 16 tiles of the block from LDS reads (ds_read_b128).
+// load the stage's fragments round-robin, in one of two forms:
+//   * LDS-DMA ring (GL, the default for qkv / o / down and 8-tile waves): global_load_lds_dwordx4
+//     straight into a P-slot LDS ring (3-6 stages, P - 1 in flight), a counted vmcnt and an
+//     lgkmcnt-only barrier per stage - no staging registers, no ds_write;
+//   * register ring (the SwiGLU gate/up form): D stages in registers, the oldest written into one
+//     of two LDS buffers per stage.
+// Wave (wm, wn) of the WM x WN grid computes MW x NW 16 x 16 tiles of the block from LDS reads
+// (ds_read_b128).  Measurements: profiles/r5x (A/Bs of both forms, whole-step tables), r5pmc.
 //
 // Epilogues: the shared decode epilogues (tile_epilogue: 0 with the fused-norm row scale,
 // 1 = SwiGLU with packed output, 3 = the residual-stream producer) straight from the accumulators,
-// or (SPLIT) fp32 partial slabs [S][M][N] for the split-K reduce launch (splitk_reduce_kernel),
-// used where K is long (down: K = 11008).
+// or (SPLIT) fp32 partial slabs [S][M][N] for the split-K reduce launch (splitk_reduce_kernel):
+// the residual-stream producers (o, down) split K in two.
 #pragma once
 #include "gemm_kernels.h"
 

@@ -23,6 +23,9 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--marker", default="sample")
     ap.add_argument("--top", type=int, default=40)
+    ap.add_argument("--seq", type=int, default=0,
+                    help="also print the mean duration of the first SEQ dispatches of a step, in order "
+                         "(tells apart projections that share one kernel instantiation)")
     a = ap.parse_args()
     c = sqlite3.connect(a.db)
     rows = c.execute("select name, start, end from kernels order by start").fetchall()
@@ -41,6 +44,15 @@ def main():
     print(f"steps={n} wall_us/step={span:.1f} busy_us/step={busy:.1f} idle_us/step={span - busy:.1f}")
     for k, (cnt, t) in sorted(agg.items(), key=lambda kv: -kv[1][1])[: a.top]:
         print(f"{t / n:9.1f} us {cnt / n:6.1f}x  {k}")
+    if a.seq:
+        steps = [rows[marks[i]:marks[i + 1]] for i in range(len(marks) - n - 1, len(marks) - 1)]
+        width = min(len(st) for st in steps)
+        if any(len(st) != width for st in steps):
+            print("# steps differ in dispatch count; per-position means use the shortest")
+        print(f"# first {min(a.seq, width)} dispatches of a step (mean us over {n} steps)")
+        for j in range(min(a.seq, width)):
+            d = sum((st[j][2] - st[j][1]) / 1e3 for st in steps) / n
+            print(f"{j:4d} {d:9.1f} us  {short(steps[0][j][0])}")
 
 
 if __name__ == "__main__":

@@ -44,8 +44,9 @@ extern "C" int mp_gemm_rwk_split(int M, int N, int K, int f8) {
   using namespace mp;
   if (M < 1 || M > 128 || N % 2048 || K % 128) return 0;
   int nt, S;
-  // the same width bound launch_gemm_rwk<MT, F8> uses (fp8 at 49..64 rows: the 16-tile group)
-  const int nt_max = (f8 != 0 && (M + 15) / 16 == 4) ? 16 : rwk_nt_max(M);
+  // the same width bound launch_gemm_rwk<MT, F8> uses, so a consumer of the partial slabs sees the
+  // split count the launch picks
+  const int nt_max = rwk_nt_max(M);
   rwk_choose(N / 16, K / 32, sk_num_cus(), f8 != 0, nt, S, nt_max);
   if (nt == 0 || (int64_t)S * M * N * 4 > RWK_SLAB_BYTES) return 0;
   return S;

@@ -88,7 +88,7 @@ def gemm_policy() -> str:
 
 
 # Library (hipBLASLt / rocBLAS) solutions for the row-major GEMMs - prefill and decode steps above
-# 128 rows - picked per shape by PyTorch TunableOp on MI355X (scripts/tune_gemms.py; the file's
+# 128 rows - picked per shape by PyTorch TunableOp on MI355X (lab/tools/tune_gemms.py; the file's
 # validator lines pin the ROCm / hipBLASLt build it was measured on, other builds ignore it).
 # Loaded read-only: tuning stays off, shapes not in the file keep the library heuristic.
 TUNED_GEMMS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned", "gemm_gfx950.csv")

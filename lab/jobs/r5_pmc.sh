@@ -8,7 +8,7 @@ cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 timeout -s KILL 60 rocprofv3 --list-avail > $O/avail.txt 2>&1 || true
 grep -oE "Counter_Name +:\s+(SQ|TCC|TA|TCP|GRBM|TD)_[A-Za-z0-9_]+" $O/avail.txt | awk '{print $NF}' | sort -u > $O/avail_names.txt || true
 wc -l < $O/avail_names.txt
-PROG="python3 scripts/t2d_bench.py --m 256 64 --splits 0 --shapes qkv --iters 10 --ring"
+PROG="python3 lab/tools/t2d_bench.py --m 256 64 --splits 0 --shapes qkv --iters 10 --ring"
 i=0
 for set in "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_INST_LEVEL_VMEM SQ_ACCUM_PREV_HIRES GRBM_GUI_ACTIVE GRBM_COUNT" \
            "TCC_HIT_sum TCC_MISS_sum TA_BUSY_avr TCP_TCC_READ_REQ_sum SQ_LDS_BANK_CONFLICT SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES"; do

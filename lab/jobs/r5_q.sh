@@ -10,7 +10,7 @@ timeout -k 10 200 python3 bench.py --batch 1 > $O/b1.json 2> $O/b1.err || exit 1
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 timeout -k 10 400 rocprofv3 --kernel-trace -d $O/prof -o run -- python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/b64_prof.json 2> $O/b64_prof.err || exit 1
 DB=$(find $O/prof -name "*.db" | head -1)
-python3 scripts/rocpd_steps.py $DB --steps 20 > $O/b64_kernels_per_step.txt && rm -f $DB
+python3 lab/tools/rocpd_steps.py $DB --steps 20 > $O/b64_kernels_per_step.txt && rm -f $DB
 for f in b64 b1; do python3 -c "
 import json
 r=json.loads([l for l in open('$O/$f.json') if l.startswith('{')][-1]); print('$f', r['ms_per_step'], r['value'])"; done

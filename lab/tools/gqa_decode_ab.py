@@ -7,7 +7,7 @@ kernel (csrc/attention_mfma.hip).  Prefill keeps the MFMA kernels either way.
 import os
 import sys
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 
 def main():

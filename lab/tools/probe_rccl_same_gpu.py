@@ -5,7 +5,7 @@ import sys
 import torch
 import torch.multiprocessing as mp
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 
 def run(rank, port, q):

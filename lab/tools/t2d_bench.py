@@ -18,7 +18,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from src import ops  # noqa: E402
 
 SHAPES = [("qkv", 12288, 4096, 0), ("o", 4096, 4096, 3), ("gate_up", 22016, 4096, 1), ("down", 4096, 11008, 3)]

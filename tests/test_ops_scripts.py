@@ -5,7 +5,7 @@ import subprocess
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SCRIPTS = ["deploy.sh", "auto_pull.sh", "setup_auto_pull.sh", "gpu_session.sh", "multi_bench.sh"]
+SCRIPTS = ["deploy.sh", "auto_pull.sh", "setup_auto_pull.sh"]
 
 
 @pytest.mark.parametrize("name", SCRIPTS)

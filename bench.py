@@ -538,6 +538,9 @@ def main(argv=None):
             "qkv_fold": {f"M{k}": bool(v) for k, v in sorted(ex.qkv_fold_by_bucket.items())},
             # the warm-up A/B behind it: (folded, unfolded) ms per step
             "qkv_fold_ab_ms": {f"M{k}": v for k, v in sorted(getattr(ex, "qkv_fold_ab_ms", {}).items())},
+            # the decode-kernel mix: the committed table (ops/tuned/decode_kernels_gfx950.json) this run
+            # loaded, the sha of the choices it actually ran, and any shape it had to time itself
+            **{k: v for k, v in ops.kernel_table_report().items()},
             "prefill_plus_first_token_s": round(prefill_s, 3),
             # the prefill round alone: every session's prompt through the whole pipeline
             # (micro-batch slots x batch x prompt-len tokens), max over ranks

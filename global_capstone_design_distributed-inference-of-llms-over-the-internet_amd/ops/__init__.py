@@ -232,6 +232,126 @@ def _use_sk(M: int, N: int, K: int, epilogue: int) -> bool:
 
 _TUNE_POOL_BYTES = 1 << 30
 
+# ---------------------------------------------------------------------------------------
+# Committed decode-kernel table (ops/tuned/decode_kernels_gfx950.json, written by
+# ``python -m src.ops.tune`` on an MI355X): the autotuners' per-shape choices and the
+# executors' end-to-end qkv-fold decisions.  Loaded by default, so two boxes running the same
+# tree run the same kernel mix (a start-up timing race used to pick a different kernel for 4 of
+# 35 Llama-2-7B shapes from box to box).  ``MPAMD_GEMM_AUTOTUNE``: "1" (default) times only
+# shapes the table lacks, "0" never times (untabled shapes take the first kernel), "force"
+# re-times every shape an executor uses.  ``MPAMD_KERNEL_TABLE``: another table, or "0" for none.
+KERNEL_TABLE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned", "decode_kernels_gfx950.json")
+_QKV_FOLD_PIN = {}  # (graph batch bucket, N, K, fp8) -> bool: the decode-graph A/B's decision
+_TABLE = {"path": None, "file_sha": None, "runtime": set()}
+
+
+def autotune_mode() -> str:
+    m = os.environ.get("MPAMD_GEMM_AUTOTUNE", "1")
+    return {"0": "off", "1": "missing", "force": "force"}.get(m, "missing")
+
+
+def _k4(k) -> str:
+    return f"M{k[0]}:N{k[1]}xK{k[2]}e{k[3]}"
+
+
+def _kfold(k, tag) -> str:
+    return f"{tag}{k[0]}:N{k[1]}xK{k[2]}:{'fp8' if k[3] else 'bf16'}"
+
+
+def _parse_key(s: str):
+    head, nk, last = (s.split(":") + [""])[:3]
+    n, k = nk[1:].split("xK")
+    if "e" in k:
+        k, e = k.split("e")
+        return int(head[1:]), int(n), int(k), int(e)
+    return int(head[1:]), int(n), int(k), last == "fp8"
+
+
+def kernel_table() -> dict:
+    """The decode-kernel choices this process currently runs, in the table's JSON form."""
+    return {"arch": "gfx950",
+            "gemm": {_k4(k): v for k, v in sorted(_SK_CHOICE.items())},
+            "w8": {_k4(k): v for k, v in sorted(_W8_CHOICE.items())},
+            "fp8": {_k4(k): v for k, v in sorted(_FP8_CHOICE.items())},
+            "qkv_fold_cand": {_kfold(k, "M"): bool(v) for k, v in sorted(_QKV_FOLD_CAND.items())},
+            "qkv_fold": {_kfold(k, "B"): bool(v) for k, v in sorted(_QKV_FOLD_PIN.items())}}
+
+
+def kernel_table_sha(table: Optional[dict] = None) -> str:
+    import hashlib
+    import json
+
+    body = json.dumps(table if table is not None else kernel_table(), sort_keys=True).encode()
+    return hashlib.sha256(body).hexdigest()[:16]
+
+
+def load_kernel_table(path: Optional[str] = None) -> Optional[str]:
+    """Load the committed choice table into the autotuners' dicts (entries already present -
+    tuned or loaded earlier in this process - are kept).  Returns the file's table sha, or None
+    when there is no table (``MPAMD_KERNEL_TABLE=0``, missing file).  Once per process."""
+    import json
+
+    if _TABLE["path"] is not None:
+        return _TABLE["file_sha"]
+    path = path or os.environ.get("MPAMD_KERNEL_TABLE") or KERNEL_TABLE
+    _TABLE["path"] = path
+    if path == "0" or not os.path.exists(path):
+        return None
+    with open(path) as f:
+        t = json.load(f)
+    for name, dst in (("gemm", _SK_CHOICE), ("w8", _W8_CHOICE), ("fp8", _FP8_CHOICE)):
+        for s, v in t.get(name, {}).items():
+            dst.setdefault(_parse_key(s), str(v))
+    for s, v in t.get("qkv_fold_cand", {}).items():
+        _QKV_FOLD_CAND.setdefault(_parse_key(s), bool(v))
+    for s, v in t.get("qkv_fold", {}).items():
+        _QKV_FOLD_PIN.setdefault(_parse_key(s), bool(v))
+    _TABLE["file_sha"] = kernel_table_sha(
+        {k: t.get(k, {}) for k in ("gemm", "w8", "fp8", "qkv_fold_cand", "qkv_fold")} | {"arch": "gfx950"})
+    return _TABLE["file_sha"]
+
+
+def save_kernel_table(path: str) -> str:
+    import json
+
+    t = kernel_table()
+    with open(path, "w") as f:
+        json.dump(t, f, indent=1, sort_keys=True)
+        f.write("\n")
+    return kernel_table_sha(t)
+
+
+def kernel_table_report() -> dict:
+    """For the bench JSON: the committed table's sha, the sha of the mix this process runs, and
+    the shapes timed at run time (not in the table; empty = the process ran the table as is)."""
+    return {"table": os.path.relpath(_TABLE["path"], os.path.dirname(os.path.abspath(__file__)))
+            if _TABLE["path"] not in (None, "0") else None,
+            "gemm_table_sha": _TABLE["file_sha"], "effective_sha": kernel_table_sha(),
+            "tuned_at_runtime": sorted(_TABLE["runtime"])}
+
+
+def _todo(table: dict, keys) -> list:
+    """Keys the autotuner must time under ``MPAMD_GEMM_AUTOTUNE`` (dropping them first on force)."""
+    mode = autotune_mode()
+    if mode == "off":
+        return []
+    if mode == "force":
+        for k in keys:
+            table.pop(k, None)
+    out = [k for k in keys if k not in table]
+    _TABLE["runtime"].update(_k4(k) if len(k) == 4 and not isinstance(k[3], bool) else _kfold(k, "M") for k in out)
+    return out
+
+
+def qkv_fold_pinned(bucket: int, N: int, K: int, fp8: bool) -> Optional[bool]:
+    if autotune_mode() == "force":
+        return None
+    return _QKV_FOLD_PIN.get((int(bucket), int(N), int(K), bool(fp8)))
+
+
+def pin_qkv_fold(bucket: int, N: int, K: int, fp8: bool, fold: bool) -> None:
+    _QKV_FOLD_PIN[(int(bucket), int(N), int(K), bool(fp8))] = bool(fold)
+
 
 def autotune_gemm(shapes, device, ms=(4, 16, 32, 48, 64), iters: int = 24, rounds: int = 3) -> dict:
     """Time every applicable decode-GEMM kernel (one-group, stream-K, shared-A variants) on each
@@ -251,7 +371,8 @@ def autotune_gemm(shapes, device, ms=(4, 16, 32, 48, 64), iters: int = 24, round
     pool = None
     try:
         for (N, K, epi) in shapes:
-            todo = [M for M in ms if (_m_bucket(M), N, K, int(epi)) not in _SK_CHOICE]
+            keys = _todo(_SK_CHOICE, list(dict.fromkeys((_m_bucket(M), N, K, int(epi)) for M in ms)))
+            todo = [M for M in dict((_m_bucket(M), M) for M in ms).values() if (_m_bucket(M), N, K, int(epi)) in keys]
             if not todo:
                 continue
             if pool is None:
@@ -954,6 +1075,10 @@ def autotune_qkv_fold(N: int, K: int, device, fp8: bool = False, ms=(16, 32, 48,
     device = torch.device(device)
     if device.type != "cuda" or os.environ.get("MPAMD_QKV_FOLD", "1") == "0":
         return {}
+    todo = _todo(_QKV_FOLD_CAND, [k for k in dict.fromkeys((_m_bucket(M), N, K, bool(fp8)) for M in ms)
+                                  if rwk_split(k[0], N, K, fp8) > 0])
+    if not todo:
+        return dict(_QKV_FOLD_CAND)
     copies = max(1, min(8, (1 << 30) // (N * K * (1 if fp8 else 2))))
     if fp8:
         ws = [torch.randint(0, 0x77, (N // 16, K // 32, 64, 8), dtype=torch.uint8, device=device)
@@ -963,7 +1088,7 @@ def autotune_qkv_fold(N: int, K: int, device, fp8: bool = False, ms=(16, 32, 48,
         ws = [(torch.randn(N // 16, K // 32, 64, 8, device=device) * 0.02).to(torch.bfloat16) for _ in range(copies)]
     for M in ms:
         key = (_m_bucket(M), N, K, bool(fp8))
-        if key in _QKV_FOLD_CAND or rwk_split(M, N, K, fp8) <= 0:
+        if key not in todo or key in _QKV_FOLD_CAND or rwk_split(M, N, K, fp8) <= 0:
             continue
         xp = pack_act(torch.randn(M, K, device=device).to(torch.bfloat16))
         y = torch.empty(M, N, dtype=torch.bfloat16, device=device)
@@ -1083,7 +1208,8 @@ def autotune_fp8(shapes, device, ms=(32, 48, 64), iters: int = 12, rounds: int =
     saved = _FP8_MODE
     try:
         for (N, K, epi) in shapes:
-            todo = [M for M in ms if (_m_bucket(M), N, K, int(epi)) not in _FP8_CHOICE]
+            keys = _todo(_FP8_CHOICE, list(dict.fromkeys((_m_bucket(M), N, K, int(epi)) for M in ms)))
+            todo = [M for M in dict((_m_bucket(M), M) for M in ms).values() if (_m_bucket(M), N, K, int(epi)) in keys]
             if not todo:
                 continue
             copies = max(1, min(8, (1 << 30) // (N * K)))
@@ -1206,7 +1332,8 @@ def autotune_w8(shapes, device, ms=(4, 16, 32, 48, 64), iters: int = 12, rounds:
     saved = _W8_MODE
     try:
         for (N, K, epi) in shapes:
-            todo = [M for M in ms if (_m_bucket(M), N, K, int(epi)) not in _W8_CHOICE]
+            keys = _todo(_W8_CHOICE, list(dict.fromkeys((_m_bucket(M), N, K, int(epi)) for M in ms)))
+            todo = [M for M in dict((_m_bucket(M), M) for M in ms).values() if (_m_bucket(M), N, K, int(epi)) in keys]
             if not todo:
                 continue
             # the ring form only (SwiGLU / narrow N) or all three, each also with the rotated k walk

@@ -137,6 +137,28 @@ class _EventWork:
         return self.ev.query()
 
 
+class _Waiter:
+    """``Channel.recv``'s completion: ``host_wait()`` blocks the host until the payload is here
+    (gloo; a no-op on the device backends, whose completion is a stream dependency), ``__call__``
+    finishes the hand-off on the current stream (stream wait, staging copy) and returns the tensor.
+    Split so that the blocking part can run outside a lock that serialises device work: a device
+    copy or allocation from this thread while another one captures a hipGraph would break that
+    capture."""
+
+    def __init__(self, host_wait, device):
+        self._host = host_wait
+        self._device = device
+
+    def host_wait(self) -> None:
+        if self._host is not None:
+            fn, self._host = self._host, None
+            fn()
+
+    def __call__(self):
+        self.host_wait()
+        return self._device()
+
+
 class _SlabRing:
     """Preallocated device byte slabs reused round-robin for RCCL payloads (no per-hop
     ``clone`` / ``empty``: the caching allocator and its cross-stream bookkeeping stay off the
@@ -295,19 +317,28 @@ class Channel:
     def recv(self, src: int, shape, dtype, which: str = "data", timeout_s: Optional[float] = None, into=None):
         """Post a receive; returns ``(tensor, waiter)``.  ``waiter()`` makes the tensor usable
         on the current stream: on RCCL it is a stream dependency (no host block), on gloo a
-        blocking wait bounded by the timeout.  ``into = (buffer, free_event)`` (direct RCCL only):
-        receive straight into ``buffer`` - a decode graph's static input - once ``free_event`` (its
-        last reader's completion, None = free now) has passed; other backends ignore it."""
+        blocking wait bounded by the timeout.  ``waiter.host_wait()`` does only the blocking host
+        part (nothing on the device): a caller may run it outside a lock that guards device work and
+        call ``waiter()`` under the lock.
+
+        ``into = (buffer, free_event)``: receive straight into ``buffer`` - e.g. the static input of
+        the decode graph the step will replay - once ``free_event`` (its last reader's completion,
+        None = free now) has passed.  Every backend honours it when shape and dtype match: RCCL and
+        ProcessGroupNCCL receive into it, host-staged gloo copies the host payload into it, CPU gloo
+        receives into it.  The returned tensor is then ``buffer`` itself."""
+        if into is not None and not (tuple(into[0].shape) == tuple(shape) and into[0].dtype == dtype and
+                                     into[0].is_contiguous() and into[0].device == self.device):
+            into = None
         if self._rc:
             return self._rccl_recv(src, shape, dtype, which, into)
         pg = self._pg(which)
         t = self.timeout_s if timeout_s is None else timeout_s
         try:
             if self.staged or self.device.type != "cuda":
-                host = torch.empty(shape, dtype=dtype)
+                host = into[0] if (into is not None and not self.staged) else torch.empty(shape, dtype=dtype)
                 work = pg.recv([host], src, 0)
 
-                def waiter():
+                def host_wait():
                     t0 = time.perf_counter()
                     try:
                         work.wait(_td(t))
@@ -315,16 +346,31 @@ class Channel:
                         raise ChannelError(f"{which} recv from {src} failed: {e}") from e
                     if self.timing:
                         self._wait_host_s.append(time.perf_counter() - t0)
-                    return host.to(self.device, non_blocking=False) if self.staged else host
 
-                return None, waiter
+                def device():
+                    if not self.staged:
+                        return host
+                    if into is None:
+                        return host.to(self.device, non_blocking=False)
+                    buf, free = into
+                    if free is not None:
+                        torch.cuda.current_stream().wait_event(free)
+                    buf.copy_(host)
+                    return buf
+
+                return (into[0] if into is not None else None), _Waiter(host_wait, device)
             ring = self._rings.get((which, "recv"))
-            if ring is not None:
+            k = None
+            if into is not None:
+                buf, free = into
+                if free is not None:  # ProcessGroupNCCL's stream waits for the current stream's work
+                    torch.cuda.current_stream().wait_event(free)
+            elif ring is not None:
                 k, buf = ring.take(tuple(shape), dtype)
             else:
                 buf = torch.empty(shape, dtype=dtype, device=self.device)
             work = pg.recv([buf], src, 0)
-            if ring is not None:
+            if k is not None:
                 ring.done(k, work)
 
             def waiter():
@@ -339,7 +385,7 @@ class Channel:
                     self._wait_events.append((e0, e1))
                 return buf
 
-            return buf, waiter
+            return buf, _Waiter(None, waiter)
         except RuntimeError as e:
             raise ChannelError(f"{which} recv from {src} failed: {e}") from e
 
@@ -400,8 +446,7 @@ class Channel:
         ring = self._rings[(which, "recv")]
         k = None
         try:
-            if into is not None and tuple(into[0].shape) == tuple(shape) and into[0].dtype == dtype and \
-                    into[0].is_contiguous():
+            if into is not None:
                 buf, free = into
                 if free is not None:  # the buffer's last reader (an earlier replay) must be done
                     st.wait_event(free)
@@ -431,7 +476,7 @@ class Channel:
                 self._wait_events.append((e0, e1))
             return buf
 
-        return buf, waiter
+        return buf, _Waiter(None, waiter)
 
     def stats(self, reset: bool = True) -> dict:
         """Hop statistics since the last reset: backend, payload bytes / sends, and the mean

@@ -767,24 +767,38 @@ class PipelineServingEngine:
             self.ch.send_msg(self.rank + 1, hdr)  # the successor plans while we compute
         recs = hdr[HDR:HDR + SEQ_REC * n_seq].reshape(n_seq, SEQ_REC)
         closes = hdr[HDR + SEQ_REC * n_seq:HDR + SEQ_REC * n_seq + n_close]
-        x = None
+        x = waiter = None
+        rows = T
         if n_seq:
-            # the payload wait happens OUTSIDE exec_lock: a predecessor that dies between its header
-            # and its payload leaves this thread blocked here until the channel times out or is
-            # aborted, and the executor must stay usable meanwhile (stage-local recovery adopts this
-            # channel's sessions into a new one, the TCP handler keeps serving)
+            # the payload's HOST wait happens outside exec_lock: a predecessor that dies between its
+            # header and its payload leaves this thread blocked here until the channel times out or
+            # is aborted, and the executor must stay usable meanwhile (stage-local recovery adopts
+            # this channel's sessions into a new one, the TCP handler keeps serving).  Everything
+            # that touches the device (stream waits, staging copies) runs under the lock: another
+            # thread may be capturing a decode graph.
             is_dec = bool((recs[:, 1] == 1).all())
             rows = self._hop_rows(T, is_dec)
             into = None
-            if self.graph_hop and is_dec:  # straight into the static input of the graph this step replays
-                into = self.ex.graph_input(T, int((recs[:, 2] + recs[:, 1]).max()), owner=self)
+            if is_dec and self.ex.graph_rows(T, True) is not None:
+                # straight into the static input of the decode graph this step replays (every
+                # backend: no receive slab, no copy into the graph input)
+                got = self.ex.graph_input(T, int((recs[:, 2] + recs[:, 1]).max()), owner=self)
+                if got is not None:
+                    into = (got[0][:rows], got[1])
+            # (posting the receive stays outside the lock too: a first RCCL receive can block on its
+            # peer's connection set-up; decode graphs are captured in thread-local mode, so this
+            # thread's stream calls never invalidate another thread's capture)
             _, waiter = self.ch.recv(self.rank - 1, (rows, self.H), self.ex.dtype, into=into)
-            x = waiter()
-            if x is not None and rows != T:
-                x = x[:T]
+            hw = getattr(waiter, "host_wait", None)
+            if hw is not None:
+                hw()
         if self.ch.closed:
             raise ChannelError("channel aborted while waiting for a payload")
         with self.ex.exec_lock:
+            if waiter is not None:
+                x = waiter()
+                if x is not None and rows != T:
+                    x = x[:T]
             for c in closes:  # before the compute: a closed handle may be re-admitted in this very step
                 self.ex.sessions.close(self._key(int(c)))
             if n_seq:
@@ -813,6 +827,7 @@ class PipelineServingEngine:
         send (idempotent; stop / failure / end of ``serve`` call it, so a shared executor never
         replays a send on a closed communicator)."""
         self.ex.clear_graph_hook(self)
+        self.ex.release_owner(self)
 
     def run_rounds(self, n: int) -> None:
         """n rounds x M slot-steps on every rank (lock-step unit of the benchmark)."""

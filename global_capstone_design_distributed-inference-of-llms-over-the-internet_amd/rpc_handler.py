@@ -250,16 +250,36 @@ class StageConnectionHandler:
                 with self._chan_lock:
                     if eng.failed is None or not eng.park_on_fail:
                         self._chan_engines.pop(name, None)
-                    dead = [k for k, e in self._chan_engines.items() if getattr(e, "failed", None) is not None]
-                    # keep only the newest failed channel nobody adopted: each holds a replay cache of
-                    # max_handles x max_len x hidden in HBM that the KV capacity exchange never counted
-                    for k in dead[:-1]:
-                        self._chan_engines.pop(k).replay = None
+                    if eng.failed is not None:
+                        eng.failed_at = time.monotonic()
+                    self._prune_failed_channels()
             with ex.exec_lock:  # (parked sessions - ``park:`` keys - wait for adoption or the session TTL)
                 for sid in [k for k in ex.sessions.sessions if k.startswith(name + ":")]:
                     ex.sessions.close(sid)
             if ch is not None:
                 ch.close()
+
+    # failed, not-yet-adopted channels keep their replay cache (max_handles x max_len x hidden in HBM,
+    # outside the KV capacity exchange) for the client's stage-local recovery: bounded by age and bytes
+    replay_keep_s = 300.0
+    replay_keep_bytes = 8 << 30
+
+    def _prune_failed_channels(self, now: Optional[float] = None) -> None:
+        """Drop the replay caches of failed channels nobody adopted: older than ``replay_keep_s``,
+        then the oldest ones while the kept caches exceed ``replay_keep_bytes`` (several clients
+        failing close together each keep theirs up to that budget).  Caller holds ``_chan_lock``."""
+        now = time.monotonic() if now is None else now
+        dead = sorted(((getattr(e, "failed_at", now), k) for k, e in self._chan_engines.items()
+                       if getattr(e, "failed", None) is not None), reverse=True)  # newest first
+        kept = 0
+        for at, k in dead:
+            e = self._chan_engines[k]
+            rc = getattr(e, "replay", None)
+            n = rc.buf.numel() * rc.buf.element_size() if rc is not None else 0
+            if now - at > self.replay_keep_s or kept + n > self.replay_keep_bytes:
+                self._chan_engines.pop(k).replay = None
+            else:
+                kept += n
 
     async def rpc_push(self, msg: Message) -> Message:
         """Server-to-server hop of a pushed chain (upstream ``rpc_push``); same body as rpc_forward."""

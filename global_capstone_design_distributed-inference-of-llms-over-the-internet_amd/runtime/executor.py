@@ -24,6 +24,7 @@ import logging
 import math
 import os
 import threading
+import weakref
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -180,8 +181,15 @@ class StageExecutor:
         self.graph_max_batch = graph_max_batch
         self._graphs: Dict[tuple, "_DecodeGraph"] = {}
         self._graph_pool = None
-        self._recv_slot: Dict[tuple, int] = {}  # graph_input: last receive graph handed out per key
-        self._recv_pin = None                   # (owner, graph key) the owner's next step replays
+        # graph_input: receive graphs are per OWNER (a channel engine): two engines sharing this
+        # executor never hand each other's hidden states to a replay.  Owner -> small tag (part of
+        # the graph key); (tag, base key) -> last receive slot handed out; tag -> (key, graph) its
+        # next step replays
+        self._owner_tags = weakref.WeakKeyDictionary()
+        self._owner_strong: Dict[int, tuple] = {}
+        self._next_tag = 1
+        self._recv_slot: Dict[tuple, int] = {}
+        self._recv_pin: Dict[int, tuple] = {}
         # qkv fold per decode-graph batch bucket (_confirm_qkv_fold's end-to-end A/B on THIS executor)
         self.qkv_fold_by_bucket: Dict[int, bool] = {}
         self._pinned = _Pinned(2 * max_tokens_per_step, 2 * max_tokens_per_step + max_sessions, self.device)
@@ -254,7 +262,8 @@ class StageExecutor:
                 ops.use_tuned_gemms()  # library GEMM solutions for the row-major shapes
                 ops.gemm_workspace(self.device)  # allocated before any hipGraph capture
                 ops.attention_counters(self.device)
-                if os.environ.get("MPAMD_GEMM_AUTOTUNE", "1") != "0":
+                ops.load_kernel_table()  # the committed per-shape kernel choices (ops.KERNEL_TABLE)
+                if ops.autotune_mode() != "off":
                     H, F = cfg.hidden_size, cfg.intermediate_size
                     shapes = [] if (weights.fp8 or not weights.layers) else \
                         [(cfg.q_dim + 2 * cfg.kv_dim, H, 0), (H, cfg.q_dim, 0), (2 * F, H, 1), (H, F, 0)]
@@ -775,6 +784,11 @@ class StageExecutor:
                 out = self.forward([(s, prompt_len) for s in sids], x, reset=[True] * batch)
                 if self.is_last:
                     self._warm_sampler(out)
+                cfg = self.cfg
+                pin = ops.qkv_fold_pinned(self._bucket(batch), cfg.q_dim + 2 * cfg.kv_dim, cfg.hidden_size,
+                                          bool(self._w8))
+                if pin is not None and cfg.model_type != "gpt2":
+                    self.qkv_fold_by_bucket[self._bucket(batch)] = pin  # capture the pinned variant below
                 for _ in range(decode_steps):
                     if self.is_first:
                         x = torch.randint(0, self.cfg.vocab_size, (batch,), device=self.device, generator=gen)
@@ -807,9 +821,17 @@ class StageExecutor:
         windows see the same clock / thermal state."""
         B = len(sids)
         cfg = self.cfg
-        key = (ops._m_bucket(B), cfg.q_dim + 2 * cfg.kv_dim, cfg.hidden_size, bool(self._w8))
-        if not self.use_graphs or B > self.graph_max_batch or not ops._QKV_FOLD_CAND.get(key) or \
-                not (self._fuse_rope and self._fused) or os.environ.get("MPAMD_QKV_FOLD", "1") == "0":
+        N = cfg.q_dim + 2 * cfg.kv_dim
+        key = (ops._m_bucket(B), N, cfg.hidden_size, bool(self._w8))
+        if not self.use_graphs or B > self.graph_max_batch or not (self._fuse_rope and self._fused) or \
+                os.environ.get("MPAMD_QKV_FOLD", "1") == "0":
+            return None
+        Bb = self._bucket(B)
+        pinned = ops.qkv_fold_pinned(Bb, N, cfg.hidden_size, bool(self._w8))
+        if pinned is not None:  # the committed table's decision for this bucket: no timing race
+            self.qkv_fold_by_bucket[Bb] = pinned
+            return None
+        if not ops._QKV_FOLD_CAND.get(key) or ops.autotune_mode() == "off":
             return None
         H = cfg.hidden_size
 
@@ -820,7 +842,6 @@ class StageExecutor:
                 x = (0.1 * torch.randn(B, H, device=self.device, generator=gen)).to(self.dtype)
             self.forward([(s, 1) for s in sids], x)
 
-        Bb = self._bucket(B)
         t = {True: 0.0, False: 0.0}
         order = (True, False, False, True, True, False, False, True)
         for fold in order:
@@ -838,6 +859,7 @@ class StageExecutor:
         # tie costs nothing either way)
         keep = t[True] < t[False]
         self.qkv_fold_by_bucket[Bb] = keep
+        ops.pin_qkv_fold(Bb, N, cfg.hidden_size, bool(self._w8), keep)  # (ops.save_kernel_table keeps it)
         self.__dict__.setdefault("qkv_fold_ab_ms", {})[Bb] = (round(t[True], 4), round(t[False], 4))
         for k in [k for k in self._graphs if k[0] == Bb and k[3] != keep]:
             del self._graphs[k]
@@ -1052,13 +1074,14 @@ class StageExecutor:
         c = max(c, 256)
         return 1 << (c - 1).bit_length()
 
-    def _graph_key(self, T: int, max_ctx: int, hooked: bool, slot: int = 0) -> tuple:
-        """(batch bucket, attention part size, parts, qkv fold, hooked, input slot).  Input slot 0 is
-        the graph every caller replays; 1 / 2 are a stage hop's two receive graphs (``graph_input``)."""
+    def _graph_key(self, T: int, max_ctx: int, hooked: bool, slot: int = 0, tag: int = 0) -> tuple:
+        """(batch bucket, attention part size, parts, qkv fold, hooked, owner tag, input slot).  Slot 0
+        (tag 0) is the graph every caller replays; slots 1 / 2 are an owner's two receive graphs
+        (``graph_input``)."""
         B = self._bucket(T)
         ctxb = min(self._ctx_bucket(max_ctx), self._ctx_bucket(self.max_seq_len))
         part = ops.attention_partition(B, self.nkv, ctxb, min_part=self._attn_min_part)
-        return (B, part[0], part[1], self._qkv_fold(B), bool(hooked), int(slot))
+        return (B, part[0], part[1], self._qkv_fold(B), bool(hooked), int(tag), int(slot))
 
     def _graph(self, key: tuple) -> "_DecodeGraph":
         g = self._graphs.get(key)
@@ -1071,35 +1094,75 @@ class StageExecutor:
 
     def _run_graph(self, plan: Plan, x: torch.Tensor, hooked: bool = False, owner=None) -> torch.Tensor:
         key = self._graph_key(plan.T, plan.max_ctx, hooked)
-        pin = self._recv_pin
-        if pin is not None and pin[0] is owner and owner is not None:
-            self._recv_pin = None
-            if pin[1][:5] == key[:5]:
-                key = pin[1]  # the receive graph whose static input the hop landed in
+        read = None  # a receive graph whose static input this replay reads without being that graph
+        tag = self._tag_of(owner)
+        pin = self._recv_pin.pop(tag, None) if tag is not None else None
+        if pin is not None:
+            pkey, pg = pin
+            if pkey[:5] == key[:5] and self._graphs.get(pkey) is pg:
+                key = pkey  # the receive graph whose static input the hop landed in
+            else:  # (step shape changed, or the graph was dropped meanwhile): copied from its input
+                read = pg
         g = self._graph(key)
         out = g.replay(plan, x)
         g.mark_replayed()
+        if read is not None:  # the next receive into that buffer must wait for this replay's copy
+            read.done_ev = g.done_ev
         return out
 
     def graph_input(self, T: int, max_ctx: int, owner=None):
-        """Receive target of a stage hop (``PipelineServingEngine`` with the graph hop): the static
-        input of the decode graph the owner's NEXT step of ``T`` rows will replay, and the event after
-        which that buffer is free (the end of its last replay), or None when that step runs eagerly.
-        The hidden states then land where the graph reads them: no receive slab, no copy.  Two
-        receive graphs per bucket alternate, so the hop of step k lands in one while step k - 1
-        still replays the other (a single buffer would serialise every receive behind the previous
-        step's compute); other callers of the executor never replay them."""
+        """Receive target of a stage hop (``PipelineServingEngine``): the static input of the decode
+        graph the owner's NEXT step of ``T`` rows will replay, and the event after which that buffer
+        is free (the end of its last replay), or None when that step runs eagerly.  The hidden
+        states then land where the graph reads them: no receive slab, no copy.  Two receive graphs
+        per (owner, bucket) alternate, so the hop of step k lands in one while step k - 1 still
+        replays the other (a single buffer would serialise every receive behind the previous step's
+        compute); other callers of the executor - other owners included - never replay them."""
         if self.is_first or not (self.use_graphs and T <= self.graph_max_batch) or owner is None:
             return None
         with self.exec_lock:
+            tag = self._tag_of(owner)
+            if tag is None:
+                tag = self._next_tag
+                self._next_tag += 1
+                try:
+                    self._owner_tags[owner] = tag
+                except TypeError:  # an owner without weak references: kept alive until release_owner
+                    self._owner_strong[id(owner)] = (owner, tag)
             hooked = self.graph_hook is not None and owner is self._hook_owner
             base = self._graph_key(T, max_ctx, hooked)
-            slot = 3 - self._recv_slot.get(base, 2)  # 1, 2, 1, ...
-            self._recv_slot[base] = slot
-            key = base[:5] + (slot,)
+            sk = (tag,) + base[:5]
+            slot = 3 - self._recv_slot.get(sk, 2)  # 1, 2, 1, ...
+            self._recv_slot[sk] = slot
+            key = base[:5] + (tag, slot)
             g = self._graph(key)
-            self._recv_pin = (owner, key)
+            self._recv_pin[tag] = (key, g)
             return g.x, g.done_ev
+
+    def _tag_of(self, owner) -> Optional[int]:
+        if owner is None:
+            return None
+        try:
+            return self._owner_tags.get(owner)
+        except TypeError:
+            got = self._owner_strong.get(id(owner))
+            return got[1] if got is not None and got[0] is owner else None
+
+    def release_owner(self, owner) -> None:
+        """Drop ``owner``'s receive graphs and pins (its engine stopped or failed)."""
+        with self.exec_lock:
+            tag = self._tag_of(owner)
+            if tag is None:
+                return
+            try:
+                self._owner_tags.pop(owner, None)
+            except TypeError:
+                self._owner_strong.pop(id(owner), None)
+            self._recv_pin.pop(tag, None)
+            for k in [k for k in self._recv_slot if k[0] == tag]:
+                del self._recv_slot[k]
+            for k in [k for k in self._graphs if k[5] == tag]:
+                del self._graphs[k]
 
     def graph_rows(self, T: int, is_decode: bool) -> Optional[int]:
         """Rows of the static output a step of ``T`` tokens would replay into (its batch bucket),
@@ -1185,7 +1248,9 @@ class _DecodeGraph:
                 ex._forward_llama(*args, decode=True)
         torch.cuda.current_stream().wait_stream(s)
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph, pool=pool):
+        # thread-local capture: another thread's stream work (a channel receive posted outside the
+        # executor lock) neither breaks this capture nor fails because of it
+        with torch.cuda.graph(self.graph, pool=pool, capture_error_mode="thread_local"):
             self.out = ex._forward_llama(*args, decode=True)
             if hook is not None:  # recorded only: the warm-up runs above never call it
                 hook(self.out)

@@ -7,6 +7,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
+# Every GPU test (and every process a test spawns) runs the committed decode-kernel table
+# (ops/tuned/decode_kernels_gfx950.json) instead of re-timing kernels at start-up: the kernel mix
+# is then the same on every box, not the winner of a timing race on this one.
+os.environ.setdefault("MPAMD_GEMM_AUTOTUNE", "0")
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU and the built HIP kernels")

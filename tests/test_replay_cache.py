@@ -58,3 +58,22 @@ def test_replay_cache_on_gpu_pinned_staging():
     torch.cuda.synchronize()
     assert torch.equal(rc.buf.cpu(), ref)
     assert torch.equal(rc.rows(3, 40).cpu(), ref[3 * 64: 3 * 64 + 40])
+
+
+def test_failed_channel_replay_caches_bounded_by_age_and_bytes():
+    """two client pipelines failing close together both keep their replay rows (the
+    handler used to keep only the newest); caches past the age or byte budget are dropped, oldest
+    first."""
+    import types
+
+    from src.rpc_handler import StageConnectionHandler
+
+    def eng(failed_at, nbytes):
+        rc = types.SimpleNamespace(buf=torch.zeros(nbytes // 4, dtype=torch.float32))
+        return types.SimpleNamespace(failed="peer died", failed_at=failed_at, replay=rc)
+
+    h = types.SimpleNamespace(replay_keep_s=300.0, replay_keep_bytes=1000,
+                              _chan_engines={"a": eng(100.0, 400), "b": eng(110.0, 400), "c": eng(120.0, 400),
+                                             "old": eng(-500.0, 4), "live": types.SimpleNamespace(failed=None)})
+    StageConnectionHandler._prune_failed_channels(h, now=130.0)
+    assert set(h._chan_engines) == {"b", "c", "live"}  # newest two fit 1000 bytes; "a" over budget, "old" aged

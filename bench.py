@@ -296,6 +296,9 @@ def main(argv=None):
                          "headline line with phase2 = timeout)")
     ap.add_argument("--phase2-hop-timeout", type=float, default=60.0,
                     help="second phase: timeout of every channel wait (a dead or stuck peer becomes a failure)")
+    ap.add_argument("--phase2-recv-into", default="on", choices=["on", "off"],
+                    help="second phase: receive decode hops straight into the graph input (on) or through a "
+                         "receive slab + copy (off) - with the headline on, 'off' checks both give the same tokens")
     ap.add_argument("--phase2-inject", default="none", choices=["none", "init", "run"],
                     help="test hook: make the second phase fail on the last stage rank at communicator set-up "
                          "(init) or in the middle of its timed steps (run)")
@@ -467,6 +470,7 @@ def main(argv=None):
     if ch is not None:
         ch.timing = False
     stage_ms = eng.stage_ms() or 0.0
+    recv_into = (eng.recvs_into, eng.recvs)  # (into a graph input, all) payload receives, whole run
     hop = ch.stats() if ch is not None else {"backend": "none", "bytes_sent": 0, "sends": 0, "recv_wait_ms": 0.0}
     data_plane = data_plane_name(ch, eng)
     n_tokens = 0
@@ -483,7 +487,8 @@ def main(argv=None):
     dt = pdist.all_max(dt_local, device)
     counted = float(n_sessions) if (stage == 0 and lane % TP == 0) else 0.0  # TP lanes mirror one replica
     per_stage = pdist.all_gather_floats([stage_ms, float(end - start), counted, float(hop["bytes_sent"]),
-                                         float(hop["sends"]), float(hop["recv_wait_ms"])], device)
+                                         float(hop["sends"]), float(hop["recv_wait_ms"]), float(recv_into[0]),
+                                         float(recv_into[1])], device)
     global_batch = int(sum(p[2] for p in per_stage))
     n_sessions_total = global_batch
     tokens = a.steps * global_batch  # every session advances one token per round
@@ -534,6 +539,10 @@ def main(argv=None):
             "hop_bytes_sent_per_rank": [int(p[3]) for p in per_stage],
             "hop_sends_per_rank": [int(p[4]) for p in per_stage],
             "hop_recv_wait_ms_per_rank": [round(p[5], 4) for p in per_stage],
+            # payload receives that landed straight in the static input of the decode graph the step
+            # replayed, per rank: [into graph input, all receives] over the whole run (decode steps
+            # only: prefill chunks run eagerly, so they always take a receive slab)
+            "hop_recv_into_graph_per_rank": [[int(p[6]), int(p[7])] for p in per_stage],
             # the qkv fold per decode row bucket, as the warm-up's decode-graph A/B left it
             "qkv_fold": {f"M{k}": bool(v) for k, v in sorted(ex.qkv_fold_by_bucket.items())},
             # the warm-up A/B behind it: (folded, unfolded) ms per step
@@ -665,8 +674,10 @@ def run_phase2(a, backend: str, ctx: dict) -> dict:
         where = "warmup"
         eng2 = PipelineServingEngine(ex, ch2, n_slots=M, batch=B, max_step_tokens=B * a.prompt_len,
                                      timeout_s=a.phase2_hop_timeout, name=f"q{lane}")
+        eng2.recv_into = a.phase2_recv_into == "on"
         out["data_plane"] = data_plane_name(ch2, eng2)
         out["graph_hop"] = bool(eng2.graph_hop)
+        out["recv_into"] = eng2.recv_into
         reqs2 = []
         if stage == 0:
             for r in ctx["reqs1"]:
@@ -704,9 +715,10 @@ def run_phase2(a, backend: str, ctx: dict) -> dict:
             ch2.abort()
     try:
         rows = agree([ok, dt_local, float(hop["bytes_sent"]), float(hop["sends"]),
-                      float(bool(tokens_match)) if tokens_match is not None else -1.0])
+                      float(bool(tokens_match)) if tokens_match is not None else -1.0,
+                      float(eng2.recvs_into if eng2 is not None else 0), float(eng2.recvs if eng2 is not None else 0)])
     except Exception as e:  # noqa: BLE001
-        rows = [[0.0, 0.0, 0.0, 0.0, -1.0]]
+        rows = [[0.0, 0.0, 0.0, 0.0, -1.0, 0.0, 0.0]]
         reason = reason or f"rank {rank}: agreement failed: {e}"
     link.close()
     if not all(r[0] for r in rows):
@@ -718,6 +730,7 @@ def run_phase2(a, backend: str, ctx: dict) -> dict:
     out.update(ok=True, value=round(a.steps * n_sess / dt, 2) if n_sess else None,
                ms_per_step=round(1000 * dt / a.steps, 3), steps=a.steps, warmup=a.warmup,
                hop_bytes_sent_per_rank=[int(r[2]) for r in rows], hop_sends_per_rank=[int(r[3]) for r in rows],
+               hop_recv_into_graph_per_rank=[[int(r[5]), int(r[6])] for r in rows],
                tokens_match_headline=bool(tokens_match) if tokens_match is not None else None,
                sessions_compared=n_cmp)
     return out

@@ -406,6 +406,11 @@ class PipelineServingEngine:
         self.failed: Optional[str] = None
         self.rounds = 0
         self.steps_run = 0
+        # decode-step hops received straight into the static input of the graph the step replays
+        # (``StageExecutor.graph_input``; every channel backend honours it) vs a receive slab + copy:
+        # ``MPAMD_RECV_INTO=0`` (or ``recv_into = False``) keeps the copy path.  Counted per engine.
+        self.recv_into = os.environ.get("MPAMD_RECV_INTO", "1") != "0"
+        self.recvs = self.recvs_into = 0
         if self.is_tail:
             self.sampler = TailSampler(self.dev, self.max_handles, executor.cfg.vocab_size)
         if self.is_head:
@@ -779,7 +784,7 @@ class PipelineServingEngine:
             is_dec = bool((recs[:, 1] == 1).all())
             rows = self._hop_rows(T, is_dec)
             into = None
-            if is_dec and self.ex.graph_rows(T, True) is not None:
+            if is_dec and (self.recv_into or self.graph_hop) and self.ex.graph_rows(T, True) is not None:
                 # straight into the static input of the decode graph this step replays (every
                 # backend: no receive slab, no copy into the graph input)
                 got = self.ex.graph_input(T, int((recs[:, 2] + recs[:, 1]).max()), owner=self)
@@ -788,7 +793,9 @@ class PipelineServingEngine:
             # (posting the receive stays outside the lock too: a first RCCL receive can block on its
             # peer's connection set-up; decode graphs are captured in thread-local mode, so this
             # thread's stream calls never invalidate another thread's capture)
-            _, waiter = self.ch.recv(self.rank - 1, (rows, self.H), self.ex.dtype, into=into)
+            t, waiter = self.ch.recv(self.rank - 1, (rows, self.H), self.ex.dtype, into=into)
+            self.recvs += 1
+            self.recvs_into += int(into is not None and t is into[0])
             hw = getattr(waiter, "host_wait", None)
             if hw is not None:
                 hw()

@@ -45,6 +45,17 @@
 #define MP_KV_LOAD(p) (*(p))
 #endif
 
+// minimum waves per SIMD the decode attention's register allocation must allow (4: 128 VGPRs; the
+// dot2 form needs 122, the round-5 form 124) - an ablation knob for MPAMD_HIPCC_EXTRA lab builds
+#ifndef MP_ATTN_MINW
+#define MP_ATTN_MINW 4
+#endif
+// waves per workgroup of the flash-decoding kernel, picked per launch from the grid size (below);
+// MP_ATTN_NW forces 4 or 8 (lab builds)
+#ifndef MP_ATTN_NW
+#define MP_ATTN_NW 0
+#endif
+
 namespace mp {
 
 template <int CTRL>
@@ -60,6 +71,15 @@ __device__ __forceinline__ float group_sum(float v) {
   v += dpp_mov<0x141>(v);  // row_half_mirror      (8-lane total)
   if constexpr (LPT == 16) v += dpp_mov<0x140>(v);  // row_mirror (16-lane total)
   return v;
+}
+
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4a;
+
+// c + a.lo * b.lo + a.hi * b.hi over packed bf16 pairs (v_dot2c_f32_bf16: fp32 accumulate, no
+// bf16 -> fp32 unpacking of either operand)
+__device__ __forceinline__ float dot2bf(unsigned a, unsigned b, float c) {
+  typedef __attribute__((ext_vector_type(2))) __bf16 v2bf;
+  return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(v2bf, a), __builtin_bit_cast(v2bf, b), c, false);
 }
 
 struct RopeFuse {
@@ -169,11 +189,12 @@ __device__ __forceinline__ void split_combine(int* cnt_slot, int NP, const float
 // while the current one computes (no dependent page-table round trip on the critical path).  The
 // 4 token groups of a wave merge by xor shuffles, the 4 waves through LDS (rescaled by their
 // maxima), and the output / split-K partials (o, m, l) have the two-pass kernel's format.
-// NW = waves per workgroup, PIPE = software-pipelined K / V stream: the launcher uses (4, true).
+// NW = waves per workgroup (4 or 8 by grid size, launch_attn), PIPE = software-pipelined K / V
+// stream (always on).
 // (16-wave workgroups for small grids stopped paying once the 4-wave form was pipelined,
 // profiles/r4o; the unpipelined form measured slower: both removed.)
 template <int D, int NREP, bool ROPE, int NW, bool PIPE, int U = 4>
-__global__ __launch_bounds__(NW * 64) void paged_attn1_kernel(
+__global__ __launch_bounds__(NW * 64, MP_ATTN_MINW) void paged_attn1_kernel(
     const bf16_t* __restrict__ q, int64_t q_stride, const bf16_t* __restrict__ kc,
     const bf16_t* __restrict__ vc, const int32_t* __restrict__ block_tables, int bt_stride,
     const int32_t* __restrict__ q_seq, const int32_t* __restrict__ q_ctx, bf16_t* __restrict__ out,
@@ -181,6 +202,7 @@ __global__ __launch_bounds__(NW * 64) void paged_attn1_kernel(
     float scale_log2, int packed_mt, RopeFuse rf, int* __restrict__ cnt) {
   constexpr int LPT = D / 8;
   constexpr int TPI = 64 / LPT;
+  static_assert(U % 2 == 0, "P V pairs the tokens u, u + 1");
   // U: tokens per lane group per iteration (U = 8 measured 32 -> 43 us at 64 x 170, profiles/r4d)
   constexpr int TPW = TPI * U;
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -248,7 +270,9 @@ __global__ __launch_bounds__(NW * 64) void paged_attn1_kernel(
     issue(start + w * TPW, pgn, kv, vv);
   }
 
-  float qf[NREP][8];
+  // q as packed bf16 pairs, unscaled (the log2 softmax scale goes on the reduced score): the QK
+  // dot products run on v_dot2c_f32_bf16 straight from the bf16 K lanes
+  u32x4a qp[NREP];
   u16x8 kn = (u16x8)(0), vn = (u16x8)(0);
   int tnew = -1;
   if constexpr (ROPE) {
@@ -263,11 +287,7 @@ __global__ __launch_bounds__(NW * 64) void paged_attn1_kernel(
       __shared__ u16x8 s_fold[(NREP + 2) * LPT];
       fold_qkv_lds<D, NREP>(rf, t, hbase, g, nh, nkv, qkv_part_scale(rf.qp, t), s_fold);
 #pragma unroll
-      for (int r = 0; r < NREP; ++r) {
-        const u16x8 v = s_fold[r * LPT + sl];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) qf[r][j] = bf2f(v[j]) * scale_log2;
-      }
+      for (int r = 0; r < NREP; ++r) qp[r] = __builtin_bit_cast(u32x4a, s_fold[r * LPT + sl]);
       kn = s_fold[NREP * LPT + sl];
       vn = s_fold[(NREP + 1) * LPT + sl];
     } else {
@@ -282,11 +302,7 @@ __global__ __launch_bounds__(NW * 64) void paged_attn1_kernel(
         return rope8(me, ot, ca, cb, sa, sb, lo);
       };
 #pragma unroll
-      for (int r = 0; r < NREP; ++r) {
-        const u16x8 v = rot((hbase + r) * D);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) qf[r][j] = bf2f(v[j]) * scale_log2;
-      }
+      for (int r = 0; r < NREP; ++r) qp[r] = __builtin_bit_cast(u32x4a, rot((hbase + r) * D));
       kn = rot((nh + g) * D);
       vn = *reinterpret_cast<const u16x8*>(row + (nh + nkv + g) * D + sl * 8);
     }
@@ -300,11 +316,8 @@ __global__ __launch_bounds__(NW * 64) void paged_attn1_kernel(
     }
   } else {
 #pragma unroll
-    for (int r = 0; r < NREP; ++r) {
-      const u16x8 v = *reinterpret_cast<const u16x8*>(q + (int64_t)t * q_stride + (hbase + r) * D + sl * 8);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) qf[r][j] = bf2f(v[j]) * scale_log2;
-    }
+    for (int r = 0; r < NREP; ++r)
+      qp[r] = *reinterpret_cast<const u32x4a*>(q + (int64_t)t * q_stride + (hbase + r) * D + sl * 8);
   }
 
   float m[NREP], l[NREP], acc[NREP][8];
@@ -317,11 +330,15 @@ __global__ __launch_bounds__(NW * 64) void paged_attn1_kernel(
   }
   auto compute = [&](int base, u16x8 (&kv)[U], u16x8 (&vv)[U]) {
     if constexpr (ROPE) {
+      // the new token's k / v from registers (its cache slot is written by this very launch):
+      // only the wave iteration that holds it pays the selects (a wave-uniform branch)
+      if (tnew >= base && tnew < base + TPW) {
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int tok = base + u * TPI + tg;
-        kv[u] = tok == tnew ? kn : kv[u];
-        vv[u] = tok == tnew ? vn : vv[u];
+        for (int u = 0; u < U; ++u) {
+          const int tok = base + u * TPI + tg;
+          kv[u] = tok == tnew ? kn : kv[u];
+          vv[u] = tok == tnew ? vn : vv[u];
+        }
       }
     }
 #pragma unroll
@@ -330,24 +347,35 @@ __global__ __launch_bounds__(NW * 64) void paged_attn1_kernel(
         float mx = m[r];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-          float d = 0.f;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) d += qf[r][j] * bf2f(kv[u][j]);
-          d = group_sum<LPT>(d);
+          const u32x4a kw = __builtin_bit_cast(u32x4a, kv[u]);
+          float d0 = dot2bf(qp[r][0], kw[0], 0.f), d1 = dot2bf(qp[r][1], kw[1], 0.f);
+          d0 = dot2bf(qp[r][2], kw[2], d0);
+          d1 = dot2bf(qp[r][3], kw[3], d1);
+          const float d = group_sum<LPT>(d0 + d1) * scale_log2;
           s[u] = base + u * TPI + tg < end ? d : -INFINITY;
           mx = fmaxf(mx, s[u]);
         }
         const float mref = mx == -INFINITY ? 0.f : mx;
-        const float sc = exp2f(m[r] - mref);
+        const float sc = __builtin_amdgcn_exp2f(m[r] - mref);
         l[r] *= sc;
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc[r][j] *= sc;
+        // P V two tokens at a time: the probabilities of tokens u, u + 1 as one bf16 pair (the FA2
+        // convention: P rounds to bf16 for the PV product; l sums the same rounded values), the
+        // two tokens' V elements paired by v_perm_b32, one v_dot2c_f32_bf16 per output element
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const float pr = exp2f(s[u] - mref);
-          l[r] += pr;
+        for (int u = 0; u < U; u += 2) {
+          // (v_exp_f32 directly: the arguments are <= 0, exp2(-inf) = 0; a result below the fp32
+          // normal range is 0 for bf16 P anyway)
+          const bf16_t b0 = f2bf(__builtin_amdgcn_exp2f(s[u] - mref)), b1 = f2bf(__builtin_amdgcn_exp2f(s[u + 1] - mref));
+          l[r] += bf2f(b0) + bf2f(b1);
+          const unsigned pp = (unsigned)b0 | ((unsigned)b1 << 16);
+          const u32x4a v0 = __builtin_bit_cast(u32x4a, vv[u]), v1 = __builtin_bit_cast(u32x4a, vv[u + 1]);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) acc[r][j] += pr * bf2f(vv[u][j]);
+          for (int jj = 0; jj < 4; ++jj) {
+            acc[r][2 * jj] = dot2bf(pp, __builtin_amdgcn_perm(v1[jj], v0[jj], 0x05040100u), acc[r][2 * jj]);
+            acc[r][2 * jj + 1] = dot2bf(pp, __builtin_amdgcn_perm(v1[jj], v0[jj], 0x07060302u), acc[r][2 * jj + 1]);
+          }
         }
         m[r] = mx;
       }
@@ -466,20 +494,42 @@ __global__ void paged_attn_reduce_kernel(const float* __restrict__ part_o, const
   }
 }
 
+template <int D, int NREP, int NW>
+static void launch_attn_nw(const void* q, int64_t q_stride, const void* kc, const void* vc, const int32_t* bt,
+                           int bt_stride, const int32_t* q_seq, const int32_t* q_ctx, void* out, float* ws_o,
+                           float* ws_ml, int T, int nkv, int nh, int page_log2, int PS, int NP, float scale_log2,
+                           int packed_mt, const RopeFuse& rf, int* cnt, hipStream_t stream) {
+  const size_t lds = (size_t)(NW * NREP * D + 2 * NW * NREP + 4) * sizeof(float);
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(NP, nh / NREP, T), dim3(64 * NW), lds, stream, (const bf16_t*)q, q_stride,
+                       (const bf16_t*)kc, (const bf16_t*)vc, bt, bt_stride, q_seq, q_ctx, (bf16_t*)out, ws_o, ws_ml,
+                       nkv, nh, page_log2, PS, NP, scale_log2, packed_mt, rf, cnt);
+  };
+  if (rf.pos) go(paged_attn1_kernel<D, NREP, true, NW, true>);
+  else go(paged_attn1_kernel<D, NREP, false, NW, true>);
+}
+
+// Waves per workgroup from the grid: one (query, head group, context part) per workgroup, so a
+// small grid (batch 1: 32 workgroups on 256 CUs) runs 8-wave workgroups - a short context is
+// covered in one or two dependent iterations (cold 1 x 170 MHA: 10.4 -> 9.9 us) - and every other
+// grid 4-wave ones.  (2-wave workgroups, the 64-session step's 2048 in one round of residency,
+// measured 36.5 -> 38.1 us cold at 64 x 170: profiles/r6attn.)
 template <int D, int NREP>
 static void launch_attn(const void* q, int64_t q_stride, const void* kc, const void* vc, const int32_t* bt,
                         int bt_stride, const int32_t* q_seq, const int32_t* q_ctx, void* out, float* ws_o,
                         float* ws_ml, int T, int nkv, int nh, int page_log2, int PS, int NP, float scale_log2,
                         int packed_mt, const RopeFuse& rf, int* cnt, hipStream_t stream) {
-  constexpr int nw = 4;
-  const size_t lds = (size_t)(nw * NREP * D + 2 * nw * NREP + 4) * sizeof(float);
-  auto go = [&](auto kern) {
-    hipLaunchKernelGGL(kern, dim3(NP, nh / NREP, T), dim3(64 * nw), lds, stream, (const bf16_t*)q, q_stride,
-                       (const bf16_t*)kc, (const bf16_t*)vc, bt, bt_stride, q_seq, q_ctx, (bf16_t*)out, ws_o, ws_ml,
-                       nkv, nh, page_log2, PS, NP, scale_log2, packed_mt, rf, cnt);
-  };
-  if (rf.pos) go(paged_attn1_kernel<D, NREP, true, nw, true>);
-  else go(paged_attn1_kernel<D, NREP, false, nw, true>);
+  const int64_t wgs = (int64_t)NP * (nh / NREP) * T;
+  const int nw = MP_ATTN_NW ? MP_ATTN_NW : (wgs <= 128 ? 8 : 4);
+#define MP_ATTN_NW_CASE(W)                                                                                     \
+  if (nw == W) {                                                                                               \
+    launch_attn_nw<D, NREP, W>(q, q_stride, kc, vc, bt, bt_stride, q_seq, q_ctx, out, ws_o, ws_ml, T, nkv, nh,  \
+                               page_log2, PS, NP, scale_log2, packed_mt, rf, cnt, stream);                     \
+    return;                                                                                                    \
+  }
+  MP_ATTN_NW_CASE(8)
+  MP_ATTN_NW_CASE(4)
+#undef MP_ATTN_NW_CASE
 }
 
 }  // namespace mp

@@ -36,15 +36,21 @@ sys.path.insert(0, HERE)
 METRIC = "tokens/sec (whole node) + per-stage ms, Llama-7B split over 1/2/4/8 stages"
 
 
-def baseline_value():
-    """Reference-equivalent number recorded in BASELINE.json (filled from a measured run)."""
+def baseline_value(batch: int = 64):
+    """Reference-equivalent per-GPU tokens/s recorded in BASELINE.json (a measured run) at THIS
+    batch: the same-batch number at its batch (64), the batch-1 number at 1, None otherwise."""
     try:
         with open(os.path.join(HERE, "BASELINE.json")) as f:
-            b = json.load(f)
-        v = b.get("measured_reference_equivalent", {}).get("decode_tokens_per_s_same_batch")  # per GPU
-        return float(v) if v else None
+            m = json.load(f).get("measured_reference_equivalent", {})
     except Exception:
         return None
+    if batch == 1:
+        v = m.get("batch1_decode_tokens_per_s")
+    elif batch == int(m.get("batch", 64)):
+        v = m.get("decode_tokens_per_s_same_batch")
+    else:
+        v = None
+    return float(v) if v else None
 
 
 def data_plane_name(ch, eng) -> str:
@@ -493,7 +499,8 @@ def main(argv=None):
     n_sessions_total = global_batch
     tokens = a.steps * global_batch  # every session advances one token per round
     value = tokens / dt
-    base = baseline_value() if a.model == "llama2-7b" else None  # the baseline is a Llama-2-7B number
+    # the baseline is a Llama-2-7B bf16 number at batch 64 (and 1)
+    base = baseline_value(B) if a.model == "llama2-7b" and not a.fp8 else None
     if rank == 0:
         rec = {
             "metric": METRIC,

@@ -19,13 +19,14 @@ ap.add_argument("--epi", type=int, default=3)
 ap.add_argument("--ms", default="1,64")
 ap.add_argument("--kern", default="auto")
 ap.add_argument("--iters", type=int, default=24)
+ap.add_argument("--copies", type=int, default=0, help="weight copies rotated (0: enough for 1 GiB, i.e. cold)")
 a = ap.parse_args()
 ops.load_library()
 ops.load_kernel_table()
 ops.set_gemm_sk(a.kern)
 dev = torch.device("cuda")
 ops.gemm_workspace(dev)
-copies = max(2, (1 << 30) // (a.N * a.K * 2))
+copies = a.copies or max(2, (1 << 30) // (a.N * a.K * 2))
 wps = [ops.pack_weight((torch.randn(a.N, a.K, device=dev) * 0.02).to(torch.bfloat16)) for _ in range(copies)]
 for M in [int(m) for m in a.ms.split(",")]:
     xp = ops.pack_act(torch.randn(M, a.K, device=dev).to(torch.bfloat16))
@@ -45,5 +46,5 @@ for M in [int(m) for m in a.ms.split(",")]:
     e1.record()
     e1.synchronize()
     us = 1000 * e0.elapsed_time(e1) / a.iters
-    print(f"M={M}: {us:.2f} us/launch, {a.N * a.K * 2 / us / 1e6:.2f} TB/s weights", flush=True)
+    print(f"N={a.N} K={a.K} copies={copies} M={M}: {us:.2f} us/launch, {a.N * a.K * 2 / us / 1e6:.2f} TB/s weights", flush=True)
 torch.cuda.synchronize()

@@ -1030,11 +1030,13 @@ _RWK_SPLIT = {}
 _QKV_FOLD_CAND = {}
 
 
-def rwk_split(M: int, N: int, K: int, fp8: bool = False) -> int:
-    """Split count of the split-K ring form for this shape (0: not covered)."""
-    key = (int(M), int(N), int(K), bool(fp8))
+def rwk_split(M: int, N: int, K: int, fp8=False) -> int:
+    """Split count of the split-K ring form for this shape (0: not covered).  ``fp8``: False (bf16
+    weights), True (W8A16) or 2 (the W8A8-MX form, ``linear_mx``)."""
+    f8 = 2 if fp8 == 2 and not isinstance(fp8, bool) else int(bool(fp8))
+    key = (int(M), int(N), int(K), f8)
     if key not in _RWK_SPLIT:
-        _RWK_SPLIT[key] = int(torch.ops.mpamd.gemm_rwk_split(int(M), int(N), int(K), int(bool(fp8))))
+        _RWK_SPLIT[key] = int(torch.ops.mpamd.gemm_rwk_split(int(M), int(N), int(K), f8))
     return _RWK_SPLIT[key]
 
 
@@ -1317,6 +1319,56 @@ def linear_w8(x, w8, w_scale, a_rows: int, out=None, epilogue: int = 0, residual
                             gemm_workspace(x.device) if _base(kern) in ("rwk", "rwki") else None, ap_out, ss_out,
                             ss_zero, ss_in,
                             1.0 / K, float(eps))
+    return out
+
+
+# ---------------------------------------------------------------------------------------
+# W8A8-MX decode GEMM (csrc/gemm_mx.hip): the W8A16 fp8 weights x MX e4m3 activations (e8m0 scale
+# per 32-element block) on gfx950's block-scaled MFMA, split-K ring form + reduce launch.
+def mx_buffers(M: int, K: int, device):
+    """(ax, as) buffers of ``quant_mx`` for M rows x K."""
+    rows = 16 * ((int(M) + 15) // 16)
+    return (torch.empty(rows * K, dtype=torch.uint8, device=device),
+            torch.full((2 * K,), 127, dtype=torch.uint8, device=device))  # [K/128][64][4]
+
+
+def quant_mx(xp: torch.Tensor, M: int, K: int, ax=None, as_=None):
+    """Packed bf16 activation (M rows, K) -> MX e4m3 bytes + e8m0 block scales (gemm_mx.hip layout)."""
+    if ax is None or as_ is None:
+        ax, as_ = mx_buffers(M, K, xp.device)
+    torch.ops.mpamd.quant_mx(xp, ax, as_, int(M), int(K))
+    return ax, as_
+
+
+def mx_block_quant(x: torch.Tensor) -> torch.Tensor:
+    """fp32 reference of ``quant_mx`` + dequantization on row-major x[M, K]: the values the MX GEMM
+    multiplies.  Block map (gemm_mx.hip): k = 128 kb + 32 s + 8 q + j, block (s >> 1, q >> 1)."""
+    M, K = x.shape
+    v = x.to(torch.bfloat16).float().view(M, K // 128, 2, 2, 2, 2, 8)  # [M, kb, sh, sl, qh, ql, j]
+    amax = v.abs().amax(dim=(3, 5, 6), keepdim=True)
+    t = amax / 448.0
+    m, ex = torch.frexp(t)
+    e = torch.where(m > 0.5, ex, ex - 1).clamp(-126, 126)  # ceil(log2(amax / 448))
+    e = torch.where(amax > 0, e, torch.zeros_like(e)).float()
+    q = (v * torch.exp2(-e)).clamp(-448.0, 448.0).to(torch.float8_e4m3fn).float()
+    return (q * torch.exp2(e)).view(M, K)
+
+
+def linear_mx(ax, as_, w8, w_scale, a_rows: int, out=None, epilogue: int = 0, residual=None, ss_in=None,
+              eps: float = 0.0, ap_out=None, ss_out=None, ss_zero=None, partials: bool = False, rot: bool = False):
+    """The W8A8-MX decode GEMM (M <= 64): epilogue 0 (optional ``ss_in`` row scale) or 3 (residual-
+    stream producer), or with ``partials`` the fp32 split-K slabs [S, M, N] (a workspace view, as
+    ``linear_partials``)."""
+    M = int(a_rows)
+    N, K = 16 * w8.shape[0], 32 * w8.shape[1]
+    ws = gemm_workspace(ax.device)
+    if out is None:
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=ax.device)
+    flags = 1 | 256 | (PART_FLAG if partials else 0) | (ROT_FLAG if rot else 0)
+    torch.ops.mpamd.gemm_mx(ax, as_, w8, w_scale, out, residual, int(epilogue), M, flags, ws, ap_out, ss_out, ss_zero,
+                            ss_in, 1.0 / K, float(eps))
+    if partials:
+        return _slab_view(ax.device, rwk_split(M, N, K, 2), M, N)
     return out
 
 

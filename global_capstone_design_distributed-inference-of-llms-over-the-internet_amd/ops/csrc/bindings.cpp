@@ -62,6 +62,10 @@ int mp_gemm_w8(const void* x, const void* wq, const float* wsc, void* y, int64_t
                int64_t res_stride, int M, int N, int K, int epilogue, int flags, void* ws, void* ap, void* ss_out,
                void* ss_zero, const void* ss_in, float inv_k, float eps, hipStream_t stream);
 int mp_pack_act(const void* x, int64_t xs, void* ap, int M, int K, hipStream_t stream);
+int mp_quant_mx(const void* ap, void* ax, void* as, int M, int K, hipStream_t stream);
+int mp_gemm_mx(const void* ax, const void* as, const void* wq, const float* wsc, void* y, int64_t y_stride,
+               const void* res, int64_t res_stride, int M, int N, int K, int epilogue, int flags, void* ws, void* ap,
+               void* ss_out, void* ss_zero, const void* ss_in, float inv_k, float eps, hipStream_t stream);
 int mp_pack_weight(const void* w, void* wp, int N, int K, hipStream_t stream);
 }
 
@@ -650,6 +654,73 @@ void quant_act_fp8(const at::Tensor& ap, at::Tensor& a8, at::Tensor& scale, int6
                "quant_act_fp8");
 }
 
+// packed bf16 activation (M rows, K) -> MX e4m3 bytes ax [K/128 * MT * 2 * 64 * 16] + e8m0 block
+// scales as [K/128 * 64 * 4] (gemm_mx.hip)
+void quant_mx(const at::Tensor& ap, at::Tensor& ax, at::Tensor& as, int64_t M, int64_t K) {
+  check_bf16_cuda(ap, "ap");
+  MP_CHECK(M >= 1 && M <= 64 && K % 128 == 0, "quant_mx: 1 <= M <= 64, K % 128 == 0");
+  MP_CHECK(ap.is_contiguous() && ap.numel() >= packed_numel(M, K), "packed activation too small");
+  const int64_t rows = ((M + 15) / 16) * 16;
+  MP_CHECK(ax.is_cuda() && ax.scalar_type() == at::kByte && ax.is_contiguous() && ax.numel() >= rows * K,
+           "ax: uint8 [ceil(M/16)*16*K]");
+  MP_CHECK(as.is_cuda() && as.scalar_type() == at::kByte && as.is_contiguous() && as.numel() >= 2 * K,
+           "as: uint8 [K/128 * 64 * 4]");
+  check_launch(mp_quant_mx(ap.data_ptr(), ax.data_ptr(), as.data_ptr(), (int)M, (int)K, cur_stream()), "quant_mx");
+}
+
+// W8A8-MX decode GEMM (gemm_mx.hip): ax / as from quant_mx, fp8 weight in the W8A16 layout + column
+// scales; epilogue 0 (optional ss_in row scale) or 3; flags bit 10 rotated k walk, bit 14 partial
+// slabs only (y unused, the slabs stay in the workspace)
+void gemm_mx(const at::Tensor& ax, const at::Tensor& as, const at::Tensor& wq, const at::Tensor& wsc, at::Tensor& y,
+             const c10::optional<at::Tensor>& residual, int64_t epilogue, int64_t M_, int64_t flags,
+             const at::Tensor& workspace, const c10::optional<at::Tensor>& ap,
+             const c10::optional<at::Tensor>& ss_out, const c10::optional<at::Tensor>& ss_zero,
+             const c10::optional<at::Tensor>& ss_in, double inv_k, double eps) {
+  MP_CHECK(wq.is_cuda() && wq.scalar_type() == at::kByte && wq.dim() == 4 && wq.size(2) == 64 && wq.size(3) == 8 &&
+               wq.is_contiguous(),
+           "wq must be an fp8 weight uint8 [N/16, K/32, 64, 8] (ops.pack_weight_w8)");
+  const int N = 16 * wq.size(0), K = 32 * wq.size(1);
+  const int M = (int)M_;
+  MP_CHECK(M >= 1 && M <= 64 && K % 128 == 0, "gemm_mx: 1 <= M <= 64, K % 128 == 0");
+  const int64_t rows = ((M + 15) / 16) * 16;
+  MP_CHECK(ax.is_cuda() && ax.scalar_type() == at::kByte && ax.is_contiguous() && ax.numel() >= rows * K, "ax size");
+  MP_CHECK(as.is_cuda() && as.scalar_type() == at::kByte && as.is_contiguous() && as.numel() >= 2 * K, "as size");
+  MP_CHECK(wsc.is_cuda() && wsc.scalar_type() == at::kFloat && wsc.is_contiguous() && wsc.numel() == N,
+           "wsc: fp32 [N] column scales");
+  MP_CHECK(epilogue == 0 || epilogue == 3, "gemm_mx: epilogue 0 or 3");
+  const bool partial = flags & 16384;
+  if (!partial) {
+    check_bf16_cuda(y, "y");
+    check_rows(y, "y");
+    MP_CHECK(y.size(0) == M && y.size(1) == N, "y shape");
+  }
+  const void* rp = nullptr;
+  int64_t rs = 0;
+  if (residual.has_value()) {
+    check_bf16_cuda(*residual, "residual");
+    check_rows(*residual, "residual");
+    MP_CHECK(residual->size(0) == M && residual->size(1) == N, "residual shape");
+    rp = residual->data_ptr();
+    rs = residual->stride(0);
+  }
+  void* app = nullptr;
+  if (ap.has_value()) {
+    check_bf16_cuda(*ap, "ap");
+    MP_CHECK(ap->is_contiguous() && ap->numel() >= packed_numel(M, N), "ap: packed [ceil(M/16)*16*N]");
+    app = ap->data_ptr();
+  }
+  MP_CHECK(epilogue != 3 || (app != nullptr && rp != nullptr), "epilogue 3 needs residual and ap");
+  MP_CHECK(workspace.is_cuda() && workspace.is_contiguous() &&
+               workspace.numel() * workspace.element_size() >= mp_gemm_workspace_bytes(),
+           "gemm workspace too small (ops.gemm_workspace)");
+  const int rc = mp_gemm_mx(ax.data_ptr(), as.data_ptr(), wq.data_ptr(), wsc.data_ptr<float>(),
+                            partial ? nullptr : y.data_ptr(), partial ? 0 : y.stride(0), rp, rs, M, N, K,
+                            (int)epilogue, (int)flags, workspace.data_ptr(), app, opt_ss(ss_out, "ss_out"),
+                            opt_ss(ss_zero, "ss_zero"), opt_ss(ss_in, "ss_in"), (float)inv_k, (float)eps, cur_stream());
+  TORCH_CHECK(rc != 1, "mpamd: gemm_mx: no split-K geometry for M=", M, " N=", N, " K=", K);
+  check_launch(rc, "gemm_mx");
+}
+
 // row-major bf16 x[M, K] -> fp8 A8 (the fp8 GEMM's A layout) + per-row scales
 void quant_rows_fp8(const at::Tensor& x, at::Tensor& a8, at::Tensor& scale) {
   check_bf16_cuda(x, "x");
@@ -764,6 +835,11 @@ TORCH_LIBRARY(mpamd, m) {
   m.def("pack_weight(Tensor w) -> Tensor");
   m.def("quant_act_fp8(Tensor ap, Tensor(a!) a8, Tensor(b!) scale, int M, int K) -> ()");
   m.def("quant_rows_fp8(Tensor x, Tensor(a!) a8, Tensor(b!) scale) -> ()");
+  m.def("quant_mx(Tensor ap, Tensor(a!) ax, Tensor(b!) as_, int M, int K) -> ()");
+  m.def(
+      "gemm_mx(Tensor ax, Tensor as_, Tensor wq, Tensor wsc, Tensor(a!) y, Tensor? residual, int epilogue, int M, "
+      "int flags, Tensor(b!) workspace, Tensor(c!)? ap=None, Tensor(d!)? ss_out=None, Tensor(e!)? ss_zero=None, "
+      "Tensor? ss_in=None, float inv_k=0., float eps=0.) -> ()");
   m.def(
       "gemm_fp8(Tensor a8, Tensor a_scale, Tensor wq, Tensor w_scale, Tensor(a!) y, Tensor? residual, int epilogue, "
       "int M, int out_packed, int kind=-1, Tensor(b!)? workspace=None) -> ()");
@@ -789,5 +865,7 @@ TORCH_LIBRARY_IMPL(mpamd, CUDA, m) {
   m.impl("pack_act", &pack_act);
   m.impl("quant_act_fp8", &quant_act_fp8);
   m.impl("quant_rows_fp8", &quant_rows_fp8);
+  m.impl("quant_mx", &quant_mx);
+  m.impl("gemm_mx", &gemm_mx);
   m.impl("gemm_fp8", &gemm_fp8);
 }

@@ -86,6 +86,7 @@ struct EpiArgs {
   int mt_out;
   const float* wsc;    // fp8 weights (W8A16 kernels): per-output-column dequantization scales
   int rot = 0;         // rotate each workgroup's k walk (rw_krot; flags bit 10, chosen per shape)
+  const uint8_t* xsc = nullptr;  // MX activations (gemm_mx.hip): e8m0 block scales [K/128][MT][64]
 };
 
 // fp8 (OCP e4m3) weight fragment -> bf16 MFMA B operand (exact: every e4m3 value is a bf16
@@ -108,6 +109,18 @@ __device__ __forceinline__ u16x8 f8w_to_bf16(const u32x2& raw) {
     r[4 * h + 3] = hi[1];
   }
   return r;
+}
+
+// MX decode GEMM (gemm_mx.hip): one 16x16x128 block-scaled e4m3 MFMA.  ``a`` / ``b``: the lane's 32
+// bytes (four consecutive 32-k slices of the W8A16 fragment order, 8 bytes each); ``sa``: the e8m0
+// scale this lane supplies in byte 0 (gfx950 takes the scale of 32-block b of a row from lane
+// 16 b + r, mx_quant_kernel writes it there); the weight's e8m0 is 127 (= 1): its per-column scale is applied
+// to the accumulators after the loop.
+typedef __attribute__((ext_vector_type(8))) unsigned u32x8;
+typedef __attribute__((ext_vector_type(8))) int i32x8_t;
+__device__ __forceinline__ f32x4 mfma_mx(const u32x8& a, const u32x8& b, unsigned sa, f32x4 c) {
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(__builtin_bit_cast(i32x8_t, a), __builtin_bit_cast(i32x8_t, b),
+                                                          c, 0, 0, 0, (int)sa, 0, 127);
 }
 
 __device__ __forceinline__ u64 fx_sq(float f) { return (u64)__float2ull_rn(f * f * SS_FX); }
@@ -991,6 +1004,12 @@ constexpr int rw_depth2() {
   }
 }
 
+// MX ring step (128 k): 8 MT + 8 NT + 1 VGPRs per slot (rsa: the step's block-scale word)
+template <int MT, int NT>
+constexpr int mx_depth() {
+  return 200 / (8 * MT + 8 * NT + 1) >= 4 ? 4 : 2;
+}
+
 // ``mt0`` / ``mta`` (row-split form, gemm_rwr_kernel): this workgroup computes the MT row tiles
 // starting at tile mt0 of an activation packed with mta row tiles (default: all rows, mta = MT).
 // NTW = false loads the weights with the default cache policy (a row-split pair re-reads them).
@@ -1327,16 +1346,26 @@ constexpr int64_t RWK_SLAB_BYTES = (int64_t)32 << 20;  // S x M x N fp32 partial
 // reduce-scatter combine, in which every split polled for its partners, was measured 2-3.5 us
 // slower than the reduce launch and needed all S splits resident at once: removed, profiles/r4_seam.)
 // Residual quads of EPI 3 are prefetched before the main loop.
-template <int MT, int NT, bool F8 = false, int INL = -1>
+// MX (with F8): the activation is MX fp8 (gemm_mx.hip: e4m3 bytes Ax[K/128][MT][64][32] in the
+// W8A16 fragment order of four consecutive k-slices, e8m0 block scales in ep.xsc) and every ring
+// step is one 128-deep k-step of v_mfma_scale_f32_16x16x128_f8f6f4: the fp8 weight fragments of
+// the step's four k-slices go to the MFMA as they are (no conversion; weight scale byte 127 = 1,
+// the column scales multiply the accumulators after the loop as in W8A16), the activation's
+// block scales ride in the instruction.  Half the activation bytes of W8A16, a quarter of the
+// MFMA instructions, no cvt.
+template <int MT, int NT, bool F8 = false, int INL = -1, bool MX = false>
 __global__ __launch_bounds__(RW_WAVES * 64) void gemm_rwk_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ wp,
                                                        float* __restrict__ part, int M, int N, int K, int S,
                                                        const EpiArgs ep, bf16_t* __restrict__ y, int64_t ys,
                                                        const bf16_t* __restrict__ res, int64_t rs,
                                                        int* __restrict__ tick) {
   clear_other(ep);
-  constexpr int R = rw_depth2<MT, NT, F8>();
+  static_assert(!MX || (F8 && INL < 0), "MX: fp8 weights, reduce launch");
+  constexpr int R = MX ? mx_depth<MT, NT>() : rw_depth2<MT, NT, F8>();
   using WT = std::conditional_t<F8, uint8_t, bf16_t>;
-  using BT = std::conditional_t<F8, u32x2, u16x8>;
+  using BT = std::conditional_t<MX, u32x8, std::conditional_t<F8, u32x2, u16x8>>;
+  using AT = std::conditional_t<MX, u32x8, u16x8>;
+  constexpr int KS = MX ? 4 : 1;  // k-slices (of 32) per ring step
   constexpr int Q = MT * NT;
   constexpr int QC = Q < RW_QC ? Q : RW_QC;
   constexpr int NQ = (Q + RW_WAVES - 1) / RW_WAVES;  // epilogue quads per wave (at most)
@@ -1356,11 +1385,14 @@ __global__ __launch_bounds__(RW_WAVES * 64) void gemm_rwk_kernel(const bf16_t* _
   }
   const int tile0 = c * NT;
   const int nks = K >> 5;
-  const int ks0 = (int)((int64_t)sp * nks / S), ks1 = (int)((int64_t)(sp + 1) * nks / S);
+  const int nst = nks / KS;  // ring steps over all of K
+  const int ks0 = (int)((int64_t)sp * nst / S), ks1 = (int)((int64_t)(sp + 1) * nst / S);
   const int cnt = (ks1 - ks0 + RW_WAVES - 1) / RW_WAVES;
   const int krot = rw_krot(ks1 - ks0, ep.rot);
   const WT* wb = reinterpret_cast<const WT*>(wp) + ((int64_t)tile0 * nks) * 512 + lane * 8;
   const bf16_t* xl = x + lane * 8;
+  const uint8_t* xm = reinterpret_cast<const uint8_t*>(x) + lane * 16;  // MX: this lane's 2 x 16 bytes
+  const unsigned* xs = reinterpret_cast<const unsigned*>(ep.xsc) + lane;  // MX: its scale word per step
   float wsc[NT];
   if constexpr (F8) {
 #pragma unroll
@@ -1381,16 +1413,33 @@ __global__ __launch_bounds__(RW_WAVES * 64) void gemm_rwk_kernel(const bf16_t* _
   for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[mt][t] = (f32x4)(0.f);
-  u16x8 ra[R][MT];
+  AT ra[R][MT];
   BT rb[R][NT];
+  unsigned rsa[MX ? R : 1];
 #define RWK_LOAD(s, i)                                                                                     \
   {                                                                                                          \
     const int k_ = ks0 + rw_rot(min(wid + RW_WAVES * (i), ks1 - ks0 - 1), krot, ks1 - ks0);                \
-    _Pragma("unroll") for (int t = 0; t < NT; ++t) rb[s][t] =                                                \
-        __builtin_nontemporal_load(reinterpret_cast<const BT*>(wb + (((int64_t)t * nks + k_) << 9)));       \
-    _Pragma("unroll") for (int mt = 0; mt < MT; ++mt) ra[s][mt] =                                            \
-        load_a_rows(xl + (((int64_t)k_ * ep.mt_out + min(mt, ep.mt_out - 1)) << 9), lane,                  \
-                    mt * 16 + (lane & 15) < M);                                                              \
+    if constexpr (MX) {                                                                                      \
+      _Pragma("unroll") for (int t = 0; t < NT; ++t) {                                                       \
+        const u32x2* p_ = reinterpret_cast<const u32x2*>(wb + (((int64_t)t * nks + 4 * k_) << 9));         \
+        const u32x2 w0 = __builtin_nontemporal_load(p_), w1 = __builtin_nontemporal_load(p_ + 64),           \
+                    w2 = __builtin_nontemporal_load(p_ + 128), w3 = __builtin_nontemporal_load(p_ + 192);   \
+        rb[s][t] = (u32x8){w0[0], w0[1], w1[0], w1[1], w2[0], w2[1], w3[0], w3[1]};                          \
+      }                                                                                                      \
+      _Pragma("unroll") for (int mt = 0; mt < MT; ++mt) {                                                    \
+        const int64_t o_ = (int64_t)k_ * ep.mt_out + min(mt, ep.mt_out - 1);                                 \
+        const u32x4 a0 = *reinterpret_cast<const u32x4*>(xm + (o_ << 11)),                                   \
+                    a1 = *reinterpret_cast<const u32x4*>(xm + (o_ << 11) + 1024);                            \
+        ra[s][mt] = (u32x8){a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};                         \
+      }                                                                                                      \
+      rsa[s] = xs[(int64_t)k_ << 6];                                                                         \
+    } else {                                                                                                 \
+      _Pragma("unroll") for (int t = 0; t < NT; ++t) rb[s][t] =                                              \
+          __builtin_nontemporal_load(reinterpret_cast<const BT*>(wb + (((int64_t)t * nks + k_) << 9)));     \
+      _Pragma("unroll") for (int mt = 0; mt < MT; ++mt) ra[s][mt] =                                          \
+          load_a_rows(xl + (((int64_t)k_ * ep.mt_out + min(mt, ep.mt_out - 1)) << 9), lane,                \
+                      mt * 16 + (lane & 15) < M);                                                            \
+    }                                                                                                        \
   }
 #pragma unroll
   for (int s = 0; s < R; ++s) RWK_LOAD(s, s)
@@ -1398,7 +1447,12 @@ __global__ __launch_bounds__(RW_WAVES * 64) void gemm_rwk_kernel(const bf16_t* _
 #pragma unroll
     for (int s = 0; s < R; ++s) {
       if (ks0 + wid + RW_WAVES * (i0 + s) < ks1) {
-        if constexpr (F8) {
+        if constexpr (MX) {
+#pragma unroll
+          for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) acc[mt][t] = mfma_mx(ra[s][mt], rb[s][t], rsa[s] >> (8 * mt), acc[mt][t]);
+        } else if constexpr (F8) {
 #pragma unroll
           for (int t = 0; t < NT; ++t) {
             const u16x8 b = f8w_to_bf16(rb[s][t]);
@@ -1628,17 +1682,17 @@ static inline int rwk_comb(int flags) {
   return (flags & 512) ? 1 : 0;
 }
 
-template <int MT, bool F8 = false>
+template <int MT, bool F8 = false, bool MX = false>
 static int launch_gemm_rwk(const void* x, const void* w, void* y, int64_t ys, const void* res, int64_t rs, int M,
                            int N, int K, int epi, const EpiArgs& ep, void* ws, hipStream_t stream,
                            int comb = 0) {
-  const bool inl = comb > 0;
+  const bool inl = comb > 0 && !MX;
   if (epi == 1 || ws == nullptr || N % 2048 != 0) return 1;
   const int tiles = N / 16, C0 = sk_num_cus(), nks = K / 32;
   int nt = 0, S = 0;
   // accumulators: 192 AGPRs up to 128 rows, all 256 beyond (MT 9..16 -> NT <= 64 / MT)
   constexpr int nt_max = rwk_nt_max_mt(MT);
-  rwk_choose(tiles, nks, C0, F8, nt, S, nt_max);
+  rwk_choose(tiles, MX ? nks / 4 : nks, C0, F8, nt, S, nt_max);
   if (nt == 0) return 1;
   if ((int64_t)S * M * N * 4 > RWK_SLAB_BYTES) return 1;
   float* part = (float*)((char*)ws + (int64_t)SK_MAX_GROUPS * sizeof(int) + SK_ZERO_BYTES +
@@ -1665,19 +1719,19 @@ static int launch_gemm_rwk(const void* x, const void* w, void* y, int64_t ys, co
     }
   }
   switch (nt) {
-    case 1: hipLaunchKernelGGL((gemm_rwk_kernel<MT, 1, F8>), g1, dim3(RW_WAVES * 64), 0, stream, (const bf16_t*)x, (const bf16_t*)w, part, M, N, K, S, ep, nullptr, 0, nullptr, 0, nullptr); break;
-    case 2: hipLaunchKernelGGL((gemm_rwk_kernel<MT, 2, F8>), g1, dim3(RW_WAVES * 64), 0, stream, (const bf16_t*)x, (const bf16_t*)w, part, M, N, K, S, ep, nullptr, 0, nullptr, 0, nullptr); break;
+    case 1: hipLaunchKernelGGL((gemm_rwk_kernel<MT, 1, F8, -1, MX>), g1, dim3(RW_WAVES * 64), 0, stream, (const bf16_t*)x, (const bf16_t*)w, part, M, N, K, S, ep, nullptr, 0, nullptr, 0, nullptr); break;
+    case 2: hipLaunchKernelGGL((gemm_rwk_kernel<MT, 2, F8, -1, MX>), g1, dim3(RW_WAVES * 64), 0, stream, (const bf16_t*)x, (const bf16_t*)w, part, M, N, K, S, ep, nullptr, 0, nullptr, 0, nullptr); break;
     case 4:
       if constexpr (4 <= nt_max)
-        hipLaunchKernelGGL((gemm_rwk_kernel<MT, 4, F8>), g1, dim3(RW_WAVES * 64), 0, stream, (const bf16_t*)x, (const bf16_t*)w, part, M, N, K, S, ep, nullptr, 0, nullptr, 0, nullptr);
+        hipLaunchKernelGGL((gemm_rwk_kernel<MT, 4, F8, -1, MX>), g1, dim3(RW_WAVES * 64), 0, stream, (const bf16_t*)x, (const bf16_t*)w, part, M, N, K, S, ep, nullptr, 0, nullptr, 0, nullptr);
       break;
     case 6:
       if constexpr (6 <= nt_max)
-        hipLaunchKernelGGL((gemm_rwk_kernel<MT, 6, F8>), g1, dim3(RW_WAVES * 64), 0, stream, (const bf16_t*)x, (const bf16_t*)w, part, M, N, K, S, ep, nullptr, 0, nullptr, 0, nullptr);
+        hipLaunchKernelGGL((gemm_rwk_kernel<MT, 6, F8, -1, MX>), g1, dim3(RW_WAVES * 64), 0, stream, (const bf16_t*)x, (const bf16_t*)w, part, M, N, K, S, ep, nullptr, 0, nullptr, 0, nullptr);
       break;
     default:
       if constexpr (8 <= nt_max)
-        hipLaunchKernelGGL((gemm_rwk_kernel<MT, 8, F8>), g1, dim3(RW_WAVES * 64), 0, stream, (const bf16_t*)x, (const bf16_t*)w, part, M, N, K, S, ep, nullptr, 0, nullptr, 0, nullptr);
+        hipLaunchKernelGGL((gemm_rwk_kernel<MT, 8, F8, -1, MX>), g1, dim3(RW_WAVES * 64), 0, stream, (const bf16_t*)x, (const bf16_t*)w, part, M, N, K, S, ep, nullptr, 0, nullptr, 0, nullptr);
       break;
   }
   if (comb < 0) return 0;  // partials only: the consumer sums the S slabs itself (rwk_split)

@@ -1,0 +1,113 @@
+"""W8A8-MX decode GEMM (ops/csrc/gemm_mx.hip): the MX activation quantizer against its fp32
+reference (``ops.mx_block_quant``) bit for bit, and the block-scaled MFMA GEMM against the fp32
+oracle x_mx @ dequant(W)^T at M in {1, 30, 64} on 7B and 70B projection shapes: epilogue 0 (with and
+without the fused-norm row scale), the residual-stream producer (epilogue 3) and the split-K partial
+slabs the qkv fold reads.  CPU part: the reference quantizer's block map and error bound."""
+import pytest
+import torch
+
+from src import ops
+
+DEV = "cuda"
+
+
+def bf(t):
+    return t.to(torch.bfloat16)
+
+
+def test_mx_block_quant_reference():
+    """Every 32-value block (k-slices 4 kb + 2 sh + {0, 1}, lane groups 2 qh + {0, 1}) shares one power
+    of two scale, the block maximum lands in (224, 448], the element error is e4m3's (<= 2^-4)."""
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(5, 256, generator=g) * torch.logspace(-3, 3, 256)[None, :]
+    x[2, 128:] = 0.0  # an all-zero step: scale 1, zeros
+    d = ops.mx_block_quant(x)
+    xb = x.to(torch.bfloat16).float()
+    assert torch.all(d[2, 128:] == 0)
+    v = xb.view(5, 2, 2, 2, 2, 2, 8)
+    dv = d.view(5, 2, 2, 2, 2, 2, 8)
+    amax = v.abs().amax(dim=(3, 5, 6), keepdim=True)
+    err = (dv - v).abs()
+    # relative to the block max: 3 mantissa bits (max rel 2^-4), subnormals near 2^-9 of the max
+    assert torch.all(err <= amax * 2.0 ** -4 + 1e-30)
+    rel = (dv - v).abs() / v.abs().clamp_min(1e-30)
+    big = v.abs() >= amax / 8
+    assert torch.all(rel[big] <= 2.0 ** -4 + 1e-6)
+
+
+def _dequant_gpu(ax, as_, M, K):
+    """Decode the kernel's MX layout back to fp32 [M, K] (lane 16 q + r, byte 8 s + j in two 16-byte
+    halves [h][lane]; the scale of block 2 (s >> 1) + (q >> 1) in byte mt of lane 16 b + r's word)."""
+    MT = (M + 15) // 16
+    nkb = K // 128
+    q8 = ax.view(torch.float8_e4m3fn).float().view(nkb, MT, 2, 4, 16, 2, 8)  # kb, mt, h, q, r, s_lo, j
+    q8 = q8.permute(0, 1, 3, 4, 2, 5, 6).reshape(nkb, MT, 4, 16, 4, 8)  # kb, mt, q, r, s = 2 h + s_lo, j
+    e = as_.float().view(nkb, 4, 16, 4)[..., :MT].permute(0, 3, 1, 2) - 127.0  # kb, mt, b, r
+    sc = torch.empty(nkb, MT, 4, 16, 4, 8, device=ax.device)
+    for q in range(4):
+        for s in range(4):
+            sc[:, :, q, :, s, :] = torch.exp2(e[:, :, 2 * (s >> 1) + (q >> 1), :])[..., None]
+    v = (q8 * sc).permute(1, 3, 0, 4, 2, 5).reshape(MT * 16, K)  # rows (mt, r), k = 128 kb + 32 s + 8 q + j
+    return v[:M]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,K", [(1, 4096), (30, 8192), (64, 28672)])
+def test_quant_mx_matches_reference(M, K):
+    ops.load_library()
+    x = bf(torch.randn(M, K, device=DEV) * torch.logspace(-2, 2, K, device=DEV)[None, :])
+    ax, as_ = ops.quant_mx(ops.pack_act(x), M, K)
+    got = _dequant_gpu(ax, as_, M, K)
+    want = ops.mx_block_quant(x.float())
+    assert torch.equal(got, want)
+    MT = (M + 15) // 16
+    if M % 16:  # rows past M: zero bytes, unit scales
+        assert torch.all(ax.view(K // 128, MT, 2, 4, 16, 16)[:, MT - 1, :, :, M % 16:] == 0)
+        assert torch.all(as_.view(K // 128, 4, 16, 4)[:, :, M % 16:, MT - 1] == 127)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M", [1, 30, 64])
+@pytest.mark.parametrize("N,K", [(12288, 4096), (4096, 11008), (10240, 8192), (8192, 8192), (8192, 28672)])
+def test_mx_gemm_matches_oracle(M, N, K):
+    ops.load_library()
+    torch.manual_seed(M * 7 + N + K)
+    x = bf(torch.randn(M, K, device=DEV))
+    w = torch.randn(N, K, device=DEV) * 0.02
+    wq, ws = ops.pack_weight_fp8(w)
+    w8 = ops.w8_from_fp8(wq)
+    wdq = ops.unpack_weight_w8(w8, ws, torch.float32)
+    xp = ops.pack_act(x)
+    ax, as_ = ops.quant_mx(xp, M, K)
+    exact = ops.mx_block_quant(x.float()) @ wdq.t()
+    y = ops.linear_mx(ax, as_, w8, ws, M)
+    assert float((y.float() - exact).norm() / exact.norm()) < 6e-3  # bf16 outputs, fp32 accumulation
+    torch.testing.assert_close(y.float(), exact, atol=3e-2, rtol=2e-2)
+    # against the unquantized product: MX e4m3 activations cost a few percent, no more
+    full = x.float() @ wdq.t()
+    assert float((y.float() - full).norm() / full.norm()) < 0.05
+    # fused-norm consumer row scale
+    ss = ops.norm_stats_buffer(DEV)[0]
+    ss.zero_()
+    sq = (x.float() ** 2).sum(1)
+    ss[0, :M] = torch.round(sq * 2.0 ** 20).long()
+    y2 = ops.linear_mx(ax, as_, w8, ws, M, ss_in=ss, eps=1e-5)
+    want = exact * torch.rsqrt(sq / K + 1e-5)[:, None]
+    assert float((y2.float() - want).norm() / want.norm()) < 6e-3
+    # partial slabs (the qkv fold's input): their sum is the unscaled product
+    S = ops.rwk_split(M, N, K, 2)
+    assert S >= 2
+    part = ops.linear_mx(ax, as_, w8, ws, M, partials=True)
+    assert part.shape == (S, M, N)
+    assert float((part.sum(0) - exact).norm() / exact.norm()) < 1e-4  # fp32 sums in another order
+    # residual-stream producer: residual, packed copy, row sums of squares
+    res = bf(torch.randn(M, N, device=DEV))
+    r0 = res.clone()
+    ap = torch.zeros(ops.packed_numel(M, N), dtype=torch.bfloat16, device=DEV)
+    ss_out, ss_zero = ops.norm_stats_buffer(DEV, 2)
+    ss_out.zero_()
+    ops.linear_mx(ax, as_, w8, ws, M, out=res, epilogue=3, residual=res, ap_out=ap, ss_out=ss_out, ss_zero=ss_zero)
+    torch.testing.assert_close(res.float(), exact + r0.float(), atol=6e-2, rtol=2e-2)
+    assert torch.equal(ops.unpack_act(ap, M, N), res)
+    got_ss = ss_out.view(-1, 64).sum(0)[:M].double() / 2.0 ** 20
+    torch.testing.assert_close(got_ss, (res.double() ** 2).sum(1), rtol=1e-4, atol=1e-3)

@@ -49,6 +49,7 @@ extern "C" int mp_gemm_rwk_split(int M, int N, int K, int f8) {
   const int nt_max = rwk_nt_max(M);
   // f8 == 2: the MX form (gemm_mx.hip), whose ring steps are 128 deep
   rwk_choose(N / 16, f8 == 2 ? K / 128 : K / 32, sk_num_cus(), f8 != 0, nt, S, nt_max);
+  if (f8 == 2 && nt) mx_geometry(N / 16, nt, S);
   if (nt == 0 || (int64_t)S * M * N * 4 > RWK_SLAB_BYTES) return 0;
   return S;
 }

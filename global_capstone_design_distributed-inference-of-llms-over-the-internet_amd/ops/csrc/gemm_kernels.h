@@ -1420,8 +1420,12 @@ __global__ __launch_bounds__(RW_WAVES * 64) void gemm_rwk_kernel(const bf16_t* _
   {                                                                                                          \
     const int k_ = ks0 + rw_rot(min(wid + RW_WAVES * (i), ks1 - ks0 - 1), krot, ks1 - ks0);                \
     if constexpr (MX) {                                                                                      \
+      /* steps past the split's end (the ring's tail) load the L2-resident activation instead of      */     \
+      /* re-streaming a weight step from HBM (non-temporal loads do not stay in L2)                   */     \
+      const bool live_ = wid + RW_WAVES * (i) < ks1 - ks0;                                                   \
       _Pragma("unroll") for (int t = 0; t < NT; ++t) {                                                       \
-        const u32x2* p_ = reinterpret_cast<const u32x2*>(wb + (((int64_t)t * nks + 4 * k_) << 9));         \
+        const u32x2* p_ = reinterpret_cast<const u32x2*>(                                                    \
+            live_ ? wb + (((int64_t)t * nks + 4 * k_) << 9) : reinterpret_cast<const WT*>(x) + lane * 8);   \
         const u32x2 w0 = __builtin_nontemporal_load(p_), w1 = __builtin_nontemporal_load(p_ + 64),           \
                     w2 = __builtin_nontemporal_load(p_ + 128), w3 = __builtin_nontemporal_load(p_ + 192);   \
         rb[s][t] = (u32x8){w0[0], w0[1], w1[0], w1[1], w2[0], w2[1], w3[0], w3[1]};                          \
@@ -1667,6 +1671,17 @@ static inline void rwk_choose(int tiles, int nks, int C0, bool f8, int& nt, int&
   }
 }
 
+// MX ring steps are 128 deep: at S splits a wave runs K / (512 S) steps, too few to fill a 2-slot
+// ring at the 70B / 7B widths (4 at the 70B o projection) - halve the split and the group width
+// (every CU keeps a workgroup).  MPAMD_MX_NT=8 keeps the W8A16 geometry (A/B runs).
+static inline void mx_geometry(int tiles, int& nt, int& S) {
+  static const int mx_nt = getenv("MPAMD_MX_NT") ? atoi(getenv("MPAMD_MX_NT")) : 4;
+  if (nt == 8 && mx_nt == 4 && S % 2 == 0 && tiles % 4 == 0) {
+    nt = 4;
+    S /= 2;
+  }
+}
+
 // Widest split-K ring column group the instantiation for M rows holds in its accumulators: 192
 // AGPRs up to 128 rows (MT 5..8), all 256 at 129..256 rows (built at MT 12 and 16).
 constexpr int rwk_nt_max_mt(int MT) { return MT > 8 ? 64 / MT : (MT > 4 ? 192 / (4 * MT) : 8); }
@@ -1693,6 +1708,7 @@ static int launch_gemm_rwk(const void* x, const void* w, void* y, int64_t ys, co
   // accumulators: 192 AGPRs up to 128 rows, all 256 beyond (MT 9..16 -> NT <= 64 / MT)
   constexpr int nt_max = rwk_nt_max_mt(MT);
   rwk_choose(tiles, MX ? nks / 4 : nks, C0, F8, nt, S, nt_max);
+  if constexpr (MX) mx_geometry(tiles, nt, S);
   if (nt == 0) return 1;
   if ((int64_t)S * M * N * 4 > RWK_SLAB_BYTES) return 1;
   float* part = (float*)((char*)ws + (int64_t)SK_MAX_GROUPS * sizeof(int) + SK_ZERO_BYTES +

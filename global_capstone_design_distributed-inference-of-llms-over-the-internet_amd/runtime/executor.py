@@ -234,12 +234,17 @@ class StageExecutor:
         self.exec_lock = threading.RLock()
         # fp8 weights: W8A16 (ops.linear_w8: fp8 weights dequantized into the bf16 MFMA, bf16
         # activations, the fused-norm path below; default) or W8A8 (MPAMD_FP8_MODE=w8a8: fp8 MFMA,
-        # activations quantized per row before every GEMM, RMSNorm kernels; also under TP)
+        # activations quantized per row before every GEMM, RMSNorm kernels; also under TP).
+        # MPAMD_FP8_MODE=mx: the W8A16 path with the o and down projections of <= 64-row decode steps
+        # on the W8A8-MX GEMM (ops.linear_mx: MX e4m3 activations, block-scaled MFMA; opt-in - with
+        # its standalone activation quantizer it is not faster end to end, docs/ROUND6.md)
+        fp8_mode = os.environ.get("MPAMD_FP8_MODE", "w8a16")
         self._w8 = (self.device.type == "cuda" and weights.fp8 and cfg.model_type != "gpt2" and not cfg.is_moe and
-                    self._tp is None and os.environ.get("MPAMD_FP8_MODE", "w8a16") == "w8a16" and
+                    self._tp is None and fp8_mode in ("w8a16", "mx") and
                     os.environ.get("MPAMD_FUSED_NORM", "1") != "0" and
                     all(d % 256 == 0 for d in (cfg.hidden_size, cfg.q_dim, cfg.intermediate_size)) and
                     (cfg.q_dim + 2 * cfg.kv_dim) % 32 == 0)
+        self._mx = bool(self._w8 and fp8_mode == "mx")
         if self._w8:
             weights.prepare_w8a16(fold_norms=True)
         # fused-norm decode path (ops/csrc/gemm.hip EpiArgs): no RMSNorm kernels between the
@@ -615,7 +620,15 @@ class StageExecutor:
             ss_in, ss_post = self._ss[0], self._ss[1]
             if self._w8:  # fp8 weights (W8A16): same launches, 1 byte per weight streamed
                 def gemm(a, L, name, **kw):
-                    return ops.linear_w8(a, getattr(L, name + "_w8"), getattr(L, name + "_ws"), T, **kw)
+                    w8, wsc = getattr(L, name + "_w8"), getattr(L, name + "_ws")
+                    if self._mx and name in ("o", "down") and T <= 64:
+                        N, K = 16 * w8.shape[0], 32 * w8.shape[1]
+                        if ops.rwk_split(T, N, K, 2) > 0:  # W8A8-MX: quantize the packed input, MX GEMM
+                            ax, as_ = ops.quant_mx(a, T, K, e(f"mx_ax{K}", (16 * ((T + 15) // 16) * K,), torch.uint8),
+                                                   e(f"mx_as{K}", (2 * K,), torch.uint8))
+                            kw.pop("out_packed", None)
+                            return ops.linear_mx(ax, as_, w8, wsc, T, **kw)
+                    return ops.linear_w8(a, w8, wsc, T, **kw)
             else:
                 def gemm(a, L, name, **kw):
                     return ops.linear(a, None, wp=getattr(L, name + "_p"), a_rows=T, **kw)

@@ -10,3 +10,5 @@ timeout -k 5 60 ./lab/hip/mx_probe.bin > $O/probe.txt 2>&1; tail -1 $O/probe.txt
 tail -2 $O/tests.log
 timeout -k 10 400 python3 lab/tools/mx_ab.py > $O/ab.jsonl 2> $O/ab.err || { tail -20 $O/ab.err; exit 1; }
 cat $O/ab.jsonl
+MPAMD_MX_NT=8 timeout -k 10 300 python3 lab/tools/mx_ab.py --ms 64 > $O/ab_nt8.jsonl 2> $O/ab_nt8.err || { tail -20 $O/ab_nt8.err; exit 1; }
+echo "--- MPAMD_MX_NT=8"; cat $O/ab_nt8.jsonl

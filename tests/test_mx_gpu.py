@@ -111,3 +111,39 @@ def test_mx_gemm_matches_oracle(M, N, K):
     assert torch.equal(ops.unpack_act(ap, M, N), res)
     got_ss = ss_out.view(-1, 64).sum(0)[:M].double() / 2.0 ** 20
     torch.testing.assert_close(got_ss, (res.double() ** 2).sum(1), rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.gpu
+def test_executor_mx_mode_tracks_w8a16(monkeypatch):
+    """MPAMD_FP8_MODE=mx (o / down on the MX GEMM) against the default W8A16 executor on the same fp8
+    weights: a 2-layer Llama-2-7B-shaped stage, 30-session prefill + graph-replayed decode steps."""
+    import dataclasses
+
+    from src.models.config import resolve_model
+    from src.models.weights import random_stage_weights
+    from src.runtime.executor import StageExecutor
+
+    cfg = dataclasses.replace(resolve_model("llama2-7b"), num_hidden_layers=2)
+    B, P = 30, 16
+    g = torch.Generator().manual_seed(5)
+    prompts = torch.randint(0, cfg.vocab_size, (B * P,), generator=g).to(DEV)
+    toks = torch.randint(0, cfg.vocab_size, (3, B), generator=g).to(DEV)
+    outs = {}
+    for mode in ("w8a16", "mx"):
+        monkeypatch.setenv("MPAMD_FP8_MODE", mode)
+        w = random_stage_weights(cfg, 0, 2, has_embed=True, has_head=True, device=DEV, seed=3, fp8=True)
+        ex = StageExecutor(cfg, w, DEV, max_sessions=B + 2, max_seq_len=64, kv_cache_bytes=1 << 30,
+                           graph_max_batch=B, max_tokens_per_step=B * P, warmup=False)
+        assert ex._mx == (mode == "mx")
+        sids = [f"s{i}" for i in range(B)]
+        ex.forward([(s, P) for s in sids], prompts, reset=[True] * B)
+        got = [ex.forward([(s, 1) for s in sids], toks[t]).float().clone() for t in range(3)]
+        outs[mode] = torch.stack(got)
+        del ex, w
+        torch.cuda.empty_cache()
+    a, b = outs["mx"], outs["w8a16"]
+    assert torch.isfinite(a).all()
+    rel = float((a - b).norm() / b.norm())
+    assert rel < 0.06, rel  # MX e4m3 activations on two of the four projections
+    agree = float((a.argmax(-1) == b.argmax(-1)).float().mean())
+    assert agree >= 0.6, agree

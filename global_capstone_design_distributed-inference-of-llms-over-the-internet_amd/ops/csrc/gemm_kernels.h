@@ -976,6 +976,10 @@ static int launch_gemm_sk(const void* x, void* y, int64_t ys, const void* w, con
 #define MP_RW_WAVES 4
 #endif
 constexpr int RW_WAVES = MP_RW_WAVES;  // waves per ring workgroup (an ablation build sets 8)
+// Ring tail: the loads a wave issues R steps ahead run past its last k-step; they are clamped to a
+// valid step and their MFMAs skipped (in-order vmcnt needs every slot loaded).  Pointing those dead
+// weight loads at the L2-resident activation helps the 128-deep MX steps (profiles/r6mx) but not
+// these rings: 7B 64 / 1 sessions and 70B fp8 unchanged or 0.1-0.5 % slower (profiles/r6tail).
 constexpr int RW_QC = 128 / RW_WAVES;  // quads per LDS combine pass (waves x RW_QC x 1 KiB = 128 KiB)
 
 // Ring slots: a power of two (K / 32 / 4 waves is a multiple of it at K = 4096, 11008: no

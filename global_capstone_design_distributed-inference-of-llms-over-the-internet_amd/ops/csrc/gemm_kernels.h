@@ -35,6 +35,7 @@
 //     decode path (2 launches per layer fewer).
 #pragma once
 #include "common.h"
+#include <stdio.h>
 #include <stdlib.h>
 #include <type_traits>
 
@@ -1672,6 +1673,24 @@ static inline void rwk_choose(int tiles, int nks, int C0, bool f8, int& nt, int&
     if (tiles % cand || cand > nt_max) continue;
     const int C = tiles / cand, s = C0 / C;
     if (s >= 2 && s <= 8 && nks >= 4 * s && C * s > best_fill) { nt = cand; S = s; best_fill = C * s; }
+  }
+  // lab override (geometry A/B runs): MPAMD_RWK_GEOM="tiles:nt:S[:f8],..." replaces the choice for
+  // that column-tile count (f8 field: 0 bf16 / 1 fp8 weights; absent = both)
+  static const char* geo = getenv("MPAMD_RWK_GEOM");
+  if (geo != nullptr) {
+    const char* p = geo;
+    while (*p) {
+      int t = 0, n = 0, s = 0, w = -1, used = 0;
+      const int got = sscanf(p, "%d:%d:%d%n:%d%n", &t, &n, &s, &used, &w, &used);
+      if (got < 3) break;
+      if (t == tiles && (w < 0 || w == (int)f8) && n > 0 && n <= nt_max && tiles % n == 0 && s >= 2 && s <= 8 &&
+          nks >= 4 * s) {
+        nt = n;
+        S = s;
+      }
+      p += used;
+      while (*p == ',') ++p;
+    }
   }
 }
 

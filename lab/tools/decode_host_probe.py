@@ -30,8 +30,12 @@ def main():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--prompt", type=int, default=128)
     ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--layers", type=int, default=0, help="stage depth (0: the whole model)")
     a = ap.parse_args()
     cfg = resolve_model(a.model)
+    if a.layers:
+        import dataclasses
+        cfg = dataclasses.replace(cfg, num_hidden_layers=a.layers)
     B, dev = a.batch, "cuda"
     w = random_stage_weights(cfg, 0, cfg.num_hidden_layers, has_embed=True, has_head=True, device=dev, seed=0)
     ex = StageExecutor(cfg, w, dev, max_sessions=B + 8, max_seq_len=a.prompt + a.steps + 16,
@@ -57,6 +61,7 @@ def main():
     inside.clear()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     host = []
+    cpu0 = time.process_time()
     e0.record()
     t0 = time.perf_counter()
     for t in range(a.steps):
@@ -65,13 +70,15 @@ def main():
         host.append(time.perf_counter() - h)
     e1.record()
     t_issue = time.perf_counter() - t0
+    cpu = time.process_time() - cpu0
     e1.synchronize()
     gpu_ms = e0.elapsed_time(e1) / a.steps
     n = max(1, len(inside))
     print(json.dumps({"batch": B, "knobs": {k: os.environ[k] for k in KNOBS if k in os.environ},
                       "ms_per_step": round(gpu_ms, 4), "host_forward_ms": round(1e3 * sum(host) / len(host), 4),
                       "host_in_graph_launch_ms": round(1e3 * sum(inside) / n, 4), "replays": len(inside),
-                      "host_issue_ms_per_step": round(1e3 * t_issue / a.steps, 4)}), flush=True)
+                      "host_issue_ms_per_step": round(1e3 * t_issue / a.steps, 4),
+                      "host_cpu_ms_per_step": round(1e3 * cpu / a.steps, 4), "layers": cfg.num_hidden_layers}), flush=True)
 
 
 if __name__ == "__main__":

@@ -67,7 +67,7 @@ def data_plane_name(ch, eng) -> str:
 def fp8_label(ex) -> str:
     """The precision path the executor actually runs for fp8 weights."""
     if getattr(ex, "_mx", False):
-        return "fp8-w8a8-mx (e4m3 weights; o / down on MX e4m3 activations with e8m0 block scales, others bf16)"
+        return "fp8-w8a8-mx (e4m3 weights; o projection on MX e4m3 activations with e8m0 block scales, others bf16)"
     if getattr(ex, "_w8", False):
         return "fp8-w8a16 (e4m3 weights, bf16 activations/KV)"
     return "fp8-w8a8 (e4m3 weights and activations, bf16 KV)"

@@ -680,11 +680,14 @@ def attention_fa(q, k_cache, v_cache, block_tables, q_seq, q_ctx, fablocks, nh, 
 
 def attention_mfma_rope(qkv, k_cache, v_cache, block_tables, q_seq, q_ctx, qblocks, positions, cos, sin, slots, nh,
                         nkv, scale, out=None, workspace=None, part_size=None, num_parts=None, max_ctx=None,
-                        packed=False, qkv_part=None):
+                        packed=False, qkv_part=None, mx_out=None):
     """GQA decode step on the MFMA kernel with RoPE of q / new k and the new token's page-slot
     write folded in (csrc/attention_mfma.hip ROPE path).  ``qblocks`` must hold one token per block,
     block i = token i (``decode_qblocks``: the kernel takes that as given and reads no qblocks); ``qkv`` is the unrotated fused projection and is not modified; with
-    ``qkv_part`` the kernel reads q / k / v from the qkv GEMM's partial slabs instead."""
+    ``qkv_part`` the kernel reads q / k / v from the qkv GEMM's partial slabs instead.  ``mx_out =
+    (ax, as_)`` (packed, one part, head_dim 128): the kernel writes its output as the W8A8-MX GEMM's
+    activation (``quant_mx`` layout) there instead of ``out`` - the o projection's input, quantized
+    in the attention epilogue."""
     if qkv_part is not None and not _native(qkv):
         qkv = reduce_qkv_part(qkv_part, qkv.dtype)
         qkv_part = None
@@ -707,7 +710,8 @@ def attention_mfma_rope(qkv, k_cache, v_cache, block_tables, q_seq, q_ctx, qbloc
         workspace = attention_workspace(T, nh, D, num_parts, qkv.device)
     torch.ops.mpamd.attention_mfma_rope(qkv, k_cache, v_cache, block_tables, q_seq, q_ctx, qblocks, positions, cos,
                                         sin, slots, out, workspace, nh, nkv, float(scale), int(part_size),
-                                        int(num_parts), int(bool(packed)), *_qkv_part_args(qkv_part))
+                                        int(num_parts), int(bool(packed)), *_qkv_part_args(qkv_part),
+                                        *(mx_out if mx_out is not None else (None, None)))
     return out
 
 

@@ -35,6 +35,7 @@
 // kernel in attention.hip, measured 12-14 % SLOWER on this kernel at 64 / 256 sessions, cold
 // caches - profiles/r3_i/attn_nt.jsonl vs attn_def.jsonl.)
 #include "common.h"
+#include "mx_common.h"
 
 namespace mp {
 
@@ -46,6 +47,8 @@ struct RopeFuseM {
   bf16_t* kw;
   bf16_t* vw;
   QkvPart qp;  // qp.part != nullptr: q / k / v from the qkv GEMM's split-K partials (ROPE path)
+  uint8_t* mx_ax = nullptr;  // non-null (single-part launches): the output as the W8A8-MX GEMM's
+  uint8_t* mx_as = nullptr;  //   activation (mx_common.h) instead of bf16 - the o projection's input
 };
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_mf;
@@ -392,6 +395,23 @@ __global__ __launch_bounds__(256, 2) void attn_mfma_kernel(
     if (NP == 1) {
       const float v = den > 0.f ? num / den : 0.f;
       const int64_t col = (int64_t)h * D + d;
+      if (rf.mx_ax != nullptr) {
+        // MX block of (row, col): the 32 dims of this row with the same bit 4 and bits 6+ of col -
+        // lanes l ^ {1, 2, 4, 8, 32} of this wave (a wave holds 64 consecutive dims of one row, so
+        // the ``continue`` above is wave-uniform)
+        const float vb = bf2f(f2bf(v));
+        float a = fabsf(vb);
+        a = fmaxf(a, __shfl_xor(a, 1, 64));
+        a = fmaxf(a, __shfl_xor(a, 2, 64));
+        a = fmaxf(a, __shfl_xor(a, 4, 64));
+        a = fmaxf(a, __shfl_xor(a, 8, 64));
+        a = fmaxf(a, __shfl_xor(a, 32, 64));
+        const int e = mx_e8m0(a);
+        const float qv = fminf(fmaxf(vb * mx_inv_scale(e), -448.f), 448.f);
+        rf.mx_ax[mx_ax_off(tok, (int)col, packed_mt)] = (uint8_t)(__builtin_amdgcn_cvt_pk_fp8_f32(qv, 0.f, 0, false) & 255);
+        if ((col & 0x2f) == 0) rf.mx_as[mx_as_off(tok, (int)col)] = (uint8_t)e;
+        continue;
+      }
       out[packed_mt > 0 ? apk_off(tok, (int)col, packed_mt) : (int64_t)tok * nh * D + col] = f2bf(v);
     } else {
       const int64_t hp = ((int64_t)tok * nh + h) * NP + p;
@@ -619,7 +639,7 @@ extern "C" int mp_attention_mfma(const void* q, int64_t q_stride, const void* kc
                                  int D, int page_size, int PS, int NP, float scale, int packed_mt,
                                  const int64_t* rope_pos, const float* cos_t, const float* sin_t,
                                  const int64_t* slots, const int32_t* sb_first, const int32_t* sb_n, int NSB,
-                                 const void* qkv_part_v, hipStream_t stream) {
+                                 const void* qkv_part_v, void* mx_ax, void* mx_as, hipStream_t stream) {
   (void)hipGetLastError();  // an earlier non-mpamd HIP call's stale error is not this launch's
   using namespace mp;
   RopeFuseM rf{rope_pos, cos_t, sin_t, slots, (bf16_t*)const_cast<void*>(kc), (bf16_t*)const_cast<void*>(vc),
@@ -628,6 +648,11 @@ extern "C" int mp_attention_mfma(const void* q, int64_t q_stride, const void* kc
   if (qkv_part != nullptr && qkv_part->part != nullptr) {
     if (rope_pos == nullptr || qkv_part->S < 1) return -4;  // partials only on the fused RoPE decode path
     rf.qp = *qkv_part;
+  }
+  if (mx_ax != nullptr) {  // MX output: the fused RoPE decode path, one part, packed rows, 128-dim heads
+    if (rope_pos == nullptr || NP != 1 || packed_mt <= 0 || D != 128 || mx_as == nullptr) return -7;
+    rf.mx_ax = (uint8_t*)mx_ax;
+    rf.mx_as = (uint8_t*)mx_as;
   }
   if (NB == 0 || T == 0) return 0;
   if (nh % nkv != 0 || PS % 128 != 0 || NP < 1 || page_size % 32 != 0) return -1;

@@ -38,7 +38,7 @@ int mp_attention_mfma(const void* q, int64_t q_stride, const void* kc, const voi
                       void* out, float* workspace, int T, int nh, int nkv, int D, int page_size, int PS, int NP,
                       float scale, int packed_mt, const int64_t* rope_pos, const float* cos_t, const float* sin_t,
                       const int64_t* slots, const int32_t* sb_first, const int32_t* sb_n, int NSB,
-                      const void* qkv_part, hipStream_t stream);
+                      const void* qkv_part, void* mx_ax, void* mx_as, hipStream_t stream);
 int mp_attention_fa(const void* q, int64_t q_stride, const void* kc, const void* vc, const int32_t* bt, int bt_stride,
                     const int32_t* q_seq, const int32_t* q_ctx, const int32_t* fb_tok0, const int32_t* fb_ntok, int NBF,
                     void* out, float* workspace, int T, int nh, int nkv, int D, int page_size, int PS, int NP,
@@ -303,7 +303,7 @@ static void attention_mfma_impl(const at::Tensor& q, const at::Tensor& k_cache, 
                                 int64_t nkv, double scale, int64_t part_size, int64_t num_parts, int64_t packed,
                                 const int64_t* rope_pos, const float* cos_t, const float* sin_t,
                                 const int64_t* slots, const c10::optional<at::Tensor>& superblocks = c10::nullopt,
-                                const QkvPartArgs* qp = nullptr) {
+                                const QkvPartArgs* qp = nullptr, void* mx_ax = nullptr, void* mx_as = nullptr) {
   check_bf16_cuda(q, "q");
   check_rows(q, "q");
   check_bf16_cuda(out, "out");
@@ -341,7 +341,7 @@ static void attention_mfma_impl(const at::Tensor& q, const at::Tensor& k_cache, 
                                  qblocks.data_ptr<int32_t>() + NB, NB, out.data_ptr(), workspace.data_ptr<float>(), T,
                                  nh, nkv, D, k_cache.size(2), part_size, num_parts, (float)scale,
                                  packed ? (int)((T + 15) / 16) : 0, rope_pos, cos_t, sin_t, slots, sbp,
-                                 sbp != nullptr ? sbp + NSB : nullptr, NSB, qp, cur_stream()),
+                                 sbp != nullptr ? sbp + NSB : nullptr, NSB, qp, mx_ax, mx_as, cur_stream()),
                "attention_mfma");
 }
 
@@ -400,7 +400,8 @@ void attention_mfma_rope(const at::Tensor& qkv, at::Tensor& k_cache, at::Tensor&
                          const at::Tensor& sin, const at::Tensor& slots, at::Tensor& out, at::Tensor& workspace,
                          int64_t nh, int64_t nkv, double scale, int64_t part_size, int64_t num_parts, int64_t packed,
                          const c10::optional<at::Tensor>& qkv_part, int64_t part_splits,
-                         const c10::optional<at::Tensor>& part_ss, double inv_k, double eps) {
+                         const c10::optional<at::Tensor>& part_ss, double inv_k, double eps,
+                         const c10::optional<at::Tensor>& mx_ax, const c10::optional<at::Tensor>& mx_as) {
   check_bf16_cuda(k_cache, "k_cache");
   check_bf16_cuda(v_cache, "v_cache");
   MP_CHECK(k_cache.dim() == 4 && k_cache.sizes() == v_cache.sizes(), "cache [pages, nkv, page, D]");
@@ -414,9 +415,21 @@ void attention_mfma_rope(const at::Tensor& qkv, at::Tensor& k_cache, at::Tensor&
   MP_CHECK(qblocks.size(1) == T, "fused RoPE needs one query token per block (decode)");
   QkvPartArgs qp;
   const bool has_qp = qkv_part_args(qkv_part, part_splits, part_ss, inv_k, eps, T, qkv.size(1), qp);
+  void* axp = nullptr;
+  void* asp = nullptr;
+  if (mx_ax.has_value()) {  // the output as the W8A8-MX GEMM's activation (ops.quant_mx layout)
+    MP_CHECK(mx_as.has_value() && packed && num_parts == 1 && D == 128, "mx output: packed, one part, D 128, as_");
+    const int64_t K = nh * D, rows = ((T + 15) / 16) * 16;
+    MP_CHECK(mx_ax->is_cuda() && mx_ax->scalar_type() == at::kByte && mx_ax->is_contiguous() && mx_ax->numel() >= rows * K,
+             "mx_ax: uint8 [ceil(T/16)*16*K]");
+    MP_CHECK(mx_as->is_cuda() && mx_as->scalar_type() == at::kByte && mx_as->is_contiguous() && mx_as->numel() >= 2 * K,
+             "mx_as: uint8 [2K]");
+    axp = mx_ax->data_ptr();
+    asp = mx_as->data_ptr();
+  }
   attention_mfma_impl(qkv, k_cache, v_cache, block_tables, q_seq, q_ctx, qblocks, out, workspace, nh, nkv, scale,
                       part_size, num_parts, packed, positions.data_ptr<int64_t>(), cos.data_ptr<float>(),
-                      sin.data_ptr<float>(), slots.data_ptr<int64_t>(), c10::nullopt, has_qp ? &qp : nullptr);
+                      sin.data_ptr<float>(), slots.data_ptr<int64_t>(), c10::nullopt, has_qp ? &qp : nullptr, axp, asp);
 }
 
 void embedding(const at::Tensor& ids, const at::Tensor& table, at::Tensor& out) {
@@ -815,7 +828,8 @@ TORCH_LIBRARY(mpamd, m) {
       "attention_mfma_rope(Tensor qkv, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor block_tables, Tensor q_seq, "
       "Tensor q_ctx, Tensor qblocks, Tensor positions, Tensor cos, Tensor sin, Tensor slots, Tensor(c!) out, "
       "Tensor(d!) workspace, int nh, int nkv, float scale, int part_size, int num_parts, int packed, "
-      "Tensor? qkv_part=None, int part_splits=0, Tensor? part_ss=None, float inv_k=0., float eps=0.) -> ()");
+      "Tensor? qkv_part=None, int part_splits=0, Tensor? part_ss=None, float inv_k=0., float eps=0., "
+      "Tensor(e!)? mx_ax=None, Tensor(f!)? mx_as=None) -> ()");
   m.def("embedding(Tensor ids, Tensor table, Tensor(a!) out) -> ()");
   m.def("swiglu(Tensor gu, Tensor(a!) out) -> ()");
   m.def("add(Tensor a, Tensor b, Tensor(a!) y) -> ()");

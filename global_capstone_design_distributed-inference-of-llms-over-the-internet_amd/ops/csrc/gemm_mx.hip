@@ -23,17 +23,9 @@
 // weight column scales after the loop) + the shared reduce launch and epilogues (row scale of the
 // fused-norm consumer, residual-stream producer) - or partial slabs only for the qkv fold.
 #include "gemm_kernels.h"
+#include "mx_common.h"
 
 namespace mp {
-
-// e8m0 exponent (biased 127) of the smallest power-of-two scale s with amax / s <= 448 (e4m3 max)
-__device__ __forceinline__ int mx_e8m0(float amax) {
-  if (!(amax > 0.f)) return 127;
-  const unsigned b = __float_as_uint(amax * (1.f / 448.f));
-  const int ex = (int)((b >> 23) & 255);
-  int e = ex + ((b & 0x7fffff) != 0 ? 1 : 0);  // ceil(log2) + 127 (normal range)
-  return e < 1 ? 1 : (e > 253 ? 253 : e);
-}
 
 // One thread per (k-step kb, row tile mt, row r): reads the row's 128 values of the step (16 x 16 B
 // of the packed bf16 activation), the four block maxima, writes the four lanes' 32 bytes and the

@@ -235,9 +235,9 @@ class StageExecutor:
         # fp8 weights: W8A16 (ops.linear_w8: fp8 weights dequantized into the bf16 MFMA, bf16
         # activations, the fused-norm path below; default) or W8A8 (MPAMD_FP8_MODE=w8a8: fp8 MFMA,
         # activations quantized per row before every GEMM, RMSNorm kernels; also under TP).
-        # MPAMD_FP8_MODE=mx: the W8A16 path with the o and down projections of <= 64-row decode steps
-        # on the W8A8-MX GEMM (ops.linear_mx: MX e4m3 activations, block-scaled MFMA; opt-in - with
-        # its standalone activation quantizer it is not faster end to end, docs/ROUND6.md)
+        # MPAMD_FP8_MODE=mx: the W8A16 path with the o projection of <= 64-row GQA decode steps on the
+        # W8A8-MX GEMM (ops.linear_mx: MX e4m3 activations, block-scaled MFMA), its input written as
+        # MX by the attention kernel's epilogue (no quantizer launch); profiles/r6mx
         fp8_mode = os.environ.get("MPAMD_FP8_MODE", "w8a16")
         self._w8 = (self.device.type == "cuda" and weights.fp8 and cfg.model_type != "gpt2" and not cfg.is_moe and
                     self._tp is None and fp8_mode in ("w8a16", "mx") and
@@ -531,18 +531,23 @@ class StageExecutor:
             ops.rwk_split(T, cfg.q_dim + 2 * cfg.kv_dim, cfg.hidden_size, bool(self._w8)) > 0
 
     def _rope_attend(self, qkv, positions, slots, kc, vc, q_seq, q_ctx, out, ws, ps, np_, packed, qblocks, max_ctx,
-                     decode, qkv_part=None):
+                     decode, qkv_part=None, mx_out=None, mx_used=None):
         """RoPE + KV write + attention.  Decode steps that run on the flash-decoding kernel do all
         three in one launch (ops.paged_attention_rope); everything else keeps rope_kv_write.
-        ``qkv_part``: q / k / v as the qkv GEMM's split-K slabs (decode RoPE paths only)."""
+        ``qkv_part``: q / k / v as the qkv GEMM's split-K slabs (decode RoPE paths only).  ``mx_out``:
+        (ax, as_) MX buffers the GQA kernel writes instead of ``out`` when it can (one part, packed,
+        head_dim 128); it then appends True to ``mx_used``."""
         if decode and qblocks is None and self._fuse_rope and self.gqa_decode_mfma and self.device.type == "cuda":
             T = qkv.shape[0]
             ps2 = 128 * math.ceil(ps / 128)
             np2 = max(1, math.ceil(ps * np_ / ps2))
+            mx = mx_out if (mx_out is not None and np2 == 1 and packed and self.D == 128) else None
+            if mx is not None and mx_used is not None:
+                mx_used.append(True)
             return ops.attention_mfma_rope(qkv, kc, vc, self.sessions.table_dev, q_seq, q_ctx, self.decode_qblocks(T),
                                            positions, self.cos, self.sin, slots, self.nh, self.nkv, self.scale,
                                            out=out, workspace=ws, part_size=ps2, num_parts=np2, packed=packed,
-                                           qkv_part=qkv_part)
+                                           qkv_part=qkv_part, mx_out=mx)
         if decode and qblocks is None and self._fuse_rope and not (
                 self.gqa_decode_mfma and self.device.type == "cuda"):
             return ops.paged_attention_rope(qkv, kc, vc, self.sessions.table_dev, q_seq, q_ctx, positions, self.cos,
@@ -620,21 +625,18 @@ class StageExecutor:
             ss_in, ss_post = self._ss[0], self._ss[1]
             if self._w8:  # fp8 weights (W8A16): same launches, 1 byte per weight streamed
                 def gemm(a, L, name, **kw):
-                    w8, wsc = getattr(L, name + "_w8"), getattr(L, name + "_ws")
-                    if self._mx and name in ("o", "down") and T <= 64:
-                        N, K = 16 * w8.shape[0], 32 * w8.shape[1]
-                        if ops.rwk_split(T, N, K, 2) > 0:  # W8A8-MX: quantize the packed input, MX GEMM
-                            ax, as_ = ops.quant_mx(a, T, K, e(f"mx_ax{K}", (16 * ((T + 15) // 16) * K,), torch.uint8),
-                                                   e(f"mx_as{K}", (2 * K,), torch.uint8))
-                            kw.pop("out_packed", None)
-                            return ops.linear_mx(ax, as_, w8, wsc, T, **kw)
-                    return ops.linear_w8(a, w8, wsc, T, **kw)
+                    return ops.linear_w8(a, getattr(L, name + "_w8"), getattr(L, name + "_ws"), T, **kw)
             else:
                 def gemm(a, L, name, **kw):
                     return ops.linear(a, None, wp=getattr(L, name + "_p"), a_rows=T, **kw)
             # decode steps whose qkv GEMM measured faster as split-K partial slabs: the attention
             # kernel sums the slabs + applies the row scale on its q / k / v loads (no reduce launch)
             fold = decode and qblocks is None and self._qkv_fold(T)
+            # W8A8-MX o projection: the attention epilogue writes the MX activation (GQA decode)
+            Q = cfg.q_dim
+            mx_o = None
+            if self._mx and decode and qblocks is None and T <= 64 and ops.rwk_split(T, H, Q, 2) > 0:
+                mx_o = (e(f"mx_ax{Q}", (16 * ((T + 15) // 16) * Q,), torch.uint8), e(f"mx_as{Q}", (2 * Q,), torch.uint8))
             for li, L in self._iter_layers(_PACKED_FIELDS):
                 if li == 0:
                     ops.rmsnorm(h, L.input_norm, eps, out=xr, residual=res, mode=3, packed=True, ss=ss_in)
@@ -648,9 +650,14 @@ class StageExecutor:
                 else:
                     gemm(xr, L, "qkv", out=qkv, ss_in=ss_in, eps=eps)
                 kc, vc = self.cache.layer(li)
+                used = []
                 self._rope_attend(qkv, positions, slots, kc, vc, q_seq, q_ctx, attn, ws, ps, np_, True, qblocks,
-                                  max_ctx, decode, qkv_part=qp)
-                gemm(attn, L, "o", out=res, epilogue=3, residual=res, ap_out=xr, ss_out=ss_post, ss_zero=ss_in)
+                                  max_ctx, decode, qkv_part=qp, mx_out=mx_o, mx_used=used)
+                if used:
+                    ops.linear_mx(mx_o[0], mx_o[1], L.o_w8, L.o_ws, T, out=res, epilogue=3, residual=res, ap_out=xr,
+                                  ss_out=ss_post, ss_zero=ss_in)
+                else:
+                    gemm(attn, L, "o", out=res, epilogue=3, residual=res, ap_out=xr, ss_out=ss_post, ss_zero=ss_in)
                 gemm(xr, L, "gate_up", out=act, epilogue=1, out_packed=True, ss_in=ss_post, eps=eps)
                 gemm(act, L, "down", out=res, epilogue=3, residual=res, ap_out=xr, ss_out=ss_in, ss_zero=ss_post)
             mlp = None

@@ -1,11 +1,12 @@
 #!/bin/bash
-# Round 6: W8A8-MX opt-in mode end to end - MX tests (incl. the executor mode), then Llama-3-70B fp8
+# Round 6: W8A8-MX opt-in mode end to end (o projection, MX input from the attention epilogue) - MX tests
+# (incl. the executor mode), then Llama-3-70B fp8
 # 64 sessions with MPAMD_FP8_MODE=mx vs the W8A16 default, interleaved.
 set -o pipefail
 O=gpurun_out/${1:-r6mx70}
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-timeout -k 10 400 python3 -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu tests/test_mx_gpu.py > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
+timeout -k 10 500 python3 -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/test_mx_gpu.py > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
 tail -2 $O/tests.log
 for r in 1 2; do
   for m in mx w8a16; do

@@ -114,16 +114,51 @@ def test_mx_gemm_matches_oracle(M, N, K):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("nh,nkv", [(32, 8), (64, 8)])
+@pytest.mark.parametrize("T", [1, 6, 33])
+def test_attention_writes_mx(nh, nkv, T):
+    """The GQA decode attention's MX output (``mx_out``) is bit for bit ``quant_mx`` of its bf16 packed
+    output: same bf16 rounding, same block maxima, same e4m3 bytes and e8m0 scales (rows < T)."""
+    import math
+
+    from tests.test_kernels_gpu import _attn_case
+
+    D = 128
+    ctxs = [((7 * i) % 190) + 1 for i in range(T)]
+    ps = 64
+    q, kc, vc, bt, q_seq, q_ctx = _attn_case(nh, nkv, D, ctxs, ps=ps)
+    pos = (q_ctx.long() - 1).clamp(min=0)
+    slots = torch.stack([bt[i, int(p) // ps].long() * ps + int(p) % ps for i, p in enumerate(pos.tolist())])
+    qb = torch.from_numpy(ops.query_blocks([1] * T, nh // nkv)).to(DEV)
+    cos, sin = ops.rope_cos_sin(D, 2048, 10000.0, DEV)
+    scale = 1 / math.sqrt(D)
+    kc2, vc2 = kc.clone(), vc.clone()
+    o = ops.attention_mfma_rope(q, kc, vc, bt, q_seq, q_ctx, qb, pos, cos, sin, slots, nh, nkv, scale, packed=True,
+                                part_size=256, num_parts=1)
+    K = nh * D
+    ax, as_ = ops.mx_buffers(T, K, DEV)
+    ops.attention_mfma_rope(q, kc2, vc2, bt, q_seq, q_ctx, qb, pos, cos, sin, slots, nh, nkv, scale, packed=True,
+                            part_size=256, num_parts=1, mx_out=(ax, as_))
+    assert torch.equal(kc, kc2) and torch.equal(vc, vc2)
+    ax2, as2 = ops.quant_mx(o, T, K)
+    assert torch.equal(_dequant_gpu(ax, as_, T, K), _dequant_gpu(ax2, as2, T, K))
+
+
+@pytest.mark.gpu
 def test_executor_mx_mode_tracks_w8a16(monkeypatch):
-    """MPAMD_FP8_MODE=mx (o / down on the MX GEMM) against the default W8A16 executor on the same fp8
-    weights: a 2-layer Llama-2-7B-shaped stage, 30-session prefill + graph-replayed decode steps."""
+    """MPAMD_FP8_MODE=mx (the o projection on the MX GEMM, its input written by the GQA attention)
+    against the default W8A16 executor on the same fp8 weights: a 2-layer Llama-3-8B-shaped stage,
+    30-session prefill + graph-replayed decode steps."""
     import dataclasses
 
     from src.models.config import resolve_model
     from src.models.weights import random_stage_weights
     from src.runtime.executor import StageExecutor
 
-    cfg = dataclasses.replace(resolve_model("llama2-7b"), num_hidden_layers=2)
+    cfg = dataclasses.replace(resolve_model("llama3-8b"), num_hidden_layers=2)
+    calls = []
+    real = ops.linear_mx
+    monkeypatch.setattr(ops, "linear_mx", lambda *a, **k: calls.append(1) or real(*a, **k))
     B, P = 30, 16
     g = torch.Generator().manual_seed(5)
     prompts = torch.randint(0, cfg.vocab_size, (B * P,), generator=g).to(DEV)
@@ -141,6 +176,7 @@ def test_executor_mx_mode_tracks_w8a16(monkeypatch):
         outs[mode] = torch.stack(got)
         del ex, w
         torch.cuda.empty_cache()
+    assert calls, "the MX o projection never ran"
     a, b = outs["mx"], outs["w8a16"]
     assert torch.isfinite(a).all()
     rel = float((a - b).norm() / b.norm())

@@ -23,3 +23,12 @@ if [ "${KTAB70:-1}" = 1 ]; then
   python3 lab/tools/rocpd_steps.py $DB --steps 10 --seq 12 > $O/b70_kernels_per_step.txt && rm -rf $O/p70 || exit 1
   head -20 $O/b70_kernels_per_step.txt
 fi
+if [ "${KTAB7:-1}" = 1 ]; then
+  for b in 64 1; do
+    timeout -k 10 400 rocprofv3 --kernel-trace -d $O/p$b -o run -- python3 bench.py --batch $b --steps 20 --warmup 5 \
+      > $O/b${b}_prof.json 2> $O/b${b}_prof.err || exit 1
+    DB=$(find $O/p$b -name "*.db" | head -1)
+    python3 lab/tools/rocpd_steps.py $DB --steps 20 --seq 16 > $O/b${b}_kernels_per_step.txt && rm -rf $O/p$b || exit 1
+    head -12 $O/b${b}_kernels_per_step.txt
+  done
+fi

@@ -635,7 +635,8 @@ class StageExecutor:
             # W8A8-MX o projection: the attention epilogue writes the MX activation (GQA decode)
             Q = cfg.q_dim
             mx_o = None
-            if self._mx and decode and qblocks is None and T <= 64 and ops.rwk_split(T, H, Q, 2) > 0:
+            if (self._mx and decode and qblocks is None and T <= 64 and self.gqa_decode_mfma and self._fuse_rope and
+                    ops.rwk_split(T, H, Q, 2) > 0):
                 mx_o = (e(f"mx_ax{Q}", (16 * ((T + 15) // 16) * Q,), torch.uint8), e(f"mx_as{Q}", (2 * Q,), torch.uint8))
             for li, L in self._iter_layers(_PACKED_FIELDS):
                 if li == 0:

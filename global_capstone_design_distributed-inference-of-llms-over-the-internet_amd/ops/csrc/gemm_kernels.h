@@ -1674,17 +1674,17 @@ static inline void rwk_choose(int tiles, int nks, int C0, bool f8, int& nt, int&
     const int C = tiles / cand, s = C0 / C;
     if (s >= 2 && s <= 8 && nks >= 4 * s && C * s > best_fill) { nt = cand; S = s; best_fill = C * s; }
   }
-  // lab override (geometry A/B runs): MPAMD_RWK_GEOM="tiles:nt:S[:f8],..." replaces the choice for
-  // that column-tile count (f8 field: 0 bf16 / 1 fp8 weights; absent = both)
+  // lab override (geometry A/B runs): MPAMD_RWK_GEOM="tiles:nt:S[:f8[:nks]],..." replaces the choice
+  // for that column-tile count (f8 field: 0 bf16 / 1 fp8 weights, -1 both; nks: only that K / 32)
   static const char* geo = getenv("MPAMD_RWK_GEOM");
   if (geo != nullptr) {
     const char* p = geo;
     while (*p) {
-      int t = 0, n = 0, s = 0, w = -1, used = 0;
-      const int got = sscanf(p, "%d:%d:%d%n:%d%n", &t, &n, &s, &used, &w, &used);
+      int t = 0, n = 0, s = 0, w = -1, k = -1, used = 0;
+      const int got = sscanf(p, "%d:%d:%d%n:%d%n:%d%n", &t, &n, &s, &used, &w, &used, &k, &used);
       if (got < 3) break;
-      if (t == tiles && (w < 0 || w == (int)f8) && n > 0 && n <= nt_max && tiles % n == 0 && s >= 2 && s <= 8 &&
-          nks >= 4 * s) {
+      if (t == tiles && (w < 0 || w == (int)f8) && (k < 0 || k == nks) && n > 0 && n <= nt_max && tiles % n == 0 &&
+          s >= 2 && s <= 8 && nks >= 4 * s) {
         nt = n;
         S = s;
       }

@@ -3,6 +3,9 @@
 // v_mfma_scale_f32_16x16x128_f8f6f4 - BASELINE config 5's "fp8 MFMA path" with the activation
 // scale local to a block, so no row-wide absmax (the W8A8 path of fp8.hip needs one, i.e. two
 // launches or a one-workgroup-per-row pass) and no per-element conversion in the GEMM.
+// Reference: the upstream server's quantized default (NF4 on CUDA, petals/server/server.py:189-190)
+// applies to the same projections (petals/llama/block.py:88-90 q / k / v, :151 o); here 8-bit
+// weights and, in this mode, 8-bit activations go through the matrix cores directly.
 //
 // Fragment / scale map of the instruction (lab/hip/mx_probe*.hip, measured): lane l = 16 q + r of
 // the A operand holds row r, byte j at k = 16 q + j (j < 16) and k = 64 + 16 q + j - 16 (j >= 16) of

@@ -498,6 +498,18 @@ def rmsnorm(x, w, eps, out=None, residual=None, mode=0, rows=None, packed=False,
     return a8 if a8 is not None else out
 
 
+def embed_stage_entry(ids, table, out, residual, ss):
+    """Embedding lookup + the fused-norm path's stage entry (``rmsnorm`` mode 3) in one launch:
+    residual[t] = table[ids[t]], ``out`` = the same rows packed, ``ss`` = their fixed-point row sums of
+    squares.  (reference: the embedding + input_layernorm of petals/llama/block.py, here the entry of a
+    first stage whose norm is folded into the qkv GEMM.)"""
+    if not _native(table):
+        h = embedding(ids, table)
+        return rmsnorm(h, table[0], 0.0, out=out, residual=residual, mode=3, packed=True, ss=ss)
+    torch.ops.mpamd.rmsnorm(table, residual, table[0], out, 0.0, 3, None, 1, ss, None, None, ids)
+    return out
+
+
 def rope_kv_write(qkv, positions, cos, sin, k_cache, v_cache, slots, nh, nkv):
     if not _native(qkv):
         return ref.rope_kv_write(qkv, positions, cos, sin, k_cache, v_cache, slots, nh, nkv)

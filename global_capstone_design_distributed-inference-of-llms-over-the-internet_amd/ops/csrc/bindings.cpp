@@ -12,7 +12,8 @@
 extern "C" {
 int mp_rmsnorm(const void* x, int64_t x_stride, void* res, int64_t res_stride, const void* w, void* y,
                int64_t y_stride, const int32_t* rows, int nrows, int H, float eps, int mode, int packed_mt,
-               void* ss_out, void* a8, float* a8_scale, hipStream_t stream);
+               void* ss_out, void* a8, float* a8_scale, const int64_t* gather, int64_t gather_n,
+               hipStream_t stream);
 int mp_rope_kv_write(void* qkv, int64_t qkv_stride, const int64_t* pos, const float* cos_t, const float* sin_t,
                      void* kc, void* vc, const int64_t* slots, int T, int nh, int nkv, int D, int page_size,
                      hipStream_t stream);
@@ -103,7 +104,8 @@ inline void* opt_ss(const c10::optional<at::Tensor>& t, const char* name) {
 
 void rmsnorm(const at::Tensor& x, at::Tensor& residual, const at::Tensor& w, at::Tensor& y, double eps, int64_t mode,
              const c10::optional<at::Tensor>& rows, int64_t packed, const c10::optional<at::Tensor>& ss,
-             const c10::optional<at::Tensor>& a8, const c10::optional<at::Tensor>& a8_scale) {
+             const c10::optional<at::Tensor>& a8, const c10::optional<at::Tensor>& a8_scale,
+             const c10::optional<at::Tensor>& gather) {
   check_bf16_cuda(x, "x");
   check_bf16_cuda(w, "w");
   check_bf16_cuda(y, "y");
@@ -116,14 +118,23 @@ void rmsnorm(const at::Tensor& x, at::Tensor& residual, const at::Tensor& w, at:
   }
   MP_CHECK(mode >= 0 && mode <= 3, "mode");
   void* ssp = opt_ss(ss, "ss");
-  MP_CHECK(mode != 3 || (ssp != nullptr && x.size(0) <= 256), "mode 3 needs ss and <= 256 rows");
+  // gather: x is an embedding table and row t of the output / residual is x[gather[t]] (stage entry)
+  const int64_t* gp = nullptr;
+  int nrows = x.size(0);
+  if (gather.has_value()) {
+    MP_CHECK(gather->is_cuda() && gather->scalar_type() == at::kLong && gather->is_contiguous() && gather->dim() == 1,
+             "gather: int64 cuda [T]");
+    MP_CHECK(mode >= 2 && !rows.has_value(), "gather with mode 2 / 3, no rows");
+    gp = gather->data_ptr<int64_t>();
+    nrows = gather->numel();
+  }
+  MP_CHECK(mode != 3 || (ssp != nullptr && nrows <= 256), "mode 3 needs ss and <= 256 rows");
   if (mode != 0) {
     check_bf16_cuda(residual, "residual");
     check_rows(residual, "residual");
-    MP_CHECK(residual.size(0) == x.size(0) && residual.size(1) == H, "residual shape");
+    MP_CHECK(residual.size(0) == nrows && residual.size(1) == H, "residual shape");
   }
   const int32_t* rp = nullptr;
-  int nrows = x.size(0);
   if (rows.has_value()) {
     MP_CHECK(rows->scalar_type() == at::kInt && rows->is_contiguous() && rows->is_cuda(), "rows: int32 cuda");
     MP_CHECK(mode == 0, "row gather only with mode 0");
@@ -150,7 +161,8 @@ void rmsnorm(const at::Tensor& x, at::Tensor& residual, const at::Tensor& w, at:
   }
   check_launch(mp_rmsnorm(x.data_ptr(), x.stride(0), mode ? residual.data_ptr() : nullptr,
                           mode ? residual.stride(0) : 0, w.data_ptr(), y.data_ptr(), packed ? 0 : y.stride(0), rp,
-                          nrows, H, (float)eps, (int)mode, pmt, ssp, a8p, a8s, cur_stream()),
+                          nrows, H, (float)eps, (int)mode, pmt, ssp, a8p, a8s, gp, gp ? x.size(0) : 0,
+                          cur_stream()),
                "rmsnorm");
 }
 
@@ -802,7 +814,7 @@ TORCH_LIBRARY(mpamd, m) {
   m.def("gemm_t2d_ok(int M, int N, int K, int epilogue, int out_packed) -> bool", &gemm_t2d_ok);
   m.def(
       "rmsnorm(Tensor x, Tensor(a!) residual, Tensor w, Tensor(b!) y, float eps, int mode, Tensor? rows, "
-      "int packed, Tensor(c!)? ss=None, Tensor(d!)? a8=None, Tensor(e!)? a8_scale=None) -> ()");
+      "int packed, Tensor(c!)? ss=None, Tensor(d!)? a8=None, Tensor(e!)? a8_scale=None, Tensor? gather=None) -> ()");
   m.def(
       "rope_kv_write(Tensor(a!) qkv, Tensor positions, Tensor cos, Tensor sin, Tensor(b!) k_cache, "
       "Tensor(c!) v_cache, Tensor slots, int nh, int nkv) -> ()");

@@ -30,15 +30,23 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(
     const bf16_t* __restrict__ x, int64_t x_stride, bf16_t* __restrict__ res, int64_t res_stride,
     const bf16_t* __restrict__ w, bf16_t* __restrict__ y, int64_t y_stride,
     const int32_t* __restrict__ rows, int H, float eps, int mode, int packed_mt,
-    unsigned long long* __restrict__ ss_out, uint8_t* __restrict__ a8, float* __restrict__ a8_scale) {
+    unsigned long long* __restrict__ ss_out, uint8_t* __restrict__ a8, float* __restrict__ a8_scale,
+    const int64_t* __restrict__ gather, int64_t gather_n) {
   __shared__ float red[16];
   __shared__ float redm[16];
   __shared__ unsigned long long redq[16];
   const int orow = blockIdx.x;
   const int irow = rows ? rows[orow] : orow;
   const int nch = H >> 3;
-  const bf16_t* xr = x + (int64_t)irow * x_stride;
-  bf16_t* rr = res + (int64_t)irow * res_stride;
+  // gather (the stage entry of a first stage): input row = the token's embedding-table row, so the
+  // embedding lookup and the stage-entry statistics are one launch; the residual row is the token's
+  int64_t xrow = irow;
+  if (gather != nullptr) {
+    const int64_t id = gather[orow];
+    xrow = (id < 0 || id >= gather_n) ? 0 : id;  // never read out of bounds; the host validates ids
+  }
+  const bf16_t* xr = x + xrow * x_stride;
+  bf16_t* rr = res + (int64_t)(gather != nullptr ? orow : irow) * res_stride;
   // every global load (x, residual, weight) is issued before the first store and before the
   // block reduction, unconditionally (clamped chunk index: no exec-masked branches between the
   // loads): one memory round trip per call instead of three
@@ -138,12 +146,14 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(
 
 extern "C" int mp_rmsnorm(const void* x, int64_t x_stride, void* res, int64_t res_stride, const void* w,
                           void* y, int64_t y_stride, const int32_t* rows, int nrows, int H, float eps,
-                          int mode, int packed_mt, void* ss_out, void* a8, float* a8_scale, hipStream_t stream) {
+                          int mode, int packed_mt, void* ss_out, void* a8, float* a8_scale,
+                          const int64_t* gather, int64_t gather_n, hipStream_t stream) {
   (void)hipGetLastError();  // an earlier non-mpamd HIP call's stale error is not this launch's
   using namespace mp;
   if (H % 8 != 0 || H > 8 * 256 * 8) return -1;
   if (mode == 3 && (ss_out == nullptr || nrows > QP_SS_ROWS)) return -2;
   if (a8 != nullptr && (packed_mt <= 0 || H % 64 || a8_scale == nullptr || mode == 3)) return -3;
+  if (gather != nullptr && (mode < 2 || rows != nullptr || gather_n <= 0)) return -4;
   if (nrows == 0) return 0;
   const int nch = H / 8;
   // threads per row: 512 (one 16-B chunk per thread at H = 4096) measured best in the decode
@@ -156,7 +166,7 @@ extern "C" int mp_rmsnorm(const void* x, int64_t x_stride, void* res, int64_t re
   auto args = [&](auto kern) {
     hipLaunchKernelGGL(kern, grid, block, 0, stream, (const bf16_t*)x, x_stride, (bf16_t*)res, res_stride,
                        (const bf16_t*)w, (bf16_t*)y, y_stride, rows, H, eps, mode, packed_mt,
-                       (unsigned long long*)ss_out, (uint8_t*)a8, a8_scale);
+                       (unsigned long long*)ss_out, (uint8_t*)a8, a8_scale, gather, gather_n);
   };
   // MAXC = chunks of 8 per thread; nch <= MAXC * nt
   const int per = (nch + nt - 1) / nt;

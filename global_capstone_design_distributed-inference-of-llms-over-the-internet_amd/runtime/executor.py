@@ -255,6 +255,9 @@ class StageExecutor:
                        os.environ.get("MPAMD_FUSED_NORM", "1") != "0" and
                        all(d % 128 == 0 for d in (cfg.hidden_size, cfg.q_dim, cfg.intermediate_size)))
         self._ss = ops.norm_stats_buffer(self.device, 2) if self._fused else None
+        # first stage on that path: the stage-entry kernel gathers the embedding rows itself
+        # (ops.embed_stage_entry; MPAMD_FUSED_ENTRY=0 keeps the separate embedding launch)
+        self._fused_entry = os.environ.get("MPAMD_FUSED_ENTRY", "1") != "0"
         # unit RMSNorm weight for > 64-row decode steps over norm-folded packed weights (made
         # here, not inside a hipGraph capture)
         self._ones = torch.ones(cfg.hidden_size, dtype=self.dtype, device=self.device) if self._fused else None
@@ -567,8 +570,13 @@ class StageExecutor:
         if bufs is None:
             bufs = {}
         e = lambda name, shape, dtype=dt: bufs.get(name) if name in bufs else torch.empty(shape, dtype=dtype, device=dev)  # noqa: E731
-        if self.is_first:
+        fp8_dec = prompt is None and self._fp8_ok(T)
+        fused_dec = (not fp8_dec and prompt is None and self._fused and self.n_layers > 0 and
+                     (T <= 64 and (self._w8 or self._packed_ok(T)) or (not self._w8 and self._fused_wide_ok(T))))
+        if self.is_first and not (fused_dec and self._fused_entry and x.dim() == 1 and x.is_contiguous()):
             h = ops.embedding(x, w.embed, out=e("h", (T, H)))
+        elif self.is_first:
+            h = None  # the fused path's stage-entry kernel gathers the embedding rows itself
         else:
             h = x
         if attn_part is None:
@@ -579,7 +587,7 @@ class StageExecutor:
         qkv = e("qkv", (T, cfg.q_dim + 2 * cfg.kv_dim))
         o = e("o", (T, H))
         mlp = e("mlp", (T, H))
-        if prompt is None and self._fp8_ok(T):
+        if fp8_dec:
             # fp8 W8A8 decode path: packed bf16 activations are quantized per row right before
             # each GEMM (csrc/fp8.hip); weights stream at 1 byte per parameter
             pk = ops.packed_numel
@@ -610,8 +618,7 @@ class StageExecutor:
                 ops.quant_rows_fp8(act, out=a8, scale=asc)
                 ops.linear_fp8(a8, asc, L.down_q, L.down_s, T, out=mlp)
                 self._ar(mlp)
-        elif prompt is None and self._fused and (T <= 64 and (self._w8 or self._packed_ok(T)) or
-                                                  (not self._w8 and self._fused_wide_ok(T))):
+        elif fused_dec:
             # fused-norm decode path: 5 launches per layer (qkv, attention, o, gate/up, down).
             # The residual stream r lives row-major in ``res`` and packed in ``xr``; o / down add
             # their product into it in their epilogue and accumulate sum(r^2) per row, and qkv /
@@ -639,7 +646,9 @@ class StageExecutor:
                     ops.rwk_split(T, H, Q, 2) > 0):
                 mx_o = (e(f"mx_ax{Q}", (16 * ((T + 15) // 16) * Q,), torch.uint8), e(f"mx_as{Q}", (2 * Q,), torch.uint8))
             for li, L in self._iter_layers(_PACKED_FIELDS):
-                if li == 0:
+                if li == 0 and h is None:  # first stage: embedding lookup + stage entry in one launch
+                    ops.embed_stage_entry(x, w.embed, xr, res, ss_in)
+                elif li == 0:
                     ops.rmsnorm(h, L.input_norm, eps, out=xr, residual=res, mode=3, packed=True, ss=ss_in)
                 qp = None
                 if fold:

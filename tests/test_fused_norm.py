@@ -345,3 +345,29 @@ def test_fused_executor_matches_unfused_and_oracle(graphs, monkeypatch):
         for i in range(3):
             r = reference_forward([w], cur[i].cuda())[-1]
             torch.testing.assert_close(lf[i].float(), r, atol=0.08, rtol=0.05)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T,H", [(1, 4096), (37, 4096), (64, 8192)])
+def test_embed_stage_entry_matches_embedding_then_mode3(T, H):
+    """The first stage's fused entry (embedding rows gathered by the mode-3 kernel) == embedding, then
+    rmsnorm mode 3: same residual rows, same packed rows, same fixed-point row statistics (bit for
+    bit); an out-of-range id reads row 0 in both."""
+    dev = "cuda"
+    g = torch.Generator(device=dev).manual_seed(T)
+    V = 1000
+    table = torch.randn(V, H, device=dev, generator=g).to(torch.bfloat16)
+    ids = torch.randint(0, V, (T,), device=dev, generator=g)
+    if T > 1:
+        ids[-1] = V + 5
+    h = ops.embedding(ids, table)
+    res1, res2 = torch.empty(T, H, dtype=torch.bfloat16, device=dev), torch.empty(T, H, dtype=torch.bfloat16, device=dev)
+    xp1 = torch.zeros(ops.packed_numel(T, H), dtype=torch.bfloat16, device=dev)
+    xp2 = torch.zeros_like(xp1)
+    ss1, ss2 = ops.norm_stats_buffer(dev, 2)
+    ss1.fill_(7)
+    ss2.fill_(9)
+    ops.rmsnorm(h, table[0], EPS, out=xp1, residual=res1, mode=3, packed=True, ss=ss1)
+    ops.embed_stage_entry(ids, table, xp2, res2, ss2)
+    assert torch.equal(res1, res2) and torch.equal(xp1, xp2)
+    assert torch.equal(ss1.view(-1, 256)[:, :T], ss2.view(-1, 256)[:, :T])

@@ -39,6 +39,12 @@
 #include <stdlib.h>
 #include <type_traits>
 
+// split-K slabs of the reduce-launch path: write-through (1, default: 64 sessions 4.286 -> 4.264 ms,
+// batch 1 2.682 -> 2.671, 70B fp8 16.89 -> 16.84; profiles/r6sc1) or plain (0) stores
+#ifndef MP_SLAB_SC1
+#define MP_SLAB_SC1 1
+#endif
+
 namespace mp {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
@@ -1548,7 +1554,15 @@ __global__ __launch_bounds__(RW_WAVES * 64) void gemm_rwk_kernel(const bf16_t* _
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = mt * 16 + q * 4 + r;
-        if (row < M) slab[(int64_t)row * N + col] = v[r];
+        if (row < M) {
+#if MP_SLAB_SC1
+          // write-through (sc1) store: the slab is not left dirty in this XCD's L2 for the
+          // kernel-end writeback (MI355X_MICROARCH boundary row: + dirty bytes / 6 TB/s)
+          __hip_atomic_store(slab + (int64_t)row * N + col, v[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+          slab[(int64_t)row * N + col] = v[r];
+#endif
+        }
       }
     }
   }
@@ -1564,7 +1578,14 @@ __global__ __launch_bounds__(RW_WAVES * 64) void gemm_rwk_kernel(const bf16_t* _
 #define MP_SKR_CPT 4
 #endif
 constexpr int SKR_CPT = MP_SKR_CPT;
-template <int EPI, int S>
+// WT: the row outputs (read by the next launch) stored write-through.  Measured per row width
+// (profiles/r6osc): 4096-wide rows (Llama-2-7B o / down, 64 sessions) 4.225 -> 4.195 ms per step;
+// 8192-wide rows (Llama-3-70B fp8) 16.87 -> 17.05 ms.  launch_splitk_reduce_e: WT iff
+// N <= MP_SKR_WT_MAXN (4096).
+#ifndef MP_SKR_WT_MAXN
+#define MP_SKR_WT_MAXN 4096
+#endif
+template <int EPI, int S, bool WT>
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ part, int M, int N,
                                                             bf16_t* __restrict__ y, int64_t ys,
                                                             const bf16_t* __restrict__ res, int64_t rs,
@@ -1618,9 +1639,18 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
         if constexpr (EPI == 3) sq += fx_sq(bf2f(o[j]));
       }
     }
-    *reinterpret_cast<uvec*>(y + (int64_t)row * ys + col) = o;
     // (packed layout: 8 consecutive columns of a row are contiguous, so CPT in {4, 8} stays one store)
-    if constexpr (EPI == 3) *reinterpret_cast<uvec*>(ep.ap + apk_off(row, col, ep.mt_out)) = o;
+    if constexpr (WT && CPT == 4) {
+      const u64 ob = __builtin_bit_cast(u64, o);
+      __hip_atomic_store(reinterpret_cast<u64*>(y + (int64_t)row * ys + col), ob, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      if constexpr (EPI == 3)
+        __hip_atomic_store(reinterpret_cast<u64*>(ep.ap + apk_off(row, col, ep.mt_out)), ob, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      *reinterpret_cast<uvec*>(y + (int64_t)row * ys + col) = o;
+      if constexpr (EPI == 3) *reinterpret_cast<uvec*>(ep.ap + apk_off(row, col, ep.mt_out)) = o;
+    }
   }
   if constexpr (EPI == 3) {
     if (ep.ss_out == nullptr) return;
@@ -1637,9 +1667,13 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 template <int EPI>
 static void launch_splitk_reduce_e(int S, dim3 g2, hipStream_t stream, const float* part, int M, int N, void* y,
                                    int64_t ys, const void* res, int64_t rs, const EpiArgs& ep) {
-#define MP_SKR(S_)                                                                                        \
-  hipLaunchKernelGGL((splitk_reduce_kernel<EPI, S_>), g2, dim3(256), 0, stream, part, M, N, (bf16_t*)y, ys, \
-                     (const bf16_t*)res, rs, ep)
+#define MP_SKR(S_)                                                                                          \
+  if (N <= MP_SKR_WT_MAXN)                                                                                  \
+    hipLaunchKernelGGL((splitk_reduce_kernel<EPI, S_, true>), g2, dim3(256), 0, stream, part, M, N, (bf16_t*)y, \
+                       ys, (const bf16_t*)res, rs, ep);                                                     \
+  else                                                                                                      \
+    hipLaunchKernelGGL((splitk_reduce_kernel<EPI, S_, false>), g2, dim3(256), 0, stream, part, M, N,          \
+                       (bf16_t*)y, ys, (const bf16_t*)res, rs, ep)
   switch (S) {
     case 2: MP_SKR(2); break;
     case 3: MP_SKR(3); break;

@@ -11,7 +11,7 @@ timeout -k 10 120 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke
 tail -1 $O/smoke.txt
 timeout -k 10 200 python3 bench.py > $O/bench_default.json 2> $O/bench_default.err || exit 1
 tail -1 $O/bench_default.json
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 bench.py > $O/bench_prof.json 2> $O/bench_prof.err || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py > $O/bench_prof.json 2> $O/bench_prof.err || exit 1
 find $O/prof -name "*kernel_stats.csv" -exec cp {} $O/kernel_stats.csv \; && rm -rf $O/prof
 head -12 $O/kernel_stats.csv | cut -c1-150
 for m in w8a16 mx; do

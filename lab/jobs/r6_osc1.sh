@@ -1,0 +1,28 @@
+#!/bin/bash
+# Round 6: write-through stores beyond the split-K slabs: bf16 GEMM / reduce outputs (ablation library
+# -DMP_OUT_SC1=1; run 1 of this job, when that switch had no bits: reduce AND epilogue outputs, now
+# MP_OUT_SC1=3) vs the default (sc1 slabs, plain outputs) vs plain slabs (-DMP_SLAB_SC1=0):
+# GEMM tests on the osc1 library, then 7B 64 / 1 sessions and 70B fp8 interleaved.
+set -o pipefail
+O=gpurun_out/${1:-r6osc1}
+mkdir -p $O
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+MPAMD_KERNEL_LIB=lab/_ab/_mpamd_osc1.so timeout -k 10 600 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_kernels_gpu.py tests/test_fused_norm.py tests/test_qkv_fold_gpu.py tests/test_mx_gpu.py > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
+tail -1 $O/tests.log
+for r in 1 2 3; do
+  for v in default osc1 plain; do
+    case $v in
+      osc1) export MPAMD_KERNEL_LIB=lab/_ab/_mpamd_osc1.so ;;
+      plain) export MPAMD_KERNEL_LIB=lab/_ab/_mpamd_plain.so ;;
+      *) unset MPAMD_KERNEL_LIB ;;
+    esac
+    for b in 64 1; do
+      timeout -k 10 200 python3 bench.py --batch $b > $O/b${b}_${v}_$r.json 2> $O/b${b}_${v}_$r.err || { tail -5 $O/b${b}_${v}_$r.err; exit 1; }
+    done
+    if [ $r -le 2 ] && [ $v != plain ]; then
+      timeout -k 10 300 python3 bench.py --model llama3-70b --fp8 --steps 20 --warmup 3 > $O/b70_${v}_$r.json 2> $O/b70_${v}_$r.err || { tail -5 $O/b70_${v}_$r.err; exit 1; }
+    fi
+    for f in b64 b1 b70; do [ -f $O/${f}_${v}_$r.json ] && python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); print(sys.argv[1], d['ms_per_step'])" $O/${f}_${v}_$r.json; done
+  done
+done
+exit 0

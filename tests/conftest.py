@@ -31,3 +31,18 @@ def pytest_collection_modifyitems(config, items):
     for it in items:
         if "gpu" in it.keywords:
             it.add_marker(skip)
+
+
+@pytest.fixture(autouse=True)
+def _restore_gemm_modes():
+    """Tests that force a decode-GEMM kernel (``ops.set_gemm_sk``) or policy put back whatever was
+    set before them, so no test's outcome depends on which module ran first."""
+    try:
+        from src import ops
+    except Exception:  # pragma: no cover - package import failure is reported by the tests
+        yield
+        return
+    sk, policy = ops._GEMM_SK, ops.gemm_policy()
+    yield
+    ops.set_gemm_sk(sk)
+    ops.set_gemm_policy(policy)

@@ -39,10 +39,13 @@
 #include <stdlib.h>
 #include <type_traits>
 
-// split-K slabs of the reduce-launch path: write-through (1, default: 64 sessions 4.286 -> 4.264 ms,
-// batch 1 2.682 -> 2.671, 70B fp8 16.89 -> 16.84; profiles/r6sc1) or plain (0) stores
-#ifndef MP_SLAB_SC1
-#define MP_SLAB_SC1 1
+// Store form of the split-K slabs of the reduce-launch path (dirty lines left in the XCD L2s are
+// written back at the kernel's end, before the next launch starts: MI355X_MICROARCH boundary row,
+// + dirty bytes / 6 TB/s).  0 plain; 1 write-through (sc1; vs plain: 64 sessions 4.286 -> 4.264 ms,
+// batch 1 2.682 -> 2.671, 70B fp8 16.89 -> 16.84, profiles/r6sc1); 2 nontemporal (default; vs sc1:
+// 64 sessions 4.250 -> 4.199, 70B fp8 16.92 -> 16.84, 4 of 4 interleaved pairs each, profiles/r6nt)
+#ifndef MP_SLAB_ST
+#define MP_SLAB_ST 2
 #endif
 
 namespace mp {
@@ -1555,10 +1558,12 @@ __global__ __launch_bounds__(RW_WAVES * 64) void gemm_rwk_kernel(const bf16_t* _
       for (int r = 0; r < 4; ++r) {
         const int row = mt * 16 + q * 4 + r;
         if (row < M) {
-#if MP_SLAB_SC1
+#if MP_SLAB_ST == 1
           // write-through (sc1) store: the slab is not left dirty in this XCD's L2 for the
           // kernel-end writeback (MI355X_MICROARCH boundary row: + dirty bytes / 6 TB/s)
           __hip_atomic_store(slab + (int64_t)row * N + col, v[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#elif MP_SLAB_ST == 2
+          __builtin_nontemporal_store(v[r], slab + (int64_t)row * N + col);
 #else
           slab[(int64_t)row * N + col] = v[r];
 #endif
@@ -1578,10 +1583,11 @@ __global__ __launch_bounds__(RW_WAVES * 64) void gemm_rwk_kernel(const bf16_t* _
 #define MP_SKR_CPT 4
 #endif
 constexpr int SKR_CPT = MP_SKR_CPT;
-// WT: the row outputs (read by the next launch) stored write-through.  Measured per row width
-// (profiles/r6osc): 4096-wide rows (Llama-2-7B o / down, 64 sessions) 4.225 -> 4.195 ms per step;
-// 8192-wide rows (Llama-3-70B fp8) 16.87 -> 17.05 ms.  launch_splitk_reduce_e: WT iff
-// N <= MP_SKR_WT_MAXN (4096).
+// Store form of the row outputs (read by the next launch), measured per row width against plain
+// stores: WT = write-through (sc1) for 4096-wide rows (Llama-2-7B o / down, 64 sessions: 4.225 ->
+// 4.195 ms per step, profiles/r6osc; on 8192-wide rows it lost: 70B fp8 16.87 -> 17.05), else
+// nontemporal stores (8192-wide, 70B fp8: 16.88 -> 16.75, profiles/r6nt).  launch_splitk_reduce_e:
+// WT iff N <= MP_SKR_WT_MAXN (4096).
 #ifndef MP_SKR_WT_MAXN
 #define MP_SKR_WT_MAXN 4096
 #endif
@@ -1648,8 +1654,9 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
         __hip_atomic_store(reinterpret_cast<u64*>(ep.ap + apk_off(row, col, ep.mt_out)), ob, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
     } else {
-      *reinterpret_cast<uvec*>(y + (int64_t)row * ys + col) = o;
-      if constexpr (EPI == 3) *reinterpret_cast<uvec*>(ep.ap + apk_off(row, col, ep.mt_out)) = o;
+      __builtin_nontemporal_store(o, reinterpret_cast<uvec*>(y + (int64_t)row * ys + col));
+      if constexpr (EPI == 3)
+        __builtin_nontemporal_store(o, reinterpret_cast<uvec*>(ep.ap + apk_off(row, col, ep.mt_out)));
     }
   }
   if constexpr (EPI == 3) {
